@@ -1,0 +1,291 @@
+// Wavefront shading kernels: camera rays, per-vertex shade (NEE + BSDF sample),
+// progressive accumulation (gfx950).
+//
+// Restates the reference kernels with the parity decisions of SURVEY §8(a):
+//   kernelPrimaryRays            src/cudaRenderer.cu:312-376  -> k_camera
+//   kernelDirectLightRays        cu:380-481                   -> NEE part of k_shade
+//   kernelProcessIntersections   cu:544-664                   -> BSDF part of k_shade
+//   leaf hit construction        cu:1201-1291                 -> hit record in k_shade
+//   kernelUpdateSSImage / kernelReconstructImage / kernelAccumulate
+//                                cu:666-742                   -> k_accum
+// Deviations (all mirrored by oracle/ptoracle.c): per-path radiance
+// accumulator (a miss keeps the light gathered so far); orthonormal frame with
+// a guide that cannot be parallel to n; counter-based Philox streams instead of
+// curand XORWOW; normalised light cosine (cu:422 uses the unnormalised
+// direction); glass, spheres and point lights; parametric bounce count.
+#include "trace.h"
+
+namespace pt {
+
+constexpr uint32_t F_EXT = 1u;     // extension ray pending in slot p
+constexpr uint32_t F_SHADOW = 2u;  // shadow ray pending in slot N + p
+constexpr uint32_t F_SPEC = 4u;    // last scattering was specular
+constexpr float INV_PI = 0.318309886183790671f;
+constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
+
+struct ShadeArgs {
+  float4* ro;
+  float4* rd;
+  unsigned long long* hit;
+  float4* ps0;  // T.xyz, flags | vertex << 8
+  float4* ps1;  // L.xyz, pixel
+  float4* ps2;  // pending shadow contribution
+  const float4* __restrict__ prims;
+  const pt_prim_shading* __restrict__ shading;
+  const pt_bsdf* __restrict__ bsdfs;
+  const uint32_t* __restrict__ pix_of;
+  pt_light light;
+  pt_camera cam;
+  uint32_t N, npix, sample_base, seed;
+  int width, height, max_bounces;
+  uint32_t flags;
+};
+
+__device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+__device__ __forceinline__ f3 xyz(float4 a) { return mk(a.x, a.y, a.z); }
+
+__global__ __launch_bounds__(TPB) void k_camera(ShadeArgs S) {
+  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
+  if (p >= S.N) return;
+  const uint32_t q = p % S.npix, j = p / S.npix;
+  const uint32_t g = S.pix_of[q];
+  const uint32_t row = g / (uint32_t)S.width, col = g - row * (uint32_t)S.width;
+  const uint32_t s = S.sample_base + j;
+  const u4 u = rng(S.seed, g, s, 0, 0);
+  // cu:338-354: ss = (x + u, y + v); k = ((ss.y/W)-.5, -((ss.x/H)-.5), 1) / |k|
+  float ssx = (float)row + u01(u.x);
+  float ssy = (float)col + u01(u.y);
+  float kx = ssy / (float)S.width - 0.5f;
+  float ky = -(ssx / (float)S.height - 0.5f);
+  float kz = 1.0f;
+  float len = sqrtf(kx * kx + ky * ky + kz * kz);
+  kx = kx / len;
+  ky = ky / len;
+  kz = kz / len;
+  const f3 L = ld3(S.cam.left), U = ld3(S.cam.up), K = ld3(S.cam.look_at);
+  f3 dir = mk(kx * L.x + ky * U.x + kz * K.x, kx * L.y + ky * U.y + kz * K.y, kx * L.z + ky * U.z + kz * K.z);
+  dir = normalize(dir);
+  S.ro[p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], __builtin_inff());
+  S.rd[p] = make_float4(dir.x, dir.y, dir.z, 0.0f);
+  S.hit[p] = PT_HIT_NONE;
+  S.ro[S.N + p] = make_float4(0.f, 0.f, 0.f, -1.0f);
+  S.hit[S.N + p] = PT_HIT_NONE;
+  S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
+  S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
+  S.ps2[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
+__global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
+  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
+  if (p >= S.N) return;
+  const float4 s0 = S.ps0[p];
+  uint32_t flags = __float_as_uint(s0.w);
+  if ((flags & (F_EXT | F_SHADOW)) == 0) return;
+  f3 T = xyz(s0);
+  const float4 s1 = S.ps1[p];
+  f3 L = xyz(s1);
+  const uint32_t g = __float_as_uint(s1.w);
+  const uint32_t sidx = S.sample_base + p / S.npix;
+
+  // 1. resolve the shadow ray of the previous vertex
+  if (flags & F_SHADOW) {
+    if (S.hit[S.N + p] == PT_HIT_NONE) L = L + xyz(S.ps2[p]);
+  }
+  bool new_ext = false, new_sh = false;
+  f3 o_new = mk(0, 0, 0), d_new = mk(0, 0, 1), sh_o = mk(0, 0, 0), sh_d = mk(0, 0, 1), C = mk(0, 0, 0);
+  float sh_tmax = -1.0f;
+  uint32_t spec = flags & F_SPEC;
+  const uint32_t vtx = (flags >> 8) & 0xffu;
+
+  // 2. shade the hit of the extension ray
+  if (flags & F_EXT) {
+    const unsigned long long h = S.hit[p];
+    if (h != PT_HIT_NONE) {
+      const float t = __uint_as_float((uint32_t)(h >> 32));
+      const uint32_t prim = (uint32_t)h;
+      const f3 o = xyz(S.ro[p]);
+      const f3 d = xyz(S.rd[p]);
+      const f3 P = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+      const float4* Q = S.prims + (size_t)prim * 6;
+      const float4 q0 = Q[0];
+      const uint32_t meta = __float_as_uint(q0.w);
+      f3 ns;
+      if ((meta >> 28) == PT_PRIM_SPHERE) {
+        ns = normalize(mk(P.x - q0.x, P.y - q0.y, P.z - q0.z));
+      } else {
+        // barycentric shading normal (cu:1213-1221)
+        const f3 A = xyz(q0), B = xyz(Q[1]), Cv = xyz(Q[2]);
+        const pt_prim_shading sh = S.shading[prim];
+        float total = length(cross(A - B, B - Cv));
+        float bC = length(cross(A - P, B - P)) / total;
+        float bA = length(cross(B - P, Cv - P)) / total;
+        float bB = length(cross(Cv - P, A - P)) / total;
+        f3 n0 = ld3(sh.n0), n1 = ld3(sh.n1), n2 = ld3(sh.n2);
+        ns = normalize(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y,
+                          bA * n0.z + bB * n1.z + bC * n2.z));
+      }
+      const bool front = dot(ns, d) < 0.0f;
+      const f3 n = front ? ns : mk(-ns.x, -ns.y, -ns.z);  // faces the incoming ray (cu:1222)
+      const f3 pt = P - d * EPS;                          // cu:1224
+      const pt_bsdf B = S.bsdfs[meta & 0x0FFFFFFFu];
+      if (B.type == PT_BSDF_EMISSION) {
+        if (!(S.flags & PT_FLAG_NO_EMISSION) && (vtx == 1u || spec))
+          L = L + mulv(T, ld3(B.albedo));
+      } else {
+        const u4 u = rng(S.seed, g, sidx, vtx, 0);
+        const f3 guide = (fabsf(n.x) < 0.9f) ? mk(1.0f, 0.0f, 0.0f) : mk(0.0f, 1.0f, 0.0f);
+        const f3 dpdu = normalize(cross(guide, n));
+        const f3 dpdv = cross(n, dpdu);
+        if (B.type == PT_BSDF_DIFFUSE) {
+          const f3 alb = ld3(B.albedo);
+          // next-event estimation toward the scene light (cu:380-481)
+          if (S.light.type == PT_LIGHT_AREA) {
+            const float sx = u01(u.x) - 0.5f, sy = u01(u.y) - 0.5f;
+            const f3 pos = ld3(S.light.position), dx = ld3(S.light.dim_x), dy = ld3(S.light.dim_y);
+            const f3 lpt = mk(pos.x + sx * dx.x + sy * dy.x, pos.y + sx * dx.y + sy * dy.y,
+                              pos.z + sx * dx.z + sy * dy.z);
+            const f3 dv = lpt - pt;
+            const float sq = dot(dv, dv);
+            const float dist = sqrtf(sq);
+            const f3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+            const float cosl = dot(w, ld3(S.light.direction));
+            const float cosn = dot(n, w);
+            if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
+              const float pdf = sq / (S.light.area * -cosl);
+              const float scale = (cosn / pdf) * INV_PI;
+              C = mulv(mulv(T, alb), ld3(S.light.radiance)) * scale;
+              new_sh = true;
+              sh_o = pt;
+              sh_d = w;
+              sh_tmax = dist - EPS;
+            }
+          } else if (S.light.type == PT_LIGHT_POINT) {
+            const f3 dv = ld3(S.light.position) - pt;
+            const float sq = dot(dv, dv);
+            const float dist = sqrtf(sq);
+            const f3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+            const float cosn = dot(n, w);
+            if (dist > 1e-2f && cosn > 0.0f) {
+              C = mulv(mulv(T, alb), ld3(S.light.radiance)) * (cosn * INV_PI);
+              new_sh = true;
+              sh_o = pt;
+              sh_d = w;
+              sh_tmax = dist - EPS;
+            }
+          }
+          // BSDF sample
+          float x, y, z, sn, cs;
+          sincos2pi(u01(u.w), &sn, &cs);
+          if (S.flags & PT_FLAG_COSINE_DIFFUSE) {
+            const float u2 = u01(u.z);
+            const float r = sqrtf(u2);
+            x = r * cs;
+            y = r * sn;
+            z = sqrtf(fmaxf(0.0f, 1.0f - u2));
+          } else {
+            // uniform hemisphere: the reference's folded uniform sphere (cu:619-622)
+            z = fabsf(2.0f * u01(u.z) - 1.0f);
+            const float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+            x = r * cs;
+            y = r * sn;
+          }
+          d_new = normalize(mk(n.x * z + x * dpdu.x + y * dpdv.x, n.y * z + x * dpdu.y + y * dpdv.y,
+                               n.z * z + x * dpdu.z + y * dpdv.z));
+          if (S.flags & PT_FLAG_COSINE_DIFFUSE) {
+            T = mulv(T, alb);
+          } else {
+            const float c = fabsf(dot(d_new, n));
+            T = mk(((T.x * c) * alb.x) * 2.0f, ((T.y * c) * alb.y) * 2.0f, ((T.z * c) * alb.z) * 2.0f);
+          }
+          o_new = pt + n * EPS;  // cu:593
+          spec = 0;
+        } else if (B.type == PT_BSDF_MIRROR) {
+          const float dn = dot(d, n);
+          d_new = normalize(d - n * (2.0f * dn));
+          T = mulv(T, ld3(B.albedo));
+          o_new = pt + n * EPS;
+          spec = F_SPEC;
+        } else {  // PT_BSDF_GLASS (Fresnel-weighted reflect / refract, bsdf.h:187-212)
+          const float ior = B.ior;
+          const float eta = front ? (1.0f / ior) : ior;
+          const float cosi = -dot(d, n);
+          const float sin2t = (eta * eta) * (1.0f - cosi * cosi);
+          bool refl = true;
+          float cost = 0.0f;
+          if (sin2t < 1.0f) {
+            cost = sqrtf(1.0f - sin2t);
+            float r0 = (1.0f - ior) / (1.0f + ior);
+            r0 = r0 * r0;
+            const float c = front ? cosi : cost;
+            const float m = 1.0f - c;
+            const float F = r0 + (1.0f - r0) * (((m * m) * (m * m)) * m);
+            const u4 u2 = rng(S.seed, g, sidx, vtx, 1);
+            refl = u01(u2.x) < F;
+          }
+          if (refl) {
+            const float dn = dot(d, n);
+            d_new = normalize(d - n * (2.0f * dn));
+            T = mulv(T, ld3(B.albedo));
+            o_new = pt + n * EPS;
+          } else {
+            d_new = normalize(d * eta + n * (eta * cosi - cost));
+            T = mulv(T, ld3(B.transmittance));
+            o_new = P - n * EPS;
+          }
+          spec = F_SPEC;
+        }
+        new_ext = (vtx <= (uint32_t)S.max_bounces) && (T.x > 0.0f || T.y > 0.0f || T.z > 0.0f);
+      }
+    }
+  }
+
+  const uint32_t fout = spec | (new_ext ? F_EXT : 0u) | (new_sh ? F_SHADOW : 0u) | ((vtx + 1u) << 8);
+  S.ps0[p] = make_float4(T.x, T.y, T.z, __uint_as_float(fout));
+  S.ps1[p] = make_float4(L.x, L.y, L.z, __uint_as_float(g));
+  if (new_sh) S.ps2[p] = make_float4(C.x, C.y, C.z, 0.0f);
+  if (new_ext) {
+    S.ro[p] = make_float4(o_new.x, o_new.y, o_new.z, __builtin_inff());
+    S.rd[p] = make_float4(d_new.x, d_new.y, d_new.z, 0.0f);
+  } else {
+    S.ro[p] = make_float4(0.f, 0.f, 0.f, -1.0f);
+  }
+  S.hit[p] = PT_HIT_NONE;
+  if (new_sh) {
+    S.ro[S.N + p] = make_float4(sh_o.x, sh_o.y, sh_o.z, sh_tmax);
+    S.rd[S.N + p] = make_float4(sh_d.x, sh_d.y, sh_d.z, 0.0f);
+  } else {
+    S.ro[S.N + p] = make_float4(0.f, 0.f, 0.f, -1.0f);
+  }
+  S.hit[S.N + p] = PT_HIT_NONE;
+}
+
+// Sum each owned pixel's samples of this batch into the accumulation buffer,
+// in sample order (deterministic; replaces kernelUpdateSSImage +
+// kernelReconstructImage + kernelAccumulate, cu:666-742).
+__global__ __launch_bounds__(TPB) void k_accum(const float4* __restrict__ ps1, float4* accum, uint32_t npix,
+                                               uint32_t spp_b) {
+  const uint32_t q = blockIdx.x * TPB + threadIdx.x;
+  if (q >= npix) return;
+  float4 a = accum[q];
+  for (uint32_t j = 0; j < spp_b; ++j) {
+    const float4 l = ps1[(size_t)j * npix + q];
+    a.x = a.x + l.x;
+    a.y = a.y + l.y;
+    a.z = a.z + l.z;
+  }
+  accum[q] = a;
+}
+
+// Repack pt_intersect's 8-float ray records into the SoA slots.
+__global__ __launch_bounds__(TPB) void k_load_rays(const float4* __restrict__ in, float4* ro, float4* rd,
+                                                   unsigned long long* hit, uint32_t n) {
+  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  ro[i] = in[2 * i];
+  float4 b = in[2 * i + 1];
+  b.w = 0.0f;
+  rd[i] = b;
+  hit[i] = PT_HIT_NONE;
+}
+
+}  // namespace pt

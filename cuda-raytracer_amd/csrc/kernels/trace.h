@@ -1,0 +1,58 @@
+// Shared definitions of the traversal and shading kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_api.h"
+#include "ptmath.h"
+
+namespace pt {
+
+constexpr int TPB = 256;          // threads per workgroup (4 waves)
+constexpr int RPT = 4;            // rays per thread in a traversal item
+constexpr int TILE = TPB * RPT;   // rays per traversal item
+constexpr int NLANE = 8;          // queue lanes (one per XCD)
+constexpr int LEVEL_GRID = 2048;  // workgroups of the per-level grid-stride kernel (8 per CU)
+
+// device statistics slots (unsigned long long)
+enum {
+  STAT_R = 0,
+  STAT_V = 1,
+  STAT_PEAKQ = 2,
+  STAT_LV0 = 8,  // 16 per-level visit counters
+  STAT_COUNT = 32
+};
+
+struct TraceArgs {
+  const pt_node* __restrict__ nodes;
+  const float4* __restrict__ prims;  // 6 float4 per primitive
+  float4* ro;                        // o.xyz, tmax (tmax < 0: empty slot)
+  const float4* __restrict__ rd;     // d.xyz, 0
+  unsigned long long* hit;           // {t bits, prim} or PT_HIT_NONE
+  uint32_t* cnt;                     // [node][lane] rays pushed into the node
+  uint32_t* qoff;                    // [node][lane] absolute queue offset
+  uint32_t* q;                       // ray-id queues (two parity halves)
+};
+
+struct LevelArgs {
+  int first;  // first node id of the level
+  int nl;     // nodes in the level
+  int maxln;  // row stride - 1 of iprefix
+  const uint32_t* iprefix;  // [lane][maxln+1] exclusive item prefix (read)
+  uint32_t* iprefix_w;      // same array (written by the scan)
+  const uint32_t* nitems;   // items of the level (read)
+  uint32_t* nitems_w;
+};
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+}  // namespace pt

@@ -1,0 +1,444 @@
+// Breadth-first 4-wide BVH traversal with dynamic ray scheduling (gfx950).
+//
+// MI355X-native restatement of the reference hot loop
+//   rayIntersectSingle           src/cudaRenderer.cu:846-1297
+//   kernelRayIntersectSingle     cu:1304-1310   (root pass)
+//   kernelScanCounts             cu:1317-1431   (per-level scan)
+//   kernelRayIntersectLevel      cu:1435-1489   (per-level pass)
+//   kernelMergeIntersections     cu:515-540     (closest-hit min reduction)
+//   sharedMemExclusiveScan       src/exclusiveScan.cu_inl:52-110
+//
+// What is kept: level-synchronous traversal, one ray queue per BVH node,
+// per-workgroup compaction of the rays that hit each child box, one atomic
+// slot reservation per workgroup per child, child queue capacity = parent's
+// ray count (cu:922, 1384), all triangles of a leaf tested per ray.
+//
+// What is MI355X-first:
+//  * queues carry 4-byte ray ids; ray geometry lives once in SoA float4 arrays
+//    (o.xyz,tmax / d.xyz) instead of 128-byte CuRay copies per queue entry;
+//  * compaction = wave64 ballot + mbcnt, cross-wave offsets through LDS
+//    (replaces the warp-32 Hillis-Steele scan, exclusiveScan.cu_inl:31-48);
+//  * an item is 1024 rays (256 threads x 4), so one atomic reserves up to 1024
+//    slots; queues and counters are split into 8 lanes (one per XCD under the
+//    observed round-robin dispatch) so top-level nodes see 8x less atomic
+//    contention; a ray's lane is fixed by its root item;
+//  * the closest hit is ONE 64-bit atomicMin on {fp32 bits of t, prim index}
+//    per ray and leaf: order independent, ties go to the lowest sorted prim
+//    index, no 16-slot candidate buffer and no merge kernel;
+//  * per-level work ranges are computed on the device (no D2H per level,
+//    cu:2237); the level kernel is a grid-stride loop over items;
+//  * node and primitive records are wave-uniform and read with scalar loads.
+#include "trace.h"
+
+namespace pt {
+
+// ---- primitive tests ----------------------------------------------------------
+
+// Reference triangle test intersectRayTriangle (cu:217-270) on precomputed
+// operands (pt_api.h pt_prim).  Returns t >= 0 or -1 on a miss.  t = -0 is
+// returned as +0 so that the {t bits, id} key orders correctly.
+__device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q0, const float4 q1,
+                                          const float4 q2, const float4 q3, const float4 q4,
+                                          const float4 q5) {
+  const f3 N = mk(q3.x, q3.y, q3.z);
+  float ndd = N.x * d.x + N.y * d.y + N.z * d.z;
+  if (fabsf(ndd) < 1e-6f) return -1.0f;
+  float t = (q1.w - (N.x * o.x + N.y * o.y + N.z * o.z)) / ndd;
+  if (t < 0.0f) return -1.0f;
+  f3 P = mk(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
+  // edge 0: cross(v1 - v0, P - v0)
+  f3 vp = mk(P.x - q0.x, P.y - q0.y, P.z - q0.z);
+  f3 e = mk(q4.x, q4.y, q4.z);
+  f3 C = cross(e, vp);
+  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
+  // edge 1: cross(v2 - v1, P - v1)
+  vp = mk(P.x - q1.x, P.y - q1.y, P.z - q1.z);
+  e = mk(q5.x, q5.y, q5.z);
+  C = cross(e, vp);
+  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
+  // edge 2: cross(v0 - v2, P - v2)
+  vp = mk(P.x - q2.x, P.y - q2.y, P.z - q2.z);
+  e = mk(q2.w, q3.w, q4.w);
+  C = cross(e, vp);
+  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
+  return t == 0.0f ? 0.0f : t;
+}
+
+// Ray-sphere (the reference has none: spheres are reinterpret_cast to
+// triangles at cu:1760).  Nearest root with t >= 0; d must be unit length.
+__device__ __forceinline__ float sphere_test(const f3 o, const f3 d, const float4 q0, const float4 q1) {
+  f3 oc = mk(o.x - q0.x, o.y - q0.y, o.z - q0.z);
+  float b = oc.x * d.x + oc.y * d.y + oc.z * d.z;
+  float cc = (oc.x * oc.x + oc.y * oc.y + oc.z * oc.z) - q1.y;
+  float disc = b * b - cc;
+  if (disc < 0.0f) return -1.0f;
+  float sq = sqrtf(disc);
+  float t0 = -b - sq;
+  float t1 = -b + sq;
+  float t = (t0 >= 0.0f) ? t0 : t1;
+  if (t < 0.0f) return -1.0f;
+  return t == 0.0f ? 0.0f : t;
+}
+
+// Slab test against one child box.  Conservative replacement of intersectBBox
+// (cu:154-207): a box is entered iff its slab interval meets [0, tmax].  Only
+// decides which queues a ray enters, never the reported hit.
+__device__ __forceinline__ bool box_hit(float bx0, float bx1, float by0, float by1, float bz0, float bz1,
+                                        const f3 oi, const f3 inv, float tmax) {
+  float tx0 = __builtin_fmaf(bx0, inv.x, -oi.x), tx1 = __builtin_fmaf(bx1, inv.x, -oi.x);
+  float ty0 = __builtin_fmaf(by0, inv.y, -oi.y), ty1 = __builtin_fmaf(by1, inv.y, -oi.y);
+  float tz0 = __builtin_fmaf(bz0, inv.z, -oi.z), tz1 = __builtin_fmaf(bz1, inv.z, -oi.z);
+  float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+  float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+  return tn <= tf;
+}
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// ---- one work item: up to TILE rays of one node's queue lane ---------------------
+// ids: implicit (root pass: base + i) or read from qin[base + i].
+template <bool IMPLICIT>
+__device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, uint32_t base, int n, int lane,
+                                             uint32_t* sh) {
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const pt_node* __restrict__ nd = A.nodes + node;
+
+  uint32_t id[RPT];
+  f3 o[RPT], d[RPT];
+  float tmax[RPT];
+  bool valid[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int i = j * TPB + tid;
+    valid[j] = i < n;
+    id[j] = 0;
+    tmax[j] = -1.0f;
+    o[j] = mk(0.f, 0.f, 0.f);
+    d[j] = mk(0.f, 0.f, 1.f);
+    if (valid[j]) {
+      id[j] = IMPLICIT ? base + (uint32_t)i : A.q[base + i];
+      float4 a = A.ro[id[j]];
+      o[j] = mk(a.x, a.y, a.z);
+      tmax[j] = a.w;
+      if (IMPLICIT) valid[j] = a.w >= 0.0f;
+      if (valid[j]) {
+        float4 b = A.rd[id[j]];
+        d[j] = mk(b.x, b.y, b.z);
+      }
+    }
+  }
+
+  uint32_t nvalid = 0;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) nvalid += valid[j] ? 1u : 0u;
+
+  const int pcount = nd->prim_count;
+  if (pcount > 0) {
+    // ---------------- leaf: all primitives against every ray -----------------
+    const int pstart = nd->prim_start;
+    float bt[RPT];
+    int bp[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      bt[j] = tmax[j];
+      bp[j] = -1;
+    }
+    const float4* __restrict__ P = A.prims + (size_t)pstart * 6;
+    for (int k = 0; k < pcount; ++k, P += 6) {
+      const float4 q0 = P[0], q1 = P[1];
+      const uint32_t meta = __float_as_uint(q0.w);
+      if ((meta >> 28) == PT_PRIM_SPHERE) {
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+          float t = sphere_test(o[j], d[j], q0, q1);
+          if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
+            bt[j] = t;
+            bp[j] = pstart + k;
+          }
+        }
+      } else {
+        const float4 q2 = P[2], q3 = P[3], q4 = P[4], q5 = P[5];
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+          float t = tri_test(o[j], d[j], q0, q1, q2, q3, q4, q5);
+          if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
+            bt[j] = t;
+            bp[j] = pstart + k;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      if (valid[j] && bp[j] >= 0) {
+        unsigned long long key =
+            ((unsigned long long)__float_as_uint(bt[j]) << 32) | (unsigned long long)(uint32_t)bp[j];
+        atomicMin(A.hit + id[j], key);
+        // racy monotone-safe tmax update: any stored value is a real hit's t,
+        // so culling boxes beyond it never loses the closest hit
+        if (bt[j] < tmax[j]) reinterpret_cast<float*>(A.ro + id[j])[3] = bt[j];
+      }
+    }
+    return nvalid;
+  }
+
+  // ---------------- interior: 4 child boxes, compaction, push -----------------
+  uint32_t bits[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    f3 inv = mk(__builtin_amdgcn_rcpf(d[j].x), __builtin_amdgcn_rcpf(d[j].y), __builtin_amdgcn_rcpf(d[j].z));
+    f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
+    uint32_t b = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      bool h = box_hit(nd->bmin_x[c], nd->bmax_x[c], nd->bmin_y[c], nd->bmax_y[c], nd->bmin_z[c],
+                       nd->bmax_z[c], oi, inv, tmax[j]);
+      b |= (valid[j] && h) ? (1u << c) : 0u;
+    }
+    bits[j] = b;
+  }
+  // per-wave counts per child -> LDS
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    uint32_t wc = 0;
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) wc += (uint32_t)__popcll(__ballot((bits[j] >> c) & 1u));
+    if ((tid & 63) == 0) sh[c * 4 + wave] = wc;
+  }
+  __syncthreads();
+  if (tid < 4) {
+    const int c = tid;
+    const int child = nd->child[c];
+    uint32_t w0 = sh[c * 4 + 0], w1 = sh[c * 4 + 1], w2 = sh[c * 4 + 2], w3 = sh[c * 4 + 3];
+    uint32_t tot = w0 + w1 + w2 + w3;
+    uint32_t b = 0;
+    if (child >= 0 && tot) b = atomicAdd(A.cnt + (size_t)child * NLANE + lane, tot);
+    sh[16 + c * 4 + 0] = b;
+    sh[16 + c * 4 + 1] = b + w0;
+    sh[16 + c * 4 + 2] = b + w0 + w1;
+    sh[16 + c * 4 + 3] = b + w0 + w1 + w2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int child = nd->child[c];
+    if (child < 0) continue;
+    uint32_t off = sh[16 + c * 4 + wave] + A.qoff[(size_t)child * NLANE + lane];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const bool h = (bits[j] >> c) & 1u;
+      const unsigned long long m = __ballot(h);
+      if (h) A.q[off + mbcnt64(m)] = id[j];
+      off += (uint32_t)__popcll(m);
+    }
+  }
+  return nvalid;
+}
+
+// ---- root pass (level 0): implicit queue = slots [r0, r1) ------------------------
+__global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, uint32_t r0, uint32_t r1,
+                                                    uint32_t* __restrict__ rootcnt) {
+  __shared__ uint32_t sh[64];
+  const uint32_t item = blockIdx.x;
+  const uint32_t first = r0 + item * TILE;
+  const int n = (int)min((uint32_t)TILE, r1 - first);
+  const int lane = item & (NLANE - 1);
+  uint32_t v = process_item<true>(A, 0, first, n, lane, sh);
+  // valid-ray count of this item (R of the roofline formula)
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[32 + (threadIdx.x >> 6)] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) rootcnt[item] = sh[32] + sh[33] + sh[34] + sh[35];
+}
+
+// ---- per-level pass: grid-stride loop over items --------------------------------
+__global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
+  __shared__ uint32_t sh[64];
+  __shared__ int s_node;
+  __shared__ uint32_t s_base;
+  __shared__ int s_n;
+  const uint32_t total = *L.nitems;
+  const int tid = threadIdx.x;
+  for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
+    const int lane = g & (NLANE - 1);
+    const uint32_t m = g >> 3;
+    const uint32_t* __restrict__ ep = L.iprefix + (size_t)lane * (L.maxln + 1);
+    if (tid < 64) {
+      // 64-ary search for the node k with ep[k] <= m < ep[k+1]
+      int lo = 0, hi = L.nl;
+      if (m >= ep[hi]) {
+        lo = -1;  // padding item of a short lane
+      } else {
+        while (hi - lo > 1) {
+          const int step = (hi - lo + 63) >> 6;
+          const int idx = lo + tid * step;
+          const bool le = idx < hi && ep[idx] <= m;
+          const unsigned long long msk = __ballot(le);
+          const int last = 63 - __clzll(msk);
+          lo = lo + last * step;
+          hi = min(lo + step, hi);
+        }
+      }
+      if (tid == 0) {
+        if (lo < 0) {
+          s_node = -1;
+        } else {
+          const int node = L.first + lo;
+          const uint32_t i = m - ep[lo];
+          const uint32_t c = A.cnt[(size_t)node * NLANE + lane];
+          s_node = node;
+          s_base = A.qoff[(size_t)node * NLANE + lane] + i * TILE;
+          s_n = (int)min((uint32_t)TILE, c - i * TILE);
+        }
+      }
+    }
+    __syncthreads();
+    const int node = __builtin_amdgcn_readfirstlane(s_node);
+    const uint32_t base = __builtin_amdgcn_readfirstlane(s_base);
+    const int n = __builtin_amdgcn_readfirstlane(s_n);
+    __syncthreads();
+    if (node >= 0) process_item<false>(A, node, base, n, lane, sh);
+    __syncthreads();
+  }
+}
+
+// ---- per-level scan: work ranges and child queue allocation ---------------------
+// One workgroup of 1024 threads.  For every (node, lane) of level l it turns the
+// node's ray count into items (exclusive prefix per lane, consumed by
+// k_trace_level) and allocates each child's queue lane with capacity = the
+// parent's count in that lane (the reference's wOffset + i*rayCount, cu:922
+// and cu:1384, without the single-warp scan and the D2H of maxBlocks).
+__global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, uint32_t lanecap,
+                                                     uint32_t out_parity_base, unsigned long long* stats,
+                                                     int level, uint32_t* err) {
+  __shared__ uint32_t wsum[16][16];
+  __shared__ uint32_t run[16];
+  __shared__ uint32_t ctot[16];
+  __shared__ unsigned long long vsum;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, ln = tid & 63;
+  if (tid < 16) run[tid] = 0;
+  if (tid == 0) vsum = 0;
+  __syncthreads();
+  unsigned long long myv = 0;
+  for (int chunk = 0; chunk < L.nl; chunk += 1024) {
+    const int k = chunk + tid;
+    const bool act = k < L.nl;
+    const int node = L.first + k;
+    int nch = 0;
+    int child[4] = {-1, -1, -1, -1};
+    if (act && A.nodes[node].prim_count == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        child[c] = A.nodes[node].child[c];
+        nch += child[c] >= 0;
+      }
+    }
+    uint32_t v[16], cnt8[NLANE];
+#pragma unroll
+    for (int s = 0; s < NLANE; ++s) {
+      uint32_t c = act ? A.cnt[(size_t)node * NLANE + s] : 0u;
+      cnt8[s] = c;
+      myv += c;
+      v[s] = (c + TILE - 1) / TILE;          // items
+      v[8 + s] = c * (uint32_t)nch;           // child capacity
+    }
+    // block exclusive scan of 16 values per thread
+    uint32_t incl[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      uint32_t x = v[q];
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(x, off, 64);
+        if (ln >= off) x += y;
+      }
+      incl[q] = x;
+      if (ln == 63) wsum[wave][q] = x;
+    }
+    __syncthreads();
+    if (tid < 16) {
+      uint32_t acc = 0;
+      for (int w = 0; w < 16; ++w) {
+        uint32_t t = wsum[w][tid];
+        wsum[w][tid] = acc;
+        acc += t;
+      }
+      ctot[tid] = acc;
+    }
+    __syncthreads();
+    uint32_t ex[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ex[q] = run[q] + wsum[wave][q] + incl[q] - v[q];
+    if (act) {
+#pragma unroll
+      for (int s = 0; s < NLANE; ++s) L.iprefix_w[(size_t)s * (L.maxln + 1) + k] = ex[s];
+      uint32_t jj = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (child[c] >= 0) {
+#pragma unroll
+          for (int s = 0; s < NLANE; ++s)
+            A.qoff[(size_t)child[c] * NLANE + s] =
+                out_parity_base + (uint32_t)s * lanecap + ex[8 + s] + jj * cnt8[s];
+          jj++;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < 16) run[tid] += ctot[tid];
+    __syncthreads();
+  }
+  // sentinel ep[nl] and item count
+  myv = wave_sum64(myv);
+  if (ln == 0) atomicAdd(&vsum, myv);
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t mx = 0;
+    bool ovf = false;
+    for (int s = 0; s < NLANE; ++s) {
+      L.iprefix_w[(size_t)s * (L.maxln + 1) + L.nl] = run[s];
+      mx = max(mx, run[s]);
+      if (run[8 + s] > lanecap) ovf = true;
+    }
+    if (ovf) {
+      *err |= 1u;
+      mx = 0;  // abandon the rest of this pass; the host reports PT_E_OVERFLOW
+    }
+    *L.nitems_w = mx * NLANE;
+    if (stats) {
+      stats[STAT_V] += vsum;
+      stats[STAT_LV0 + level] += vsum;
+      unsigned long long need = 0;
+      for (int s = 0; s < NLANE; ++s) need = max(need, (unsigned long long)run[8 + s]);
+      if (need * NLANE > stats[STAT_PEAKQ]) stats[STAT_PEAKQ] = need * NLANE;
+    }
+  }
+}
+
+// R of the roofline formula: sum of the root pass's per-item valid counts.
+__global__ __launch_bounds__(1024) void k_sum_root(const uint32_t* __restrict__ rootcnt, int n,
+                                                   unsigned long long* stats) {
+  __shared__ unsigned long long part[16];
+  unsigned long long s = 0;
+  for (int i = threadIdx.x; i < n; i += 1024) s += rootcnt[i];
+  s = wave_sum64(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < 16; ++w) t += part[w];
+    stats[STAT_R] += t;
+    stats[STAT_V] += t;
+    stats[STAT_LV0] += t;
+  }
+}
+
+}  // namespace pt

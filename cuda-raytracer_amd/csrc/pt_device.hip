@@ -1,0 +1,563 @@
+// pt_ctx: device context, memory layout and pass orchestration behind pt_api.h.
+//
+// Replaces CudaRenderer::setup / render / renderFrame / rayIntersect /
+// processLevel (src/cudaRenderer.cu:1872-2564) with a wavefront schedule that
+// never synchronises with the host inside a batch:
+//
+//   batch b (N = npix * spp_b paths):
+//     k_camera                                 (pass 0 rays: camera)
+//     for pass = 0 .. max_bounces + 1:
+//       trace(slots):  memset(cnt) ; k_trace_root ; { k_scan_level ; k_trace_level } per level
+//       k_shade                                (resolve shadows, shade, emit rays of next pass)
+//     k_accum
+//
+// Ray slots: [0, N) extension rays, [N, 2N) shadow rays of the same paths, so a
+// pass traces both at once (the reference traces them in separate passes,
+// cu:2499-2533).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels/trace.hip"
+#include "kernels/shade.hip"
+
+using namespace pt;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace
+
+struct pt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  // scene
+  bool have_scene = false;
+  int n_prims = 0, n_nodes = 0, n_levels = 0;
+  std::vector<int32_t> level_start;
+  int max_level_nodes = 0;
+  bool root_leaf = true;
+  std::vector<pt_node> nodes_host;
+  pt_light light{};
+  pt_camera camera{};
+  pt_node* d_nodes = nullptr;
+  float4* d_prims = nullptr;
+  pt_prim_shading* d_shading = nullptr;
+  pt_bsdf* d_bsdfs = nullptr;
+
+  // wavefront buffers (sized for N paths = 2N ray slots)
+  uint32_t cap_paths = 0;
+  float4 *d_ro = nullptr, *d_rd = nullptr;
+  unsigned long long* d_hit = nullptr;
+  float4 *d_ps0 = nullptr, *d_ps1 = nullptr, *d_ps2 = nullptr;
+  uint32_t* d_q = nullptr;
+  size_t qcap = 0;  // entries per parity half
+  uint32_t* d_cnt = nullptr;
+  uint32_t* d_qoff = nullptr;
+  uint32_t* d_iprefix = nullptr;
+  uint32_t* d_nitems = nullptr;  // one per level
+  uint32_t* d_rootcnt = nullptr;
+  unsigned long long* d_stats = nullptr;
+  uint32_t* d_err = nullptr;
+
+  // framebuffer
+  int fb_w = 0, fb_h = 0, fb_tile = 0, fb_rank = 0, fb_nranks = 0;
+  std::vector<uint32_t> pix_of;  // owned pixel slot -> global pixel
+  uint32_t* d_pix_of = nullptr;
+  float4* d_accum = nullptr;
+  int32_t samples = 0;
+
+  pt_stats stats{};
+  hipEvent_t ev[8] = {};
+};
+
+#define HIPCHK(ctx, call)                                                                 \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);                    \
+      return PT_E_HIP;                                                                    \
+    }                                                                                     \
+  } while (0)
+
+static int fail(pt_ctx* ctx, int code, const std::string& m) {
+  if (ctx) ctx->err = m;
+  return code;
+}
+
+template <class T>
+static int dalloc(pt_ctx* ctx, T** p, size_t count) {
+  if (*p) {
+    hipFree(*p);
+    *p = nullptr;
+  }
+  if (count == 0) count = 1;
+  HIPCHK(ctx, hipMalloc((void**)p, count * sizeof(T)));
+  return PT_OK;
+}
+
+static void free_all(pt_ctx* c) {
+  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ro,     c->d_rd,
+                  c->d_hit,   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_q,      c->d_cnt,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_rootcnt, c->d_stats,  c->d_err,
+                  c->d_pix_of, c->d_accum};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+}
+
+// Buffers for N paths (2N ray slots).  Queue halves hold QFACTOR * 2N ids.
+static constexpr size_t QFACTOR = 24;
+
+static int ensure_paths(pt_ctx* c, uint32_t N) {
+  if (N <= c->cap_paths) return PT_OK;
+  const size_t slots = 2 * (size_t)N;
+  int rc;
+  if ((rc = dalloc(c, &c->d_ro, slots))) return rc;
+  if ((rc = dalloc(c, &c->d_rd, slots))) return rc;
+  if ((rc = dalloc(c, &c->d_hit, slots))) return rc;
+  if ((rc = dalloc(c, &c->d_ps0, N))) return rc;
+  if ((rc = dalloc(c, &c->d_ps1, N))) return rc;
+  if ((rc = dalloc(c, &c->d_ps2, N))) return rc;
+  c->qcap = QFACTOR * slots;
+  c->qcap = (c->qcap + NLANE * 64 - 1) / (NLANE * 64) * (NLANE * 64);
+  if ((rc = dalloc(c, &c->d_q, 2 * c->qcap))) return rc;
+  if ((rc = dalloc(c, &c->d_rootcnt, (slots + TILE - 1) / TILE))) return rc;
+  c->cap_paths = N;
+  return PT_OK;
+}
+
+// Queue offsets of the root's children: root item k belongs to lane k % 8, so
+// lane s sees at most ceil(items/8) * TILE rays; child jj of the root gets that
+// many slots in lane s of the odd-parity half.
+static int set_root_child_offsets(pt_ctx* c) {
+  if (c->root_leaf) return PT_OK;
+  const size_t slots = 2 * (size_t)c->cap_paths;
+  const size_t items = (slots + TILE - 1) / TILE;
+  const size_t per_lane = (items + NLANE - 1) / NLANE * TILE;
+  const size_t lanecap = c->qcap / NLANE;
+  if (4 * per_lane > lanecap) return fail(c, PT_E_OVERFLOW, "root queue capacity");
+  const pt_node& root = c->nodes_host[0];
+  int jj = 0;
+  for (int k = 0; k < 4; ++k) {
+    if (root.child[k] < 0) continue;
+    uint32_t off[NLANE];
+    for (int s = 0; s < NLANE; ++s) off[s] = (uint32_t)(c->qcap + (size_t)s * lanecap + (size_t)jj * per_lane);
+    HIPCHK(c, hipMemcpy(c->d_qoff + (size_t)root.child[k] * NLANE, off, sizeof(off), hipMemcpyHostToDevice));
+    jj++;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PT_OK;
+}
+
+static TraceArgs trace_args(pt_ctx* c) {
+  TraceArgs A;
+  A.nodes = c->d_nodes;
+  A.prims = c->d_prims;
+  A.ro = c->d_ro;
+  A.rd = c->d_rd;
+  A.hit = c->d_hit;
+  A.cnt = c->d_cnt;
+  A.qoff = c->d_qoff;
+  A.q = c->d_q;
+  return A;
+}
+
+// One breadth-first traversal pass over ray slots [r0, r1).
+static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1, bool timed) {
+  if (r1 <= r0) return PT_OK;
+  TraceArgs A = trace_args(c);
+  const uint32_t items = (r1 - r0 + TILE - 1) / TILE;
+  HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)c->n_nodes * NLANE * 4, c->stream));
+  if (timed) hipEventRecord(c->ev[0], c->stream);
+  hipLaunchKernelGGL(k_trace_root, dim3(items), dim3(TPB), 0, c->stream, A, r0, r1, c->d_rootcnt);
+  hipLaunchKernelGGL(k_sum_root, dim3(1), dim3(1024), 0, c->stream, c->d_rootcnt, (int)items, c->d_stats);
+  if (timed) {
+    hipEventRecord(c->ev[1], c->stream);
+    hipEventSynchronize(c->ev[1]);
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+    c->stats.ms_trace_level[0] += ms;
+    c->stats.ms_trace += ms;
+  }
+  const size_t lanecap = c->qcap / NLANE;
+  for (int l = 1; l < c->n_levels; ++l) {
+    LevelArgs L;
+    L.first = c->level_start[l];
+    L.nl = c->level_start[l + 1] - c->level_start[l];
+    L.maxln = c->max_level_nodes;
+    L.iprefix = c->d_iprefix;
+    L.iprefix_w = c->d_iprefix;
+    L.nitems = c->d_nitems + l;
+    L.nitems_w = c->d_nitems + l;
+    const uint32_t out_base = (uint32_t)(((l + 1) & 1) ? c->qcap : 0);
+    if (timed) hipEventRecord(c->ev[0], c->stream);
+    hipLaunchKernelGGL(k_scan_level, dim3(1), dim3(1024), 0, c->stream, A, L, (uint32_t)lanecap, out_base,
+                       c->d_stats, l, c->d_err);
+    hipLaunchKernelGGL(k_trace_level, dim3(LEVEL_GRID), dim3(TPB), 0, c->stream, A, L);
+    if (timed) {
+      hipEventRecord(c->ev[1], c->stream);
+      hipEventSynchronize(c->ev[1]);
+      float ms = 0;
+      hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+      if (l < 16) c->stats.ms_trace_level[l] += ms;
+      c->stats.ms_trace += ms;
+    }
+  }
+  HIPCHK(c, hipGetLastError());
+  c->stats.passes++;
+  return PT_OK;
+}
+
+static int read_device_stats(pt_ctx* c) {
+  unsigned long long st[STAT_COUNT];
+  uint32_t e = 0;
+  HIPCHK(c, hipMemcpyAsync(st, c->d_stats, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->stats.rays = st[STAT_R];
+  c->stats.visits = st[STAT_V];
+  c->stats.peak_queue_entries = st[STAT_PEAKQ];
+  for (int l = 0; l < 16; ++l) c->stats.level_visits[l] = st[STAT_LV0 + l];
+  if (e) return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded");
+  return PT_OK;
+}
+
+static void build_owned_pixels(pt_ctx* c, int W, int H, int T, int rank, int nranks) {
+  c->pix_of.clear();
+  const int ntx = (W + T - 1) / T, nty = (H + T - 1) / T;
+  for (int t = 0; t < ntx * nty; ++t) {
+    if (t % nranks != rank) continue;
+    const int ty = t / ntx, tx = t % ntx;
+    for (int r = ty * T; r < std::min(H, (ty + 1) * T); ++r)
+      for (int col = tx * T; col < std::min(W, (tx + 1) * T); ++col) c->pix_of.push_back((uint32_t)(r * W + col));
+  }
+}
+
+extern "C" {
+
+int pt_device_count(int* n) {
+  if (!n) return PT_E_INVALID;
+  hipError_t e = hipGetDeviceCount(n);
+  if (e != hipSuccess) {
+    *n = 0;
+    return PT_E_NODEVICE;
+  }
+  return PT_OK;
+}
+
+int pt_create(pt_ctx** out, int device) {
+  if (!out) return PT_E_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return PT_E_NODEVICE;
+  if (device < 0 || device >= n) return PT_E_INVALID;
+  pt_ctx* c = new pt_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return PT_E_HIP;
+  }
+  for (auto& e : c->ev) hipEventCreate(&e);
+  if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
+      hipMalloc((void**)&c->d_err, 4) != hipSuccess) {
+    delete c;
+    return PT_E_HIP;
+  }
+  hipMemset(c->d_stats, 0, STAT_COUNT * 8);
+  hipMemset(c->d_err, 0, 4);
+  *out = c;
+  return PT_OK;
+}
+
+void pt_destroy(pt_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  free_all(c);
+  for (auto& e : c->ev)
+    if (e) hipEventDestroy(e);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* pt_last_error(const pt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
+  if (!c || !s || s->n_prims <= 0 || s->n_nodes <= 0 || s->n_levels <= 0) return fail(c, PT_E_INVALID, "empty scene");
+  hipSetDevice(c->device);
+  int rc;
+  c->n_prims = s->n_prims;
+  c->n_nodes = s->n_nodes;
+  c->n_levels = s->n_levels;
+  c->level_start.assign(s->level_start, s->level_start + s->n_levels + 1);
+  c->max_level_nodes = 0;
+  for (int l = 0; l < s->n_levels; ++l)
+    c->max_level_nodes = std::max(c->max_level_nodes, c->level_start[l + 1] - c->level_start[l]);
+  c->nodes_host.assign(s->nodes, s->nodes + s->n_nodes);
+  c->root_leaf = c->nodes_host[0].prim_count > 0;
+  for (int i = 0; i < s->n_nodes; ++i) {
+    const pt_node& nd = s->nodes[i];
+    if (nd.prim_start < 0 || nd.prim_count < 0 || nd.prim_start + nd.prim_count > s->n_prims)
+      return fail(c, PT_E_INVALID, "node primitive range out of bounds");
+    for (int k = 0; k < 4; ++k)
+      if (nd.child[k] >= s->n_nodes || (nd.child[k] >= 0 && nd.child[k] <= i))
+        return fail(c, PT_E_INVALID, "node child out of range / not breadth-first");
+  }
+  for (int i = 0; i < s->n_prims; ++i) {
+    uint32_t meta;
+    memcpy(&meta, &s->prims[i].q[3], 4);
+    if ((int)(meta & 0x0FFFFFFFu) >= s->n_bsdfs) return fail(c, PT_E_INVALID, "primitive bsdf out of range");
+  }
+  if ((rc = dalloc(c, &c->d_nodes, s->n_nodes))) return rc;
+  if ((rc = dalloc(c, &c->d_prims, (size_t)s->n_prims * 6))) return rc;
+  if ((rc = dalloc(c, &c->d_shading, s->n_prims))) return rc;
+  if ((rc = dalloc(c, &c->d_bsdfs, std::max(1, s->n_bsdfs)))) return rc;
+  if ((rc = dalloc(c, &c->d_cnt, (size_t)s->n_nodes * NLANE))) return rc;
+  if ((rc = dalloc(c, &c->d_qoff, (size_t)s->n_nodes * NLANE))) return rc;
+  if ((rc = dalloc(c, &c->d_iprefix, (size_t)NLANE * (c->max_level_nodes + 1)))) return rc;
+  if ((rc = dalloc(c, &c->d_nitems, std::max(1, s->n_levels)))) return rc;
+  HIPCHK(c, hipMemcpy(c->d_nodes, s->nodes, sizeof(pt_node) * s->n_nodes, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_prims, s->prims, sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_shading, s->shading, sizeof(pt_prim_shading) * s->n_prims, hipMemcpyHostToDevice));
+  if (s->n_bsdfs > 0)
+    HIPCHK(c, hipMemcpy(c->d_bsdfs, s->bsdfs, sizeof(pt_bsdf) * s->n_bsdfs, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemset(c->d_cnt, 0, (size_t)s->n_nodes * NLANE * 4));
+  HIPCHK(c, hipMemset(c->d_qoff, 0, (size_t)s->n_nodes * NLANE * 4));
+  c->light = s->light;
+  c->camera = s->camera;
+  c->have_scene = true;
+  c->cap_paths = 0;  // force re-derivation of root queue offsets
+  return PT_OK;
+}
+
+int pt_set_camera(pt_ctx* c, const pt_camera* cam) {
+  if (!c || !cam) return PT_E_INVALID;
+  c->camera = *cam;
+  return pt_clear(c);
+}
+
+int pt_clear(pt_ctx* c) {
+  if (!c) return PT_E_INVALID;
+  hipSetDevice(c->device);
+  if (c->d_accum && !c->pix_of.empty())
+    HIPCHK(c, hipMemsetAsync(c->d_accum, 0, c->pix_of.size() * sizeof(float4), c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->samples = 0;
+  return PT_OK;
+}
+
+int pt_reset_stats(pt_ctx* c) {
+  if (!c) return PT_E_INVALID;
+  hipSetDevice(c->device);
+  HIPCHK(c, hipMemset(c->d_stats, 0, STAT_COUNT * 8));
+  memset(&c->stats, 0, sizeof(c->stats));
+  return PT_OK;
+}
+
+int pt_get_stats(pt_ctx* c, pt_stats* out) {
+  if (!c || !out) return PT_E_INVALID;
+  hipSetDevice(c->device);
+  int rc = read_device_stats(c);
+  c->stats.n_levels = c->n_levels;
+  *out = c->stats;
+  return rc == PT_E_OVERFLOW ? PT_OK : rc;
+}
+
+int pt_render(pt_ctx* c, const pt_render_params* P) {
+  if (!c || !P) return PT_E_INVALID;
+  if (!c->have_scene) return fail(c, PT_E_NOSCENE, "no scene loaded");
+  if (P->width <= 0 || P->height <= 0 || P->spp <= 0 || P->max_bounces < 0 || P->max_bounces > 250)
+    return fail(c, PT_E_INVALID, "bad render parameters");
+  const int nranks = P->nranks > 0 ? P->nranks : 1;
+  const int rank = P->rank;
+  if (rank < 0 || rank >= nranks) return fail(c, PT_E_INVALID, "bad rank");
+  const int tile = P->tile_size > 0 ? P->tile_size : 32;
+  hipSetDevice(c->device);
+  int rc;
+  // framebuffer / owned pixels
+  if (P->width != c->fb_w || P->height != c->fb_h || tile != c->fb_tile || rank != c->fb_rank ||
+      nranks != c->fb_nranks) {
+    build_owned_pixels(c, P->width, P->height, tile, rank, nranks);
+    c->fb_w = P->width;
+    c->fb_h = P->height;
+    c->fb_tile = tile;
+    c->fb_rank = rank;
+    c->fb_nranks = nranks;
+    if ((rc = dalloc(c, &c->d_pix_of, c->pix_of.size()))) return rc;
+    if ((rc = dalloc(c, &c->d_accum, c->pix_of.size()))) return rc;
+    if (!c->pix_of.empty())
+      HIPCHK(c, hipMemcpy(c->d_pix_of, c->pix_of.data(), c->pix_of.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemset(c->d_accum, 0, std::max<size_t>(1, c->pix_of.size()) * sizeof(float4)));
+    c->samples = 0;
+  }
+  const uint32_t npix = (uint32_t)c->pix_of.size();
+  if (npix == 0) {
+    c->samples += P->spp;
+    return PT_OK;
+  }
+  // batch: spp_b samples of every owned pixel
+  uint32_t target = P->batch_paths > 0 ? (uint32_t)P->batch_paths : (4u << 20);
+  uint32_t spp_b = std::max<uint32_t>(1, target / npix);
+  spp_b = std::min<uint32_t>(spp_b, (uint32_t)P->spp);
+  const uint32_t Nmax = npix * spp_b;
+  const bool realloc = Nmax > c->cap_paths;
+  if ((rc = ensure_paths(c, Nmax))) return rc;
+  if (realloc && (rc = set_root_child_offsets(c))) return rc;
+  HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+  const bool timed = (P->flags & PT_FLAG_STATS) != 0;
+  c->stats.batch_paths = (int32_t)Nmax;
+
+  ShadeArgs S;
+  S.ro = c->d_ro;
+  S.rd = c->d_rd;
+  S.hit = c->d_hit;
+  S.ps0 = c->d_ps0;
+  S.ps1 = c->d_ps1;
+  S.ps2 = c->d_ps2;
+  S.prims = c->d_prims;
+  S.shading = c->d_shading;
+  S.bsdfs = c->d_bsdfs;
+  S.pix_of = c->d_pix_of;
+  S.light = c->light;
+  S.cam = c->camera;
+  S.npix = npix;
+  S.seed = P->seed;
+  S.width = P->width;
+  S.height = P->height;
+  S.max_bounces = P->max_bounces;
+  S.flags = P->flags;
+
+  hipEvent_t t0 = c->ev[6], t1 = c->ev[7];
+  hipEventRecord(t0, c->stream);
+  float shade_ms = 0;
+  for (int done = 0; done < P->spp;) {
+    const uint32_t sb = std::min<uint32_t>(spp_b, (uint32_t)(P->spp - done));
+    const uint32_t N = npix * sb;
+    S.N = N;
+    S.sample_base = (uint32_t)(P->sample_offset + done);
+    const dim3 grid((N + TPB - 1) / TPB);
+    if (timed) hipEventRecord(c->ev[2], c->stream);
+    hipLaunchKernelGGL(k_camera, grid, dim3(TPB), 0, c->stream, S);
+    if (timed) {
+      hipEventRecord(c->ev[3], c->stream);
+      hipEventSynchronize(c->ev[3]);
+      float ms;
+      hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+      shade_ms += ms;
+    }
+    const int passes = P->max_bounces + 2;
+    for (int pass = 0; pass < passes; ++pass) {
+      // pass 0: camera rays only; last pass: shadow rays only
+      const uint32_t r0 = (pass == passes - 1) ? N : 0;
+      const uint32_t r1 = (pass == 0) ? N : 2 * N;
+      // slots of a smaller final batch: shadow rays live at [N, 2N) of THIS batch
+      if ((rc = trace_pass(c, r0, r1, timed))) return rc;
+      if (timed) hipEventRecord(c->ev[2], c->stream);
+      hipLaunchKernelGGL(k_shade, grid, dim3(TPB), 0, c->stream, S);
+      if (timed) {
+        hipEventRecord(c->ev[3], c->stream);
+        hipEventSynchronize(c->ev[3]);
+        float ms;
+        hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+        shade_ms += ms;
+      }
+    }
+    hipLaunchKernelGGL(k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), 0, c->stream, c->d_ps1, c->d_accum,
+                       npix, sb);
+    HIPCHK(c, hipGetLastError());
+    done += (int)sb;
+    c->stats.batches++;
+  }
+  hipEventRecord(t1, c->stream);
+  HIPCHK(c, hipEventSynchronize(t1));
+  float total = 0;
+  hipEventElapsedTime(&total, t0, t1);
+  c->stats.ms_total = total;
+  c->stats.ms_shade += shade_ms;
+  c->samples += P->spp;
+  uint32_t e = 0;
+  HIPCHK(c, hipMemcpy(&e, c->d_err, 4, hipMemcpyDeviceToHost));
+  if (e) return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded; lower batch_paths");
+  return PT_OK;
+}
+
+int pt_samples(pt_ctx* c, int32_t* spp) {
+  if (!c || !spp) return PT_E_INVALID;
+  *spp = c->samples;
+  return PT_OK;
+}
+
+int pt_get_image(pt_ctx* c, float* rgba, size_t n_floats) {
+  if (!c || !rgba) return PT_E_INVALID;
+  if ((size_t)c->fb_w * c->fb_h * 4 > n_floats) return fail(c, PT_E_INVALID, "image buffer too small");
+  hipSetDevice(c->device);
+  std::vector<float4> acc(c->pix_of.size());
+  if (!acc.empty())
+    HIPCHK(c, hipMemcpy(acc.data(), c->d_accum, acc.size() * sizeof(float4), hipMemcpyDeviceToHost));
+  memset(rgba, 0, (size_t)c->fb_w * c->fb_h * 4 * sizeof(float));
+  const float ns = (float)(c->samples > 0 ? c->samples : 1);
+  for (size_t q = 0; q < acc.size(); ++q) {
+    float* px = rgba + (size_t)c->pix_of[q] * 4;
+    px[0] = acc[q].x / ns;
+    px[1] = acc[q].y / ns;
+    px[2] = acc[q].z / ns;
+    px[3] = 1.0f;
+  }
+  return PT_OK;
+}
+
+int pt_owned_pixels(pt_ctx* c, int32_t* n_pixels, int32_t* pixel_index, size_t max_idx, void** device_sums) {
+  if (!c || !n_pixels) return PT_E_INVALID;
+  *n_pixels = (int32_t)c->pix_of.size();
+  if (pixel_index)
+    for (size_t i = 0; i < c->pix_of.size() && i < max_idx; ++i) pixel_index[i] = (int32_t)c->pix_of[i];
+  if (device_sums) *device_sums = c->d_accum;
+  return PT_OK;
+}
+
+int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) {
+  if (!c || (!rays && n > 0) || (!hits && n > 0) || n < 0) return PT_E_INVALID;
+  if (!c->have_scene) return fail(c, PT_E_NOSCENE, "no scene loaded");
+  if (n == 0) return PT_OK;
+  hipSetDevice(c->device);
+  int rc;
+  const uint32_t N = ((uint32_t)n + 1) / 2;
+  const bool realloc = N > c->cap_paths;
+  if ((rc = ensure_paths(c, N))) return rc;
+  if (realloc && (rc = set_root_child_offsets(c))) return rc;
+  float4* d_in = nullptr;
+  HIPCHK(c, hipMalloc((void**)&d_in, (size_t)n * 32));
+  HIPCHK(c, hipMemcpyAsync(d_in, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+  hipLaunchKernelGGL(k_load_rays, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, d_in, c->d_ro, c->d_rd,
+                     c->d_hit, (uint32_t)n);
+  hipEventRecord(c->ev[6], c->stream);
+  rc = trace_pass(c, 0, (uint32_t)n, false);
+  hipEventRecord(c->ev[7], c->stream);
+  if (rc) {
+    hipFree(d_in);
+    return rc;
+  }
+  HIPCHK(c, hipMemcpyAsync(hits, c->d_hit, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  float ms = 0;
+  hipEventElapsedTime(&ms, c->ev[6], c->ev[7]);
+  c->stats.ms_total = ms;
+  hipFree(d_in);
+  uint32_t e = 0;
+  HIPCHK(c, hipMemcpy(&e, c->d_err, 4, hipMemcpyDeviceToHost));
+  if (e) return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded");
+  return PT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,129 @@
+// pt_scene_* entry points of pt_api.h: the host-side input adapter that
+// CudaRenderer::loadScene implements inline (src/cudaRenderer.cu:1679-1842).
+#include <cstring>
+#include <exception>
+
+#include "scene_internal.h"
+
+using ptscene::Scene;
+
+extern "C" {
+
+int pt_scene_load_dae(const char* path, pt_scene** out, char* errbuf, size_t errbuf_len) {
+  if (!out || !path) return PT_E_INVALID;
+  *out = nullptr;
+  auto* sc = new pt_scene();
+  std::string err;
+  bool ok = false;
+  try {
+    ok = ptscene::load_dae(path, sc->s, err);
+    if (ok && sc->s.prims.empty()) {
+      err = "scene has no primitives";
+      ok = false;
+    }
+    if (ok) ptscene::build_bvh_and_flatten(sc->s, 32);
+  } catch (const std::exception& e) {
+    err = e.what();
+    ok = false;
+  }
+  if (!ok) {
+    if (errbuf && errbuf_len) {
+      strncpy(errbuf, err.c_str(), errbuf_len - 1);
+      errbuf[errbuf_len - 1] = 0;
+    }
+    delete sc;
+    return PT_E_IO;
+  }
+  *out = sc;
+  return PT_OK;
+}
+
+int pt_scene_from_triangles(const float* positions, int32_t n_tris, const pt_bsdf* bsdf0,
+                            const pt_light* light, const pt_camera* camera, pt_scene** out) {
+  if (!out || !positions || n_tris <= 0) return PT_E_INVALID;
+  auto* sc = new pt_scene();
+  Scene& S = sc->s;
+  ptscene::Mesh m;
+  for (int32_t t = 0; t < n_tris; ++t) {
+    ptscene::V3 p[3];
+    for (int k = 0; k < 3; ++k)
+      p[k] = ptscene::V3(positions[t * 9 + k * 3 + 0], positions[t * 9 + k * 3 + 1],
+                         positions[t * 9 + k * 3 + 2]);
+    ptscene::V3 n = ptscene::cross(p[1] - p[0], p[2] - p[0]);
+    double len = n.norm();
+    n = len > 0 ? n / len : ptscene::V3(0, 0, 1);
+    ptscene::Prim pr;
+    pr.kind = PT_PRIM_TRIANGLE;
+    pr.object = 0;
+    pr.mesh = 0;
+    for (int k = 0; k < 3; ++k) {
+      pr.v[k] = (int)m.positions.size();
+      m.positions.push_back(p[k]);
+      m.normals.push_back(n);
+    }
+    S.prims.push_back(pr);
+  }
+  S.meshes.push_back(std::move(m));
+  ptscene::Material mat;
+  if (bsdf0) {
+    mat.type = bsdf0->type;
+    for (int k = 0; k < 3; ++k) {
+      mat.albedo[k] = bsdf0->albedo[k];
+      mat.trans[k] = bsdf0->transmittance[k];
+    }
+    mat.ior = bsdf0->ior;
+  } else {
+    mat.albedo[0] = mat.albedo[1] = mat.albedo[2] = 0.5f;
+  }
+  S.materials.push_back(mat);
+  if (light) S.light = *light;
+  if (camera) {
+    S.camera = *camera;
+    S.have_camera = true;
+  }
+  try {
+    ptscene::build_bvh_and_flatten(S, 32);
+  } catch (const std::exception&) {
+    delete sc;
+    return PT_E_INVALID;
+  }
+  *out = sc;
+  return PT_OK;
+}
+
+void pt_scene_free(pt_scene* s) { delete s; }
+
+int pt_scene_get_desc(const pt_scene* sc, pt_scene_desc* d) {
+  if (!sc || !d) return PT_E_INVALID;
+  const Scene& S = sc->s;
+  memset(d, 0, sizeof(*d));
+  d->n_prims = (int32_t)S.dprims.size();
+  d->prims = S.dprims.data();
+  d->shading = S.dshading.data();
+  d->n_nodes = (int32_t)S.dnodes.size();
+  d->nodes = S.dnodes.data();
+  d->n_levels = (int32_t)S.level_start.size() - 1;
+  d->level_start = S.level_start.data();
+  d->n_bsdfs = (int32_t)S.dbsdfs.size();
+  d->bsdfs = S.dbsdfs.data();
+  d->light = S.light;
+  d->camera = S.camera;
+  return PT_OK;
+}
+
+int pt_scene_level_counts(const pt_scene* sc, int32_t* counts, int32_t max_levels, int32_t* n_levels) {
+  if (!sc || !n_levels) return PT_E_INVALID;
+  const auto& lc = sc->s.level_counts;
+  *n_levels = (int32_t)lc.size();
+  for (int32_t i = 0; counts && i < max_levels && i < (int32_t)lc.size(); ++i) counts[i] = lc[i];
+  return PT_OK;
+}
+
+int pt_scene_sorted_to_input(const pt_scene* sc, int32_t* out, int32_t n) {
+  if (!sc || !out) return PT_E_INVALID;
+  const auto& v = sc->s.sorted_to_input;
+  for (int32_t i = 0; i < n && i < (int32_t)v.size(); ++i) out[i] = v[i];
+  return PT_OK;
+}
+
+}  // extern "C"

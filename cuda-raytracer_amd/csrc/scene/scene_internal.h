@@ -1,0 +1,142 @@
+// Host-side scene representation behind the opaque pt_scene of pt_api.h.
+//
+// The loader restates the reference's scene-ingest chain so the hot path sees
+// the same triangles, in the same order, with the same BVH:
+//   Collada::ColladaParser::load        src/collada/collada.cpp:116-950
+//   DynamicScene::Mesh / HalfedgeMesh   src/dynamic_scene/mesh.cpp:21-45,
+//                                       src/halfEdgeMesh.cpp:47-418
+//   StaticScene::Mesh (vertex normals)  src/static_scene/object.cpp:17-71,
+//                                       src/halfEdgeMesh.h:619-644
+//   BVHAccel + compactTree + compress   src/bvh.cpp:48-365
+//   CudaRenderer::loadScene flattening  src/cudaRenderer.cu:1679-1842
+#pragma once
+
+#include <array>
+#include <cmath>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "pt_api.h"
+
+namespace ptscene {
+
+// Double-precision vector with the operation order of CMU462::Vector3D
+// (CMU462/include/CMU462/vector3D.h).
+struct V3 {
+  double x = 0, y = 0, z = 0;
+  V3() = default;
+  V3(double a, double b, double c) : x(a), y(b), z(c) {}
+  V3 operator+(const V3& o) const { return V3(x + o.x, y + o.y, z + o.z); }
+  V3 operator-(const V3& o) const { return V3(x - o.x, y - o.y, z - o.z); }
+  V3 operator-() const { return V3(-x, -y, -z); }
+  V3 operator*(double c) const { return V3(x * c, y * c, z * c); }
+  V3 operator/(double c) const {
+    const double rc = 1.0 / c;
+    return V3(rc * x, rc * y, rc * z);
+  }
+  V3& operator+=(const V3& o) {
+    x += o.x;
+    y += o.y;
+    z += o.z;
+    return *this;
+  }
+  double norm2() const { return x * x + y * y + z * z; }
+  double norm() const;
+  V3 unit() const { return *this / norm(); }
+  double operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+};
+inline V3 cross(const V3& u, const V3& v) {
+  return V3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
+}
+inline double dot(const V3& u, const V3& v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
+
+// Column-major 4x4 like CMU462::Matrix4x4; m(i,j) = row i, column j.
+struct M4 {
+  double e[4][4];  // e[col][row]
+  double& operator()(int i, int j) { return e[j][i]; }
+  double operator()(int i, int j) const { return e[j][i]; }
+  static M4 identity();
+  M4 operator*(const M4& B) const;
+  // Matrix4x4 * Vector4D: x0*col0 + x1*col1 + x2*col2 + x3*col3 (matrix4x4.cpp:187)
+  void mul4(const double in[4], double out[4]) const;
+};
+
+// Axis-aligned box with the semantics of CMU462::BBox (src/bbox.h).
+struct BBox {
+  V3 max{-INFINITY, -INFINITY, -INFINITY};
+  V3 min{INFINITY, INFINITY, INFINITY};
+  V3 extent{-INFINITY, -INFINITY, -INFINITY};
+  BBox() { extent = max - min; }
+  BBox(double x0, double y0, double z0, double x1, double y1, double z1)
+      : max(x1, y1, z1), min(x0, y0, z0) {
+    extent = max - min;
+  }
+  void expand(const BBox& b);
+  V3 centroid() const { return (min + max) / 2; }
+  bool empty() const { return min.x > max.x || min.y > max.y || min.z > max.z; }
+  double surface_area() const {
+    if (empty()) return 0.0;
+    return 2 * (extent.x * extent.z + extent.x * extent.y + extent.y * extent.z);
+  }
+};
+
+struct Material {
+  int type = PT_BSDF_DIFFUSE;
+  float albedo[3] = {1, 1, 1};  // Spectrum is float (CMU462 spectrum.h)
+  float trans[3] = {0, 0, 0};
+  float ior = 1.0f;
+};
+
+// A primitive in input order (mesh triangles in face order, spheres).
+struct Prim {
+  int kind = 0;  // PT_PRIM_*
+  int object = 0;
+  int mesh = -1;
+  int v[3] = {0, 0, 0};  // indices into that mesh's positions/normals
+  V3 centre;
+  double radius = 0;
+  BBox bbox() const;
+};
+
+struct Mesh {
+  std::vector<V3> positions;
+  std::vector<V3> normals;
+};
+
+struct Scene {
+  // input-order data
+  std::vector<Mesh> meshes;
+  std::vector<Prim> prims;
+  std::vector<Material> materials;  // one per scene object (cu:1694-1723)
+  pt_light light{};
+  pt_camera camera{};
+  bool have_camera = false;
+
+  // flattened output
+  std::vector<int32_t> sorted_to_input;
+  std::vector<pt_prim> dprims;
+  std::vector<pt_prim_shading> dshading;
+  std::vector<pt_node> dnodes;
+  std::vector<int32_t> level_start;
+  std::vector<int32_t> level_counts;  // reference levelCounts (DFS compress)
+  std::vector<pt_bsdf> dbsdfs;
+};
+
+// bvh_ref.cpp: restated BVHAccel / compactTree / compress + BFS flattening.
+void build_bvh_and_flatten(Scene& s, size_t max_leaf_size = 32);
+
+// dae.cpp
+bool load_dae(const std::string& path, Scene& s, std::string& err);
+
+// halfedge.cpp: vertex order, triangle (v1,v2,v3) order and area-weighted
+// vertex normals exactly as HalfedgeMesh::build + StaticScene::Mesh produce.
+bool build_static_mesh(const std::vector<std::vector<size_t>>& polygons,
+                       const std::vector<V3>& vertex_positions, Mesh& out,
+                       std::vector<std::array<int, 3>>& tris, std::string& err);
+
+}  // namespace ptscene
+
+struct pt_scene {
+  ptscene::Scene s;
+};

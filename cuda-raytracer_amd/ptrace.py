@@ -1,0 +1,305 @@
+"""ctypes binding of include/pt_api.h (the C-ABI boundary of the MI355X path tracer).
+
+Python is plumbing here (tests, bench, torch.distributed gather); the product
+is libptcore.so: the C++ scene adapter and the gfx950 HIP kernels.  Importing
+this module never falls back to anything else: if the library is missing the
+import raises.
+
+Reference surface mirrored (src/cudaRenderer.h:173-272):
+    CudaRenderer.loadScene(path)   -> Scene.load_dae(path) + Context.load_scene(scene)
+    CudaRenderer.render()          -> Context.render(...)
+    CudaRenderer.getImage()        -> Context.get_image()
+    CudaRenderer.setViewpoint(...) -> Context.set_camera(...)
+    CudaRenderer.clearImage()      -> Context.clear()
+    BVHAccel::intersect(ray, isect)-> Context.intersect(rays)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("PTCORE_LIB", HERE / "lib" / "libptcore.so"))
+
+PT_OK = 0
+PT_E_INVALID, PT_E_IO, PT_E_NOSCENE, PT_E_HIP, PT_E_OVERFLOW, PT_E_UNSUPPORTED, PT_E_NODEVICE = (
+    -1, -2, -3, -4, -5, -6, -7)
+PT_HIT_NONE = 0xFFFFFFFFFFFFFFFF
+PT_FLAG_COSINE_DIFFUSE = 0x1
+PT_FLAG_NO_EMISSION = 0x2
+PT_FLAG_STATS = 0x4
+PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION = 0, 1, 2, 3
+PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT = 0, 1, 2
+
+
+class pt_prim(C.Structure):
+    _fields_ = [("q", C.c_float * 24)]
+
+
+class pt_prim_shading(C.Structure):
+    _fields_ = [("n0", C.c_float * 4), ("n1", C.c_float * 4), ("n2", C.c_float * 4)]
+
+
+class pt_node(C.Structure):
+    _fields_ = [("bmin_x", C.c_float * 4), ("bmax_x", C.c_float * 4),
+                ("bmin_y", C.c_float * 4), ("bmax_y", C.c_float * 4),
+                ("bmin_z", C.c_float * 4), ("bmax_z", C.c_float * 4),
+                ("child", C.c_int32 * 4), ("prim_start", C.c_int32), ("prim_count", C.c_int32),
+                ("level", C.c_int32), ("ref_id", C.c_int32)]
+
+
+class pt_bsdf(C.Structure):
+    _fields_ = [("type", C.c_int32), ("albedo", C.c_float * 3),
+                ("transmittance", C.c_float * 3), ("ior", C.c_float)]
+
+
+class pt_light(C.Structure):
+    _fields_ = [("type", C.c_int32), ("radiance", C.c_float * 3), ("position", C.c_float * 3),
+                ("direction", C.c_float * 3), ("dim_x", C.c_float * 3), ("dim_y", C.c_float * 3),
+                ("area", C.c_float), ("pad", C.c_float * 2)]
+
+
+class pt_camera(C.Structure):
+    _fields_ = [("origin", C.c_float * 3), ("look_at", C.c_float * 3),
+                ("left", C.c_float * 3), ("up", C.c_float * 3)]
+
+
+class pt_scene_desc(C.Structure):
+    _fields_ = [("n_prims", C.c_int32), ("prims", C.POINTER(pt_prim)),
+                ("shading", C.POINTER(pt_prim_shading)),
+                ("n_nodes", C.c_int32), ("nodes", C.POINTER(pt_node)),
+                ("n_levels", C.c_int32), ("level_start", C.POINTER(C.c_int32)),
+                ("n_bsdfs", C.c_int32), ("bsdfs", C.POINTER(pt_bsdf)),
+                ("light", pt_light), ("camera", pt_camera)]
+
+
+class pt_render_params(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
+                ("max_bounces", C.c_int32), ("seed", C.c_uint32), ("sample_offset", C.c_int32),
+                ("batch_paths", C.c_int32), ("tile_size", C.c_int32), ("rank", C.c_int32),
+                ("nranks", C.c_int32), ("flags", C.c_uint32)]
+
+
+class pt_stats(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("visits", C.c_uint64), ("passes", C.c_uint64),
+                ("batches", C.c_uint64), ("ms_total", C.c_double), ("ms_trace", C.c_double),
+                ("ms_shade", C.c_double), ("ms_trace_level", C.c_double * 16),
+                ("level_visits", C.c_uint64 * 16), ("peak_queue_entries", C.c_uint64),
+                ("n_levels", C.c_int32), ("batch_paths", C.c_int32)]
+
+
+# every symbol include/pt_api.h declares (tests check the library exports them)
+API_SYMBOLS = [
+    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_free", "pt_scene_get_desc",
+    "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
+    "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
+    "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect",
+    "pt_get_stats", "pt_reset_stats",
+]
+
+
+def _load():
+    if not LIB_PATH.exists():
+        raise ImportError(f"libptcore.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    lib = C.CDLL(str(LIB_PATH))
+    P, I32, U32, SZ = C.c_void_p, C.c_int32, C.c_uint32, C.c_size_t
+    sigs = {
+        "pt_scene_load_dae": (C.c_int, [C.c_char_p, C.POINTER(P), C.c_char_p, SZ]),
+        "pt_scene_from_triangles": (C.c_int, [C.POINTER(C.c_float), I32, C.POINTER(pt_bsdf),
+                                              C.POINTER(pt_light), C.POINTER(pt_camera), C.POINTER(P)]),
+        "pt_scene_free": (None, [P]),
+        "pt_scene_get_desc": (C.c_int, [P, C.POINTER(pt_scene_desc)]),
+        "pt_scene_level_counts": (C.c_int, [P, C.POINTER(I32), I32, C.POINTER(I32)]),
+        "pt_scene_sorted_to_input": (C.c_int, [P, C.POINTER(I32), I32]),
+        "pt_create": (C.c_int, [C.POINTER(P), C.c_int]),
+        "pt_destroy": (None, [P]),
+        "pt_last_error": (C.c_char_p, [P]),
+        "pt_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+        "pt_load_scene": (C.c_int, [P, C.POINTER(pt_scene_desc)]),
+        "pt_set_camera": (C.c_int, [P, C.POINTER(pt_camera)]),
+        "pt_render": (C.c_int, [P, C.POINTER(pt_render_params)]),
+        "pt_clear": (C.c_int, [P]),
+        "pt_get_image": (C.c_int, [P, C.POINTER(C.c_float), SZ]),
+        "pt_owned_pixels": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32), SZ, C.POINTER(P)]),
+        "pt_samples": (C.c_int, [P, C.POINTER(I32)]),
+        "pt_intersect": (C.c_int, [P, C.POINTER(C.c_float), I32, C.POINTER(C.c_uint64)]),
+        "pt_get_stats": (C.c_int, [P, C.POINTER(pt_stats)]),
+        "pt_reset_stats": (C.c_int, [P]),
+    }
+    for name, (res, args) in sigs.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+LIB = _load()
+
+
+class PTError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"pt error {code}: {msg}")
+        self.code = code
+
+
+def _ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+class Scene:
+    """Host-side scene: COLLADA subset -> reference BVH -> flattened arrays."""
+
+    def __init__(self, handle):
+        self.h = C.c_void_p(handle) if not isinstance(handle, C.c_void_p) else handle
+
+    @classmethod
+    def load_dae(cls, path):
+        h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = LIB.pt_scene_load_dae(str(path).encode(), C.byref(h), err, 512)
+        if rc != PT_OK:
+            raise PTError(rc, err.value.decode())
+        return cls(h)
+
+    @classmethod
+    def from_triangles(cls, tris, bsdf=None, light=None, camera=None):
+        tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+        h = C.c_void_p()
+        rc = LIB.pt_scene_from_triangles(_ptr(tris, C.c_float), len(tris),
+                                         C.byref(bsdf) if bsdf else None,
+                                         C.byref(light) if light else None,
+                                         C.byref(camera) if camera else None, C.byref(h))
+        if rc != PT_OK:
+            raise PTError(rc, "pt_scene_from_triangles failed")
+        return cls(h)
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value:
+            LIB.pt_scene_free(self.h)
+            self.h = C.c_void_p()
+
+    def desc(self) -> pt_scene_desc:
+        d = pt_scene_desc()
+        rc = LIB.pt_scene_get_desc(self.h, C.byref(d))
+        if rc != PT_OK:
+            raise PTError(rc, "pt_scene_get_desc")
+        return d
+
+    def level_counts(self):
+        counts = (C.c_int32 * 256)()
+        n = C.c_int32()
+        LIB.pt_scene_level_counts(self.h, counts, 256, C.byref(n))
+        return [counts[i] for i in range(n.value)]
+
+    def sorted_to_input(self):
+        d = self.desc()
+        out = np.zeros(d.n_prims, dtype=np.int32)
+        LIB.pt_scene_sorted_to_input(self.h, _ptr(out, C.c_int32), d.n_prims)
+        return out
+
+    # numpy views (copies) of the flattened arrays
+    def prims(self):
+        d = self.desc()
+        return np.ctypeslib.as_array(C.cast(d.prims, C.POINTER(C.c_float)), shape=(d.n_prims, 24)).copy()
+
+    def nodes(self):
+        d = self.desc()
+        return [d.nodes[i] for i in range(d.n_nodes)]
+
+
+class Context:
+    """One device context (one GPU).  Mirrors cutracer::CudaRenderer."""
+
+    def __init__(self, device=0):
+        self.h = C.c_void_p()
+        rc = LIB.pt_create(C.byref(self.h), device)
+        if rc != PT_OK:
+            raise PTError(rc, "pt_create failed (no GPU visible?)")
+        self.width = self.height = 0
+
+    def close(self):
+        if self.h and self.h.value:
+            LIB.pt_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+    def _chk(self, rc):
+        if rc != PT_OK:
+            raise PTError(rc, LIB.pt_last_error(self.h).decode(errors="replace"))
+
+    def load_scene(self, scene: Scene):
+        self._desc = scene.desc()
+        self._scene = scene  # keep arrays alive while the context uses them
+        self._chk(LIB.pt_load_scene(self.h, C.byref(self._desc)))
+
+    def set_camera(self, cam: pt_camera):
+        self._chk(LIB.pt_set_camera(self.h, C.byref(cam)))
+
+    def render(self, width, height, spp, max_bounces=8, seed=15618, sample_offset=0,
+               batch_paths=0, tile_size=32, rank=0, nranks=1, flags=0):
+        p = pt_render_params(width, height, spp, max_bounces, seed, sample_offset, batch_paths,
+                             tile_size, rank, nranks, flags)
+        self.width, self.height = width, height
+        self._chk(LIB.pt_render(self.h, C.byref(p)))
+
+    def clear(self):
+        self._chk(LIB.pt_clear(self.h))
+
+    def samples(self):
+        n = C.c_int32()
+        self._chk(LIB.pt_samples(self.h, C.byref(n)))
+        return n.value
+
+    def get_image(self):
+        img = np.zeros((self.height, self.width, 4), dtype=np.float32)
+        self._chk(LIB.pt_get_image(self.h, _ptr(img, C.c_float), img.size))
+        return img
+
+    def owned_pixels(self):
+        n = C.c_int32()
+        self._chk(LIB.pt_owned_pixels(self.h, C.byref(n), None, 0, None))
+        idx = np.zeros(max(1, n.value), dtype=np.int32)
+        dptr = C.c_void_p()
+        self._chk(LIB.pt_owned_pixels(self.h, C.byref(n), _ptr(idx, C.c_int32), idx.size, C.byref(dptr)))
+        return idx[: n.value], dptr.value
+
+    def intersect(self, rays):
+        """rays: (n, 8) float32 [o.xyz, tmax, d.xyz, 0] -> uint64 hit keys."""
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        hits = np.zeros(len(rays), dtype=np.uint64)
+        self._chk(LIB.pt_intersect(self.h, _ptr(rays, C.c_float), len(rays), _ptr(hits, C.c_uint64)))
+        return hits
+
+    def stats(self) -> pt_stats:
+        s = pt_stats()
+        self._chk(LIB.pt_get_stats(self.h, C.byref(s)))
+        return s
+
+    def reset_stats(self):
+        self._chk(LIB.pt_reset_stats(self.h))
+
+
+def device_count():
+    n = C.c_int()
+    LIB.pt_device_count(C.byref(n))
+    return n.value
+
+
+def hit_t(keys):
+    """fp32 t of uint64 hit keys (inf for misses)."""
+    keys = np.asarray(keys, dtype=np.uint64)
+    t = (keys >> np.uint64(32)).astype(np.uint32).view(np.float32).copy()
+    t[keys == np.uint64(PT_HIT_NONE)] = np.inf
+    return t
+
+
+def hit_prim(keys):
+    keys = np.asarray(keys, dtype=np.uint64)
+    p = (keys & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    p[keys == np.uint64(PT_HIT_NONE)] = -1
+    return p

@@ -1,0 +1,259 @@
+/*
+ * pt_api.h -- C ABI of the MI355X (gfx950) breadth-first wide-BVH path tracer.
+ *
+ * This is the drop-in boundary for the hot path of saipraveenb25/cuda-raytracer
+ * ("CUDA-SCOTTY").  Every entry point replaces one member of the reference's
+ * `cutracer::CudaRenderer` class (src/cudaRenderer.h:173-272) or one piece of the
+ * Scotty3D CPU surface the north star keeps (src/pathtracer.h:51-257,
+ * src/camera.h:81, src/bvh.h:111-149).  The signatures carry only plain C types
+ * and pointers; no HIP, torch or C++ types cross the boundary.
+ *
+ *   reference member / function                        replaced by
+ *   -------------------------------------------------  -------------------------
+ *   CudaRenderer::CudaRenderer()        cu:1496         pt_create
+ *   CudaRenderer::~CudaRenderer()       cu:1510         pt_destroy
+ *   CudaRenderer::loadScene(path)       cu:1679-1842    pt_scene_load_dae + pt_load_scene
+ *     (COLLADA parse, BVHAccel build, compactedTree, compress, flatten)
+ *   CudaRenderer::setup()               cu:1872-2113    pt_load_scene (device upload)
+ *   CudaRenderer::allocOutputImage(w,h) cu:2119         pt_render_params.width/height
+ *   CudaRenderer::render()/renderAccumulate()/renderFrame()
+ *                                       cu:2411-2564    pt_render
+ *   CudaRenderer::getImage()            cu:1539-1570    pt_get_image
+ *   CudaRenderer::setViewpoint(o,look)  cu:1845-1870    pt_set_camera (+ pt_clear)
+ *   CudaRenderer::clearImage()          cu:2131         pt_clear
+ *   rayIntersect() + kernelMergeIntersections
+ *                                       cu:2304-2331,515 pt_intersect (closest hit)
+ *   BVHAccel::intersect(ray, isect)     bvh.cpp:422     pt_intersect (one ray)
+ *   lapTimer per-kernel timing          cu:2366-2376    pt_get_stats
+ *
+ * Conventions
+ *  - Every call returns 0 (PT_OK) or a negative PT_E* code; the message of the
+ *    last failure on a context is available from pt_last_error().  Nothing in
+ *    this library calls exit() (the reference exits on every failure, §5).
+ *  - pt_scene_* objects are host-side and own their arrays.  pt_load_scene copies
+ *    the arrays to the device; the caller keeps ownership of the pt_scene.
+ *  - One pt_ctx per GPU.  Calls on one ctx must be serialised by the caller;
+ *    distinct contexts may be used from distinct threads / processes.
+ *  - Images are float4 RGBA, row-major, rows counted bottom-up; pixel (row r,
+ *    col c) is element r*width + c.  For square images this is the same memory
+ *    order as the reference's x*H + y indexing (cu:327, 705-718).
+ */
+#ifndef PT_API_H
+#define PT_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_API_VERSION 1
+
+/* ---- error codes ---------------------------------------------------------- */
+#define PT_OK 0
+#define PT_E_INVALID (-1)     /* bad argument                                 */
+#define PT_E_IO (-2)          /* file not found / parse error                 */
+#define PT_E_NOSCENE (-3)     /* render/intersect before pt_load_scene        */
+#define PT_E_HIP (-4)         /* HIP runtime error (message has details)      */
+#define PT_E_OVERFLOW (-5)    /* ray queue capacity exceeded during a pass     */
+#define PT_E_UNSUPPORTED (-6) /* scene feature not supported                  */
+#define PT_E_NODEVICE (-7)    /* no GPU visible / HIP kernels not loaded       */
+
+/* ---- device record formats (also the flattened scene format) -------------- */
+
+/* Primitive kinds (bits 28..31 of pt_prim.meta; bits 0..27 = bsdf index). */
+#define PT_PRIM_TRIANGLE 0u
+#define PT_PRIM_SPHERE 1u
+
+/* One intersectable primitive, 96 bytes = 6 x float4, in BVH-sorted order
+ * (the order of BVHAccel::getSortedPrimitives(), bvh.cpp:384).  Triangles store
+ * exactly the operands the reference triangle test derives (cu:217-270):
+ *   q0 = v0.xyz, meta        q1 = v1.xyz, dN = dot(N, v0)
+ *   q2 = v2.xyz, e2.x        q3 = N.xyz (= cross(v1-v0, v2-v0)), e2.y
+ *   q4 = e0.xyz (= v1-v0), e2.z   q5 = e1.xyz (= v2-v1), 0
+ * with e2 = v0-v2.  All derived values are fp32 computed from the fp32 vertices
+ * with the reference's operation order, so the kernel's results are those of
+ * the reference formula.  Spheres: q0 = centre.xyz, meta; q1.x = radius,
+ * q1.y = radius^2; rest 0.                                                     */
+typedef struct pt_prim {
+  float q[24];
+} pt_prim;
+
+/* Shading data of a primitive (same index as pt_prim): the three vertex
+ * normals of a triangle (CuTriangle.n0..n2, cudaRenderer.h:118-120). */
+typedef struct pt_prim_shading {
+  float n0[4];
+  float n1[4];
+  float n2[4];
+} pt_prim_shading;
+
+/* One 4-wide BVH node, 128 bytes (one cache line of the MI355X L2).  Children
+ * are stored as SoA boxes.  child[i] < 0 marks an empty outlet (the reference's
+ * (uint64_t)-1, bvh.cpp:267).  prim_count > 0 marks a leaf (range != 0,
+ * cu:862).  Nodes are stored level-major (breadth-first), so the nodes of BVH
+ * level l are the contiguous id range [level_start[l], level_start[l+1]). */
+typedef struct pt_node {
+  float bmin_x[4], bmax_x[4];
+  float bmin_y[4], bmax_y[4];
+  float bmin_z[4], bmax_z[4];
+  int32_t child[4];
+  int32_t prim_start;
+  int32_t prim_count;
+  int32_t level;
+  int32_t ref_id; /* DFS pre-order id of BVHSubTree::compress (bvh.cpp:234) */
+} pt_node;
+
+/* BSDF kinds */
+#define PT_BSDF_DIFFUSE 0
+#define PT_BSDF_MIRROR 1
+#define PT_BSDF_GLASS 2
+#define PT_BSDF_EMISSION 3
+
+/* 32 bytes; CuBSDF (cudaRenderer.h:135-140) extended with glass and emission. */
+typedef struct pt_bsdf {
+  int32_t type;
+  float albedo[3];        /* diffuse albedo / mirror+glass reflectance / emitted radiance */
+  float transmittance[3]; /* glass */
+  float ior;              /* glass */
+} pt_bsdf;
+
+/* Light kinds */
+#define PT_LIGHT_NONE 0
+#define PT_LIGHT_AREA 1
+#define PT_LIGHT_POINT 2
+
+/* CuEmitter (cudaRenderer.h:126-133) + kind. */
+typedef struct pt_light {
+  int32_t type;
+  float radiance[3];
+  float position[3];
+  float direction[3];
+  float dim_x[3];
+  float dim_y[3];
+  float area;
+  float pad[2];
+} pt_light;
+
+/* Camera in the reference GPU model (cu:80-86, set up at cu:1590-1607): fixed
+ * 53.13 degree field of view, direction = k.x*left + k.y*up + k.z*lookAt. */
+typedef struct pt_camera {
+  float origin[3];
+  float look_at[3];
+  float left[3];
+  float up[3];
+} pt_camera;
+
+/* Flattened scene handed to the device (what CudaRenderer::loadScene builds). */
+typedef struct pt_scene_desc {
+  int32_t n_prims;
+  const pt_prim* prims;
+  const pt_prim_shading* shading;
+  int32_t n_nodes;
+  const pt_node* nodes;
+  int32_t n_levels;
+  const int32_t* level_start; /* n_levels + 1 entries */
+  int32_t n_bsdfs;
+  const pt_bsdf* bsdfs;
+  pt_light light;
+  pt_camera camera;
+} pt_scene_desc;
+
+/* ---- host-side scene loading (input adapter, runs on the CPU) -------------- */
+typedef struct pt_scene pt_scene; /* opaque, owns its arrays */
+
+/* Parse a COLLADA file (the CMU462 subset used by media/pathtracer), build the
+ * reference BVH (bvh.cpp:48-365, max leaf 32), compact it to the 4-wide tree
+ * (bvh.cpp:275-337) and flatten it.  On failure *out is NULL and errbuf (if not
+ * NULL) receives a message. */
+int pt_scene_load_dae(const char* path, pt_scene** out, char* errbuf, size_t errbuf_len);
+/* Build a scene from a plain triangle soup (tests, synthetic scenes).  All
+ * triangles use bsdf 0; positions are n_tris*9 floats. */
+int pt_scene_from_triangles(const float* positions, int32_t n_tris, const pt_bsdf* bsdf0,
+                            const pt_light* light, const pt_camera* camera, pt_scene** out);
+void pt_scene_free(pt_scene* s);
+/* Borrowed view of the flattened arrays (valid until pt_scene_free). */
+int pt_scene_get_desc(const pt_scene* s, pt_scene_desc* out);
+/* Reference-layout statistics of the compacted tree: number of wide nodes,
+ * leaves and per-level node counts (the reference's levelCounts). */
+int pt_scene_level_counts(const pt_scene* s, int32_t* counts, int32_t max_levels,
+                          int32_t* n_levels);
+/* Primitive permutation: sorted_to_input[i] = index of sorted prim i in the
+ * scene's input order (triangles in mesh order, then spheres). */
+int pt_scene_sorted_to_input(const pt_scene* s, int32_t* out, int32_t n);
+
+/* ---- device context --------------------------------------------------------- */
+typedef struct pt_ctx pt_ctx;
+
+int pt_create(pt_ctx** out, int device);
+void pt_destroy(pt_ctx* ctx);
+const char* pt_last_error(const pt_ctx* ctx);
+int pt_device_count(int* n);
+
+int pt_load_scene(pt_ctx* ctx, const pt_scene_desc* scene);
+int pt_set_camera(pt_ctx* ctx, const pt_camera* camera);
+
+/* Render parameters. */
+#define PT_FLAG_COSINE_DIFFUSE 0x1u /* cosine-weighted diffuse sampling instead of
+                                       the reference's uniform hemisphere (cu:619) */
+#define PT_FLAG_NO_EMISSION 0x2u    /* do not count emissive surfaces (REAL_TIME,
+                                       cudaRenderer.h:76, cu:1242-1246)        */
+#define PT_FLAG_STATS 0x4u          /* collect R/V counters and per-pass timing  */
+
+typedef struct pt_render_params {
+  int32_t width, height;
+  int32_t spp;         /* samples per pixel rendered by this call             */
+  int32_t max_bounces; /* indirect (BSDF-sampled) rays per path; vertices = +1 */
+  uint32_t seed;       /* Philox key; reference seed 15618 (samplers.cu_inl:8) */
+  int32_t sample_offset; /* index of the first sample (progressive rendering) */
+  int32_t batch_paths; /* paths in flight per wavefront batch; 0 = auto       */
+  int32_t tile_size;   /* framebuffer tile edge for sharding (0 = 32)          */
+  int32_t rank, nranks; /* this context renders tiles t with t % nranks == rank */
+  uint32_t flags;
+} pt_render_params;
+
+/* Render params->spp samples per owned pixel and ADD them to the context's
+ * accumulation buffer (progressive, like renderAccumulate, cu:2419-2457).
+ * Blocks until the GPU work is complete. */
+int pt_render(pt_ctx* ctx, const pt_render_params* params);
+/* Zero the accumulation buffer and sample count (kernelClearAccumulate, cu:744). */
+int pt_clear(pt_ctx* ctx);
+/* Copy the current image (accumulated radiance / samples) of the whole frame,
+ * width*height*4 floats.  Pixels this rank does not own are 0. */
+int pt_get_image(pt_ctx* ctx, float* rgba, size_t n_floats);
+/* Owned-pixel view for the multi-GPU gather: *n_pixels owned pixels, their
+ * global indices (row*width+col, host array filled if not NULL) and a device
+ * pointer to their float4 radiance sums (not divided by spp). */
+int pt_owned_pixels(pt_ctx* ctx, int32_t* n_pixels, int32_t* pixel_index, size_t max_idx,
+                    void** device_sums);
+/* Samples per pixel accumulated so far. */
+int pt_samples(pt_ctx* ctx, int32_t* spp);
+
+/* Closest-hit query through the breadth-first traversal.  rays: n records of
+ * 8 floats (o.xyz, tmax, d.xyz, unused).  hits: n records of
+ * (uint64) ((float bits of t) << 32 | sorted prim index), or
+ * PT_HIT_NONE when nothing is hit with t <= tmax. */
+#define PT_HIT_NONE 0xFFFFFFFFFFFFFFFFull
+int pt_intersect(pt_ctx* ctx, const float* rays, int32_t n, uint64_t* hits);
+
+typedef struct pt_stats {
+  uint64_t rays;      /* R: valid rays entering the root, summed over passes */
+  uint64_t visits;    /* V: (ray, node) visits including the root          */
+  uint64_t passes;    /* traversal passes                                  */
+  uint64_t batches;
+  double ms_total;    /* GPU time of the last pt_render / pt_intersect     */
+  double ms_trace;    /* of which in traversal kernels                     */
+  double ms_shade;    /* of which in camera/shade/accumulate kernels       */
+  double ms_trace_level[16]; /* per BVH level (level 0 = root pass)       */
+  uint64_t level_visits[16];
+  uint64_t peak_queue_entries;
+  int32_t n_levels;
+  int32_t batch_paths;
+} pt_stats;
+int pt_get_stats(pt_ctx* ctx, pt_stats* out);
+int pt_reset_stats(pt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_API_H */

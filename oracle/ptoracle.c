@@ -1,0 +1,537 @@
+/*
+ * ptoracle.c -- CPU ORACLE (test infrastructure only).
+ *
+ * A plain-C restatement of the reference's hot-path arithmetic, used ONLY by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+ * checker.  The product path (libptcore.so) never links, loads or calls it.
+ *
+ * It restates, with the parity decisions of SURVEY.md §8(a):
+ *   intersectRayTriangle         src/cudaRenderer.cu:217-270   -> pto_tri
+ *   kernelMergeIntersections     cu:515-540 (min over candidates) -> pto_closest_brute
+ *   rayIntersectSingle leaf loop cu:1144-1169                   -> pto_closest_bvh
+ *   kernelPrimaryRays            cu:312-376                     -> camera_ray
+ *   leaf hit record              cu:1201-1291                   -> shade_normal
+ *   kernelDirectLightRays        cu:380-481                     -> NEE in path_radiance
+ *   kernelProcessIntersections   cu:544-664                     -> BSDF in path_radiance
+ *   kernelAccumulate / Reconstruct cu:705-742                   -> accumulation order
+ *   PathTracer::start_raytracing / worker_thread / raytrace_tile / raytrace_pixel
+ *                                src/pathtracer.cpp:183-213, 499-558 -> pto_render
+ *                                (32x32 tiles pulled from a shared queue by N threads)
+ * The RNG is Philox4x32-10 (Salmon et al. 2011), not curand XORWOW: the
+ * reference's streams are not reproducible without the CUDA toolkit
+ * (parity unpinned for RNG streams).
+ *
+ * Every float expression keeps the operation order of the HIP kernels and is
+ * compiled with -ffp-contract=off, so per-sample radiance is bit-identical.
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/pt_api.h"
+
+typedef struct {
+  float x, y, z;
+} v3;
+static inline v3 mk(float x, float y, float z) {
+  v3 r = {x, y, z};
+  return r;
+}
+static inline v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 scl(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+static inline v3 mulv(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline v3 cross(v3 a, v3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static inline float len3(v3 a) { return sqrtf(dot(a, a)); }
+static inline v3 nrm(v3 a) {
+  float inv = 1.0f / sqrtf(dot(a, a));
+  return scl(a, inv);
+}
+static inline v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+
+/* ---- Philox4x32-10 --------------------------------------------------------- */
+typedef struct {
+  uint32_t v[4];
+} u4;
+static inline uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+static u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = mulhi32(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    uint32_t hi1 = mulhi32(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0;
+    c1 = n1;
+    c2 = n2;
+    c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  u4 o = {{c0, c1, c2, c3}};
+  return o;
+}
+static inline float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
+static inline u4 rng(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t vertex, uint32_t call) {
+  return philox(pixel, sample, vertex * 2u + call, 0x50540000u, seed, 0x2545F491u);
+}
+void pto_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t* out) {
+  u4 r = philox(c0, c1, c2, c3, k0, k1);
+  memcpy(out, r.v, 16);
+}
+
+/* sin/cos of 2*pi*u: quadrant reduction on u, Taylor polynomials on [0, pi/2) */
+static void sincos2pi(float u, float* s, float* c) {
+  float x4 = u * 4.0f;
+  float q = floorf(x4);
+  float f = x4 - q;
+  float th = f * 1.57079637f;
+  float t2 = th * th;
+  float sp = -2.50521084e-08f;
+  sp = sp * t2 + 2.75573192e-06f;
+  sp = sp * t2 + -1.98412698e-04f;
+  sp = sp * t2 + 8.33333333e-03f;
+  sp = sp * t2 + -1.66666667e-01f;
+  sp = sp * t2 + 1.0f;
+  float sn = sp * th;
+  float cp = 2.08767570e-09f;
+  cp = cp * t2 + -2.75573192e-07f;
+  cp = cp * t2 + 2.48015873e-05f;
+  cp = cp * t2 + -1.38888889e-03f;
+  cp = cp * t2 + 4.16666667e-02f;
+  cp = cp * t2 + -0.5f;
+  cp = cp * t2 + 1.0f;
+  int iq = ((int)q) & 3;
+  float rs = sn, rc = cp;
+  if (iq == 1) {
+    rs = cp;
+    rc = -sn;
+  } else if (iq == 2) {
+    rs = -sn;
+    rc = -cp;
+  } else if (iq == 3) {
+    rs = -cp;
+    rc = sn;
+  }
+  *s = rs;
+  *c = rc;
+}
+void pto_sincos2pi(float u, float* s, float* c) { sincos2pi(u, s, c); }
+
+/* ---- primitive tests -------------------------------------------------------- */
+/* intersectRayTriangle, cu:217-270: plane hit then three edge sign tests. */
+static float pto_tri(v3 o, v3 d, const float* q) {
+  v3 N = mk(q[12], q[13], q[14]);
+  float ndd = N.x * d.x + N.y * d.y + N.z * d.z;
+  if (fabsf(ndd) < 1e-6f) return -1.0f;
+  float t = (q[7] - (N.x * o.x + N.y * o.y + N.z * o.z)) / ndd;
+  if (t < 0.0f) return -1.0f;
+  v3 P = mk(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
+  v3 vp = mk(P.x - q[0], P.y - q[1], P.z - q[2]);
+  v3 C = cross(mk(q[16], q[17], q[18]), vp);
+  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
+  vp = mk(P.x - q[4], P.y - q[5], P.z - q[6]);
+  C = cross(mk(q[20], q[21], q[22]), vp);
+  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
+  vp = mk(P.x - q[8], P.y - q[9], P.z - q[10]);
+  C = cross(mk(q[11], q[15], q[19]), vp);
+  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
+  return t == 0.0f ? 0.0f : t;
+}
+static float pto_sphere(v3 o, v3 d, const float* q) {
+  v3 oc = mk(o.x - q[0], o.y - q[1], o.z - q[2]);
+  float b = oc.x * d.x + oc.y * d.y + oc.z * d.z;
+  float cc = (oc.x * oc.x + oc.y * oc.y + oc.z * oc.z) - q[5];
+  float disc = b * b - cc;
+  if (disc < 0.0f) return -1.0f;
+  float sq = sqrtf(disc);
+  float t0 = -b - sq, t1 = -b + sq;
+  float t = (t0 >= 0.0f) ? t0 : t1;
+  if (t < 0.0f) return -1.0f;
+  return t == 0.0f ? 0.0f : t;
+}
+static inline float prim_test(const pt_prim* p, v3 o, v3 d) {
+  uint32_t meta;
+  memcpy(&meta, &p->q[3], 4);
+  return (meta >> 28) == PT_PRIM_SPHERE ? pto_sphere(o, d, p->q) : pto_tri(o, d, p->q);
+}
+static inline uint64_t key(float t, uint32_t prim) {
+  uint32_t b;
+  memcpy(&b, &t, 4);
+  return ((uint64_t)b << 32) | prim;
+}
+
+/* Closest hit by brute force: min over all primitives of (t, index), t <= tmax. */
+uint64_t pto_closest_brute(const pt_scene_desc* S, const float* ray) {
+  v3 o = mk(ray[0], ray[1], ray[2]), d = mk(ray[4], ray[5], ray[6]);
+  float tmax = ray[3];
+  uint64_t best = PT_HIT_NONE;
+  for (int i = 0; i < S->n_prims; ++i) {
+    float t = prim_test(&S->prims[i], o, d);
+    if (t >= 0.0f && t <= tmax) {
+      uint64_t k = key(t, (uint32_t)i);
+      if (k < best) best = k;
+    }
+  }
+  return best;
+}
+
+/* Closest hit through the wide BVH, depth-first with a stack.  The box test is
+ * done in double precision on the (outward-rounded) fp32 boxes. */
+static int box_hit_d(const pt_node* nd, int c, v3 o, v3 d, double tmax) {
+  double t0 = 0.0, t1 = tmax;
+  const float* mn[3] = {nd->bmin_x, nd->bmin_y, nd->bmin_z};
+  const float* mx[3] = {nd->bmax_x, nd->bmax_y, nd->bmax_z};
+  double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+  for (int a = 0; a < 3; ++a) {
+    double lo = mn[a][c], hi = mx[a][c];
+    if (dd[a] == 0.0) {
+      if (oo[a] < lo || oo[a] > hi) return 0;
+      continue;
+    }
+    double inv = 1.0 / dd[a];
+    double ta = (lo - oo[a]) * inv, tb = (hi - oo[a]) * inv;
+    if (ta > tb) {
+      double x = ta;
+      ta = tb;
+      tb = x;
+    }
+    if (ta > t0) t0 = ta;
+    if (tb < t1) t1 = tb;
+    if (t0 > t1) return 0;
+  }
+  return 1;
+}
+uint64_t pto_closest_bvh(const pt_scene_desc* S, const float* ray) {
+  v3 o = mk(ray[0], ray[1], ray[2]), d = mk(ray[4], ray[5], ray[6]);
+  float tmax = ray[3];
+  uint64_t best = PT_HIT_NONE;
+  int stack[256];
+  int sp = 0;
+  stack[sp++] = 0;
+  while (sp) {
+    const pt_node* nd = &S->nodes[stack[--sp]];
+    if (nd->prim_count > 0) {
+      for (int k = 0; k < nd->prim_count; ++k) {
+        int i = nd->prim_start + k;
+        float t = prim_test(&S->prims[i], o, d);
+        if (t >= 0.0f && t <= tmax) {
+          uint64_t kk = key(t, (uint32_t)i);
+          if (kk < best) best = kk;
+        }
+      }
+      continue;
+    }
+    double lim = tmax;
+    if (best != PT_HIT_NONE) {
+      uint32_t b = (uint32_t)(best >> 32);
+      float bt;
+      memcpy(&bt, &b, 4);
+      if (bt < lim) lim = bt;
+    }
+    for (int c = 0; c < 4; ++c)
+      if (nd->child[c] >= 0 && sp < 256 && box_hit_d(nd, c, o, d, lim)) stack[sp++] = nd->child[c];
+  }
+  return best;
+}
+
+void pto_intersect(const pt_scene_desc* S, const float* rays, int n, uint64_t* hits, int use_bvh) {
+  for (int i = 0; i < n; ++i) hits[i] = use_bvh ? pto_closest_bvh(S, rays + 8 * i) : pto_closest_brute(S, rays + 8 * i);
+}
+
+/* Level-synchronous breadth-first traversal statistics: R rays, V (ray, node)
+ * visits, per level, with the same conservative box test as pto_closest_bvh but
+ * no culling by the best hit (an upper bound of the GPU's V). */
+void pto_bfs_visits(const pt_scene_desc* S, const float* rays, int n, uint64_t* level_visits, int max_levels) {
+  for (int l = 0; l < max_levels; ++l) level_visits[l] = 0;
+  for (int i = 0; i < n; ++i) {
+    const float* r = rays + 8 * i;
+    if (r[3] < 0.0f) continue;
+    v3 o = mk(r[0], r[1], r[2]), d = mk(r[4], r[5], r[6]);
+    int stack[256];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+      int id = stack[--sp];
+      const pt_node* nd = &S->nodes[id];
+      if (nd->level < max_levels) level_visits[nd->level]++;
+      if (nd->prim_count > 0) continue;
+      for (int c = 0; c < 4; ++c)
+        if (nd->child[c] >= 0 && sp < 256 && box_hit_d(nd, c, o, d, r[3])) stack[sp++] = nd->child[c];
+    }
+  }
+}
+
+/* ---- path tracing ------------------------------------------------------------ */
+typedef struct {
+  const pt_scene_desc* S;
+  int W, H, spp, max_bounces, sample_offset, use_bvh;
+  uint32_t seed, flags;
+  int tile, rank, nranks;
+  const uint32_t* owned_tiles;
+  int n_owned_tiles;
+  atomic_int next_tile;
+  float* img;
+  atomic_ulong rays;
+} job_t;
+
+static uint64_t trace(const job_t* J, v3 o, v3 d, float tmax) {
+  float r[8] = {o.x, o.y, o.z, tmax, d.x, d.y, d.z, 0.0f};
+  return J->use_bvh ? pto_closest_bvh(J->S, r) : pto_closest_brute(J->S, r);
+}
+
+/* Radiance of sample s of pixel g: the per-path state machine of k_shade. */
+static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays) {
+  const pt_scene_desc* S = J->S;
+  const float INV_PI = 0.318309886183790671f, EPS = 1e-3f;
+  uint32_t row = g / (uint32_t)J->W, col = g - row * (uint32_t)J->W;
+  u4 u = rng(J->seed, g, s, 0, 0);
+  /* camera ray, cu:338-354 */
+  float ssx = (float)row + u01(u.v[0]);
+  float ssy = (float)col + u01(u.v[1]);
+  float kx = ssy / (float)J->W - 0.5f;
+  float ky = -(ssx / (float)J->H - 0.5f);
+  float kz = 1.0f;
+  float len = sqrtf(kx * kx + ky * ky + kz * kz);
+  kx = kx / len;
+  ky = ky / len;
+  kz = kz / len;
+  v3 Lf = ld3(S->camera.left), Up = ld3(S->camera.up), K = ld3(S->camera.look_at);
+  v3 d = nrm(mk(kx * Lf.x + ky * Up.x + kz * K.x, kx * Lf.y + ky * Up.y + kz * K.y, kx * Lf.z + ky * Up.z + kz * K.z));
+  v3 o = ld3(S->camera.origin);
+  v3 T = mk(1.0f, 1.0f, 1.0f), L = mk(0.0f, 0.0f, 0.0f);
+  int spec = 0;
+  for (uint32_t vtx = 1;; ++vtx) {
+    uint64_t h = trace(J, o, d, INFINITY);
+    (*nrays)++;
+    if (h == PT_HIT_NONE) break;
+    uint32_t tb = (uint32_t)(h >> 32), prim = (uint32_t)h;
+    float t;
+    memcpy(&t, &tb, 4);
+    v3 P = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+    const float* q = S->prims[prim].q;
+    uint32_t meta;
+    memcpy(&meta, &q[3], 4);
+    v3 ns;
+    if ((meta >> 28) == PT_PRIM_SPHERE) {
+      ns = nrm(mk(P.x - q[0], P.y - q[1], P.z - q[2]));
+    } else { /* barycentric shading normal, cu:1213-1221 */
+      v3 A = mk(q[0], q[1], q[2]), B = mk(q[4], q[5], q[6]), Cv = mk(q[8], q[9], q[10]);
+      const pt_prim_shading* sh = &S->shading[prim];
+      float total = len3(cross(sub(A, B), sub(B, Cv)));
+      float bC = len3(cross(sub(A, P), sub(B, P))) / total;
+      float bA = len3(cross(sub(B, P), sub(Cv, P))) / total;
+      float bB = len3(cross(sub(Cv, P), sub(A, P))) / total;
+      v3 n0 = ld3(sh->n0), n1 = ld3(sh->n1), n2 = ld3(sh->n2);
+      ns = nrm(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y, bA * n0.z + bB * n1.z + bC * n2.z));
+    }
+    int front = dot(ns, d) < 0.0f;
+    v3 n = front ? ns : mk(-ns.x, -ns.y, -ns.z);
+    v3 pt = sub(P, scl(d, EPS));
+    const pt_bsdf* Bs = &S->bsdfs[meta & 0x0FFFFFFFu];
+    if (Bs->type == PT_BSDF_EMISSION) {
+      if (!(J->flags & PT_FLAG_NO_EMISSION) && (vtx == 1 || spec)) L = add(L, mulv(T, ld3(Bs->albedo)));
+      break;
+    }
+    u4 r = rng(J->seed, g, s, vtx, 0);
+    v3 guide = (fabsf(n.x) < 0.9f) ? mk(1.0f, 0.0f, 0.0f) : mk(0.0f, 1.0f, 0.0f);
+    v3 dpdu = nrm(cross(guide, n));
+    v3 dpdv = cross(n, dpdu);
+    v3 dn, on;
+    if (Bs->type == PT_BSDF_DIFFUSE) {
+      v3 alb = ld3(Bs->albedo);
+      int have_sh = 0;
+      v3 C = mk(0, 0, 0), sw = mk(0, 0, 1);
+      float stmax = -1.0f;
+      if (S->light.type == PT_LIGHT_AREA) {
+        float sx = u01(r.v[0]) - 0.5f, sy = u01(r.v[1]) - 0.5f;
+        v3 pos = ld3(S->light.position), dx = ld3(S->light.dim_x), dy = ld3(S->light.dim_y);
+        v3 lpt = mk(pos.x + sx * dx.x + sy * dy.x, pos.y + sx * dx.y + sy * dy.y, pos.z + sx * dx.z + sy * dy.z);
+        v3 dv = sub(lpt, pt);
+        float sq = dot(dv, dv);
+        float dist = sqrtf(sq);
+        v3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+        float cosl = dot(w, ld3(S->light.direction));
+        float cosn = dot(n, w);
+        if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
+          float pdf = sq / (S->light.area * -cosl);
+          float scale = (cosn / pdf) * INV_PI;
+          C = scl(mulv(mulv(T, alb), ld3(S->light.radiance)), scale);
+          have_sh = 1;
+          sw = w;
+          stmax = dist - EPS;
+        }
+      } else if (S->light.type == PT_LIGHT_POINT) {
+        v3 dv = sub(ld3(S->light.position), pt);
+        float sq = dot(dv, dv);
+        float dist = sqrtf(sq);
+        v3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+        float cosn = dot(n, w);
+        if (dist > 1e-2f && cosn > 0.0f) {
+          C = scl(mulv(mulv(T, alb), ld3(S->light.radiance)), cosn * INV_PI);
+          have_sh = 1;
+          sw = w;
+          stmax = dist - EPS;
+        }
+      }
+      float x, y, z, sn, cs;
+      sincos2pi(u01(r.v[3]), &sn, &cs);
+      if (J->flags & PT_FLAG_COSINE_DIFFUSE) {
+        float u2 = u01(r.v[2]);
+        float rr = sqrtf(u2);
+        x = rr * cs;
+        y = rr * sn;
+        z = sqrtf(fmaxf(0.0f, 1.0f - u2));
+      } else {
+        z = fabsf(2.0f * u01(r.v[2]) - 1.0f);
+        float rr = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+        x = rr * cs;
+        y = rr * sn;
+      }
+      dn = nrm(mk(n.x * z + x * dpdu.x + y * dpdv.x, n.y * z + x * dpdu.y + y * dpdv.y, n.z * z + x * dpdu.z + y * dpdv.z));
+      if (J->flags & PT_FLAG_COSINE_DIFFUSE) {
+        T = mulv(T, alb);
+      } else {
+        float c = fabsf(dot(dn, n));
+        T = mk(((T.x * c) * alb.x) * 2.0f, ((T.y * c) * alb.y) * 2.0f, ((T.z * c) * alb.z) * 2.0f);
+      }
+      on = add(pt, scl(n, EPS));
+      spec = 0;
+      if (have_sh) {
+        uint64_t hs = trace(J, pt, sw, stmax);
+        (*nrays)++;
+        if (hs == PT_HIT_NONE) L = add(L, C);
+      }
+    } else if (Bs->type == PT_BSDF_MIRROR) {
+      float dd = dot(d, n);
+      dn = nrm(sub(d, scl(n, 2.0f * dd)));
+      T = mulv(T, ld3(Bs->albedo));
+      on = add(pt, scl(n, EPS));
+      spec = 1;
+    } else { /* glass */
+      float ior = Bs->ior;
+      float eta = front ? (1.0f / ior) : ior;
+      float cosi = -dot(d, n);
+      float sin2t = (eta * eta) * (1.0f - cosi * cosi);
+      int refl = 1;
+      float cost = 0.0f;
+      if (sin2t < 1.0f) {
+        cost = sqrtf(1.0f - sin2t);
+        float r0 = (1.0f - ior) / (1.0f + ior);
+        r0 = r0 * r0;
+        float c = front ? cosi : cost;
+        float m = 1.0f - c;
+        float F = r0 + (1.0f - r0) * (((m * m) * (m * m)) * m);
+        u4 r2 = rng(J->seed, g, s, vtx, 1);
+        refl = u01(r2.v[0]) < F;
+      }
+      if (refl) {
+        float dd = dot(d, n);
+        dn = nrm(sub(d, scl(n, 2.0f * dd)));
+        T = mulv(T, ld3(Bs->albedo));
+        on = add(pt, scl(n, EPS));
+      } else {
+        dn = nrm(add(scl(d, eta), scl(n, eta * cosi - cost)));
+        T = mulv(T, ld3(Bs->transmittance));
+        on = sub(P, scl(n, EPS));
+      }
+      spec = 1;
+    }
+    if (!(vtx <= (uint32_t)J->max_bounces && (T.x > 0.0f || T.y > 0.0f || T.z > 0.0f))) break;
+    o = on;
+    d = dn;
+  }
+  return L;
+}
+
+static void* worker(void* arg) {
+  job_t* J = (job_t*)arg;
+  const int T = J->tile;
+  const int ntx = (J->W + T - 1) / T;
+  uint64_t nrays = 0;
+  for (;;) {
+    int k = atomic_fetch_add(&J->next_tile, 1);
+    if (k >= J->n_owned_tiles) break;
+    int t = (int)J->owned_tiles[k];
+    int ty = t / ntx, tx = t % ntx;
+    for (int r = ty * T; r < (ty + 1) * T && r < J->H; ++r)
+      for (int c = tx * T; c < (tx + 1) * T && c < J->W; ++c) {
+        uint32_t g = (uint32_t)(r * J->W + c);
+        float ax = 0.0f, ay = 0.0f, az = 0.0f;
+        for (int s = 0; s < J->spp; ++s) {
+          v3 l = path_radiance(J, g, (uint32_t)(J->sample_offset + s), &nrays);
+          ax = ax + l.x;
+          ay = ay + l.y;
+          az = az + l.z;
+        }
+        float* px = J->img + (size_t)g * 4;
+        px[0] = ax;
+        px[1] = ay;
+        px[2] = az;
+        px[3] = 1.0f;
+      }
+  }
+  atomic_fetch_add(&J->rays, nrays);
+  return NULL;
+}
+
+/* Render spp samples of the pixels owned by (rank, nranks) and write the SUM of
+ * their radiance (not divided) into sums[W*H*4]; other pixels are left as is.
+ * Returns the number of rays cast. */
+uint64_t pto_render(const pt_scene_desc* S, int W, int H, int spp, int max_bounces, uint32_t seed,
+                    int sample_offset, uint32_t flags, int tile, int rank, int nranks, int nthreads,
+                    int use_bvh, float* sums) {
+  if (tile <= 0) tile = 32;
+  if (nranks <= 0) nranks = 1;
+  if (nthreads <= 0) nthreads = 1;
+  int ntx = (W + tile - 1) / tile, nty = (H + tile - 1) / tile;
+  uint32_t* owned = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(ntx * nty + 1));
+  int no = 0;
+  for (int t = 0; t < ntx * nty; ++t)
+    if (t % nranks == rank) owned[no++] = (uint32_t)t;
+  job_t J;
+  J.S = S;
+  J.W = W;
+  J.H = H;
+  J.spp = spp;
+  J.max_bounces = max_bounces;
+  J.sample_offset = sample_offset;
+  J.use_bvh = use_bvh;
+  J.seed = seed;
+  J.flags = flags;
+  J.tile = tile;
+  J.rank = rank;
+  J.nranks = nranks;
+  J.owned_tiles = owned;
+  J.n_owned_tiles = no;
+  atomic_init(&J.next_tile, 0);
+  J.img = sums;
+  atomic_init(&J.rays, 0);
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  for (int i = 0; i < nthreads; ++i) pthread_create(&th[i], NULL, worker, &J);
+  for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+  free(th);
+  free(owned);
+  return (uint64_t)atomic_load(&J.rays);
+}
+
+/* Radiance of one sample (tests of the per-sample state machine). */
+void pto_sample(const pt_scene_desc* S, int W, int H, int max_bounces, uint32_t seed, uint32_t flags, uint32_t g,
+                uint32_t s, float* out3) {
+  job_t J;
+  memset(&J, 0, sizeof(J));
+  J.S = S;
+  J.W = W;
+  J.H = H;
+  J.max_bounces = max_bounces;
+  J.seed = seed;
+  J.flags = flags;
+  J.use_bvh = 1;
+  uint64_t nr = 0;
+  v3 l = path_radiance(&J, g, s, &nr);
+  out3[0] = l.x;
+  out3[1] = l.y;
+  out3[2] = l.z;
+}
