@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s and ms/frame of the breadth-first wide-BVH path
+tracer at 1024x1024, 256 spp, 8 bounces (BASELINE.json metric), on N GPUs.
+
+A step is one full frame: every rank renders its interleaved 32x32 tiles of the
+1024x1024 image at 256 spp (strong scaling: the frame is fixed, ranks split it),
+then the framebuffer is gathered to rank 0 over RCCL.  Rays are every ray cast
+through the traversal (camera + extension + shadow), counted on the device.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  roofline: the dominant kernel k_trace_level,
+algorithmic bytes = sum over levels l>=1 of 32 B per (ray, node) visit (4 B
+queue id + 28 B ray o/d/tmax) + 4 B per id pushed to the next level
+(BASELINE.md §3), divided by its summed launch time from HIP events recorded on
+the library's stream inside the timed region.  cpu_baseline: the CPU oracle
+(oracle/ptoracle.c, the Scotty3D-structured tile renderer) on a bounded sample
+of the same frame on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "cuda-raytracer_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--scene", default="CBbunny")
+    p.add_argument("--width", type=int, default=1024)
+    p.add_argument("--height", type=int, default=1024)
+    p.add_argument("--spp", type=int, default=256)
+    p.add_argument("--bounces", type=int, default=8)
+    p.add_argument("--batch", type=int, default=0, help="paths in flight per batch (0 = auto)")
+    p.add_argument("--tile", type=int, default=32)
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--seed", type=int, default=15618)
+    return p.parse_args()
+
+
+def cpu_baseline(desc, args):
+    """Oracle renderer on this host: bounded sample of the same frame."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import pyoracle
+    threads = min(16, os.cpu_count() or 1)
+    # sample: 1/64 of the frame's tiles (interleaved), spp scaled to ~cpu_seconds
+    nr = 64
+    t0 = time.perf_counter()
+    _, rays = pyoracle.render(desc, args.width, args.height, 1, max_bounces=args.bounces, seed=args.seed,
+                              tile=args.tile, rank=0, nranks=nr, threads=threads)
+    t1 = time.perf_counter() - t0
+    spp = int(max(1, min(args.spp, args.cpu_seconds / max(t1, 1e-3))))
+    t0 = time.perf_counter()
+    _, rays = pyoracle.render(desc, args.width, args.height, spp, max_bounces=args.bounces, seed=args.seed,
+                              sample_offset=1, tile=args.tile, rank=0, nranks=nr, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{args.scene} {args.width}x{args.height}, tiles t%{nr}==0 ({args.width * args.height // nr} px), "
+                      f"{spp} spp, {args.bounces} bounces, {rays} rays in {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    import ptrace
+    import ptdist
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    scene = ptrace.ArrayScene.load(ROOT / "tests" / "golden" / "scenes" / f"{args.scene}.npz")
+    ctx = ptrace.Context(local)
+    ctx.load_scene(scene)
+
+    def frame(stats):
+        ctx.clear()
+        ctx.render(args.width, args.height, args.spp, max_bounces=args.bounces, seed=args.seed,
+                   batch_paths=args.batch, tile_size=args.tile, rank=rank, nranks=world,
+                   flags=ptrace.PT_FLAG_STATS if stats else 0)
+        if world > 1:
+            ptdist.gather_frame(ptdist.local_sums_tensor(ctx, dev), args.width, args.height, args.tile, args.spp)
+
+    for _ in range(args.warmup):
+        frame(False)
+    ctx.reset_stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    st = ctx.stats()
+    rays = st.rays
+    lvl_ms = sum(st.ms_level[l] for l in range(1, 16))
+    V = [st.level_visits[l] for l in range(16)]
+    lvl_bytes = sum(32 * V[l] for l in range(1, 16)) + sum(4 * V[l] for l in range(2, 16))
+    launches = sum(st.level_launches[l] for l in range(1, 16))
+    trace_bytes = 36 * st.rays + 36 * st.visits
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([rays, lvl_bytes, trace_bytes], dtype=torch.float64, device=dev)
+        dist.all_reduce(r)
+        rays, lvl_bytes_all, trace_bytes_all = (float(x) for x in r.tolist())
+    if rank == 0:
+        ms_step = elapsed / args.steps * 1e3
+        value = rays / elapsed / 1e6
+        ach = (lvl_bytes / (lvl_ms * 1e-3) / 1e9) if lvl_ms > 0 else 0.0
+        out = {
+            "metric": f"Mrays/sec at {args.width}x{args.height}, {args.spp} spp, {args.bounces} bounces",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"scene {args.scene}.dae (reference media, flattened fixture); rays sampled with Philox seed {args.seed}",
+            "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.spp}spp {args.bounces} bounces",
+                       "scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
+                       "max_bounces": args.bounces, "batch_paths": st.batch_paths,
+                       "parallelism": f"tiles{args.tile}x{world}"},
+            "ms_per_frame": round(ms_step, 2),
+            "rays_per_frame": int(rays / args.steps),
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "k_trace_level", "launches": int(launches),
+                         "avg_launch_us": round(lvl_ms * 1e3 / max(1, launches), 2),
+                         "bytes_per_launch": int(lvl_bytes / max(1, launches))},
+            "trace": {"visits_per_ray": round(st.visits / max(1, st.rays), 2),
+                      "ms_trace": round(st.ms_trace, 1), "ms_shade": round(st.ms_shade, 1),
+                      "ms_root": round(st.ms_root, 1), "ms_scan": round(st.ms_scan, 1),
+                      "ms_levels": round(lvl_ms, 1),
+                      "algorithmic_GBps_traversal": round(trace_bytes / max(st.ms_trace, 1e-9) / 1e6, 1)},
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(scene.desc(), args)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

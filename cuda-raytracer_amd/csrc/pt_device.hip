@@ -79,6 +79,30 @@ struct pt_ctx {
 
   pt_stats stats{};
   hipEvent_t ev[8] = {};
+
+  // kernel timing with a pool of events, read back once per render
+  enum { K_CAM, K_ROOT, K_SCAN, K_LEVEL, K_SHADE, K_ACCUM };
+  struct Mark {
+    int cls, level;
+    size_t e0, e1;
+  };
+  bool timing = false;
+  std::vector<hipEvent_t> evpool;
+  size_t evn = 0;
+  std::vector<Mark> marks;
+  size_t begin(void) {
+    if (evn == evpool.size()) {
+      hipEvent_t e;
+      hipEventCreate(&e);
+      evpool.push_back(e);
+    }
+    hipEventRecord(evpool[evn], stream);
+    return evn++;
+  }
+  void mark(int cls, int level, size_t e0) {
+    size_t e1 = begin();
+    marks.push_back(Mark{cls, level, e0, e1});
+  }
 };
 
 #define HIPCHK(ctx, call)                                                                 \
@@ -173,22 +197,16 @@ static TraceArgs trace_args(pt_ctx* c) {
 }
 
 // One breadth-first traversal pass over ray slots [r0, r1).
-static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1, bool timed) {
+static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
   if (r1 <= r0) return PT_OK;
   TraceArgs A = trace_args(c);
+  const bool timed = c->timing;
   const uint32_t items = (r1 - r0 + TILE - 1) / TILE;
   HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)c->n_nodes * NLANE * 4, c->stream));
-  if (timed) hipEventRecord(c->ev[0], c->stream);
+  size_t e0 = timed ? c->begin() : 0;
   hipLaunchKernelGGL(k_trace_root, dim3(items), dim3(TPB), 0, c->stream, A, r0, r1, c->d_rootcnt);
   hipLaunchKernelGGL(k_sum_root, dim3(1), dim3(1024), 0, c->stream, c->d_rootcnt, (int)items, c->d_stats);
-  if (timed) {
-    hipEventRecord(c->ev[1], c->stream);
-    hipEventSynchronize(c->ev[1]);
-    float ms = 0;
-    hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
-    c->stats.ms_trace_level[0] += ms;
-    c->stats.ms_trace += ms;
-  }
+  if (timed) c->mark(pt_ctx::K_ROOT, 0, e0);
   const size_t lanecap = c->qcap / NLANE;
   for (int l = 1; l < c->n_levels; ++l) {
     LevelArgs L;
@@ -200,22 +218,50 @@ static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1, bool timed) {
     L.nitems = c->d_nitems + l;
     L.nitems_w = c->d_nitems + l;
     const uint32_t out_base = (uint32_t)(((l + 1) & 1) ? c->qcap : 0);
-    if (timed) hipEventRecord(c->ev[0], c->stream);
+    if (timed) e0 = c->begin();
     hipLaunchKernelGGL(k_scan_level, dim3(1), dim3(1024), 0, c->stream, A, L, (uint32_t)lanecap, out_base,
                        c->d_stats, l, c->d_err);
-    hipLaunchKernelGGL(k_trace_level, dim3(LEVEL_GRID), dim3(TPB), 0, c->stream, A, L);
     if (timed) {
-      hipEventRecord(c->ev[1], c->stream);
-      hipEventSynchronize(c->ev[1]);
-      float ms = 0;
-      hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
-      if (l < 16) c->stats.ms_trace_level[l] += ms;
-      c->stats.ms_trace += ms;
+      c->mark(pt_ctx::K_SCAN, l, e0);
+      e0 = c->begin();
     }
+    hipLaunchKernelGGL(k_trace_level, dim3(LEVEL_GRID), dim3(TPB), 0, c->stream, A, L);
+    if (timed) c->mark(pt_ctx::K_LEVEL, l, e0);
   }
   HIPCHK(c, hipGetLastError());
   c->stats.passes++;
   return PT_OK;
+}
+
+// Fold the recorded kernel intervals into the stats (after the stream is idle).
+static void collect_marks(pt_ctx* c) {
+  for (const auto& m : c->marks) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->evpool[m.e0], c->evpool[m.e1]) != hipSuccess) continue;
+    switch (m.cls) {
+      case pt_ctx::K_ROOT:
+        c->stats.ms_root += ms;
+        c->stats.root_launches++;
+        c->stats.ms_trace += ms;
+        break;
+      case pt_ctx::K_SCAN:
+        c->stats.ms_scan += ms;
+        c->stats.ms_trace += ms;
+        break;
+      case pt_ctx::K_LEVEL:
+        if (m.level < 16) {
+          c->stats.ms_level[m.level] += ms;
+          c->stats.level_launches[m.level]++;
+        }
+        c->stats.ms_trace += ms;
+        break;
+      default:
+        c->stats.ms_shade += ms;
+        break;
+    }
+  }
+  c->marks.clear();
+  c->evn = 0;
 }
 
 static int read_device_stats(pt_ctx* c) {
@@ -228,6 +274,7 @@ static int read_device_stats(pt_ctx* c) {
   c->stats.visits = st[STAT_V];
   c->stats.peak_queue_entries = st[STAT_PEAKQ];
   for (int l = 0; l < 16; ++l) c->stats.level_visits[l] = st[STAT_LV0 + l];
+  c->stats.n_levels = c->n_levels;
   if (e) return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded");
   return PT_OK;
 }
@@ -284,6 +331,7 @@ void pt_destroy(pt_ctx* c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   free_all(c);
+  for (auto& e : c->evpool) hipEventDestroy(e);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -414,7 +462,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   if ((rc = ensure_paths(c, Nmax))) return rc;
   if (realloc && (rc = set_root_child_offsets(c))) return rc;
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
-  const bool timed = (P->flags & PT_FLAG_STATS) != 0;
+  c->timing = (P->flags & PT_FLAG_STATS) != 0;
+  const bool timed = c->timing;
   c->stats.batch_paths = (int32_t)Nmax;
 
   ShadeArgs S;
@@ -438,52 +487,41 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   S.flags = P->flags;
 
   hipEvent_t t0 = c->ev[6], t1 = c->ev[7];
-  hipEventRecord(t0, c->stream);
-  float shade_ms = 0;
+  HIPCHK(c, hipEventRecord(t0, c->stream));
   for (int done = 0; done < P->spp;) {
     const uint32_t sb = std::min<uint32_t>(spp_b, (uint32_t)(P->spp - done));
     const uint32_t N = npix * sb;
     S.N = N;
     S.sample_base = (uint32_t)(P->sample_offset + done);
     const dim3 grid((N + TPB - 1) / TPB);
-    if (timed) hipEventRecord(c->ev[2], c->stream);
+    size_t e0 = timed ? c->begin() : 0;
     hipLaunchKernelGGL(k_camera, grid, dim3(TPB), 0, c->stream, S);
-    if (timed) {
-      hipEventRecord(c->ev[3], c->stream);
-      hipEventSynchronize(c->ev[3]);
-      float ms;
-      hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
-      shade_ms += ms;
-    }
+    if (timed) c->mark(pt_ctx::K_CAM, 0, e0);
     const int passes = P->max_bounces + 2;
     for (int pass = 0; pass < passes; ++pass) {
       // pass 0: camera rays only; last pass: shadow rays only
       const uint32_t r0 = (pass == passes - 1) ? N : 0;
       const uint32_t r1 = (pass == 0) ? N : 2 * N;
-      // slots of a smaller final batch: shadow rays live at [N, 2N) of THIS batch
-      if ((rc = trace_pass(c, r0, r1, timed))) return rc;
-      if (timed) hipEventRecord(c->ev[2], c->stream);
+      if ((rc = trace_pass(c, r0, r1))) return rc;
+      if (timed) e0 = c->begin();
       hipLaunchKernelGGL(k_shade, grid, dim3(TPB), 0, c->stream, S);
-      if (timed) {
-        hipEventRecord(c->ev[3], c->stream);
-        hipEventSynchronize(c->ev[3]);
-        float ms;
-        hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
-        shade_ms += ms;
-      }
+      if (timed) c->mark(pt_ctx::K_SHADE, 0, e0);
     }
+    if (timed) e0 = c->begin();
     hipLaunchKernelGGL(k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), 0, c->stream, c->d_ps1, c->d_accum,
                        npix, sb);
+    if (timed) c->mark(pt_ctx::K_ACCUM, 0, e0);
     HIPCHK(c, hipGetLastError());
     done += (int)sb;
     c->stats.batches++;
   }
-  hipEventRecord(t1, c->stream);
+  HIPCHK(c, hipEventRecord(t1, c->stream));
   HIPCHK(c, hipEventSynchronize(t1));
   float total = 0;
   hipEventElapsedTime(&total, t0, t1);
   c->stats.ms_total = total;
-  c->stats.ms_shade += shade_ms;
+  if (timed) collect_marks(c);
+  c->timing = false;
   c->samples += P->spp;
   uint32_t e = 0;
   HIPCHK(c, hipMemcpy(&e, c->d_err, 4, hipMemcpyDeviceToHost));
@@ -542,7 +580,7 @@ int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) {
   hipLaunchKernelGGL(k_load_rays, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, d_in, c->d_ro, c->d_rd,
                      c->d_hit, (uint32_t)n);
   hipEventRecord(c->ev[6], c->stream);
-  rc = trace_pass(c, 0, (uint32_t)n, false);
+  rc = trace_pass(c, 0, (uint32_t)n);
   hipEventRecord(c->ev[7], c->stream);
   if (rc) {
     hipFree(d_in);

@@ -86,9 +86,10 @@ class pt_render_params(C.Structure):
 class pt_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("visits", C.c_uint64), ("passes", C.c_uint64),
                 ("batches", C.c_uint64), ("ms_total", C.c_double), ("ms_trace", C.c_double),
-                ("ms_shade", C.c_double), ("ms_trace_level", C.c_double * 16),
-                ("level_visits", C.c_uint64 * 16), ("peak_queue_entries", C.c_uint64),
-                ("n_levels", C.c_int32), ("batch_paths", C.c_int32)]
+                ("ms_shade", C.c_double), ("ms_root", C.c_double), ("ms_scan", C.c_double),
+                ("ms_level", C.c_double * 16), ("level_launches", C.c_uint64 * 16),
+                ("level_visits", C.c_uint64 * 16), ("root_launches", C.c_uint64),
+                ("peak_queue_entries", C.c_uint64), ("n_levels", C.c_int32), ("batch_paths", C.c_int32)]
 
 
 # every symbol include/pt_api.h declares (tests check the library exports them)
@@ -204,6 +205,61 @@ class Scene:
     def prims(self):
         d = self.desc()
         return np.ctypeslib.as_array(C.cast(d.prims, C.POINTER(C.c_float)), shape=(d.n_prims, 24)).copy()
+
+    def nodes(self):
+        d = self.desc()
+        return [d.nodes[i] for i in range(d.n_nodes)]
+
+
+def scene_to_arrays(scene: "Scene") -> dict:
+    """The flattened pt_scene_desc of a Scene as plain numpy arrays."""
+    d = scene.desc()
+    f32 = lambda p, n, k: np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), shape=(n, k)).copy()
+    nodes = np.frombuffer(C.string_at(d.nodes, C.sizeof(pt_node) * d.n_nodes), dtype=np.uint8).copy()
+    bsdfs = np.frombuffer(C.string_at(d.bsdfs, C.sizeof(pt_bsdf) * d.n_bsdfs), dtype=np.uint8).copy()
+    return {
+        "prims": f32(d.prims, d.n_prims, 24),
+        "shading": f32(d.shading, d.n_prims, 12),
+        "nodes": nodes,
+        "level_start": np.ctypeslib.as_array(d.level_start, shape=(d.n_levels + 1,)).copy(),
+        "bsdfs": bsdfs,
+        "light": np.frombuffer(bytes(d.light), dtype=np.uint8).copy(),
+        "camera": np.frombuffer(bytes(d.camera), dtype=np.uint8).copy(),
+    }
+
+
+class ArrayScene:
+    """A flattened scene held in numpy arrays (fixtures, synthetic scenes).
+    Exposes the same desc() as Scene, so Context.load_scene accepts it."""
+
+    def __init__(self, arrays: dict):
+        self.a = {k: np.ascontiguousarray(v) for k, v in arrays.items()}
+
+    @classmethod
+    def load(cls, path):
+        with np.load(path, allow_pickle=False) as z:
+            return cls({k: z[k] for k in z.files})
+
+    def desc(self) -> pt_scene_desc:
+        a = self.a
+        d = pt_scene_desc()
+        d.n_prims = len(a["prims"])
+        d.prims = a["prims"].ctypes.data_as(C.POINTER(pt_prim))
+        d.shading = a["shading"].ctypes.data_as(C.POINTER(pt_prim_shading))
+        d.n_nodes = len(a["nodes"]) // C.sizeof(pt_node)
+        d.nodes = a["nodes"].ctypes.data_as(C.POINTER(pt_node))
+        ls = a["level_start"].astype(np.int32)
+        self.a["level_start"] = ls
+        d.n_levels = len(ls) - 1
+        d.level_start = ls.ctypes.data_as(C.POINTER(C.c_int32))
+        d.n_bsdfs = len(a["bsdfs"]) // C.sizeof(pt_bsdf)
+        d.bsdfs = a["bsdfs"].ctypes.data_as(C.POINTER(pt_bsdf))
+        d.light = pt_light.from_buffer_copy(a["light"].tobytes())
+        d.camera = pt_camera.from_buffer_copy(a["camera"].tobytes())
+        return d
+
+    def level_counts(self):
+        return [int(x) for x in self.a.get("level_counts", [])]
 
     def nodes(self):
         d = self.desc()

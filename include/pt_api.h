@@ -242,10 +242,16 @@ typedef struct pt_stats {
   uint64_t passes;    /* traversal passes                                  */
   uint64_t batches;
   double ms_total;    /* GPU time of the last pt_render / pt_intersect     */
-  double ms_trace;    /* of which in traversal kernels                     */
-  double ms_shade;    /* of which in camera/shade/accumulate kernels       */
-  double ms_trace_level[16]; /* per BVH level (level 0 = root pass)       */
-  uint64_t level_visits[16];
+  /* per-kernel GPU time, summed over the renders since pt_reset_stats;
+   * collected only when PT_FLAG_STATS is set (HIP events, no host sync)    */
+  double ms_trace;    /* root + scan + level kernels                        */
+  double ms_shade;    /* camera + shade + accumulate kernels                */
+  double ms_root;     /* k_trace_root (+ its ray-count reduction)           */
+  double ms_scan;     /* k_scan_level                                       */
+  double ms_level[16];       /* k_trace_level per BVH level                 */
+  uint64_t level_launches[16];
+  uint64_t level_visits[16]; /* V per level (level 0 = R)                   */
+  uint64_t root_launches;
   uint64_t peak_queue_entries;
   int32_t n_levels;
   int32_t batch_paths;
