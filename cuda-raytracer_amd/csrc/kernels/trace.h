@@ -6,6 +6,10 @@
 #include "pt_api.h"
 #include "ptmath.h"
 
+// Pointer into the constant address space: uniform loads through it become
+// scalar (s_load) instead of per-lane vector loads.
+#define CPTR(T) __attribute__((address_space(4))) T*
+
 namespace pt {
 
 constexpr int TPB = 256;          // threads per workgroup (4 waves)

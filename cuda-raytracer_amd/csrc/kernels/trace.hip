@@ -39,12 +39,13 @@ namespace pt {
 // returned as +0 so that the {t bits, id} key orders correctly.
 __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q0, const float4 q1,
                                           const float4 q2, const float4 q3, const float4 q4,
-                                          const float4 q5) {
+                                          const float4 q5, const float tbest) {
   const f3 N = mk(q3.x, q3.y, q3.z);
   float ndd = N.x * d.x + N.y * d.y + N.z * d.z;
   if (fabsf(ndd) < 1e-6f) return -1.0f;
   float t = (q1.w - (N.x * o.x + N.y * o.y + N.z * o.z)) / ndd;
-  if (t < 0.0f) return -1.0f;
+  // t > tbest cannot win (ties need t == tbest): skip the edge tests
+  if (t < 0.0f || t > tbest) return -1.0f;
   f3 P = mk(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
   // edge 0: cross(v1 - v0, P - v0)
   f3 vp = mk(P.x - q0.x, P.y - q0.y, P.z - q0.z);
@@ -107,7 +108,9 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
                                              uint32_t* sh) {
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
-  const pt_node* __restrict__ nd = A.nodes + node;
+  // node and primitive records are wave-uniform: read them through the
+  // constant address space so they land in SGPRs via s_load
+  const CPTR(pt_node) nd = (const CPTR(pt_node))(A.nodes + node);
 
   uint32_t id[RPT];
   f3 o[RPT], d[RPT];
@@ -149,7 +152,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
       bt[j] = tmax[j];
       bp[j] = -1;
     }
-    const float4* __restrict__ P = A.prims + (size_t)pstart * 6;
+    const CPTR(float4) P = (const CPTR(float4))(A.prims + (size_t)pstart * 6);
     for (int k = 0; k < pcount; ++k, P += 6) {
       const float4 q0 = P[0], q1 = P[1];
       const uint32_t meta = __float_as_uint(q0.w);
@@ -166,7 +169,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
         const float4 q2 = P[2], q3 = P[3], q4 = P[4], q5 = P[5];
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {
-          float t = tri_test(o[j], d[j], q0, q1, q2, q3, q4, q5);
+          float t = tri_test(o[j], d[j], q0, q1, q2, q3, q4, q5, bt[j]);
           if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
             bt[j] = t;
             bp[j] = pstart + k;

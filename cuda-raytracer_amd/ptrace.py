@@ -103,6 +103,15 @@ API_SYMBOLS = [
 
 
 def _load():
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME
+    # libamdhip64.so.7, but its libraries NEED the plain file name), so if
+    # libptcore.so were loaded first a second runtime would be mapped when
+    # torch initialises and the two would fight over the device.  Loading torch
+    # first makes libptcore.so bind to the already-loaded runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not LIB_PATH.exists():
         raise ImportError(f"libptcore.so not built ({LIB_PATH}); run __graft_entry__.build()")
     lib = C.CDLL(str(LIB_PATH))

@@ -22,11 +22,8 @@ def pytest_configure(config):
 
 
 def have_gpu():
-    try:
-        import torch
-        return torch.cuda.is_available()
-    except Exception:
-        return False
+    import ptrace
+    return ptrace.device_count() > 0
 
 
 @pytest.fixture(scope="session")
