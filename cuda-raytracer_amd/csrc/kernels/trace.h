@@ -12,6 +12,9 @@
 
 namespace pt {
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 f4(f4v v) { return make_float4(v.x, v.y, v.z, v.w); }
+
 constexpr int TPB = 256;          // threads per workgroup (4 waves)
 constexpr int RPT = 4;            // rays per thread in a traversal item
 constexpr int TILE = TPB * RPT;   // rays per traversal item

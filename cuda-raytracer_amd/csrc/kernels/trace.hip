@@ -152,9 +152,9 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
       bt[j] = tmax[j];
       bp[j] = -1;
     }
-    const CPTR(float4) P = (const CPTR(float4))(A.prims + (size_t)pstart * 6);
+    const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);
     for (int k = 0; k < pcount; ++k, P += 6) {
-      const float4 q0 = P[0], q1 = P[1];
+      const float4 q0 = f4(P[0]), q1 = f4(P[1]);
       const uint32_t meta = __float_as_uint(q0.w);
       if ((meta >> 28) == PT_PRIM_SPHERE) {
 #pragma unroll
@@ -166,7 +166,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
           }
         }
       } else {
-        const float4 q2 = P[2], q3 = P[3], q4 = P[4], q5 = P[5];
+        const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {
           float t = tri_test(o[j], d[j], q0, q1, q2, q3, q4, q5, bt[j]);

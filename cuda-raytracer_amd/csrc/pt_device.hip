@@ -152,7 +152,12 @@ static int ensure_paths(pt_ctx* c, uint32_t N) {
   if ((rc = dalloc(c, &c->d_ps0, N))) return rc;
   if ((rc = dalloc(c, &c->d_ps1, N))) return rc;
   if ((rc = dalloc(c, &c->d_ps2, N))) return rc;
-  c->qcap = QFACTOR * slots;
+  // every root child needs ceil(items/8)*TILE slots per lane (see
+  // set_root_child_offsets); deeper levels need at most 4x the visits of the
+  // level above, which QFACTOR covers for the scenes measured (peak_queue_entries)
+  const size_t items = (slots + TILE - 1) / TILE;
+  const size_t root_need = (size_t)NLANE * 4 * ((items + NLANE - 1) / NLANE * TILE);
+  c->qcap = std::max(QFACTOR * slots, 2 * root_need);
   c->qcap = (c->qcap + NLANE * 64 - 1) / (NLANE * 64) * (NLANE * 64);
   if ((rc = dalloc(c, &c->d_q, 2 * c->qcap))) return rc;
   if ((rc = dalloc(c, &c->d_rootcnt, (slots + TILE - 1) / TILE))) return rc;

@@ -17,6 +17,8 @@ step() {  # step <name> <seconds> <cmd...>
   if fatal $rc; then echo "FATAL in $name (rc=$rc), stopping"; exit $rc; fi
   return 0
 }
+# the shipped libraries must be up to date with their sources
+make -s -C cuda-raytracer_amd check || { echo "rebuild before gpurun"; exit 3; }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
   step pytest_gpu 900 python -m pytest tests -m gpu -x -q
