@@ -94,6 +94,10 @@ __device__ __forceinline__ bool box_hit(float bx0, float bx1, float by0, float b
   return tn <= tf;
 }
 
+__device__ __forceinline__ float safe_dir(float x) {
+  return fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x;
+}
+
 __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
@@ -195,7 +199,11 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
   uint32_t bits[RPT];
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
-    f3 inv = mk(__builtin_amdgcn_rcpf(d[j].x), __builtin_amdgcn_rcpf(d[j].y), __builtin_amdgcn_rcpf(d[j].z));
+    // |d| components below 1e-20 are clamped so 1/d stays finite: the FMA slab
+    // form t = b*inv - o*inv would turn an axis-parallel ray (inv = inf) lying
+    // inside a slab into inf - inf = NaN and wrongly miss the box
+    f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
+                __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
     f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
     uint32_t b = 0;
 #pragma unroll
