@@ -196,6 +196,7 @@ class Scene:
         rc = LIB.pt_scene_get_desc(self.h, C.byref(d))
         if rc != PT_OK:
             raise PTError(rc, "pt_scene_get_desc")
+        d._owner = self  # the desc borrows the scene's arrays
         return d
 
     def level_counts(self):
@@ -265,6 +266,7 @@ class ArrayScene:
         d.bsdfs = a["bsdfs"].ctypes.data_as(C.POINTER(pt_bsdf))
         d.light = pt_light.from_buffer_copy(a["light"].tobytes())
         d.camera = pt_camera.from_buffer_copy(a["camera"].tobytes())
+        d._owner = self  # the desc points into our arrays: keep them alive
         return d
 
     def level_counts(self):

@@ -1,0 +1,70 @@
+"""The CPU oracle pinned: Philox known-answer vectors, sampling math, BVH walk ==
+brute force, tmax/tie semantics, thread-count independence and a committed
+golden render (regression pin of the oracle itself)."""
+import math
+
+import numpy as np
+import pytest
+
+import ptrace
+import pyoracle
+from conftest import ROOT, load_fixture
+from rays import camera_rays, interior_rays
+
+GOLDEN = ROOT / "tests" / "golden"
+
+
+def test_philox_known_answers():
+    # Random123 kat_vectors, philox4x32_10
+    assert pyoracle.philox([0, 0, 0, 0], [0, 0]) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert pyoracle.philox([0xFFFFFFFF] * 4, [0xFFFFFFFF] * 2) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    assert pyoracle.philox([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], [0xA4093822, 0x299F31D0]) == [
+        0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_sincos2pi_accuracy():
+    for u in np.linspace(0, 1, 4097, endpoint=False, dtype=np.float32):
+        s, c = pyoracle.sincos2pi(float(u))
+        assert abs(s - math.sin(2 * math.pi * float(u))) < 2e-7
+        assert abs(c - math.cos(2 * math.pi * float(u))) < 2e-7
+
+
+@pytest.mark.parametrize("name", ["CBempty", "CBspheres", "CBgems", "CBcoil", "CBbunny"])
+def test_bvh_walk_equals_brute_force(name):
+    d = load_fixture(name).desc()
+    rays = np.concatenate([camera_rays(d, 1500, seed=3), interior_rays(d, 1500, seed=4),
+                           interior_rays(d, 500, seed=5, tmax=0.3)])
+    b = pyoracle.intersect(d, rays, use_bvh=False)
+    v = pyoracle.intersect(d, rays, use_bvh=True)
+    assert np.array_equal(b, v)
+    assert (b != ptrace.PT_HIT_NONE).mean() > 0.3
+
+
+def test_tmax_is_inclusive():
+    d = load_fixture("CBcoil").desc()
+    r = np.array([[0, 0.75, 3, np.inf, 0, 0, -1, 0]], np.float32)
+    t = ptrace.hit_t(pyoracle.intersect(d, r))[0]
+    r[0, 3] = t
+    assert ptrace.hit_t(pyoracle.intersect(d, r))[0] == t
+    r[0, 3] = np.nextafter(t, np.float32(0))
+    assert pyoracle.intersect(d, r)[0] == ptrace.PT_HIT_NONE
+
+
+def test_render_thread_independent_and_progressive():
+    d = load_fixture("CBgems").desc()
+    a, ra = pyoracle.render(d, 24, 20, 3, max_bounces=6, threads=1)
+    b, rb = pyoracle.render(d, 24, 20, 3, max_bounces=6, threads=8)
+    assert np.array_equal(a, b) and ra == rb
+    # per-pixel sums are sums over samples: s[0:3] == s[0:1] + s[1:3] is NOT
+    # bitwise (fp association), but the samples themselves are independent:
+    c1, _ = pyoracle.render(d, 24, 20, 1, max_bounces=6, sample_offset=2)
+    c2, _ = pyoracle.render(d, 24, 20, 1, max_bounces=6, sample_offset=2, threads=3)
+    assert np.array_equal(c1, c2)
+
+
+def test_golden_render_regression():
+    g = np.load(GOLDEN / "render_CBgems_16x16x2.npz", allow_pickle=False)
+    d = load_fixture("CBgems").desc()
+    sums, rays = pyoracle.render(d, 16, 16, 2, max_bounces=8, seed=15618)
+    assert int(g["rays"]) == rays
+    assert np.array_equal(g["sums"], sums)
