@@ -50,24 +50,29 @@ def parse():
 
 
 def cpu_baseline(desc, args):
-    """Oracle renderer on this host: bounded sample of the same frame."""
+    """Oracle renderer on this host: a bounded sample of the same frame (same
+    spp and bounces, a 1/nr subset of its interleaved tiles), sized to about
+    --cpu-seconds of CPU work."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle
     threads = min(16, os.cpu_count() or 1)
-    # sample: 1/64 of the frame's tiles (interleaved), spp scaled to ~cpu_seconds
-    nr = 64
+    cal_nr, cal_spp = 64, 4
     t0 = time.perf_counter()
-    _, rays = pyoracle.render(desc, args.width, args.height, 1, max_bounces=args.bounces, seed=args.seed,
-                              tile=args.tile, rank=0, nranks=nr, threads=threads)
-    t1 = time.perf_counter() - t0
-    spp = int(max(1, min(args.spp, args.cpu_seconds / max(t1, 1e-3))))
-    t0 = time.perf_counter()
-    _, rays = pyoracle.render(desc, args.width, args.height, spp, max_bounces=args.bounces, seed=args.seed,
-                              sample_offset=1, tile=args.tile, rank=0, nranks=nr, threads=threads)
+    _, rays = pyoracle.render(desc, args.width, args.height, cal_spp, max_bounces=args.bounces, seed=args.seed,
+                              tile=args.tile, rank=0, nranks=cal_nr, threads=threads)
     dt = time.perf_counter() - t0
+    full_s = dt * cal_nr * args.spp / cal_spp  # estimated CPU seconds for the whole frame
+    nr = 1
+    while full_s / nr > args.cpu_seconds and nr < 4096:
+        nr *= 2
+    t0 = time.perf_counter()
+    _, rays = pyoracle.render(desc, args.width, args.height, args.spp, max_bounces=args.bounces, seed=args.seed,
+                              tile=args.tile, rank=0, nranks=nr, threads=threads)
+    dt = time.perf_counter() - t0
+    npx = len(__import__("ptdist").owned_pixels(args.width, args.height, args.tile, 0, nr))
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{args.scene} {args.width}x{args.height}, tiles t%{nr}==0 ({args.width * args.height // nr} px), "
-                      f"{spp} spp, {args.bounces} bounces, {rays} rays in {dt:.1f} s"}
+            "sample": f"{args.scene} {args.width}x{args.height}: tiles t%{nr}==0 ({npx} px), {args.spp} spp, "
+                      f"{args.bounces} bounces; {rays} rays in {dt:.1f} s on {threads} threads"}
 
 
 def main():
@@ -159,7 +164,11 @@ def main():
                       "ms_trace": round(st.ms_trace, 1), "ms_shade": round(st.ms_shade, 1),
                       "ms_root": round(st.ms_root, 1), "ms_scan": round(st.ms_scan, 1),
                       "ms_levels": round(lvl_ms, 1),
-                      "algorithmic_GBps_traversal": round(trace_bytes / max(st.ms_trace, 1e-9) / 1e6, 1)},
+                      "algorithmic_GBps_traversal": round(trace_bytes / max(st.ms_trace, 1e-9) / 1e6, 1),
+                      "levels": [{"level": l, "ms": round(st.ms_level[l], 2), "visits": int(st.level_visits[l]),
+                                  "leaf_visits": int(st.level_leaf_visits[l]), "items": int(st.level_items[l]),
+                                  "Gvisits_per_s": round(st.level_visits[l] / max(st.ms_level[l], 1e-9) / 1e6, 2)}
+                                 for l in range(1, st.n_levels)]},
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(scene.desc(), args)

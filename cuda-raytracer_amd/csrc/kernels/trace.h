@@ -26,8 +26,10 @@ enum {
   STAT_R = 0,
   STAT_V = 1,
   STAT_PEAKQ = 2,
-  STAT_LV0 = 8,  // 16 per-level visit counters
-  STAT_COUNT = 32
+  STAT_LV0 = 8,     // 16 per-level visit counters
+  STAT_LEAF0 = 24,  // 16 per-level leaf-visit counters
+  STAT_ITEMS0 = 40, // 16 per-level item counters
+  STAT_COUNT = 56
 };
 
 struct TraceArgs {

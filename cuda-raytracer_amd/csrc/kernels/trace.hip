@@ -332,20 +332,21 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
   __shared__ uint32_t wsum[16][16];
   __shared__ uint32_t run[16];
   __shared__ uint32_t ctot[16];
-  __shared__ unsigned long long vsum;
+  __shared__ unsigned long long vsum, lsum;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, ln = tid & 63;
   if (tid < 16) run[tid] = 0;
-  if (tid == 0) vsum = 0;
+  if (tid == 0) vsum = lsum = 0;
   __syncthreads();
-  unsigned long long myv = 0;
+  unsigned long long myv = 0, myleaf = 0;
   for (int chunk = 0; chunk < L.nl; chunk += 1024) {
     const int k = chunk + tid;
     const bool act = k < L.nl;
     const int node = L.first + k;
     int nch = 0;
     int child[4] = {-1, -1, -1, -1};
-    if (act && A.nodes[node].prim_count == 0) {
+    const bool leaf = act && A.nodes[node].prim_count > 0;
+    if (act && !leaf) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         child[c] = A.nodes[node].child[c];
@@ -358,6 +359,7 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
       uint32_t c = act ? A.cnt[(size_t)node * NLANE + s] : 0u;
       cnt8[s] = c;
       myv += c;
+      if (leaf) myleaf += c;
       v[s] = (c + TILE - 1) / TILE;          // items
       v[8 + s] = c * (uint32_t)nch;           // child capacity
     }
@@ -409,7 +411,11 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
   }
   // sentinel ep[nl] and item count
   myv = wave_sum64(myv);
-  if (ln == 0) atomicAdd(&vsum, myv);
+  myleaf = wave_sum64(myleaf);
+  if (ln == 0) {
+    atomicAdd(&vsum, myv);
+    atomicAdd(&lsum, myleaf);
+  }
   __syncthreads();
   if (tid == 0) {
     uint32_t mx = 0;
@@ -426,7 +432,13 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
     *L.nitems_w = mx * NLANE;
     if (stats) {
       stats[STAT_V] += vsum;
-      stats[STAT_LV0 + level] += vsum;
+      if (level < 16) {
+        stats[STAT_LV0 + level] += vsum;
+        stats[STAT_LEAF0 + level] += lsum;
+        unsigned long long it = 0;
+        for (int s = 0; s < NLANE; ++s) it += run[s];
+        stats[STAT_ITEMS0 + level] += it;
+      }
       unsigned long long need = 0;
       for (int s = 0; s < NLANE; ++s) need = max(need, (unsigned long long)run[8 + s]);
       if (need * NLANE > stats[STAT_PEAKQ]) stats[STAT_PEAKQ] = need * NLANE;

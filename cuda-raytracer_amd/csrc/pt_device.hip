@@ -278,7 +278,12 @@ static int read_device_stats(pt_ctx* c) {
   c->stats.rays = st[STAT_R];
   c->stats.visits = st[STAT_V];
   c->stats.peak_queue_entries = st[STAT_PEAKQ];
-  for (int l = 0; l < 16; ++l) c->stats.level_visits[l] = st[STAT_LV0 + l];
+  for (int l = 0; l < 16; ++l) {
+    c->stats.level_visits[l] = st[STAT_LV0 + l];
+    c->stats.level_leaf_visits[l] = st[STAT_LEAF0 + l];
+    c->stats.level_items[l] = st[STAT_ITEMS0 + l];
+  }
+  if (c->root_leaf) c->stats.level_leaf_visits[0] = st[STAT_LV0];
   c->stats.n_levels = c->n_levels;
   if (e) return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded");
   return PT_OK;

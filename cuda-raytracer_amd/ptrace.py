@@ -88,7 +88,8 @@ class pt_stats(C.Structure):
                 ("batches", C.c_uint64), ("ms_total", C.c_double), ("ms_trace", C.c_double),
                 ("ms_shade", C.c_double), ("ms_root", C.c_double), ("ms_scan", C.c_double),
                 ("ms_level", C.c_double * 16), ("level_launches", C.c_uint64 * 16),
-                ("level_visits", C.c_uint64 * 16), ("root_launches", C.c_uint64),
+                ("level_visits", C.c_uint64 * 16), ("level_leaf_visits", C.c_uint64 * 16),
+                ("level_items", C.c_uint64 * 16), ("root_launches", C.c_uint64),
                 ("peak_queue_entries", C.c_uint64), ("n_levels", C.c_int32), ("batch_paths", C.c_int32)]
 
 

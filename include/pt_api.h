@@ -251,6 +251,8 @@ typedef struct pt_stats {
   double ms_level[16];       /* k_trace_level per BVH level                 */
   uint64_t level_launches[16];
   uint64_t level_visits[16]; /* V per level (level 0 = R)                   */
+  uint64_t level_leaf_visits[16]; /* of which at leaf nodes                 */
+  uint64_t level_items[16];  /* work items (<= 1024 rays of one node lane)  */
   uint64_t root_launches;
   uint64_t peak_queue_entries;
   int32_t n_levels;
