@@ -18,7 +18,12 @@ __device__ __forceinline__ float4 f4(f4v v) { return make_float4(v.x, v.y, v.z, 
 constexpr int TPB = 256;          // threads per workgroup (4 waves)
 constexpr int RPT = 4;            // rays per thread in a traversal item
 constexpr int TILE = TPB * RPT;   // rays per traversal item
+constexpr int RPTW = 4;           // rays per lane in a wave-sized item
+constexpr int WTILE = 64 * RPTW;  // rays per wave item (levels >= 1)
 constexpr int NLANE = 8;          // queue lanes (one per XCD)
+constexpr int CSTRIDE = 32;       // u32 per queue counter: each (node, lane) counter owns a 128-B line
+constexpr uint32_t MODE_WAVE = 0, MODE_BLOCK = 1;
+constexpr uint32_t BLOCK_MODE_RAYS_PER_PAIR = 512;  // level mode threshold (mean rays per queue lane)
 constexpr int LEVEL_GRID = 2048;  // workgroups of the per-level grid-stride kernel (8 per CU)
 
 // device statistics slots (unsigned long long)
@@ -43,6 +48,8 @@ struct TraceArgs {
   uint32_t* q;                       // ray-id queues (two parity halves)
 };
 
+__host__ __device__ inline size_t cnt_idx(int node, int lane) { return ((size_t)node * NLANE + lane) * CSTRIDE; }
+
 struct LevelArgs {
   int first;  // first node id of the level
   int nl;     // nodes in the level
@@ -51,6 +58,8 @@ struct LevelArgs {
   uint32_t* iprefix_w;      // same array (written by the scan)
   const uint32_t* nitems;   // items of the level (read)
   uint32_t* nitems_w;
+  const uint32_t* mode;  // MODE_WAVE / MODE_BLOCK, chosen by the scan
+  uint32_t* mode_w;
 };
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {

@@ -229,7 +229,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
     uint32_t w0 = sh[c * 4 + 0], w1 = sh[c * 4 + 1], w2 = sh[c * 4 + 2], w3 = sh[c * 4 + 3];
     uint32_t tot = w0 + w1 + w2 + w3;
     uint32_t b = 0;
-    if (child >= 0 && tot) b = atomicAdd(A.cnt + (size_t)child * NLANE + lane, tot);
+    if (child >= 0 && tot) b = atomicAdd(A.cnt + cnt_idx(child, lane), tot);
     sh[16 + c * 4 + 0] = b;
     sh[16 + c * 4 + 1] = b + w0;
     sh[16 + c * 4 + 2] = b + w0 + w1;
@@ -269,54 +269,184 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, uint32_t r0, ui
   if (threadIdx.x == 0) rootcnt[item] = sh[32] + sh[33] + sh[34] + sh[35];
 }
 
-// ---- per-level pass: grid-stride loop over items --------------------------------
-__global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
-  __shared__ uint32_t sh[64];
-  __shared__ int s_node;
-  __shared__ uint32_t s_base;
-  __shared__ int s_n;
-  const uint32_t total = *L.nitems;
-  const int tid = threadIdx.x;
-  for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
-    const int lane = g & (NLANE - 1);
-    const uint32_t m = g >> 3;
-    const uint32_t* __restrict__ ep = L.iprefix + (size_t)lane * (L.maxln + 1);
-    if (tid < 64) {
-      // 64-ary search for the node k with ep[k] <= m < ep[k+1]
-      int lo = 0, hi = L.nl;
-      if (m >= ep[hi]) {
-        lo = -1;  // padding item of a short lane
+// ---- one wave-sized item: up to WTILE rays of one node's queue lane ---------------
+// Levels >= 1 are processed at wave granularity: no LDS, no workgroup barrier,
+// one returning atomic per wave per child.  Deep levels hold many nodes with a
+// few hundred rays each, where 1024-ray workgroup items would run mostly empty.
+__device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane) {
+  const uint32_t lid = lane_id();
+  const CPTR(pt_node) nd = (const CPTR(pt_node))(A.nodes + node);
+  uint32_t id[RPTW];
+  f3 o[RPTW], d[RPTW];
+  float tmax[RPTW];
+  bool valid[RPTW];
+#pragma unroll
+  for (int j = 0; j < RPTW; ++j) {
+    const int i = j * 64 + (int)lid;
+    valid[j] = i < n;
+    id[j] = valid[j] ? A.q[base + i] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < RPTW; ++j) {
+    float4 a = make_float4(0.f, 0.f, 0.f, -1.f), b = make_float4(0.f, 0.f, 1.f, 0.f);
+    if (valid[j]) {
+      a = A.ro[id[j]];
+      b = A.rd[id[j]];
+    }
+    o[j] = mk(a.x, a.y, a.z);
+    tmax[j] = a.w;
+    d[j] = mk(b.x, b.y, b.z);
+  }
+  const int pcount = nd->prim_count;
+  if (pcount > 0) {
+    const int pstart = nd->prim_start;
+    float bt[RPTW];
+    int bp[RPTW];
+#pragma unroll
+    for (int j = 0; j < RPTW; ++j) {
+      bt[j] = tmax[j];
+      bp[j] = -1;
+    }
+    const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);
+    for (int k = 0; k < pcount; ++k, P += 6) {
+      const float4 q0 = f4(P[0]), q1 = f4(P[1]);
+      const uint32_t meta = __float_as_uint(q0.w);
+      if ((meta >> 28) == PT_PRIM_SPHERE) {
+#pragma unroll
+        for (int j = 0; j < RPTW; ++j) {
+          float t = sphere_test(o[j], d[j], q0, q1);
+          if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
+            bt[j] = t;
+            bp[j] = pstart + k;
+          }
+        }
       } else {
-        while (hi - lo > 1) {
-          const int step = (hi - lo + 63) >> 6;
-          const int idx = lo + tid * step;
-          const bool le = idx < hi && ep[idx] <= m;
-          const unsigned long long msk = __ballot(le);
-          const int last = 63 - __clzll(msk);
-          lo = lo + last * step;
-          hi = min(lo + step, hi);
+        const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
+#pragma unroll
+        for (int j = 0; j < RPTW; ++j) {
+          float t = tri_test(o[j], d[j], q0, q1, q2, q3, q4, q5, bt[j]);
+          if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
+            bt[j] = t;
+            bp[j] = pstart + k;
+          }
         }
       }
-      if (tid == 0) {
-        if (lo < 0) {
-          s_node = -1;
-        } else {
+    }
+#pragma unroll
+    for (int j = 0; j < RPTW; ++j) {
+      if (valid[j] && bp[j] >= 0) {
+        unsigned long long key =
+            ((unsigned long long)__float_as_uint(bt[j]) << 32) | (unsigned long long)(uint32_t)bp[j];
+        atomicMin(A.hit + id[j], key);
+        if (bt[j] < tmax[j]) reinterpret_cast<float*>(A.ro + id[j])[3] = bt[j];
+      }
+    }
+    return;
+  }
+  uint32_t bits[RPTW];
+#pragma unroll
+  for (int j = 0; j < RPTW; ++j) {
+    f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
+                __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
+    f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
+    uint32_t b = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      bool h = box_hit(nd->bmin_x[c], nd->bmax_x[c], nd->bmin_y[c], nd->bmax_y[c], nd->bmin_z[c],
+                       nd->bmax_z[c], oi, inv, tmax[j]);
+      b |= (valid[j] && h) ? (1u << c) : 0u;
+    }
+    bits[j] = b;
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int child = nd->child[c];
+    if (child < 0) continue;
+    unsigned long long m[RPTW];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int j = 0; j < RPTW; ++j) {
+      m[j] = __ballot((bits[j] >> c) & 1u);
+      tot += (uint32_t)__popcll(m[j]);
+    }
+    if (tot == 0) continue;
+    uint32_t b = 0;
+    if (lid == 0) b = atomicAdd(A.cnt + cnt_idx(child, lane), tot);
+    b = __builtin_amdgcn_readfirstlane(b);
+    uint32_t off = b + A.qoff[(size_t)child * NLANE + lane];
+#pragma unroll
+    for (int j = 0; j < RPTW; ++j) {
+      if ((bits[j] >> c) & 1u) A.q[off + mbcnt64(m[j])] = id[j];
+      off += (uint32_t)__popcll(m[j]);
+    }
+  }
+}
+
+// ---- per-level pass: every wave walks the items of its block's lane ----------------
+// Lane s's items are processed by blocks b with b % 8 == s (same XCD under the
+// observed round-robin placement: a speed hint only).
+__global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
+  const int lane = blockIdx.x & (NLANE - 1);
+  const uint32_t lid = lane_id();
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t* __restrict__ ep = L.iprefix + (size_t)lane * (L.maxln + 1);
+  const uint32_t M = ep[L.nl];  // items of this lane
+  if (*L.mode == MODE_BLOCK) {
+    // few nodes with many rays: 1024-ray items, one atomic per workgroup per child
+    __shared__ uint32_t sh[64];
+    __shared__ int s_node;
+    __shared__ uint32_t s_base;
+    __shared__ int s_n;
+    for (uint32_t m = blockIdx.x / NLANE; m < M; m += gridDim.x / NLANE) {
+      if (wave == 0) {
+        int lo = 0, hi = L.nl;
+        while (hi - lo > 1) {
+          const int step = (hi - lo + 63) >> 6;
+          const int idx = lo + (int)lid * step;
+          const bool le = idx < hi && ep[idx] <= m;
+          const unsigned long long msk = __ballot(le);
+          lo = lo + (63 - __clzll(msk)) * step;
+          hi = min(lo + step, hi);
+        }
+        if (lid == 0) {
           const int node = L.first + lo;
           const uint32_t i = m - ep[lo];
-          const uint32_t c = A.cnt[(size_t)node * NLANE + lane];
+          const uint32_t c = A.cnt[cnt_idx(node, lane)];
           s_node = node;
           s_base = A.qoff[(size_t)node * NLANE + lane] + i * TILE;
           s_n = (int)min((uint32_t)TILE, c - i * TILE);
         }
       }
+      __syncthreads();
+      const int node = __builtin_amdgcn_readfirstlane(s_node);
+      const uint32_t base = __builtin_amdgcn_readfirstlane(s_base);
+      const int n = __builtin_amdgcn_readfirstlane(s_n);
+      __syncthreads();
+      process_item<false>(A, node, base, n, lane, sh);
+      __syncthreads();
     }
-    __syncthreads();
-    const int node = __builtin_amdgcn_readfirstlane(s_node);
-    const uint32_t base = __builtin_amdgcn_readfirstlane(s_base);
-    const int n = __builtin_amdgcn_readfirstlane(s_n);
-    __syncthreads();
-    if (node >= 0) process_item<false>(A, node, base, n, lane, sh);
-    __syncthreads();
+    return;
+  }
+  // many nodes with few rays each: every wave walks its own 256-ray items
+  const uint32_t stride = (gridDim.x / NLANE) * (TPB / 64);
+  for (uint32_t m = (blockIdx.x / NLANE) * (TPB / 64) + wave; m < M; m += stride) {
+    // 64-ary search for the node k with ep[k] <= m < ep[k+1]
+    int lo = 0, hi = L.nl;
+    while (hi - lo > 1) {
+      const int step = (hi - lo + 63) >> 6;
+      const int idx = lo + (int)lid * step;
+      const bool le = idx < hi && ep[idx] <= m;
+      const unsigned long long msk = __ballot(le);
+      lo = lo + (63 - __clzll(msk)) * step;
+      hi = min(lo + step, hi);
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    const int node = L.first + lo;
+    const uint32_t i = m - ep[lo];
+    const uint32_t c = A.cnt[cnt_idx(node, lane)];
+    const uint32_t base = A.qoff[(size_t)node * NLANE + lane] + i * WTILE;
+    const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
+    process_wave(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane);
   }
 }
 
@@ -338,6 +468,32 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
   if (tid < 16) run[tid] = 0;
   if (tid == 0) vsum = lsum = 0;
   __syncthreads();
+  // pick the item shape of this level: workgroup items when the (node, lane)
+  // queues are long (few nodes, high atomic contention), wave items otherwise
+  __shared__ uint32_t s_mode;
+  {
+    unsigned long long v = 0, pairs = 0;
+    for (int k = tid; k < L.nl; k += 1024)
+      for (int s = 0; s < NLANE; ++s) {
+        uint32_t c = A.cnt[cnt_idx(L.first + k, s)];
+        v += c;
+        pairs += c ? 1 : 0;
+      }
+    v = wave_sum64(v);
+    pairs = wave_sum64(pairs);
+    if (ln == 0) {
+      atomicAdd(&vsum, v);
+      atomicAdd(&lsum, pairs);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      s_mode = (vsum >= (unsigned long long)BLOCK_MODE_RAYS_PER_PAIR * max(lsum, 1ull)) ? MODE_BLOCK : MODE_WAVE;
+      *L.mode_w = s_mode;
+      vsum = lsum = 0;
+    }
+    __syncthreads();
+  }
+  const uint32_t itile = s_mode == MODE_BLOCK ? TILE : WTILE;
   unsigned long long myv = 0, myleaf = 0;
   for (int chunk = 0; chunk < L.nl; chunk += 1024) {
     const int k = chunk + tid;
@@ -356,11 +512,11 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
     uint32_t v[16], cnt8[NLANE];
 #pragma unroll
     for (int s = 0; s < NLANE; ++s) {
-      uint32_t c = act ? A.cnt[(size_t)node * NLANE + s] : 0u;
+      uint32_t c = act ? A.cnt[cnt_idx(node, s)] : 0u;
       cnt8[s] = c;
       myv += c;
       if (leaf) myleaf += c;
-      v[s] = (c + TILE - 1) / TILE;          // items
+      v[s] = (c + itile - 1) / itile;        // items
       v[8 + s] = c * (uint32_t)nch;           // child capacity
     }
     // block exclusive scan of 16 values per thread

@@ -207,7 +207,7 @@ static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
   TraceArgs A = trace_args(c);
   const bool timed = c->timing;
   const uint32_t items = (r1 - r0 + TILE - 1) / TILE;
-  HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)c->n_nodes * NLANE * 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)c->n_nodes * NLANE * CSTRIDE * 4, c->stream));
   size_t e0 = timed ? c->begin() : 0;
   hipLaunchKernelGGL(k_trace_root, dim3(items), dim3(TPB), 0, c->stream, A, r0, r1, c->d_rootcnt);
   hipLaunchKernelGGL(k_sum_root, dim3(1), dim3(1024), 0, c->stream, c->d_rootcnt, (int)items, c->d_stats);
@@ -222,6 +222,8 @@ static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
     L.iprefix_w = c->d_iprefix;
     L.nitems = c->d_nitems + l;
     L.nitems_w = c->d_nitems + l;
+    L.mode = c->d_nitems + c->n_levels + l;
+    L.mode_w = c->d_nitems + c->n_levels + l;
     const uint32_t out_base = (uint32_t)(((l + 1) & 1) ? c->qcap : 0);
     if (timed) e0 = c->begin();
     hipLaunchKernelGGL(k_scan_level, dim3(1), dim3(1024), 0, c->stream, A, L, (uint32_t)lanecap, out_base,
@@ -380,16 +382,16 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   if ((rc = dalloc(c, &c->d_prims, (size_t)s->n_prims * 6))) return rc;
   if ((rc = dalloc(c, &c->d_shading, s->n_prims))) return rc;
   if ((rc = dalloc(c, &c->d_bsdfs, std::max(1, s->n_bsdfs)))) return rc;
-  if ((rc = dalloc(c, &c->d_cnt, (size_t)s->n_nodes * NLANE))) return rc;
+  if ((rc = dalloc(c, &c->d_cnt, (size_t)s->n_nodes * NLANE * CSTRIDE))) return rc;
   if ((rc = dalloc(c, &c->d_qoff, (size_t)s->n_nodes * NLANE))) return rc;
   if ((rc = dalloc(c, &c->d_iprefix, (size_t)NLANE * (c->max_level_nodes + 1)))) return rc;
-  if ((rc = dalloc(c, &c->d_nitems, std::max(1, s->n_levels)))) return rc;
+  if ((rc = dalloc(c, &c->d_nitems, 2 * std::max(1, s->n_levels)))) return rc;
   HIPCHK(c, hipMemcpy(c->d_nodes, s->nodes, sizeof(pt_node) * s->n_nodes, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_prims, s->prims, sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_shading, s->shading, sizeof(pt_prim_shading) * s->n_prims, hipMemcpyHostToDevice));
   if (s->n_bsdfs > 0)
     HIPCHK(c, hipMemcpy(c->d_bsdfs, s->bsdfs, sizeof(pt_bsdf) * s->n_bsdfs, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemset(c->d_cnt, 0, (size_t)s->n_nodes * NLANE * 4));
+  HIPCHK(c, hipMemset(c->d_cnt, 0, (size_t)s->n_nodes * NLANE * CSTRIDE * 4));
   HIPCHK(c, hipMemset(c->d_qoff, 0, (size_t)s->n_nodes * NLANE * 4));
   c->light = s->light;
   c->camera = s->camera;
