@@ -1,0 +1,284 @@
+// scotty_pt.h -- header-only C++ surface of the reference over the C ABI.
+//
+// Keeps the class/method names a Scotty3D / CUDA-SCOTTY caller uses so the
+// MI355X path drops in behind them:
+//   cutracer::CudaRenderer   src/cudaRenderer.h:173-272   -> scotty::CudaRenderer
+//   CMU462::Camera::generate_ray   src/camera.h:81          -> scotty::Camera::generate_ray
+//   StaticScene::BVHAccel(prims, 32), intersect(ray[, isect])
+//                            src/bvh.h:111-149            -> scotty::BVHAccel
+//   CMU462::PathTracer set_scene / set_camera / set_frame_size /
+//     start_raytracing / is_done / raytrace_pixel / save_image
+//                            src/pathtracer.h:51-179      -> scotty::PathTracer
+// Everything is plain C++17 on top of include/pt_api.h; no HIP types here.
+// Errors throw scotty::Error carrying the pt_* code and message (the
+// reference printf()s and exit()s instead).
+#pragma once
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "pt_api.h"
+
+namespace scotty {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m + " (pt error " + std::to_string(c) + ")"), code(c) {}
+};
+
+struct Vector3D {
+  double x = 0, y = 0, z = 0;
+  Vector3D() = default;
+  Vector3D(double a, double b, double c) : x(a), y(b), z(c) {}
+};
+
+// CMU462::Ray subset (src/ray.h): origin, direction, [min_t, max_t]
+struct Ray {
+  Vector3D o, d;
+  double min_t = 0.0, max_t = INFINITY;
+  Ray() = default;
+  Ray(const Vector3D& o_, const Vector3D& d_, double maxt = INFINITY) : o(o_), d(d_), max_t(maxt) {}
+};
+
+// CMU462::Intersection subset (src/intersection.h)
+struct Intersection {
+  double t = INFINITY;
+  int primitive = -1;  // index into the BVH-sorted primitive array
+  Vector3D n;          // geometric normal facing the ray
+  int bsdf = -1;
+};
+
+class Scene {
+ public:
+  explicit Scene(const std::string& dae_path) {
+    char err[512] = {0};
+    int rc = pt_scene_load_dae(dae_path.c_str(), &s_, err, sizeof err);
+    if (rc) throw Error(rc, std::string("loadScene: ") + err);
+    pt_scene_get_desc(s_, &d_);
+  }
+  ~Scene() { pt_scene_free(s_); }
+  Scene(const Scene&) = delete;
+  Scene& operator=(const Scene&) = delete;
+  const pt_scene_desc& desc() const { return d_; }
+
+ private:
+  pt_scene* s_ = nullptr;
+  pt_scene_desc d_{};
+};
+
+class Device {
+ public:
+  explicit Device(int device = 0) {
+    int rc = pt_create(&c_, device);
+    if (rc) throw Error(rc, "pt_create");
+  }
+  ~Device() { pt_destroy(c_); }
+  Device(const Device&) = delete;
+  Device& operator=(const Device&) = delete;
+  pt_ctx* get() const { return c_; }
+  void check(int rc, const char* what) const {
+    if (rc) throw Error(rc, std::string(what) + ": " + pt_last_error(c_));
+  }
+
+ private:
+  pt_ctx* c_ = nullptr;
+};
+
+// The reference GPU camera (cu:80-86, cu:1590-1607, cu:338-354): fixed
+// 53.13 degree field of view; (x, y) are normalised screen coordinates in [0,1].
+class Camera {
+ public:
+  Camera() = default;
+  explicit Camera(const pt_camera& c) : c_(c) {}
+  const pt_camera& params() const { return c_; }
+  Ray generate_ray(double x, double y) const {
+    double kx = x - 0.5, ky = -(y - 0.5), kz = 1.0;
+    double len = std::sqrt(kx * kx + ky * ky + kz * kz);
+    kx /= len;
+    ky /= len;
+    kz /= len;
+    Vector3D d(kx * c_.left[0] + ky * c_.up[0] + kz * c_.look_at[0],
+               kx * c_.left[1] + ky * c_.up[1] + kz * c_.look_at[1],
+               kx * c_.left[2] + ky * c_.up[2] + kz * c_.look_at[2]);
+    double dl = std::sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
+    return Ray(Vector3D(c_.origin[0], c_.origin[1], c_.origin[2]), Vector3D(d.x / dl, d.y / dl, d.z / dl));
+  }
+
+ private:
+  pt_camera c_{};
+};
+
+// BVHAccel over the GPU breadth-first traversal.  Single rays work, but the
+// path is built for batches: intersect(std::vector<Ray>) is the fast form.
+class BVHAccel {
+ public:
+  BVHAccel(Device& dev, const Scene& scene, size_t max_leaf_size = 32) : dev_(dev), d_(scene.desc()) {
+    if (max_leaf_size != 32) throw Error(PT_E_UNSUPPORTED, "BVHAccel: max_leaf_size must be 32 (bvh.h:111)");
+    dev_.check(pt_load_scene(dev_.get(), &d_), "pt_load_scene");
+  }
+  std::vector<Intersection> intersect(const std::vector<Ray>& rays) const {
+    std::vector<float> r(rays.size() * 8);
+    for (size_t i = 0; i < rays.size(); ++i) {
+      float* p = &r[i * 8];
+      p[0] = (float)rays[i].o.x;
+      p[1] = (float)rays[i].o.y;
+      p[2] = (float)rays[i].o.z;
+      p[3] = (float)rays[i].max_t;
+      p[4] = (float)rays[i].d.x;
+      p[5] = (float)rays[i].d.y;
+      p[6] = (float)rays[i].d.z;
+      p[7] = 0.f;
+    }
+    std::vector<uint64_t> h(rays.size());
+    dev_.check(pt_intersect(dev_.get(), r.data(), (int32_t)rays.size(), h.data()), "pt_intersect");
+    std::vector<Intersection> out(rays.size());
+    for (size_t i = 0; i < rays.size(); ++i) {
+      if (h[i] == PT_HIT_NONE) continue;
+      uint32_t tb = (uint32_t)(h[i] >> 32);
+      float t;
+      memcpy(&t, &tb, 4);
+      Intersection& is = out[i];
+      is.t = t;
+      is.primitive = (int)(uint32_t)h[i];
+      const float* q = d_.prims[is.primitive].q;
+      uint32_t meta;
+      memcpy(&meta, &q[3], 4);
+      is.bsdf = (int)(meta & 0x0FFFFFFFu);
+      Vector3D n;
+      if ((meta >> 28) == PT_PRIM_SPHERE) {
+        n = Vector3D(rays[i].o.x + t * rays[i].d.x - q[0], rays[i].o.y + t * rays[i].d.y - q[1],
+                     rays[i].o.z + t * rays[i].d.z - q[2]);
+      } else {
+        n = Vector3D(q[12], q[13], q[14]);
+      }
+      double nl = std::sqrt(n.x * n.x + n.y * n.y + n.z * n.z);
+      double s = (n.x * rays[i].d.x + n.y * rays[i].d.y + n.z * rays[i].d.z) < 0 ? 1.0 / nl : -1.0 / nl;
+      is.n = Vector3D(n.x * s, n.y * s, n.z * s);
+    }
+    return out;
+  }
+  bool intersect(const Ray& r, Intersection* isect) const {
+    Intersection i = intersect(std::vector<Ray>{r})[0];
+    if (i.primitive < 0 || i.t < r.min_t) return false;
+    if (isect) *isect = i;
+    return true;
+  }
+  bool intersect(const Ray& r) const { return intersect(r, nullptr); }
+
+ private:
+  Device& dev_;
+  pt_scene_desc d_;
+};
+
+struct Image {  // src/cuda_image.h: float RGBA, rows bottom-up
+  int width = 0, height = 0;
+  std::vector<float> data;
+};
+
+// cutracer::CudaRenderer with the reference's member functions.
+class CudaRenderer {
+ public:
+  explicit CudaRenderer(int device = 0) : dev_(device) {}
+  void allocOutputImage(int w, int h) {  // cu:2119
+    image_.width = w;
+    image_.height = h;
+    image_.data.assign((size_t)w * h * 4, 0.f);
+  }
+  void loadScene(const std::string& path) {  // cu:1679
+    scene_ = std::make_unique<Scene>(path);
+    camera_ = Camera(scene_->desc().camera);
+  }
+  void setup() { dev_.check(pt_load_scene(dev_.get(), &scene_->desc()), "pt_load_scene"); }  // cu:1872
+  // one progressive frame of spp samples (renderAccumulate, cu:2419-2457)
+  void render(int spp = 2, int max_bounces = 2, uint32_t flags = 0) {
+    pt_render_params p{};
+    p.width = image_.width;
+    p.height = image_.height;
+    p.spp = spp;
+    p.max_bounces = max_bounces;
+    p.seed = 15618;
+    p.sample_offset = samples_;
+    p.tile_size = 32;
+    p.nranks = 1;
+    p.flags = flags;
+    dev_.check(pt_render(dev_.get(), &p), "pt_render");
+    samples_ += spp;
+  }
+  const Image* getImage() {  // cu:1539
+    dev_.check(pt_get_image(dev_.get(), image_.data.data(), image_.data.size()), "pt_get_image");
+    return &image_;
+  }
+  void setViewpoint(const Vector3D& origin, const Vector3D& lookAt) {  // cu:1845
+    pt_camera c = camera_.params();
+    c.origin[0] = (float)origin.x;
+    c.origin[1] = (float)origin.y;
+    c.origin[2] = (float)origin.z;
+    c.look_at[0] = (float)lookAt.x;
+    c.look_at[1] = (float)lookAt.y;
+    c.look_at[2] = (float)lookAt.z;
+    camera_ = Camera(c);
+    dev_.check(pt_set_camera(dev_.get(), &c), "pt_set_camera");
+    samples_ = 0;
+  }
+  void clearImage() {  // cu:2131
+    dev_.check(pt_clear(dev_.get()), "pt_clear");
+    samples_ = 0;
+  }
+  Device& device() { return dev_; }
+  const Camera& camera() const { return camera_; }
+
+ private:
+  Device dev_;
+  std::unique_ptr<Scene> scene_;
+  Camera camera_;
+  Image image_;
+  int samples_ = 0;
+};
+
+// CMU462::PathTracer surface: the whole frame is traced on the GPU by
+// start_raytracing(); raytrace_pixel(x, y) returns the pixel's estimate.
+class PathTracer {
+ public:
+  PathTracer(size_t ns_aa = 1, size_t max_ray_depth = 4, size_t /*ns_area_light*/ = 1, size_t /*ns_diff*/ = 1,
+             size_t /*ns_glsy*/ = 1, size_t /*ns_refr*/ = 1, size_t /*num_threads*/ = 1)
+      : ns_aa_(ns_aa), max_depth_(max_ray_depth) {}
+  void set_scene(const std::string& dae_path) {
+    r_.loadScene(dae_path);
+    r_.setup();
+  }
+  void set_camera(const Camera&) {}  // the scene's camera is used (cu:1590-1607)
+  void set_frame_size(size_t w, size_t h) { r_.allocOutputImage((int)w, (int)h); }
+  void start_raytracing() {
+    r_.clearImage();
+    r_.render((int)ns_aa_, (int)max_depth_);
+    img_ = r_.getImage();
+  }
+  bool is_done() const { return img_ != nullptr; }
+  Vector3D raytrace_pixel(size_t x, size_t y) const {
+    if (!img_) throw Error(PT_E_INVALID, "raytrace_pixel before start_raytracing");
+    const float* p = &img_->data[((size_t)y * img_->width + x) * 4];
+    return Vector3D(p[0], p[1], p[2]);
+  }
+  // PFM (float RGB, bottom-up rows: the framebuffer's own order)
+  void save_image(const std::string& filename) const {
+    if (!img_) throw Error(PT_E_INVALID, "save_image before start_raytracing");
+    FILE* f = fopen(filename.c_str(), "wb");
+    if (!f) throw Error(PT_E_IO, "save_image: cannot open " + filename);
+    fprintf(f, "PF\n%d %d\n-1.0\n", img_->width, img_->height);
+    for (size_t i = 0; i < (size_t)img_->width * img_->height; ++i) fwrite(&img_->data[i * 4], 4, 3, f);
+    fclose(f);
+  }
+  CudaRenderer& renderer() { return r_; }
+
+ private:
+  size_t ns_aa_, max_depth_;
+  CudaRenderer r_;
+  const Image* img_ = nullptr;
+};
+
+}  // namespace scotty

@@ -1,0 +1,48 @@
+// ptrender -- headless replacement of the reference's scottyCuda driver
+// (src/cudaMain.cpp:30-104 + display.cpp's GLUT loop): load a COLLADA scene,
+// render W x H at S spp on one GPU through the C ABI, write a PFM.
+//
+//   ptrender scene.dae [-w 1024] [-h 1024] [-s 256] [-m 8] [-o out.pfm] [-d device]
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+
+#include "../scotty/scotty_pt.h"
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::cerr << "usage: ptrender scene.dae [-w W] [-h H] [-s spp] [-m bounces] [-o out.pfm] [-d device]\n";
+    return 2;
+  }
+  int w = 512, h = 512, spp = 16, bounces = 8, dev = 0;
+  std::string out = "out.pfm";
+  for (int i = 2; i + 1 < argc; i += 2) {
+    std::string k = argv[i];
+    if (k == "-w") w = atoi(argv[i + 1]);
+    else if (k == "-h") h = atoi(argv[i + 1]);
+    else if (k == "-s") spp = atoi(argv[i + 1]);
+    else if (k == "-m") bounces = atoi(argv[i + 1]);
+    else if (k == "-o") out = argv[i + 1];
+    else if (k == "-d") dev = atoi(argv[i + 1]);
+  }
+  try {
+    scotty::PathTracer pt(spp, bounces);
+    pt.renderer();  // device context created here
+    pt.set_frame_size(w, h);
+    pt.set_scene(argv[1]);
+    auto t0 = std::chrono::steady_clock::now();
+    pt.start_raytracing();
+    double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    pt_stats st{};
+    pt_get_stats(pt.renderer().device().get(), &st);
+    std::cout << w << "x" << h << " " << spp << " spp " << bounces << " bounces: " << s * 1e3 << " ms, "
+              << st.rays / s / 1e6 << " Mrays/s\n";
+    pt.save_image(out);
+    (void)dev;
+  } catch (const std::exception& e) {
+    std::cerr << "ptrender: " << e.what() << "\n";
+    return 1;
+  }
+  return 0;
+}
