@@ -56,6 +56,8 @@ struct LevelArgs {
   int maxln;  // row stride - 1 of iprefix
   const uint32_t* iprefix;  // [lane][maxln+1] exclusive item prefix (read)
   uint32_t* iprefix_w;      // same array (written by the scan)
+  const uint32_t* icnt;     // [lane][maxln+1] ray count snapshot of the level (read)
+  uint32_t* icnt_w;
   const uint32_t* nitems;   // items of the level (read)
   uint32_t* nitems_w;
   const uint32_t* mode;  // MODE_WAVE / MODE_BLOCK, chosen by the scan

@@ -254,19 +254,23 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 
 // ---- root pass (level 0): implicit queue = slots [r0, r1) ------------------------
 __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, uint32_t r0, uint32_t r1,
-                                                    uint32_t* __restrict__ rootcnt) {
+                                                    unsigned long long* __restrict__ rcount) {
   __shared__ uint32_t sh[64];
   const uint32_t item = blockIdx.x;
   const uint32_t first = r0 + item * TILE;
   const int n = (int)min((uint32_t)TILE, r1 - first);
   const int lane = item & (NLANE - 1);
   uint32_t v = process_item<true>(A, 0, first, n, lane, sh);
-  // valid-ray count of this item (R of the roofline formula)
+  // valid-ray count (R of the roofline formula): one fire-and-forget atomic per
+  // workgroup into this lane's counter line
   v = wave_sum(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) sh[32 + (threadIdx.x >> 6)] = v;
   __syncthreads();
-  if (threadIdx.x == 0) rootcnt[item] = sh[32] + sh[33] + sh[34] + sh[35];
+  if (threadIdx.x == 0) {
+    const uint32_t t = sh[32] + sh[33] + sh[34] + sh[35];
+    if (t) atomicAdd(rcount + (size_t)lane * 16, (unsigned long long)t);
+  }
 }
 
 // ---- one wave-sized item: up to WTILE rays of one node's queue lane ---------------
@@ -411,7 +415,7 @@ __global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
         if (lid == 0) {
           const int node = L.first + lo;
           const uint32_t i = m - ep[lo];
-          const uint32_t c = A.cnt[cnt_idx(node, lane)];
+          const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
           s_node = node;
           s_base = A.qoff[(size_t)node * NLANE + lane] + i * TILE;
           s_n = (int)min((uint32_t)TILE, c - i * TILE);
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
     lo = __builtin_amdgcn_readfirstlane(lo);
     const int node = L.first + lo;
     const uint32_t i = m - ep[lo];
-    const uint32_t c = A.cnt[cnt_idx(node, lane)];
+    const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
     const uint32_t base = A.qoff[(size_t)node * NLANE + lane] + i * WTILE;
     const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
     process_wave(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane);
@@ -451,82 +455,92 @@ __global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
 }
 
 // ---- per-level scan: work ranges and child queue allocation ---------------------
-// One workgroup of 1024 threads.  For every (node, lane) of level l it turns the
-// node's ray count into items (exclusive prefix per lane, consumed by
-// k_trace_level) and allocates each child's queue lane with capacity = the
-// parent's count in that lane (the reference's wOffset + i*rayCount, cu:922
-// and cu:1384, without the single-warp scan and the D2H of maxBlocks).
+// One workgroup of 1024 threads.  For every (node, lane) of level l it
+//  1. snapshots the node's ray count into a dense per-level array (read by
+//     k_trace_level) and re-zeroes the atomic counter for the next pass;
+//  2. picks the level's item shape (workgroup or wave items);
+//  3. turns counts into items (exclusive prefix per lane) and allocates each
+//     child's queue lane with capacity = the parent's count in that lane (the
+//     reference's wOffset + i*rayCount, cu:922 and cu:1384, without the
+//     single-warp scan and the D2H of maxBlocks, cu:2237).
 __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, uint32_t lanecap,
                                                      uint32_t out_parity_base, unsigned long long* stats,
                                                      int level, uint32_t* err) {
   __shared__ uint32_t wsum[16][16];
   __shared__ uint32_t run[16];
   __shared__ uint32_t ctot[16];
-  __shared__ unsigned long long vsum, lsum;
+  __shared__ unsigned long long red[3][16];
   const int tid = threadIdx.x;
   const int wave = tid >> 6, ln = tid & 63;
+  const size_t row = (size_t)L.maxln + 1;
   if (tid < 16) run[tid] = 0;
-  if (tid == 0) vsum = lsum = 0;
-  __syncthreads();
-  // pick the item shape of this level: workgroup items when the (node, lane)
-  // queues are long (few nodes, high atomic contention), wave items otherwise
-  __shared__ uint32_t s_mode;
-  {
-    unsigned long long v = 0, pairs = 0;
-    for (int k = tid; k < L.nl; k += 1024)
-      for (int s = 0; s < NLANE; ++s) {
-        uint32_t c = A.cnt[cnt_idx(L.first + k, s)];
-        v += c;
-        pairs += c ? 1 : 0;
-      }
-    v = wave_sum64(v);
-    pairs = wave_sum64(pairs);
-    if (ln == 0) {
-      atomicAdd(&vsum, v);
-      atomicAdd(&lsum, pairs);
+
+  // pass 1: snapshot + zero the counters, totals for the mode decision
+  unsigned long long v = 0, pairs = 0, leafv = 0;
+  for (int k = tid; k < L.nl; k += 1024) {
+    const int node = L.first + k;
+    const bool leaf = A.nodes[node].prim_count > 0;
+#pragma unroll
+    for (int s = 0; s < NLANE; ++s) {
+      const uint32_t c = A.cnt[cnt_idx(node, s)];
+      L.icnt_w[s * row + k] = c;
+      v += c;
+      pairs += c ? 1 : 0;
+      if (leaf) leafv += c;
     }
-    __syncthreads();
-    if (tid == 0) {
-      s_mode = (vsum >= (unsigned long long)BLOCK_MODE_RAYS_PER_PAIR * max(lsum, 1ull)) ? MODE_BLOCK : MODE_WAVE;
-      *L.mode_w = s_mode;
-      vsum = lsum = 0;
-    }
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < NLANE; ++s) A.cnt[cnt_idx(node, s)] = 0u;
   }
-  const uint32_t itile = s_mode == MODE_BLOCK ? TILE : WTILE;
-  unsigned long long myv = 0, myleaf = 0;
+  v = wave_sum64(v);
+  pairs = wave_sum64(pairs);
+  leafv = wave_sum64(leafv);
+  if (ln == 0) {
+    red[0][wave] = v;
+    red[1][wave] = pairs;
+    red[2][wave] = leafv;
+  }
+  __syncthreads();
+  unsigned long long V = 0, PAIRS = 0, LEAFV = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    V += red[0][w];
+    PAIRS += red[1][w];
+    LEAFV += red[2][w];
+  }
+  // workgroup items when the (node, lane) queues are long (few nodes, high
+  // atomic contention), wave items otherwise
+  const bool block_mode = V >= (unsigned long long)BLOCK_MODE_RAYS_PER_PAIR * (PAIRS ? PAIRS : 1ull);
+  const uint32_t itile = block_mode ? TILE : WTILE;
+
+  // pass 2: items and child capacities, block exclusive scan of 16 values
   for (int chunk = 0; chunk < L.nl; chunk += 1024) {
     const int k = chunk + tid;
     const bool act = k < L.nl;
     const int node = L.first + k;
     int nch = 0;
     int child[4] = {-1, -1, -1, -1};
-    const bool leaf = act && A.nodes[node].prim_count > 0;
-    if (act && !leaf) {
+    if (act && A.nodes[node].prim_count == 0) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         child[c] = A.nodes[node].child[c];
         nch += child[c] >= 0;
       }
     }
-    uint32_t v[16], cnt8[NLANE];
+    uint32_t vv[16], cnt8[NLANE];
 #pragma unroll
     for (int s = 0; s < NLANE; ++s) {
-      uint32_t c = act ? A.cnt[cnt_idx(node, s)] : 0u;
+      const uint32_t c = act ? L.icnt_w[s * row + k] : 0u;
       cnt8[s] = c;
-      myv += c;
-      if (leaf) myleaf += c;
-      v[s] = (c + itile - 1) / itile;        // items
-      v[8 + s] = c * (uint32_t)nch;           // child capacity
+      vv[s] = (c + itile - 1) / itile;  // items
+      vv[8 + s] = c * (uint32_t)nch;    // child capacity
     }
-    // block exclusive scan of 16 values per thread
     uint32_t incl[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      uint32_t x = v[q];
+      uint32_t x = vv[q];
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
-        uint32_t y = __shfl_up(x, off, 64);
+        const uint32_t y = __shfl_up(x, off, 64);
         if (ln >= off) x += y;
       }
       incl[q] = x;
@@ -536,7 +550,7 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
     if (tid < 16) {
       uint32_t acc = 0;
       for (int w = 0; w < 16; ++w) {
-        uint32_t t = wsum[w][tid];
+        const uint32_t t = wsum[w][tid];
         wsum[w][tid] = acc;
         acc += t;
       }
@@ -545,10 +559,10 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
     __syncthreads();
     uint32_t ex[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) ex[q] = run[q] + wsum[wave][q] + incl[q] - v[q];
+    for (int q = 0; q < 16; ++q) ex[q] = run[q] + wsum[wave][q] + incl[q] - vv[q];
     if (act) {
 #pragma unroll
-      for (int s = 0; s < NLANE; ++s) L.iprefix_w[(size_t)s * (L.maxln + 1) + k] = ex[s];
+      for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + k] = ex[s];
       uint32_t jj = 0;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -565,58 +579,28 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
     if (tid < 16) run[tid] += ctot[tid];
     __syncthreads();
   }
-  // sentinel ep[nl] and item count
-  myv = wave_sum64(myv);
-  myleaf = wave_sum64(myleaf);
-  if (ln == 0) {
-    atomicAdd(&vsum, myv);
-    atomicAdd(&lsum, myleaf);
-  }
-  __syncthreads();
   if (tid == 0) {
-    uint32_t mx = 0;
     bool ovf = false;
+    unsigned long long items = 0, need = 0;
     for (int s = 0; s < NLANE; ++s) {
-      L.iprefix_w[(size_t)s * (L.maxln + 1) + L.nl] = run[s];
-      mx = max(mx, run[s]);
       if (run[8 + s] > lanecap) ovf = true;
+      items += run[s];
+      need = max(need, (unsigned long long)run[8 + s]);
     }
-    if (ovf) {
-      *err |= 1u;
-      mx = 0;  // abandon the rest of this pass; the host reports PT_E_OVERFLOW
-    }
-    *L.nitems_w = mx * NLANE;
-    if (stats) {
-      stats[STAT_V] += vsum;
+    // sentinels ep[nl] = items per lane; an overflowing level runs no items
+    // (the rest of the pass is abandoned and the host reports PT_E_OVERFLOW)
+    for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + L.nl] = ovf ? 0u : run[s];
+    *L.mode_w = block_mode ? MODE_BLOCK : MODE_WAVE;
+    if (ovf) atomicOr(err, 1u);
+    if (stats) {  // fire-and-forget atomics: no round trip on the critical path
+      atomicAdd(stats + STAT_V, V);
       if (level < 16) {
-        stats[STAT_LV0 + level] += vsum;
-        stats[STAT_LEAF0 + level] += lsum;
-        unsigned long long it = 0;
-        for (int s = 0; s < NLANE; ++s) it += run[s];
-        stats[STAT_ITEMS0 + level] += it;
+        atomicAdd(stats + STAT_LV0 + level, V);
+        atomicAdd(stats + STAT_LEAF0 + level, LEAFV);
+        atomicAdd(stats + STAT_ITEMS0 + level, items);
       }
-      unsigned long long need = 0;
-      for (int s = 0; s < NLANE; ++s) need = max(need, (unsigned long long)run[8 + s]);
-      if (need * NLANE > stats[STAT_PEAKQ]) stats[STAT_PEAKQ] = need * NLANE;
+      atomicMax(stats + STAT_PEAKQ, need * NLANE);
     }
-  }
-}
-
-// R of the roofline formula: sum of the root pass's per-item valid counts.
-__global__ __launch_bounds__(1024) void k_sum_root(const uint32_t* __restrict__ rootcnt, int n,
-                                                   unsigned long long* stats) {
-  __shared__ unsigned long long part[16];
-  unsigned long long s = 0;
-  for (int i = threadIdx.x; i < n; i += 1024) s += rootcnt[i];
-  s = wave_sum64(s);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long t = 0;
-    for (int w = 0; w < 16; ++w) t += part[w];
-    stats[STAT_R] += t;
-    stats[STAT_V] += t;
-    stats[STAT_LV0] += t;
   }
 }
 

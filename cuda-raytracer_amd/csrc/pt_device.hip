@@ -14,6 +14,7 @@
 // Ray slots: [0, N) extension rays, [N, 2N) shadow rays of the same paths, so a
 // pass traces both at once (the reference traces them in separate passes,
 // cu:2499-2533).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -66,7 +67,8 @@ struct pt_ctx {
   uint32_t* d_qoff = nullptr;
   uint32_t* d_iprefix = nullptr;
   uint32_t* d_nitems = nullptr;  // one per level
-  uint32_t* d_rootcnt = nullptr;
+  uint32_t* d_icnt = nullptr;
+  unsigned long long* d_rcount = nullptr;  // valid root rays, one 128-B line per lane
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
 
@@ -86,22 +88,31 @@ struct pt_ctx {
     int cls, level;
     size_t e0, e1;
   };
+  template <typename K, typename... Args>
+  void launch(int cls, int level, K kernel, dim3 grid, dim3 block, Args... args) {
+    if (timing) {
+      auto e = pair(cls, level);
+      hipExtLaunchKernelGGL(kernel, grid, block, 0, stream, e.first, e.second, 0, args...);
+    } else {
+      hipLaunchKernelGGL(kernel, grid, block, 0, stream, args...);
+    }
+  }
   bool timing = false;
   std::vector<hipEvent_t> evpool;
   size_t evn = 0;
   std::vector<Mark> marks;
-  size_t begin(void) {
-    if (evn == evpool.size()) {
+  // two pool events for one kernel launch; they are handed to
+  // hipExtLaunchKernelGGL, which timestamps the dispatch packet itself (no
+  // extra barrier packets in the stream)
+  std::pair<hipEvent_t, hipEvent_t> pair(int cls, int level) {
+    while (evn + 2 > evpool.size()) {
       hipEvent_t e;
       hipEventCreate(&e);
       evpool.push_back(e);
     }
-    hipEventRecord(evpool[evn], stream);
-    return evn++;
-  }
-  void mark(int cls, int level, size_t e0) {
-    size_t e1 = begin();
-    marks.push_back(Mark{cls, level, e0, e1});
+    marks.push_back(Mark{cls, level, evn, evn + 1});
+    evn += 2;
+    return {evpool[evn - 2], evpool[evn - 1]};
   }
 };
 
@@ -133,7 +144,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ro,     c->d_rd,
                   c->d_hit,   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_q,      c->d_cnt,
-                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_rootcnt, c->d_stats,  c->d_err,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err,
                   c->d_pix_of, c->d_accum};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -160,7 +171,6 @@ static int ensure_paths(pt_ctx* c, uint32_t N) {
   c->qcap = std::max(QFACTOR * slots, 2 * root_need);
   c->qcap = (c->qcap + NLANE * 64 - 1) / (NLANE * 64) * (NLANE * 64);
   if ((rc = dalloc(c, &c->d_q, 2 * c->qcap))) return rc;
-  if ((rc = dalloc(c, &c->d_rootcnt, (slots + TILE - 1) / TILE))) return rc;
   c->cap_paths = N;
   return PT_OK;
 }
@@ -205,13 +215,10 @@ static TraceArgs trace_args(pt_ctx* c) {
 static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
   if (r1 <= r0) return PT_OK;
   TraceArgs A = trace_args(c);
-  const bool timed = c->timing;
   const uint32_t items = (r1 - r0 + TILE - 1) / TILE;
-  HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)c->n_nodes * NLANE * CSTRIDE * 4, c->stream));
-  size_t e0 = timed ? c->begin() : 0;
-  hipLaunchKernelGGL(k_trace_root, dim3(items), dim3(TPB), 0, c->stream, A, r0, r1, c->d_rootcnt);
-  hipLaunchKernelGGL(k_sum_root, dim3(1), dim3(1024), 0, c->stream, c->d_rootcnt, (int)items, c->d_stats);
-  if (timed) c->mark(pt_ctx::K_ROOT, 0, e0);
+  // the (node, lane) counters are zero here: each level's scan re-zeroes them
+  // after taking its snapshot (pt_load_scene zeroes them once)
+  c->launch(pt_ctx::K_ROOT, 0, k_trace_root, dim3(items), dim3(TPB), A, r0, r1, c->d_rcount);
   const size_t lanecap = c->qcap / NLANE;
   for (int l = 1; l < c->n_levels; ++l) {
     LevelArgs L;
@@ -220,20 +227,16 @@ static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
     L.maxln = c->max_level_nodes;
     L.iprefix = c->d_iprefix;
     L.iprefix_w = c->d_iprefix;
+    L.icnt = c->d_icnt;
+    L.icnt_w = c->d_icnt;
     L.nitems = c->d_nitems + l;
     L.nitems_w = c->d_nitems + l;
     L.mode = c->d_nitems + c->n_levels + l;
     L.mode_w = c->d_nitems + c->n_levels + l;
     const uint32_t out_base = (uint32_t)(((l + 1) & 1) ? c->qcap : 0);
-    if (timed) e0 = c->begin();
-    hipLaunchKernelGGL(k_scan_level, dim3(1), dim3(1024), 0, c->stream, A, L, (uint32_t)lanecap, out_base,
-                       c->d_stats, l, c->d_err);
-    if (timed) {
-      c->mark(pt_ctx::K_SCAN, l, e0);
-      e0 = c->begin();
-    }
-    hipLaunchKernelGGL(k_trace_level, dim3(LEVEL_GRID), dim3(TPB), 0, c->stream, A, L);
-    if (timed) c->mark(pt_ctx::K_LEVEL, l, e0);
+    c->launch(pt_ctx::K_SCAN, l, k_scan_level, dim3(1), dim3(1024), A, L, (uint32_t)lanecap, out_base,
+              c->d_stats, l, c->d_err);
+    c->launch(pt_ctx::K_LEVEL, l, k_trace_level, dim3(LEVEL_GRID), dim3(TPB), A, L);
   }
   HIPCHK(c, hipGetLastError());
   c->stats.passes++;
@@ -274,11 +277,16 @@ static void collect_marks(pt_ctx* c) {
 static int read_device_stats(pt_ctx* c) {
   unsigned long long st[STAT_COUNT];
   uint32_t e = 0;
+  unsigned long long rl[NLANE * 16];
   HIPCHK(c, hipMemcpyAsync(st, c->d_stats, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(rl, c->d_rcount, sizeof(rl), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->stats.rays = st[STAT_R];
-  c->stats.visits = st[STAT_V];
+  unsigned long long R = 0;
+  for (int s = 0; s < NLANE; ++s) R += rl[s * 16];
+  c->stats.rays = R;
+  c->stats.visits = st[STAT_V] + R;
+  st[STAT_LV0] += R;
   c->stats.peak_queue_entries = st[STAT_PEAKQ];
   for (int l = 0; l < 16; ++l) {
     c->stats.level_visits[l] = st[STAT_LV0 + l];
@@ -328,11 +336,13 @@ int pt_create(pt_ctx** out, int device) {
   }
   for (auto& e : c->ev) hipEventCreate(&e);
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
+      hipMalloc((void**)&c->d_rcount, NLANE * 16 * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_err, 4) != hipSuccess) {
     delete c;
     return PT_E_HIP;
   }
   hipMemset(c->d_stats, 0, STAT_COUNT * 8);
+  hipMemset(c->d_rcount, 0, NLANE * 16 * 8);
   hipMemset(c->d_err, 0, 4);
   *out = c;
   return PT_OK;
@@ -385,6 +395,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   if ((rc = dalloc(c, &c->d_cnt, (size_t)s->n_nodes * NLANE * CSTRIDE))) return rc;
   if ((rc = dalloc(c, &c->d_qoff, (size_t)s->n_nodes * NLANE))) return rc;
   if ((rc = dalloc(c, &c->d_iprefix, (size_t)NLANE * (c->max_level_nodes + 1)))) return rc;
+  if ((rc = dalloc(c, &c->d_icnt, (size_t)NLANE * (c->max_level_nodes + 1)))) return rc;
   if ((rc = dalloc(c, &c->d_nitems, 2 * std::max(1, s->n_levels)))) return rc;
   HIPCHK(c, hipMemcpy(c->d_nodes, s->nodes, sizeof(pt_node) * s->n_nodes, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_prims, s->prims, sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));
@@ -420,6 +431,7 @@ int pt_reset_stats(pt_ctx* c) {
   if (!c) return PT_E_INVALID;
   hipSetDevice(c->device);
   HIPCHK(c, hipMemset(c->d_stats, 0, STAT_COUNT * 8));
+  HIPCHK(c, hipMemset(c->d_rcount, 0, NLANE * 16 * 8));
   memset(&c->stats, 0, sizeof(c->stats));
   return PT_OK;
 }
@@ -476,6 +488,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
   c->timing = (P->flags & PT_FLAG_STATS) != 0;
   const bool timed = c->timing;
+  (void)timed;
   c->stats.batch_paths = (int32_t)Nmax;
 
   ShadeArgs S;
@@ -506,23 +519,17 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.N = N;
     S.sample_base = (uint32_t)(P->sample_offset + done);
     const dim3 grid((N + TPB - 1) / TPB);
-    size_t e0 = timed ? c->begin() : 0;
-    hipLaunchKernelGGL(k_camera, grid, dim3(TPB), 0, c->stream, S);
-    if (timed) c->mark(pt_ctx::K_CAM, 0, e0);
+    c->launch(pt_ctx::K_CAM, 0, k_camera, grid, dim3(TPB), S);
     const int passes = P->max_bounces + 2;
     for (int pass = 0; pass < passes; ++pass) {
       // pass 0: camera rays only; last pass: shadow rays only
       const uint32_t r0 = (pass == passes - 1) ? N : 0;
       const uint32_t r1 = (pass == 0) ? N : 2 * N;
       if ((rc = trace_pass(c, r0, r1))) return rc;
-      if (timed) e0 = c->begin();
-      hipLaunchKernelGGL(k_shade, grid, dim3(TPB), 0, c->stream, S);
-      if (timed) c->mark(pt_ctx::K_SHADE, 0, e0);
+      c->launch(pt_ctx::K_SHADE, 0, k_shade, grid, dim3(TPB), S);
     }
-    if (timed) e0 = c->begin();
-    hipLaunchKernelGGL(k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), 0, c->stream, c->d_ps1, c->d_accum,
-                       npix, sb);
-    if (timed) c->mark(pt_ctx::K_ACCUM, 0, e0);
+    c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_ps1,
+              c->d_accum, npix, sb);
     HIPCHK(c, hipGetLastError());
     done += (int)sb;
     c->stats.batches++;
