@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--seed", type=int, default=15618)
+    p.add_argument("--stats-in-timed", action="store_true",
+                   help="record per-kernel HIP events inside the timed steps (default: one extra instrumented frame)")
     return p.parse_args()
 
 
@@ -113,13 +115,21 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        frame(True)
+        frame(args.stats_in_timed)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    rays = ctx.stats().rays  # device counters, no instrumentation needed
+    if not args.stats_in_timed:
+        # per-kernel times of one more, instrumented frame (HIP events attached
+        # to each dispatch packet); the headline above ran without them
+        ctx.reset_stats()
+        t1 = time.perf_counter()
+        frame(True)
+        torch.cuda.synchronize()
+        instrumented_ms = (time.perf_counter() - t1) * 1e3
     st = ctx.stats()
-    rays = st.rays
     lvl_ms = sum(st.ms_level[l] for l in range(1, 16))
     V = [st.level_visits[l] for l in range(16)]
     lvl_bytes = sum(32 * V[l] for l in range(1, 16)) + sum(4 * V[l] for l in range(2, 16))
@@ -161,6 +171,7 @@ def main():
                          "avg_launch_us": round(lvl_ms * 1e3 / max(1, launches), 2),
                          "bytes_per_launch": int(lvl_bytes / max(1, launches))},
             "trace": {"visits_per_ray": round(st.visits / max(1, st.rays), 2),
+                      "instrumented_frame_ms": None if args.stats_in_timed else round(instrumented_ms, 2),
                       "ms_trace": round(st.ms_trace, 1), "ms_shade": round(st.ms_shade, 1),
                       "ms_root": round(st.ms_root, 1), "ms_scan": round(st.ms_scan, 1),
                       "ms_levels": round(lvl_ms, 1),

@@ -58,6 +58,11 @@ struct LevelArgs {
   uint32_t* iprefix_w;      // same array (written by the scan)
   const uint32_t* icnt;     // [lane][maxln+1] ray count snapshot of the level (read)
   uint32_t* icnt_w;
+  const uint4* items;       // [lane][itemcap] {node, queue base, rays}
+  uint4* items_w;
+  uint32_t itemcap;
+  const uint32_t* itemcount;  // [lane] items of the level
+  uint32_t* itemcount_w;
   const uint32_t* nitems;   // items of the level (read)
   uint32_t* nitems_w;
   const uint32_t* mode;  // MODE_WAVE / MODE_BLOCK, chosen by the scan

@@ -145,6 +145,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 #pragma unroll
   for (int j = 0; j < RPT; ++j) nvalid += valid[j] ? 1u : 0u;
 
+  const int nj = (n + TPB - 1) / TPB;  // ray groups with at least one valid thread (uniform)
   const int pcount = nd->prim_count;
   if (pcount > 0) {
     // ---------------- leaf: all primitives against every ray -----------------
@@ -163,6 +164,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
       if ((meta >> 28) == PT_PRIM_SPHERE) {
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {
+          if (j >= nj) break;
           float t = sphere_test(o[j], d[j], q0, q1);
           if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
             bt[j] = t;
@@ -173,6 +175,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
         const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {
+          if (j >= nj) break;
           float t = tri_test(o[j], d[j], q0, q1, q2, q3, q4, q5, bt[j]);
           if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
             bt[j] = t;
@@ -199,6 +202,8 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
   uint32_t bits[RPT];
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
+    bits[j] = 0;
+    if (j >= nj) continue;
     // |d| components below 1e-20 are clamped so 1/d stays finite: the FMA slab
     // form t = b*inv - o*inv would turn an axis-parallel ray (inv = inf) lying
     // inside a slab into inf - inf = NaN and wrongly miss the box
@@ -301,6 +306,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     tmax[j] = a.w;
     d[j] = mk(b.x, b.y, b.z);
   }
+  const int nj = (n + 63) >> 6;  // ray groups with at least one valid lane (uniform)
   const int pcount = nd->prim_count;
   if (pcount > 0) {
     const int pstart = nd->prim_start;
@@ -318,6 +324,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
       if ((meta >> 28) == PT_PRIM_SPHERE) {
 #pragma unroll
         for (int j = 0; j < RPTW; ++j) {
+          if (j >= nj) break;
           float t = sphere_test(o[j], d[j], q0, q1);
           if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
             bt[j] = t;
@@ -328,6 +335,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
         const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
 #pragma unroll
         for (int j = 0; j < RPTW; ++j) {
+          if (j >= nj) break;
           float t = tri_test(o[j], d[j], q0, q1, q2, q3, q4, q5, bt[j]);
           if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
             bt[j] = t;
@@ -350,6 +358,8 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
   uint32_t bits[RPTW];
 #pragma unroll
   for (int j = 0; j < RPTW; ++j) {
+    bits[j] = 0;
+    if (j >= nj) continue;
     f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
                 __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
     f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
@@ -391,42 +401,16 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 // observed round-robin placement: a speed hint only).
 __global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
   const int lane = blockIdx.x & (NLANE - 1);
-  const uint32_t lid = lane_id();
   const uint32_t wave = threadIdx.x >> 6;
-  const uint32_t* __restrict__ ep = L.iprefix + (size_t)lane * (L.maxln + 1);
-  const uint32_t M = ep[L.nl];  // items of this lane
+  const uint32_t M = L.itemcount[lane];  // items of this lane (written by the scan)
+  const uint4* __restrict__ items = L.items + (size_t)lane * L.itemcap;
   if (*L.mode == MODE_BLOCK) {
     // few nodes with many rays: 1024-ray items, one atomic per workgroup per child
     __shared__ uint32_t sh[64];
-    __shared__ int s_node;
-    __shared__ uint32_t s_base;
-    __shared__ int s_n;
     for (uint32_t m = blockIdx.x / NLANE; m < M; m += gridDim.x / NLANE) {
-      if (wave == 0) {
-        int lo = 0, hi = L.nl;
-        while (hi - lo > 1) {
-          const int step = (hi - lo + 63) >> 6;
-          const int idx = lo + (int)lid * step;
-          const bool le = idx < hi && ep[idx] <= m;
-          const unsigned long long msk = __ballot(le);
-          lo = lo + (63 - __clzll(msk)) * step;
-          hi = min(lo + step, hi);
-        }
-        if (lid == 0) {
-          const int node = L.first + lo;
-          const uint32_t i = m - ep[lo];
-          const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
-          s_node = node;
-          s_base = A.qoff[(size_t)node * NLANE + lane] + i * TILE;
-          s_n = (int)min((uint32_t)TILE, c - i * TILE);
-        }
-      }
-      __syncthreads();
-      const int node = __builtin_amdgcn_readfirstlane(s_node);
-      const uint32_t base = __builtin_amdgcn_readfirstlane(s_base);
-      const int n = __builtin_amdgcn_readfirstlane(s_n);
-      __syncthreads();
-      process_item<false>(A, node, base, n, lane, sh);
+      const uint4 it = items[m];  // {node, queue base, rays}: uniform
+      process_item<false>(A, __builtin_amdgcn_readfirstlane((int)it.x), __builtin_amdgcn_readfirstlane(it.y),
+                          __builtin_amdgcn_readfirstlane((int)it.z), lane, sh);
       __syncthreads();
     }
     return;
@@ -434,23 +418,9 @@ __global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
   // many nodes with few rays each: every wave walks its own 256-ray items
   const uint32_t stride = (gridDim.x / NLANE) * (TPB / 64);
   for (uint32_t m = (blockIdx.x / NLANE) * (TPB / 64) + wave; m < M; m += stride) {
-    // 64-ary search for the node k with ep[k] <= m < ep[k+1]
-    int lo = 0, hi = L.nl;
-    while (hi - lo > 1) {
-      const int step = (hi - lo + 63) >> 6;
-      const int idx = lo + (int)lid * step;
-      const bool le = idx < hi && ep[idx] <= m;
-      const unsigned long long msk = __ballot(le);
-      lo = lo + (63 - __clzll(msk)) * step;
-      hi = min(lo + step, hi);
-    }
-    lo = __builtin_amdgcn_readfirstlane(lo);
-    const int node = L.first + lo;
-    const uint32_t i = m - ep[lo];
-    const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
-    const uint32_t base = A.qoff[(size_t)node * NLANE + lane] + i * WTILE;
-    const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
-    process_wave(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane);
+    const uint4 it = items[m];
+    process_wave(A, __builtin_amdgcn_readfirstlane((int)it.x), __builtin_amdgcn_readfirstlane(it.y),
+                 __builtin_amdgcn_readfirstlane((int)it.z), lane);
   }
 }
 
@@ -562,7 +532,15 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
     for (int q = 0; q < 16; ++q) ex[q] = run[q] + wsum[wave][q] + incl[q] - vv[q];
     if (act) {
 #pragma unroll
-      for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + k] = ex[s];
+      for (int s = 0; s < NLANE; ++s) {
+        // item records {node, queue base, rays} of this (node, lane)
+        if (ex[s] + vv[s] <= L.itemcap) {
+          uint4* it = L.items_w + (size_t)s * L.itemcap;
+          const uint32_t q0 = A.qoff[(size_t)node * NLANE + s];
+          for (uint32_t i = 0; i < vv[s]; ++i)
+            it[ex[s] + i] = make_uint4((uint32_t)node, q0 + i * itile, min(itile, cnt8[s] - i * itile), 0u);
+        }
+      }
       uint32_t jj = 0;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -583,13 +561,13 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
     bool ovf = false;
     unsigned long long items = 0, need = 0;
     for (int s = 0; s < NLANE; ++s) {
-      if (run[8 + s] > lanecap) ovf = true;
+      if (run[8 + s] > lanecap || run[s] > L.itemcap) ovf = true;
       items += run[s];
       need = max(need, (unsigned long long)run[8 + s]);
     }
-    // sentinels ep[nl] = items per lane; an overflowing level runs no items
-    // (the rest of the pass is abandoned and the host reports PT_E_OVERFLOW)
-    for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + L.nl] = ovf ? 0u : run[s];
+    // items per lane; an overflowing level runs no items (the rest of the
+    // pass is abandoned and the host reports PT_E_OVERFLOW)
+    for (int s = 0; s < NLANE; ++s) L.itemcount_w[s] = ovf ? 0u : run[s];
     *L.mode_w = block_mode ? MODE_BLOCK : MODE_WAVE;
     if (ovf) atomicOr(err, 1u);
     if (stats) {  // fire-and-forget atomics: no round trip on the critical path

@@ -68,6 +68,8 @@ struct pt_ctx {
   uint32_t* d_iprefix = nullptr;
   uint32_t* d_nitems = nullptr;  // one per level
   uint32_t* d_icnt = nullptr;
+  uint4* d_items = nullptr;  // per-lane item tables of the current level
+  uint32_t itemcap = 0;
   unsigned long long* d_rcount = nullptr;  // valid root rays, one 128-B line per lane
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
@@ -144,7 +146,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ro,     c->d_rd,
                   c->d_hit,   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_q,      c->d_cnt,
-                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_items, c->d_rcount, c->d_stats,  c->d_err,
                   c->d_pix_of, c->d_accum};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -171,6 +173,10 @@ static int ensure_paths(pt_ctx* c, uint32_t N) {
   c->qcap = std::max(QFACTOR * slots, 2 * root_need);
   c->qcap = (c->qcap + NLANE * 64 - 1) / (NLANE * 64) * (NLANE * 64);
   if ((rc = dalloc(c, &c->d_q, 2 * c->qcap))) return rc;
+  // items of one level and lane: at most (lane capacity / wave item) + one
+  // partial item per node
+  c->itemcap = (uint32_t)(c->qcap / NLANE / WTILE + c->max_level_nodes + 64);
+  if ((rc = dalloc(c, &c->d_items, (size_t)NLANE * c->itemcap))) return rc;
   c->cap_paths = N;
   return PT_OK;
 }
@@ -229,6 +235,11 @@ static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
     L.iprefix_w = c->d_iprefix;
     L.icnt = c->d_icnt;
     L.icnt_w = c->d_icnt;
+    L.items = c->d_items;
+    L.items_w = c->d_items;
+    L.itemcap = c->itemcap;
+    L.itemcount = c->d_nitems + 2 * c->n_levels;
+    L.itemcount_w = c->d_nitems + 2 * c->n_levels;
     L.nitems = c->d_nitems + l;
     L.nitems_w = c->d_nitems + l;
     L.mode = c->d_nitems + c->n_levels + l;
@@ -396,7 +407,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   if ((rc = dalloc(c, &c->d_qoff, (size_t)s->n_nodes * NLANE))) return rc;
   if ((rc = dalloc(c, &c->d_iprefix, (size_t)NLANE * (c->max_level_nodes + 1)))) return rc;
   if ((rc = dalloc(c, &c->d_icnt, (size_t)NLANE * (c->max_level_nodes + 1)))) return rc;
-  if ((rc = dalloc(c, &c->d_nitems, 2 * std::max(1, s->n_levels)))) return rc;
+  if ((rc = dalloc(c, &c->d_nitems, 2 * std::max(1, s->n_levels) + NLANE))) return rc;
   HIPCHK(c, hipMemcpy(c->d_nodes, s->nodes, sizeof(pt_node) * s->n_nodes, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_prims, s->prims, sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_shading, s->shading, sizeof(pt_prim_shading) * s->n_prims, hipMemcpyHostToDevice));
