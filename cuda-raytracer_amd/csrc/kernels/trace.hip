@@ -401,16 +401,42 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 // observed round-robin placement: a speed hint only).
 __global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
   const int lane = blockIdx.x & (NLANE - 1);
+  const uint32_t lid = lane_id();
   const uint32_t wave = threadIdx.x >> 6;
-  const uint32_t M = L.itemcount[lane];  // items of this lane (written by the scan)
-  const uint4* __restrict__ items = L.items + (size_t)lane * L.itemcap;
+  const uint32_t* __restrict__ ep = L.iprefix + (size_t)lane * (L.maxln + 1);
+  const uint32_t M = ep[L.nl];  // items of this lane
   if (*L.mode == MODE_BLOCK) {
     // few nodes with many rays: 1024-ray items, one atomic per workgroup per child
     __shared__ uint32_t sh[64];
+    __shared__ int s_node;
+    __shared__ uint32_t s_base;
+    __shared__ int s_n;
     for (uint32_t m = blockIdx.x / NLANE; m < M; m += gridDim.x / NLANE) {
-      const uint4 it = items[m];  // {node, queue base, rays}: uniform
-      process_item<false>(A, __builtin_amdgcn_readfirstlane((int)it.x), __builtin_amdgcn_readfirstlane(it.y),
-                          __builtin_amdgcn_readfirstlane((int)it.z), lane, sh);
+      if (wave == 0) {
+        int lo = 0, hi = L.nl;
+        while (hi - lo > 1) {
+          const int step = (hi - lo + 63) >> 6;
+          const int idx = lo + (int)lid * step;
+          const bool le = idx < hi && ep[idx] <= m;
+          const unsigned long long msk = __ballot(le);
+          lo = lo + (63 - __clzll(msk)) * step;
+          hi = min(lo + step, hi);
+        }
+        if (lid == 0) {
+          const int node = L.first + lo;
+          const uint32_t i = m - ep[lo];
+          const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
+          s_node = node;
+          s_base = A.qoff[(size_t)node * NLANE + lane] + i * TILE;
+          s_n = (int)min((uint32_t)TILE, c - i * TILE);
+        }
+      }
+      __syncthreads();
+      const int node = __builtin_amdgcn_readfirstlane(s_node);
+      const uint32_t base = __builtin_amdgcn_readfirstlane(s_base);
+      const int n = __builtin_amdgcn_readfirstlane(s_n);
+      __syncthreads();
+      process_item<false>(A, node, base, n, lane, sh);
       __syncthreads();
     }
     return;
@@ -418,9 +444,23 @@ __global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
   // many nodes with few rays each: every wave walks its own 256-ray items
   const uint32_t stride = (gridDim.x / NLANE) * (TPB / 64);
   for (uint32_t m = (blockIdx.x / NLANE) * (TPB / 64) + wave; m < M; m += stride) {
-    const uint4 it = items[m];
-    process_wave(A, __builtin_amdgcn_readfirstlane((int)it.x), __builtin_amdgcn_readfirstlane(it.y),
-                 __builtin_amdgcn_readfirstlane((int)it.z), lane);
+    // 64-ary search for the node k with ep[k] <= m < ep[k+1]
+    int lo = 0, hi = L.nl;
+    while (hi - lo > 1) {
+      const int step = (hi - lo + 63) >> 6;
+      const int idx = lo + (int)lid * step;
+      const bool le = idx < hi && ep[idx] <= m;
+      const unsigned long long msk = __ballot(le);
+      lo = lo + (63 - __clzll(msk)) * step;
+      hi = min(lo + step, hi);
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    const int node = L.first + lo;
+    const uint32_t i = m - ep[lo];
+    const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
+    const uint32_t base = A.qoff[(size_t)node * NLANE + lane] + i * WTILE;
+    const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
+    process_wave(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane);
   }
 }
 
@@ -532,15 +572,7 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
     for (int q = 0; q < 16; ++q) ex[q] = run[q] + wsum[wave][q] + incl[q] - vv[q];
     if (act) {
 #pragma unroll
-      for (int s = 0; s < NLANE; ++s) {
-        // item records {node, queue base, rays} of this (node, lane)
-        if (ex[s] + vv[s] <= L.itemcap) {
-          uint4* it = L.items_w + (size_t)s * L.itemcap;
-          const uint32_t q0 = A.qoff[(size_t)node * NLANE + s];
-          for (uint32_t i = 0; i < vv[s]; ++i)
-            it[ex[s] + i] = make_uint4((uint32_t)node, q0 + i * itile, min(itile, cnt8[s] - i * itile), 0u);
-        }
-      }
+      for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + k] = ex[s];
       uint32_t jj = 0;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -561,13 +593,13 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
     bool ovf = false;
     unsigned long long items = 0, need = 0;
     for (int s = 0; s < NLANE; ++s) {
-      if (run[8 + s] > lanecap || run[s] > L.itemcap) ovf = true;
+      if (run[8 + s] > lanecap) ovf = true;
       items += run[s];
       need = max(need, (unsigned long long)run[8 + s]);
     }
-    // items per lane; an overflowing level runs no items (the rest of the
-    // pass is abandoned and the host reports PT_E_OVERFLOW)
-    for (int s = 0; s < NLANE; ++s) L.itemcount_w[s] = ovf ? 0u : run[s];
+    // sentinels ep[nl] = items per lane; an overflowing level runs no items
+    // (the rest of the pass is abandoned and the host reports PT_E_OVERFLOW)
+    for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + L.nl] = ovf ? 0u : run[s];
     *L.mode_w = block_mode ? MODE_BLOCK : MODE_WAVE;
     if (ovf) atomicOr(err, 1u);
     if (stats) {  // fire-and-forget atomics: no round trip on the critical path
