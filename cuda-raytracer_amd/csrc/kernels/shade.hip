@@ -65,10 +65,10 @@ __global__ __launch_bounds__(TPB) void k_camera(ShadeArgs S) {
   const f3 L = ld3(S.cam.left), U = ld3(S.cam.up), K = ld3(S.cam.look_at);
   f3 dir = mk(kx * L.x + ky * U.x + kz * K.x, kx * L.y + ky * U.y + kz * K.y, kx * L.z + ky * U.z + kz * K.z);
   dir = normalize(dir);
-  S.ro[p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], __builtin_inff());
-  S.rd[p] = make_float4(dir.x, dir.y, dir.z, 0.0f);
+  S.ro[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], __builtin_inff());
+  S.rd[RSTRIDE * p] = make_float4(dir.x, dir.y, dir.z, 0.0f);
   S.hit[p] = PT_HIT_NONE;
-  S.ro[S.N + p] = make_float4(0.f, 0.f, 0.f, -1.0f);
+  S.ro[RSTRIDE * (S.N + p)] = make_float4(0.f, 0.f, 0.f, -1.0f);
   S.hit[S.N + p] = PT_HIT_NONE;
   S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
   S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
@@ -103,8 +103,8 @@ __global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
     if (h != PT_HIT_NONE) {
       const float t = __uint_as_float((uint32_t)(h >> 32));
       const uint32_t prim = (uint32_t)h;
-      const f3 o = xyz(S.ro[p]);
-      const f3 d = xyz(S.rd[p]);
+      const f3 o = xyz(S.ro[RSTRIDE * p]);
+      const f3 d = xyz(S.rd[RSTRIDE * p]);
       const f3 P = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
       const float4* Q = S.prims + (size_t)prim * 6;
       const float4 q0 = Q[0];
@@ -244,17 +244,17 @@ __global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
   S.ps1[p] = make_float4(L.x, L.y, L.z, __uint_as_float(g));
   if (new_sh) S.ps2[p] = make_float4(C.x, C.y, C.z, 0.0f);
   if (new_ext) {
-    S.ro[p] = make_float4(o_new.x, o_new.y, o_new.z, __builtin_inff());
-    S.rd[p] = make_float4(d_new.x, d_new.y, d_new.z, 0.0f);
+    S.ro[RSTRIDE * p] = make_float4(o_new.x, o_new.y, o_new.z, __builtin_inff());
+    S.rd[RSTRIDE * p] = make_float4(d_new.x, d_new.y, d_new.z, 0.0f);
   } else {
-    S.ro[p] = make_float4(0.f, 0.f, 0.f, -1.0f);
+    S.ro[RSTRIDE * p] = make_float4(0.f, 0.f, 0.f, -1.0f);
   }
   S.hit[p] = PT_HIT_NONE;
   if (new_sh) {
-    S.ro[S.N + p] = make_float4(sh_o.x, sh_o.y, sh_o.z, sh_tmax);
-    S.rd[S.N + p] = make_float4(sh_d.x, sh_d.y, sh_d.z, 0.0f);
+    S.ro[RSTRIDE * (S.N + p)] = make_float4(sh_o.x, sh_o.y, sh_o.z, sh_tmax);
+    S.rd[RSTRIDE * (S.N + p)] = make_float4(sh_d.x, sh_d.y, sh_d.z, 0.0f);
   } else {
-    S.ro[S.N + p] = make_float4(0.f, 0.f, 0.f, -1.0f);
+    S.ro[RSTRIDE * (S.N + p)] = make_float4(0.f, 0.f, 0.f, -1.0f);
   }
   S.hit[S.N + p] = PT_HIT_NONE;
 }
@@ -281,10 +281,10 @@ __global__ __launch_bounds__(TPB) void k_load_rays(const float4* __restrict__ in
                                                    unsigned long long* hit, uint32_t n) {
   const uint32_t i = blockIdx.x * TPB + threadIdx.x;
   if (i >= n) return;
-  ro[i] = in[2 * i];
+  ro[RSTRIDE * i] = in[2 * i];
   float4 b = in[2 * i + 1];
   b.w = 0.0f;
-  rd[i] = b;
+  rd[RSTRIDE * i] = b;
   hit[i] = PT_HIT_NONE;
 }
 

@@ -15,6 +15,9 @@ namespace pt {
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 f4(f4v v) { return make_float4(v.x, v.y, v.z, v.w); }
 
+// a ray record is 32 B: float4 {o.xyz, tmax} then float4 {d.xyz, 0}, so a
+// scattered gather of one ray touches one 64-B half line, not two lines
+constexpr int RSTRIDE = 2;        // float4 per ray record
 constexpr int TPB = 256;          // threads per workgroup (4 waves)
 constexpr int RPT = 4;            // rays per thread in a traversal item
 constexpr int TILE = TPB * RPT;   // rays per traversal item
@@ -24,6 +27,7 @@ constexpr int NLANE = 8;          // queue lanes (one per XCD)
 constexpr int CSTRIDE = 32;       // u32 per queue counter: each (node, lane) counter owns a 128-B line
 constexpr uint32_t MODE_WAVE = 0, MODE_BLOCK = 1;
 constexpr uint32_t BLOCK_MODE_RAYS_PER_PAIR = 512;  // level mode threshold (mean rays per queue lane)
+constexpr int LEAF_CHUNK = 32;    // primitives staged in LDS at a time (max leaf size)
 constexpr int LEVEL_GRID = 2048;  // workgroups of the per-level grid-stride kernel (8 per CU)
 
 // device statistics slots (unsigned long long)
@@ -40,8 +44,8 @@ enum {
 struct TraceArgs {
   const pt_node* __restrict__ nodes;
   const float4* __restrict__ prims;  // 6 float4 per primitive
-  float4* ro;                        // o.xyz, tmax (tmax < 0: empty slot)
-  const float4* __restrict__ rd;     // d.xyz, 0
+  float4* ro;                        // ray records (stride RSTRIDE): o.xyz, tmax (tmax < 0: empty slot)
+  const float4* __restrict__ rd;     // ro + 1: d.xyz, 0
   unsigned long long* hit;           // {t bits, prim} or PT_HIT_NONE
   uint32_t* cnt;                     // [node][lane] rays pushed into the node
   uint32_t* qoff;                    // [node][lane] absolute queue offset
@@ -58,11 +62,6 @@ struct LevelArgs {
   uint32_t* iprefix_w;      // same array (written by the scan)
   const uint32_t* icnt;     // [lane][maxln+1] ray count snapshot of the level (read)
   uint32_t* icnt_w;
-  const uint4* items;       // [lane][itemcap] {node, queue base, rays}
-  uint4* items_w;
-  uint32_t itemcap;
-  const uint32_t* itemcount;  // [lane] items of the level
-  uint32_t* itemcount_w;
   const uint32_t* nitems;   // items of the level (read)
   uint32_t* nitems_w;
   const uint32_t* mode;  // MODE_WAVE / MODE_BLOCK, chosen by the scan

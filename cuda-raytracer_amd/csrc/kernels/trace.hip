@@ -130,12 +130,12 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
     d[j] = mk(0.f, 0.f, 1.f);
     if (valid[j]) {
       id[j] = IMPLICIT ? base + (uint32_t)i : A.q[base + i];
-      float4 a = A.ro[id[j]];
+      float4 a = A.ro[RSTRIDE * id[j]];
       o[j] = mk(a.x, a.y, a.z);
       tmax[j] = a.w;
       if (IMPLICIT) valid[j] = a.w >= 0.0f;
       if (valid[j]) {
-        float4 b = A.rd[id[j]];
+        float4 b = A.rd[RSTRIDE * id[j]];
         d[j] = mk(b.x, b.y, b.z);
       }
     }
@@ -192,7 +192,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
         atomicMin(A.hit + id[j], key);
         // racy monotone-safe tmax update: any stored value is a real hit's t,
         // so culling boxes beyond it never loses the closest hit
-        if (bt[j] < tmax[j]) reinterpret_cast<float*>(A.ro + id[j])[3] = bt[j];
+        if (bt[j] < tmax[j]) reinterpret_cast<float*>(A.ro + RSTRIDE * id[j])[3] = bt[j];
       }
     }
     return nvalid;
@@ -282,7 +282,8 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, uint32_t r0, ui
 // Levels >= 1 are processed at wave granularity: no LDS, no workgroup barrier,
 // one returning atomic per wave per child.  Deep levels hold many nodes with a
 // few hundred rays each, where 1024-ray workgroup items would run mostly empty.
-__device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane) {
+__device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane,
+                                             float4* lbuf) {
   const uint32_t lid = lane_id();
   const CPTR(pt_node) nd = (const CPTR(pt_node))(A.nodes + node);
   uint32_t id[RPTW];
@@ -299,8 +300,8 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
   for (int j = 0; j < RPTW; ++j) {
     float4 a = make_float4(0.f, 0.f, 0.f, -1.f), b = make_float4(0.f, 0.f, 1.f, 0.f);
     if (valid[j]) {
-      a = A.ro[id[j]];
-      b = A.rd[id[j]];
+      a = A.ro[RSTRIDE * id[j]];
+      b = A.rd[RSTRIDE * id[j]];
     }
     o[j] = mk(a.x, a.y, a.z);
     tmax[j] = a.w;
@@ -317,6 +318,55 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
       bt[j] = tmax[j];
       bp[j] = -1;
     }
+#if defined(PT_LEAF_LDS)
+    // the leaf's records (<= 32 x 96 B) are staged in the wave's LDS slice with
+    // three coalesced vector loads, then read back as broadcasts
+    const float4* src = A.prims + (size_t)pstart * 6;
+    for (int k0 = 0; k0 < pcount; k0 += LEAF_CHUNK) {
+      const int ne = min(LEAF_CHUNK, pcount - k0) * 6;
+      float4 tmp[LEAF_CHUNK * 6 / 64];
+#pragma unroll
+      for (int r = 0; r < LEAF_CHUNK * 6 / 64; ++r) {
+        const int e = (int)lid + r * 64;
+        if (e < ne) tmp[r] = src[(size_t)k0 * 6 + e];
+      }
+#pragma unroll
+      for (int r = 0; r < LEAF_CHUNK * 6 / 64; ++r) {
+        const int e = (int)lid + r * 64;
+        if (e < ne) lbuf[e] = tmp[r];
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int kc = ne / 6;
+      for (int k = 0; k < kc; ++k) {
+        const float4* P = lbuf + k * 6;
+        const float4 q0 = P[0], q1 = P[1];
+        const uint32_t meta = __float_as_uint(q0.w);
+        if ((meta >> 28) == PT_PRIM_SPHERE) {
+#pragma unroll
+          for (int j = 0; j < RPTW; ++j) {
+            if (j >= nj) break;
+            float t = sphere_test(o[j], d[j], q0, q1);
+            if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
+              bt[j] = t;
+              bp[j] = pstart + k0 + k;
+            }
+          }
+        } else {
+          const float4 q2 = P[2], q3 = P[3], q4 = P[4], q5 = P[5];
+#pragma unroll
+          for (int j = 0; j < RPTW; ++j) {
+            if (j >= nj) break;
+            float t = tri_test(o[j], d[j], q0, q1, q2, q3, q4, q5, bt[j]);
+            if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
+              bt[j] = t;
+              bp[j] = pstart + k0 + k;
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+#else
     const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);
     for (int k = 0; k < pcount; ++k, P += 6) {
       const float4 q0 = f4(P[0]), q1 = f4(P[1]);
@@ -344,13 +394,14 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
         }
       }
     }
+#endif
 #pragma unroll
     for (int j = 0; j < RPTW; ++j) {
       if (valid[j] && bp[j] >= 0) {
         unsigned long long key =
             ((unsigned long long)__float_as_uint(bt[j]) << 32) | (unsigned long long)(uint32_t)bp[j];
         atomicMin(A.hit + id[j], key);
-        if (bt[j] < tmax[j]) reinterpret_cast<float*>(A.ro + id[j])[3] = bt[j];
+        if (bt[j] < tmax[j]) reinterpret_cast<float*>(A.ro + RSTRIDE * id[j])[3] = bt[j];
       }
     }
     return;
@@ -442,6 +493,7 @@ __global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
     return;
   }
   // many nodes with few rays each: every wave walks its own 256-ray items
+  __shared__ float4 leafbuf[TPB / 64][LEAF_CHUNK * 6];
   const uint32_t stride = (gridDim.x / NLANE) * (TPB / 64);
   for (uint32_t m = (blockIdx.x / NLANE) * (TPB / 64) + wave; m < M; m += stride) {
     // 64-ary search for the node k with ep[k] <= m < ep[k+1]
@@ -460,7 +512,8 @@ __global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
     const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
     const uint32_t base = A.qoff[(size_t)node * NLANE + lane] + i * WTILE;
     const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
-    process_wave(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane);
+    process_wave(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane,
+                 leafbuf[wave]);
   }
 }
 

@@ -58,7 +58,7 @@ struct pt_ctx {
 
   // wavefront buffers (sized for N paths = 2N ray slots)
   uint32_t cap_paths = 0;
-  float4 *d_ro = nullptr, *d_rd = nullptr;
+  float4 *d_ro = nullptr, *d_rd = nullptr;  // one array of 32-B ray records; d_rd = d_ro + 1
   unsigned long long* d_hit = nullptr;
   float4 *d_ps0 = nullptr, *d_ps1 = nullptr, *d_ps2 = nullptr;
   uint32_t* d_q = nullptr;
@@ -68,8 +68,6 @@ struct pt_ctx {
   uint32_t* d_iprefix = nullptr;
   uint32_t* d_nitems = nullptr;  // one per level
   uint32_t* d_icnt = nullptr;
-  uint4* d_items = nullptr;  // per-lane item tables of the current level
-  uint32_t itemcap = 0;
   unsigned long long* d_rcount = nullptr;  // valid root rays, one 128-B line per lane
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
@@ -144,9 +142,9 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 }
 
 static void free_all(pt_ctx* c) {
-  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ro,     c->d_rd,
+  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ro,
                   c->d_hit,   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_q,      c->d_cnt,
-                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_items, c->d_rcount, c->d_stats,  c->d_err,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err,
                   c->d_pix_of, c->d_accum};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -154,13 +152,18 @@ static void free_all(pt_ctx* c) {
 
 // Buffers for N paths (2N ray slots).  Queue halves hold QFACTOR * 2N ids.
 static constexpr size_t QFACTOR = 24;
+// Paths in flight per batch.  Large batches amortise the per-level launches
+// (deep levels hold few rays per pass); queue offsets are u32, so both parity
+// halves (2 x QFACTOR x 2N ids) must stay below 2^32.
+static constexpr uint32_t DEFAULT_BATCH_PATHS = 32u << 20;
+static constexpr uint32_t MAX_BATCH_PATHS = (uint32_t)((1ull << 32) / (2 * QFACTOR * 2)) & ~4095u;
 
 static int ensure_paths(pt_ctx* c, uint32_t N) {
   if (N <= c->cap_paths) return PT_OK;
   const size_t slots = 2 * (size_t)N;
   int rc;
-  if ((rc = dalloc(c, &c->d_ro, slots))) return rc;
-  if ((rc = dalloc(c, &c->d_rd, slots))) return rc;
+  if ((rc = dalloc(c, &c->d_ro, slots * RSTRIDE))) return rc;
+  c->d_rd = c->d_ro + 1;
   if ((rc = dalloc(c, &c->d_hit, slots))) return rc;
   if ((rc = dalloc(c, &c->d_ps0, N))) return rc;
   if ((rc = dalloc(c, &c->d_ps1, N))) return rc;
@@ -173,10 +176,6 @@ static int ensure_paths(pt_ctx* c, uint32_t N) {
   c->qcap = std::max(QFACTOR * slots, 2 * root_need);
   c->qcap = (c->qcap + NLANE * 64 - 1) / (NLANE * 64) * (NLANE * 64);
   if ((rc = dalloc(c, &c->d_q, 2 * c->qcap))) return rc;
-  // items of one level and lane: at most (lane capacity / wave item) + one
-  // partial item per node
-  c->itemcap = (uint32_t)(c->qcap / NLANE / WTILE + c->max_level_nodes + 64);
-  if ((rc = dalloc(c, &c->d_items, (size_t)NLANE * c->itemcap))) return rc;
   c->cap_paths = N;
   return PT_OK;
 }
@@ -235,11 +234,6 @@ static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
     L.iprefix_w = c->d_iprefix;
     L.icnt = c->d_icnt;
     L.icnt_w = c->d_icnt;
-    L.items = c->d_items;
-    L.items_w = c->d_items;
-    L.itemcap = c->itemcap;
-    L.itemcount = c->d_nitems + 2 * c->n_levels;
-    L.itemcount_w = c->d_nitems + 2 * c->n_levels;
     L.nitems = c->d_nitems + l;
     L.nitems_w = c->d_nitems + l;
     L.mode = c->d_nitems + c->n_levels + l;
@@ -489,10 +483,12 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     return PT_OK;
   }
   // batch: spp_b samples of every owned pixel
-  uint32_t target = P->batch_paths > 0 ? (uint32_t)P->batch_paths : (4u << 20);
+  uint32_t target = P->batch_paths > 0 ? (uint32_t)P->batch_paths : DEFAULT_BATCH_PATHS;
+  target = std::min<uint32_t>(target, MAX_BATCH_PATHS);
   uint32_t spp_b = std::max<uint32_t>(1, target / npix);
   spp_b = std::min<uint32_t>(spp_b, (uint32_t)P->spp);
   const uint32_t Nmax = npix * spp_b;
+  if ((size_t)npix > MAX_BATCH_PATHS) return fail(c, PT_E_UNSUPPORTED, "more owned pixels than one batch holds");
   const bool realloc = Nmax > c->cap_paths;
   if ((rc = ensure_paths(c, Nmax))) return rc;
   if (realloc && (rc = set_root_child_offsets(c))) return rc;
