@@ -24,9 +24,7 @@ constexpr float INV_PI = 0.318309886183790671f;
 constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
 
 struct ShadeArgs {
-  float4* ro;
-  float4* rd;
-  unsigned long long* hit;
+  float4* ray;  // ray records (trace.h): ext ray of path p in slot p, shadow ray in slot N + p
   float4* ps0;  // T.xyz, flags | vertex << 8
   float4* ps1;  // L.xyz, pixel
   float4* ps2;  // pending shadow contribution
@@ -65,11 +63,9 @@ __global__ __launch_bounds__(TPB) void k_camera(ShadeArgs S) {
   const f3 L = ld3(S.cam.left), U = ld3(S.cam.up), K = ld3(S.cam.look_at);
   f3 dir = mk(kx * L.x + ky * U.x + kz * K.x, kx * L.y + ky * U.y + kz * K.y, kx * L.z + ky * U.z + kz * K.z);
   dir = normalize(dir);
-  S.ro[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], __builtin_inff());
-  S.rd[RSTRIDE * p] = make_float4(dir.x, dir.y, dir.z, 0.0f);
-  S.hit[p] = PT_HIT_NONE;
-  S.ro[RSTRIDE * (S.N + p)] = make_float4(0.f, 0.f, 0.f, -1.0f);
-  S.hit[S.N + p] = PT_HIT_NONE;
+  S.ray[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], dir.x);
+  S.ray[RSTRIDE * p + 1] = rec_r1(dir.y, dir.z, __builtin_inff());
+  S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
   S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
   S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
   S.ps2[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -89,7 +85,7 @@ __global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
 
   // 1. resolve the shadow ray of the previous vertex
   if (flags & F_SHADOW) {
-    if (S.hit[S.N + p] == PT_HIT_NONE) L = L + xyz(S.ps2[p]);
+    if (__float_as_uint(S.ray[RSTRIDE * (S.N + p) + 1].z) == PT_PRIM_NONE) L = L + xyz(S.ps2[p]);
   }
   bool new_ext = false, new_sh = false;
   f3 o_new = mk(0, 0, 0), d_new = mk(0, 0, 1), sh_o = mk(0, 0, 0), sh_d = mk(0, 0, 1), C = mk(0, 0, 0);
@@ -99,12 +95,13 @@ __global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
 
   // 2. shade the hit of the extension ray
   if (flags & F_EXT) {
-    const unsigned long long h = S.hit[p];
-    if (h != PT_HIT_NONE) {
-      const float t = __uint_as_float((uint32_t)(h >> 32));
-      const uint32_t prim = (uint32_t)h;
-      const f3 o = xyz(S.ro[RSTRIDE * p]);
-      const f3 d = xyz(S.rd[RSTRIDE * p]);
+    const float4 r1 = S.ray[RSTRIDE * p + 1];
+    const uint32_t prim = __float_as_uint(r1.z);
+    if (prim != PT_PRIM_NONE) {
+      const float t = r1.w;
+      const float4 r0 = S.ray[RSTRIDE * p];
+      const f3 o = xyz(r0);
+      const f3 d = mk(r0.w, r1.x, r1.y);
       const f3 P = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
       const float4* Q = S.prims + (size_t)prim * 6;
       const float4 q0 = Q[0];
@@ -244,19 +241,17 @@ __global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
   S.ps1[p] = make_float4(L.x, L.y, L.z, __uint_as_float(g));
   if (new_sh) S.ps2[p] = make_float4(C.x, C.y, C.z, 0.0f);
   if (new_ext) {
-    S.ro[RSTRIDE * p] = make_float4(o_new.x, o_new.y, o_new.z, __builtin_inff());
-    S.rd[RSTRIDE * p] = make_float4(d_new.x, d_new.y, d_new.z, 0.0f);
+    S.ray[RSTRIDE * p] = make_float4(o_new.x, o_new.y, o_new.z, d_new.x);
+    S.ray[RSTRIDE * p + 1] = rec_r1(d_new.y, d_new.z, __builtin_inff());
   } else {
-    S.ro[RSTRIDE * p] = make_float4(0.f, 0.f, 0.f, -1.0f);
+    S.ray[RSTRIDE * p + 1] = rec_r1(0.f, 0.f, -1.0f);
   }
-  S.hit[p] = PT_HIT_NONE;
   if (new_sh) {
-    S.ro[RSTRIDE * (S.N + p)] = make_float4(sh_o.x, sh_o.y, sh_o.z, sh_tmax);
-    S.rd[RSTRIDE * (S.N + p)] = make_float4(sh_d.x, sh_d.y, sh_d.z, 0.0f);
+    S.ray[RSTRIDE * (S.N + p)] = make_float4(sh_o.x, sh_o.y, sh_o.z, sh_d.x);
+    S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(sh_d.y, sh_d.z, sh_tmax);
   } else {
-    S.ro[RSTRIDE * (S.N + p)] = make_float4(0.f, 0.f, 0.f, -1.0f);
+    S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
   }
-  S.hit[S.N + p] = PT_HIT_NONE;
 }
 
 // Sum each owned pixel's samples of this batch into the accumulation buffer,
@@ -276,16 +271,24 @@ __global__ __launch_bounds__(TPB) void k_accum(const float4* __restrict__ ps1, f
   accum[q] = a;
 }
 
-// Repack pt_intersect's 8-float ray records into the SoA slots.
-__global__ __launch_bounds__(TPB) void k_load_rays(const float4* __restrict__ in, float4* ro, float4* rd,
-                                                   unsigned long long* hit, uint32_t n) {
+// Repack pt_intersect's 8-float rays {o, tmax, d, 0} into ray records.
+__global__ __launch_bounds__(TPB) void k_load_rays(const float4* __restrict__ in, float4* ray, uint32_t n) {
   const uint32_t i = blockIdx.x * TPB + threadIdx.x;
   if (i >= n) return;
-  ro[RSTRIDE * i] = in[2 * i];
-  float4 b = in[2 * i + 1];
-  b.w = 0.0f;
-  rd[RSTRIDE * i] = b;
-  hit[i] = PT_HIT_NONE;
+  const float4 a = in[2 * i], b = in[2 * i + 1];
+  ray[RSTRIDE * i] = make_float4(a.x, a.y, a.z, b.x);
+  ray[RSTRIDE * i + 1] = rec_r1(b.y, b.z, a.w);
+}
+
+// Closest-hit keys of pt_intersect: {t bits, prim} or PT_HIT_NONE.
+__global__ __launch_bounds__(TPB) void k_store_hits(const float4* __restrict__ ray, unsigned long long* out,
+                                                    uint32_t n) {
+  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  const float4 r1 = ray[RSTRIDE * i + 1];
+  const uint32_t prim = __float_as_uint(r1.z);
+  out[i] = prim == PT_PRIM_NONE ? PT_HIT_NONE
+                                : (((unsigned long long)__float_as_uint(r1.w) << 32) | (unsigned long long)prim);
 }
 
 }  // namespace pt

@@ -15,9 +15,13 @@ namespace pt {
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 f4(f4v v) { return make_float4(v.x, v.y, v.z, v.w); }
 
-// a ray record is 32 B: float4 {o.xyz, tmax} then float4 {d.xyz, 0}, so a
-// scattered gather of one ray touches one 64-B half line, not two lines
+// A ray record is 32 B, two float4 (a scattered gather of one ray touches one
+// 64-B half line):  r0 = {o.x, o.y, o.z, d.x},  r1 = {d.y, d.z, prim, t}.
+// {prim (low dword), t bits (high dword)} is the 64-bit closest-hit key: it
+// starts as {PT_PRIM_NONE, tmax} (t < 0 marks an empty slot) and leaves lower
+// it with atomicMin, so t is also the ray's current tmax (inclusive).
 constexpr int RSTRIDE = 2;        // float4 per ray record
+constexpr uint32_t PT_PRIM_NONE = 0xFFFFFFFFu;
 constexpr int TPB = 256;          // threads per workgroup (4 waves)
 constexpr int RPT = 4;            // rays per thread in a traversal item
 constexpr int TILE = TPB * RPT;   // rays per traversal item
@@ -27,7 +31,6 @@ constexpr int NLANE = 8;          // queue lanes (one per XCD)
 constexpr int CSTRIDE = 32;       // u32 per queue counter: each (node, lane) counter owns a 128-B line
 constexpr uint32_t MODE_WAVE = 0, MODE_BLOCK = 1;
 constexpr uint32_t BLOCK_MODE_RAYS_PER_PAIR = 512;  // level mode threshold (mean rays per queue lane)
-constexpr int LEAF_CHUNK = 32;    // primitives staged in LDS at a time (max leaf size)
 constexpr int LEVEL_GRID = 2048;  // workgroups of the per-level grid-stride kernel (8 per CU)
 
 // device statistics slots (unsigned long long)
@@ -44,13 +47,18 @@ enum {
 struct TraceArgs {
   const pt_node* __restrict__ nodes;
   const float4* __restrict__ prims;  // 6 float4 per primitive
-  float4* ro;                        // ray records (stride RSTRIDE): o.xyz, tmax (tmax < 0: empty slot)
-  const float4* __restrict__ rd;     // ro + 1: d.xyz, 0
-  unsigned long long* hit;           // {t bits, prim} or PT_HIT_NONE
+  float4* ray;                       // ray records (RSTRIDE float4 each)
   uint32_t* cnt;                     // [node][lane] rays pushed into the node
   uint32_t* qoff;                    // [node][lane] absolute queue offset
   uint32_t* q;                       // ray-id queues (two parity halves)
 };
+
+__device__ __forceinline__ unsigned long long* rec_key(float4* ray, uint32_t id) {
+  return reinterpret_cast<unsigned long long*>(ray + (size_t)RSTRIDE * id + 1) + 1;
+}
+__device__ __forceinline__ float4 rec_r1(float dy, float dz, float tmax) {
+  return make_float4(dy, dz, __uint_as_float(PT_PRIM_NONE), tmax);
+}
 
 __host__ __device__ inline size_t cnt_idx(int node, int lane) { return ((size_t)node * NLANE + lane) * CSTRIDE; }
 

@@ -14,17 +14,20 @@
 // ray count (cu:922, 1384), all triangles of a leaf tested per ray.
 //
 // What is MI355X-first:
-//  * queues carry 4-byte ray ids; ray geometry lives once in SoA float4 arrays
-//    (o.xyz,tmax / d.xyz) instead of 128-byte CuRay copies per queue entry;
+//  * queues carry 4-byte ray ids; each ray lives once in a 32-byte record
+//    (o, d, and its closest-hit word) instead of 128-byte CuRay copies per
+//    queue entry;
 //  * compaction = wave64 ballot + mbcnt, cross-wave offsets through LDS
 //    (replaces the warp-32 Hillis-Steele scan, exclusiveScan.cu_inl:31-48);
 //  * an item is 1024 rays (256 threads x 4), so one atomic reserves up to 1024
 //    slots; queues and counters are split into 8 lanes (one per XCD under the
 //    observed round-robin dispatch) so top-level nodes see 8x less atomic
 //    contention; a ray's lane is fixed by its root item;
-//  * the closest hit is ONE 64-bit atomicMin on {fp32 bits of t, prim index}
-//    per ray and leaf: order independent, ties go to the lowest sorted prim
-//    index, no 16-slot candidate buffer and no merge kernel;
+//  * the closest hit is ONE 64-bit atomicMin on the record's {fp32 bits of t,
+//    prim index} word per ray and leaf: order independent, ties go to the
+//    lowest sorted prim index, no 16-slot candidate buffer and no merge kernel;
+//    its t doubles as the ray's tmax, so every later box test culls against
+//    the closest hit found so far;
 //  * per-level work ranges are computed on the device (no D2H per level,
 //    cu:2237); the level kernel is a grid-stride loop over items;
 //  * node and primitive records are wave-uniform and read with scalar loads.
@@ -107,7 +110,22 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
 
 // ---- one work item: up to TILE rays of one node's queue lane ---------------------
 // ids: implicit (root pass: base + i) or read from qin[base + i].
-template <bool IMPLICIT>
+// NC = 4: the node's children.  NC = 16 (root pass only): the node's
+// grandchildren, i.e. the first interior level is skipped -- every box is
+// conservative for its subtree, so testing a grandchild box directly never
+// drops a ray that would hit a primitive below it.
+template <int NC>
+__device__ __forceinline__ const CPTR(pt_node) child_slot(const TraceArgs& A, const CPTR(pt_node) nd, int c,
+                                                          int& k) {
+  if (NC == 4) {
+    k = c;
+    return nd;
+  }
+  k = c & 3;
+  return (const CPTR(pt_node))(A.nodes + nd->child[c >> 2]);
+}
+
+template <bool IMPLICIT, int NC = 4>
 __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, uint32_t base, int n, int lane,
                                              uint32_t* sh) {
   const int tid = threadIdx.x;
@@ -130,13 +148,13 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
     d[j] = mk(0.f, 0.f, 1.f);
     if (valid[j]) {
       id[j] = IMPLICIT ? base + (uint32_t)i : A.q[base + i];
-      float4 a = A.ro[RSTRIDE * id[j]];
-      o[j] = mk(a.x, a.y, a.z);
-      tmax[j] = a.w;
-      if (IMPLICIT) valid[j] = a.w >= 0.0f;
+      const float4 b = A.ray[RSTRIDE * id[j] + 1];
+      tmax[j] = b.w;
+      if (IMPLICIT) valid[j] = b.w >= 0.0f;
       if (valid[j]) {
-        float4 b = A.rd[RSTRIDE * id[j]];
-        d[j] = mk(b.x, b.y, b.z);
+        const float4 a = A.ray[RSTRIDE * id[j]];
+        o[j] = mk(a.x, a.y, a.z);
+        d[j] = mk(a.w, b.x, b.y);
       }
     }
   }
@@ -189,16 +207,15 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
       if (valid[j] && bp[j] >= 0) {
         unsigned long long key =
             ((unsigned long long)__float_as_uint(bt[j]) << 32) | (unsigned long long)(uint32_t)bp[j];
-        atomicMin(A.hit + id[j], key);
-        // racy monotone-safe tmax update: any stored value is a real hit's t,
-        // so culling boxes beyond it never loses the closest hit
-        if (bt[j] < tmax[j]) reinterpret_cast<float*>(A.ro + RSTRIDE * id[j])[3] = bt[j];
+        // the record's {prim, t} word: later box tests of this ray read the
+        // tightened t as their tmax
+        atomicMin(rec_key(A.ray, id[j]), key);
       }
     }
     return nvalid;
   }
 
-  // ---------------- interior: 4 child boxes, compaction, push -----------------
+  // ---------------- interior: NC child boxes, compaction, push ----------------
   uint32_t bits[RPT];
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
@@ -212,40 +229,46 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
     f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
     uint32_t b = 0;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      bool h = box_hit(nd->bmin_x[c], nd->bmax_x[c], nd->bmin_y[c], nd->bmax_y[c], nd->bmin_z[c],
-                       nd->bmax_z[c], oi, inv, tmax[j]);
+    for (int c = 0; c < NC; ++c) {
+      int k;
+      const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
+      bool h = box_hit(cn->bmin_x[k], cn->bmax_x[k], cn->bmin_y[k], cn->bmax_y[k], cn->bmin_z[k], cn->bmax_z[k],
+                       oi, inv, tmax[j]);
       b |= (valid[j] && h) ? (1u << c) : 0u;
     }
     bits[j] = b;
   }
-  // per-wave counts per child -> LDS
+  // per-wave counts per child -> LDS sh[c*4 + wave]; bases -> sh[NC*4 + c*4 + wave]
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < NC; ++c) {
     uint32_t wc = 0;
 #pragma unroll
     for (int j = 0; j < RPT; ++j) wc += (uint32_t)__popcll(__ballot((bits[j] >> c) & 1u));
     if ((tid & 63) == 0) sh[c * 4 + wave] = wc;
   }
   __syncthreads();
-  if (tid < 4) {
+  if (tid < NC) {
     const int c = tid;
-    const int child = nd->child[c];
+    int k;
+    const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
+    const int child = cn->child[k];
     uint32_t w0 = sh[c * 4 + 0], w1 = sh[c * 4 + 1], w2 = sh[c * 4 + 2], w3 = sh[c * 4 + 3];
     uint32_t tot = w0 + w1 + w2 + w3;
     uint32_t b = 0;
     if (child >= 0 && tot) b = atomicAdd(A.cnt + cnt_idx(child, lane), tot);
-    sh[16 + c * 4 + 0] = b;
-    sh[16 + c * 4 + 1] = b + w0;
-    sh[16 + c * 4 + 2] = b + w0 + w1;
-    sh[16 + c * 4 + 3] = b + w0 + w1 + w2;
+    sh[NC * 4 + c * 4 + 0] = b;
+    sh[NC * 4 + c * 4 + 1] = b + w0;
+    sh[NC * 4 + c * 4 + 2] = b + w0 + w1;
+    sh[NC * 4 + c * 4 + 3] = b + w0 + w1 + w2;
   }
   __syncthreads();
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int child = nd->child[c];
+  for (int c = 0; c < NC; ++c) {
+    int k;
+    const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
+    const int child = cn->child[k];
     if (child < 0) continue;
-    uint32_t off = sh[16 + c * 4 + wave] + A.qoff[(size_t)child * NLANE + lane];
+    uint32_t off = sh[NC * 4 + c * 4 + wave] + A.qoff[(size_t)child * NLANE + lane];
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
       const bool h = (bits[j] >> c) & 1u;
@@ -258,22 +281,24 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 }
 
 // ---- root pass (level 0): implicit queue = slots [r0, r1) ------------------------
+// NC = 16: rays go straight to the level-2 queues (host: skip_l1).
+template <int NC>
 __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, uint32_t r0, uint32_t r1,
                                                     unsigned long long* __restrict__ rcount) {
-  __shared__ uint32_t sh[64];
+  __shared__ uint32_t sh[NC * 8 + 4];
   const uint32_t item = blockIdx.x;
   const uint32_t first = r0 + item * TILE;
   const int n = (int)min((uint32_t)TILE, r1 - first);
   const int lane = item & (NLANE - 1);
-  uint32_t v = process_item<true>(A, 0, first, n, lane, sh);
+  uint32_t v = process_item<true, NC>(A, 0, first, n, lane, sh);
   // valid-ray count (R of the roofline formula): one fire-and-forget atomic per
   // workgroup into this lane's counter line
   v = wave_sum(v);
   __syncthreads();
-  if ((threadIdx.x & 63) == 0) sh[32 + (threadIdx.x >> 6)] = v;
+  if ((threadIdx.x & 63) == 0) sh[NC * 8 + (threadIdx.x >> 6)] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t t = sh[32] + sh[33] + sh[34] + sh[35];
+    const uint32_t t = sh[NC * 8] + sh[NC * 8 + 1] + sh[NC * 8 + 2] + sh[NC * 8 + 3];
     if (t) atomicAdd(rcount + (size_t)lane * 16, (unsigned long long)t);
   }
 }
@@ -282,8 +307,7 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, uint32_t r0, ui
 // Levels >= 1 are processed at wave granularity: no LDS, no workgroup barrier,
 // one returning atomic per wave per child.  Deep levels hold many nodes with a
 // few hundred rays each, where 1024-ray workgroup items would run mostly empty.
-__device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane,
-                                             float4* lbuf) {
+__device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane) {
   const uint32_t lid = lane_id();
   const CPTR(pt_node) nd = (const CPTR(pt_node))(A.nodes + node);
   uint32_t id[RPTW];
@@ -298,14 +322,14 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
   }
 #pragma unroll
   for (int j = 0; j < RPTW; ++j) {
-    float4 a = make_float4(0.f, 0.f, 0.f, -1.f), b = make_float4(0.f, 0.f, 1.f, 0.f);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = make_float4(1.f, 0.f, 0.f, -1.f);
     if (valid[j]) {
-      a = A.ro[RSTRIDE * id[j]];
-      b = A.rd[RSTRIDE * id[j]];
+      a = A.ray[RSTRIDE * id[j]];
+      b = A.ray[RSTRIDE * id[j] + 1];
     }
     o[j] = mk(a.x, a.y, a.z);
-    tmax[j] = a.w;
-    d[j] = mk(b.x, b.y, b.z);
+    tmax[j] = b.w;
+    d[j] = mk(a.w, b.x, b.y);
   }
   const int nj = (n + 63) >> 6;  // ray groups with at least one valid lane (uniform)
   const int pcount = nd->prim_count;
@@ -318,55 +342,6 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
       bt[j] = tmax[j];
       bp[j] = -1;
     }
-#if defined(PT_LEAF_LDS)
-    // the leaf's records (<= 32 x 96 B) are staged in the wave's LDS slice with
-    // three coalesced vector loads, then read back as broadcasts
-    const float4* src = A.prims + (size_t)pstart * 6;
-    for (int k0 = 0; k0 < pcount; k0 += LEAF_CHUNK) {
-      const int ne = min(LEAF_CHUNK, pcount - k0) * 6;
-      float4 tmp[LEAF_CHUNK * 6 / 64];
-#pragma unroll
-      for (int r = 0; r < LEAF_CHUNK * 6 / 64; ++r) {
-        const int e = (int)lid + r * 64;
-        if (e < ne) tmp[r] = src[(size_t)k0 * 6 + e];
-      }
-#pragma unroll
-      for (int r = 0; r < LEAF_CHUNK * 6 / 64; ++r) {
-        const int e = (int)lid + r * 64;
-        if (e < ne) lbuf[e] = tmp[r];
-      }
-      __builtin_amdgcn_wave_barrier();
-      const int kc = ne / 6;
-      for (int k = 0; k < kc; ++k) {
-        const float4* P = lbuf + k * 6;
-        const float4 q0 = P[0], q1 = P[1];
-        const uint32_t meta = __float_as_uint(q0.w);
-        if ((meta >> 28) == PT_PRIM_SPHERE) {
-#pragma unroll
-          for (int j = 0; j < RPTW; ++j) {
-            if (j >= nj) break;
-            float t = sphere_test(o[j], d[j], q0, q1);
-            if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
-              bt[j] = t;
-              bp[j] = pstart + k0 + k;
-            }
-          }
-        } else {
-          const float4 q2 = P[2], q3 = P[3], q4 = P[4], q5 = P[5];
-#pragma unroll
-          for (int j = 0; j < RPTW; ++j) {
-            if (j >= nj) break;
-            float t = tri_test(o[j], d[j], q0, q1, q2, q3, q4, q5, bt[j]);
-            if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
-              bt[j] = t;
-              bp[j] = pstart + k0 + k;
-            }
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-#else
     const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);
     for (int k = 0; k < pcount; ++k, P += 6) {
       const float4 q0 = f4(P[0]), q1 = f4(P[1]);
@@ -394,14 +369,12 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
         }
       }
     }
-#endif
 #pragma unroll
     for (int j = 0; j < RPTW; ++j) {
       if (valid[j] && bp[j] >= 0) {
         unsigned long long key =
             ((unsigned long long)__float_as_uint(bt[j]) << 32) | (unsigned long long)(uint32_t)bp[j];
-        atomicMin(A.hit + id[j], key);
-        if (bt[j] < tmax[j]) reinterpret_cast<float*>(A.ro + RSTRIDE * id[j])[3] = bt[j];
+        atomicMin(rec_key(A.ray, id[j]), key);
       }
     }
     return;
@@ -493,7 +466,6 @@ __global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
     return;
   }
   // many nodes with few rays each: every wave walks its own 256-ray items
-  __shared__ float4 leafbuf[TPB / 64][LEAF_CHUNK * 6];
   const uint32_t stride = (gridDim.x / NLANE) * (TPB / 64);
   for (uint32_t m = (blockIdx.x / NLANE) * (TPB / 64) + wave; m < M; m += stride) {
     // 64-ary search for the node k with ep[k] <= m < ep[k+1]
@@ -512,8 +484,7 @@ __global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
     const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
     const uint32_t base = A.qoff[(size_t)node * NLANE + lane] + i * WTILE;
     const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
-    process_wave(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane,
-                 leafbuf[wave]);
+    process_wave(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane);
   }
 }
 

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -48,6 +49,7 @@ struct pt_ctx {
   std::vector<int32_t> level_start;
   int max_level_nodes = 0;
   bool root_leaf = true;
+  bool skip_l1 = false;  // root pass pushes straight into the level-2 queues
   std::vector<pt_node> nodes_host;
   pt_light light{};
   pt_camera camera{};
@@ -58,8 +60,7 @@ struct pt_ctx {
 
   // wavefront buffers (sized for N paths = 2N ray slots)
   uint32_t cap_paths = 0;
-  float4 *d_ro = nullptr, *d_rd = nullptr;  // one array of 32-B ray records; d_rd = d_ro + 1
-  unsigned long long* d_hit = nullptr;
+  float4* d_ray = nullptr;  // 2N ray records (trace.h), RSTRIDE float4 each
   float4 *d_ps0 = nullptr, *d_ps1 = nullptr, *d_ps2 = nullptr;
   uint32_t* d_q = nullptr;
   size_t qcap = 0;  // entries per parity half
@@ -142,8 +143,8 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 }
 
 static void free_all(pt_ctx* c) {
-  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ro,
-                  c->d_hit,   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_q,      c->d_cnt,
+  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ray,
+                  c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_q,      c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err,
                   c->d_pix_of, c->d_accum};
   for (void* p : ptrs)
@@ -162,17 +163,15 @@ static int ensure_paths(pt_ctx* c, uint32_t N) {
   if (N <= c->cap_paths) return PT_OK;
   const size_t slots = 2 * (size_t)N;
   int rc;
-  if ((rc = dalloc(c, &c->d_ro, slots * RSTRIDE))) return rc;
-  c->d_rd = c->d_ro + 1;
-  if ((rc = dalloc(c, &c->d_hit, slots))) return rc;
+  if ((rc = dalloc(c, &c->d_ray, slots * RSTRIDE))) return rc;
   if ((rc = dalloc(c, &c->d_ps0, N))) return rc;
   if ((rc = dalloc(c, &c->d_ps1, N))) return rc;
   if ((rc = dalloc(c, &c->d_ps2, N))) return rc;
-  // every root child needs ceil(items/8)*TILE slots per lane (see
+  // every root target needs ceil(items/8)*TILE slots per lane (see
   // set_root_child_offsets); deeper levels need at most 4x the visits of the
   // level above, which QFACTOR covers for the scenes measured (peak_queue_entries)
   const size_t items = (slots + TILE - 1) / TILE;
-  const size_t root_need = (size_t)NLANE * 4 * ((items + NLANE - 1) / NLANE * TILE);
+  const size_t root_need = (size_t)NLANE * 16 * ((items + NLANE - 1) / NLANE * TILE);  // <= 16 root targets
   c->qcap = std::max(QFACTOR * slots, 2 * root_need);
   c->qcap = (c->qcap + NLANE * 64 - 1) / (NLANE * 64) * (NLANE * 64);
   if ((rc = dalloc(c, &c->d_q, 2 * c->qcap))) return rc;
@@ -189,15 +188,26 @@ static int set_root_child_offsets(pt_ctx* c) {
   const size_t items = (slots + TILE - 1) / TILE;
   const size_t per_lane = (items + NLANE - 1) / NLANE * TILE;
   const size_t lanecap = c->qcap / NLANE;
-  if (4 * per_lane > lanecap) return fail(c, PT_E_OVERFLOW, "root queue capacity");
   const pt_node& root = c->nodes_host[0];
-  int jj = 0;
+  // targets: the root's children (level 1, odd half) or, when level 1 is
+  // skipped, its grandchildren (level 2, even half)
+  std::vector<int> targets;
   for (int k = 0; k < 4; ++k) {
     if (root.child[k] < 0) continue;
+    if (!c->skip_l1) {
+      targets.push_back(root.child[k]);
+      continue;
+    }
+    const pt_node& ch = c->nodes_host[root.child[k]];
+    for (int g = 0; g < 4; ++g)
+      if (ch.child[g] >= 0) targets.push_back(ch.child[g]);
+  }
+  if (targets.size() * per_lane > lanecap) return fail(c, PT_E_OVERFLOW, "root queue capacity");
+  const size_t half = c->skip_l1 ? 0 : c->qcap;
+  for (size_t jj = 0; jj < targets.size(); ++jj) {
     uint32_t off[NLANE];
-    for (int s = 0; s < NLANE; ++s) off[s] = (uint32_t)(c->qcap + (size_t)s * lanecap + (size_t)jj * per_lane);
-    HIPCHK(c, hipMemcpy(c->d_qoff + (size_t)root.child[k] * NLANE, off, sizeof(off), hipMemcpyHostToDevice));
-    jj++;
+    for (int s = 0; s < NLANE; ++s) off[s] = (uint32_t)(half + (size_t)s * lanecap + jj * per_lane);
+    HIPCHK(c, hipMemcpy(c->d_qoff + (size_t)targets[jj] * NLANE, off, sizeof(off), hipMemcpyHostToDevice));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return PT_OK;
@@ -207,9 +217,7 @@ static TraceArgs trace_args(pt_ctx* c) {
   TraceArgs A;
   A.nodes = c->d_nodes;
   A.prims = c->d_prims;
-  A.ro = c->d_ro;
-  A.rd = c->d_rd;
-  A.hit = c->d_hit;
+  A.ray = c->d_ray;
   A.cnt = c->d_cnt;
   A.qoff = c->d_qoff;
   A.q = c->d_q;
@@ -223,9 +231,12 @@ static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
   const uint32_t items = (r1 - r0 + TILE - 1) / TILE;
   // the (node, lane) counters are zero here: each level's scan re-zeroes them
   // after taking its snapshot (pt_load_scene zeroes them once)
-  c->launch(pt_ctx::K_ROOT, 0, k_trace_root, dim3(items), dim3(TPB), A, r0, r1, c->d_rcount);
+  if (c->skip_l1)
+    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<16>, dim3(items), dim3(TPB), A, r0, r1, c->d_rcount);
+  else
+    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<4>, dim3(items), dim3(TPB), A, r0, r1, c->d_rcount);
   const size_t lanecap = c->qcap / NLANE;
-  for (int l = 1; l < c->n_levels; ++l) {
+  for (int l = c->skip_l1 ? 2 : 1; l < c->n_levels; ++l) {
     LevelArgs L;
     L.first = c->level_start[l];
     L.nl = c->level_start[l + 1] - c->level_start[l];
@@ -380,6 +391,13 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     c->max_level_nodes = std::max(c->max_level_nodes, c->level_start[l + 1] - c->level_start[l]);
   c->nodes_host.assign(s->nodes, s->nodes + s->n_nodes);
   c->root_leaf = c->nodes_host[0].prim_count > 0;
+  // skip the first interior level when every child of the root is interior:
+  // the root pass tests the 16 grandchild boxes (PT_NO_SKIP_L1=1 disables it)
+  c->skip_l1 = !c->root_leaf && c->n_levels >= 3 && !getenv("PT_NO_SKIP_L1");
+  for (int k = 0; k < 4 && c->skip_l1; ++k) {
+    const int ch = c->nodes_host[0].child[k];
+    if (ch >= 0 && c->nodes_host[ch].prim_count > 0) c->skip_l1 = false;
+  }
   for (int i = 0; i < s->n_nodes; ++i) {
     const pt_node& nd = s->nodes[i];
     if (nd.prim_start < 0 || nd.prim_count < 0 || nd.prim_start + nd.prim_count > s->n_prims)
@@ -499,9 +517,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   c->stats.batch_paths = (int32_t)Nmax;
 
   ShadeArgs S;
-  S.ro = c->d_ro;
-  S.rd = c->d_rd;
-  S.hit = c->d_hit;
+  S.ray = c->d_ray;
   S.ps0 = c->d_ps0;
   S.ps1 = c->d_ps1;
   S.ps2 = c->d_ps2;
@@ -600,11 +616,11 @@ int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) {
   if ((rc = ensure_paths(c, N))) return rc;
   if (realloc && (rc = set_root_child_offsets(c))) return rc;
   float4* d_in = nullptr;
-  HIPCHK(c, hipMalloc((void**)&d_in, (size_t)n * 32));
+  HIPCHK(c, hipMalloc((void**)&d_in, (size_t)n * 32));  // rays in, then hit keys out
   HIPCHK(c, hipMemcpyAsync(d_in, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
-  hipLaunchKernelGGL(k_load_rays, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, d_in, c->d_ro, c->d_rd,
-                     c->d_hit, (uint32_t)n);
+  hipLaunchKernelGGL(k_load_rays, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, d_in, c->d_ray,
+                     (uint32_t)n);
   hipEventRecord(c->ev[6], c->stream);
   rc = trace_pass(c, 0, (uint32_t)n);
   hipEventRecord(c->ev[7], c->stream);
@@ -612,7 +628,9 @@ int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) {
     hipFree(d_in);
     return rc;
   }
-  HIPCHK(c, hipMemcpyAsync(hits, c->d_hit, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+  hipLaunchKernelGGL(k_store_hits, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, c->d_ray,
+                     (unsigned long long*)d_in, (uint32_t)n);
+  HIPCHK(c, hipMemcpyAsync(hits, d_in, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   float ms = 0;
   hipEventElapsedTime(&ms, c->ev[6], c->ev[7]);

@@ -1,57 +1,64 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes per kernel.
+"""Summarise rocprofv3 --pmc passes per kernel (and per traversal level).
 
-  python scripts/pmc_summary.py <fetch_run_counter_collection.csv> <write_...csv> [--levels L]
+  python scripts/pmc_summary.py <run_counter_collection.csv>... [--levels L]
 
 FETCH_SIZE and WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE counts 128-B
 memory-side requests at 64 B (MI355X_MICROARCH.md, HBM section), so the
-corrected read bytes are 2 x FETCH_SIZE.  With --levels L, the k_trace_level
-dispatches are split by level (launch order cycles through levels 1..L-1 in
-every traversal pass).
+corrected read bytes are 2 x FETCH_SIZE; the table shows them as READ_GB and
+WRITE_GB.  With --levels L, k_trace_level dispatches are split by level
+(launch order cycles through levels 1..L-1 in every traversal pass).
 """
 import csv
 import sys
 from collections import defaultdict
 
 
-def load(path):
-    rows = []
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"]),
-                         int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
-    rows.sort()
-    return rows
-
-
 def short(name):
-    n = name.split("(")[0]
-    return n.replace("pt::", "")
+    return name.split("(")[0].replace("pt::", "")
 
 
 def main():
-    fpath, wpath = sys.argv[1], sys.argv[2]
-    levels = int(sys.argv[sys.argv.index("--levels") + 1]) if "--levels" in sys.argv else 0
-    F, W = load(fpath), load(wpath)
-    agg = defaultdict(lambda: [0, 0.0, 0.0])
-    lvl = defaultdict(lambda: [0, 0.0, 0.0])
-    li = 0
-    for (d, k, fv, _), (_, _, wv, _) in zip(F, W):
-        a = agg[short(k)]
-        a[0] += 1
-        a[1] += 2 * fv * 1024
-        a[2] += wv * 1024
-        if levels and short(k) == "k_trace_level":
-            b = lvl[li % (levels - 1) + 1]
-            li += 1
-            b[0] += 1
-            b[1] += 2 * fv * 1024
-            b[2] += wv * 1024
-    print(f"{'kernel':24s} {'disp':>6s} {'read GB':>9s} {'write GB':>9s} {'MB/disp':>9s}")
-    for k, (n, rb, wb) in sorted(agg.items(), key=lambda x: -(x[1][1] + x[1][2])):
-        print(f"{k:24s} {n:6d} {rb/1e9:9.3f} {wb/1e9:9.3f} {(rb+wb)/n/1e6:9.2f}")
-    for l, (n, rb, wb) in sorted(lvl.items()):
-        print(f"  level {l}: {n} dispatches, read {rb/1e9:.3f} GB, write {wb/1e9:.3f} GB")
+    args = sys.argv[1:]
+    levels = 0
+    if "--levels" in args:
+        i = args.index("--levels")
+        levels = int(args[i + 1])
+        del args[i:i + 2]
+    agg = defaultdict(lambda: defaultdict(float))  # key -> counter -> value
+    ndisp = defaultdict(set)
+    for path in args:
+        rows = []
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                rows.append(r)
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        lvl_of = {}
+        li = 0
+        for r in rows:
+            d = int(r["Dispatch_Id"])
+            k = short(r["Kernel_Name"])
+            if levels and k == "k_trace_level" and d not in lvl_of:
+                lvl_of[d] = li % (levels - 1) + 1
+                li += 1
+        for r in rows:
+            d = int(r["Dispatch_Id"])
+            k = short(r["Kernel_Name"])
+            c = r["Counter_Name"]
+            v = float(r["Counter_Value"])
+            if c == "FETCH_SIZE":
+                c, v = "READ_GB", 2 * v * 1024 / 1e9
+            elif c == "WRITE_SIZE":
+                c, v = "WRITE_GB", v * 1024 / 1e9
+            keys = [k] + ([f"{k}[L{lvl_of[d]}]"] if d in lvl_of else [])
+            for key in keys:
+                agg[key][c] += v
+                ndisp[key].add((path, d))
+    counters = sorted({c for a in agg.values() for c in a})
+    print(f"{'kernel':22s} {'disp':>5s} " + " ".join(f"{c[:16]:>16s}" for c in counters))
+    for key in sorted(agg, key=lambda k: (k.split("[")[0], k)):
+        a = agg[key]
+        print(f"{key:22s} {len(ndisp[key]):5d} " + " ".join(f"{a.get(c, 0):16.4g}" for c in counters))
 
 
 if __name__ == "__main__":

@@ -38,6 +38,24 @@ def test_closest_hit_bit_exact(gpu_ctx, name):
     assert np.array_equal(pyoracle.intersect(d, sub, use_bvh=True), pyoracle.intersect(d, sub, use_bvh=False))
 
 
+@pytest.mark.parametrize("name", ["CBbunny", "CBcoil"])
+def test_level_skip_off_matches(gpu_ctx, name, monkeypatch):
+    """PT_NO_SKIP_L1=1 restores the root -> level-1 pass; both schedules must
+    report the same closest hits (the traversal order never changes results)."""
+    sc = load_fixture(name)
+    d = sc.desc()
+    rays = np.concatenate([camera_rays(d, 20000, seed=17), interior_rays(d, 20000, seed=18)])
+    gpu_ctx.load_scene(sc)
+    g_skip = gpu_ctx.intersect(rays)
+    monkeypatch.setenv("PT_NO_SKIP_L1", "1")
+    gpu_ctx.load_scene(sc)
+    g_full = gpu_ctx.intersect(rays)
+    monkeypatch.delenv("PT_NO_SKIP_L1")
+    gpu_ctx.load_scene(sc)
+    assert np.array_equal(g_skip, g_full)
+    assert np.array_equal(g_skip, pyoracle.intersect(d, rays, use_bvh=True))
+
+
 def test_tie_break_lowest_prim(gpu_ctx):
     # two identical triangles: every hit must report the lower sorted index
     tri = np.array([[-1, -1, 0, 1, -1, 0, 0, 1, 0]] * 2, np.float32)
