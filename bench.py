@@ -2,21 +2,35 @@
 """Headline benchmark: Mrays/s and ms/frame of the breadth-first wide-BVH path
 tracer at 1024x1024, 256 spp, 8 bounces (BASELINE.json metric), on N GPUs.
 
+The headline workload is BASELINE.json configs[1]:
+the diffuse Cornell box CBempty.dae.  The same JSON line carries the other
+single-GPU configs of the metric (config 3: CBspheres, glass + mirror; config
+4: CBbunny, 28,588 triangles, deep wide BVH) measured the same way in the same
+run, under "configs".
+
 A step is one full frame: every rank renders its interleaved 32x32 tiles of the
 1024x1024 image at 256 spp (strong scaling: the frame is fixed, ranks split it),
 then the framebuffer is gathered to rank 0 over RCCL.  Rays are every ray cast
-through the traversal (camera + extension + shadow), counted on the device.
+(camera + extension + shadow), counted on the device.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
-Rank 0 prints one JSON line.  roofline: the dominant kernel k_trace_level,
-algorithmic bytes = sum over levels l>=1 of 32 B per (ray, node) visit (4 B
-queue id + 28 B ray o/d/tmax) + 4 B per id pushed to the next level
-(BASELINE.md §3), divided by its summed launch time from HIP events recorded on
-the library's stream inside the timed region.  cpu_baseline: the CPU oracle
-(oracle/ptoracle.c, the Scotty3D-structured tile renderer) on a bounded sample
-of the same frame on this host.
+Rank 0 prints one JSON line.  "roofline" describes the workload's dominant
+kernel, timed by HIP events attached to its dispatch packets in one extra,
+instrumented frame (the headline frames run without events):
+  * k_trace_level (BVH levels >= 1, HBM-bound): algorithmic bytes = 32 B per
+    (ray, node) visit (4 B queue id + 28 B of ray) + 4 B per id pushed to the
+    next level (BASELINE.md §3);
+  * k_path_leaf (scenes whose BVH root is a leaf: each path runs to completion
+    in registers, no HBM stream): VALU-bound, algorithmic FP32 operations of
+    the primitive tests (69 per ray-triangle test, 20 per ray-sphere test,
+    every primitive of the leaf per ray) against the 157.3 TFLOP/s vector peak.
+"traffic" is HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x 2 +
+WRITE_SIZE, MI355X_MICROARCH.md) when a matching summary is committed under
+profiles/ (scripts/pmc.sh, scripts/pmc_summary.py), else null.
+cpu_baseline: the CPU oracle (oracle/ptoracle.c, the Scotty3D-structured tile
+renderer) on a bounded sample of the headline frame on this host.
 """
 import argparse
 import json
@@ -28,7 +42,10 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "cuda-raytracer_amd"))
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+VALU_PEAK_TFLOPS = 157.3    # MI355X FP32 vector peak, same guide
+FLOP_TRI, FLOP_SPHERE = 69, 20
+PMC_DIR = ROOT / "profiles" / "r01"
 
 
 def parse():
@@ -36,7 +53,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--scene", default="CBbunny")
+    p.add_argument("--scene", default="CBempty", help="headline scene (configs[1] = CBempty)")
+    p.add_argument("--configs", default="CBspheres,CBbunny",
+                   help="other single-GPU configs measured in the same run ('' = none)")
     p.add_argument("--width", type=int, default=1024)
     p.add_argument("--height", type=int, default=1024)
     p.add_argument("--spp", type=int, default=256)
@@ -77,27 +96,41 @@ def cpu_baseline(desc, args):
                       f"{args.bounces} bounces; {rays} rays in {dt:.1f} s on {threads} threads"}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def pmc_traffic(scene, kernel):
+    """HBM bytes per launch of `kernel` from a committed PMC summary, if any."""
+    f = PMC_DIR / f"pmc_{scene}.json"
+    if not f.exists():
+        return None, None
+    try:
+        d = json.loads(f.read_text())
+        k = d["kernels"][kernel]
+        return k["hbm_bytes_per_launch"], f"{f.relative_to(ROOT)} ({d.get('config', '')})"
+    except (KeyError, ValueError):
+        return None, None
+
+
+def root_leaf_flops(desc):
+    """(flop per ray, prims) of the single-leaf test: every primitive of the root leaf."""
     import numpy as np
+    import ctypes as C
+    n = desc.nodes[0]
+    if n.prim_count <= 0:
+        return 0, 0
+    q = np.ctypeslib.as_array(C.cast(desc.prims, C.POINTER(C.c_float)), shape=(desc.n_prims, 24))
+    meta = q[n.prim_start:n.prim_start + n.prim_count, 3].view(np.uint32) >> 28
+    import ptrace
+    nsph = int((meta == ptrace.PT_PRIM_SPHERE).sum())
+    ntri = n.prim_count - nsph
+    return ntri * FLOP_TRI + nsph * FLOP_SPHERE, n.prim_count
+
+
+def run_workload(name, args, ctx, rank, world, dev, dist):
     import torch
     import ptrace
     import ptdist
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    scene = ptrace.ArrayScene.load(ROOT / "tests" / "golden" / "scenes" / f"{args.scene}.npz")
-    ctx = ptrace.Context(local)
+    scene = ptrace.ArrayScene.load(ROOT / "tests" / "golden" / "scenes" / f"{name}.npz")
     ctx.load_scene(scene)
+    desc = scene.desc()
 
     def frame(stats):
         ctx.clear()
@@ -121,9 +154,10 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     rays = ctx.stats().rays  # device counters, no instrumentation needed
+    instrumented_ms = None
     if not args.stats_in_timed:
         # per-kernel times of one more, instrumented frame (HIP events attached
-        # to each dispatch packet); the headline above ran without them
+        # to each dispatch packet); the timed frames above ran without them
         ctx.reset_stats()
         t1 = time.perf_counter()
         frame(True)
@@ -133,27 +167,85 @@ def main():
     lvl_ms = sum(st.ms_level[l] for l in range(1, 16))
     V = [st.level_visits[l] for l in range(16)]
     lvl_bytes = sum(32 * V[l] for l in range(1, 16)) + sum(4 * V[l] for l in range(2, 16))
-    launches = sum(st.level_launches[l] for l in range(1, 16))
-    trace_bytes = 36 * st.rays + 36 * st.visits
+    lvl_launches = sum(st.level_launches[l] for l in range(1, 16))
+    flop_ray, _ = root_leaf_flops(desc)
+    path_flops = flop_ray * st.rays
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        r = torch.tensor([rays, lvl_bytes, trace_bytes], dtype=torch.float64, device=dev)
+        r = torch.tensor([rays], dtype=torch.float64, device=dev)
         dist.all_reduce(r)
-        rays, lvl_bytes_all, trace_bytes_all = (float(x) for x in r.tolist())
-    if rank == 0:
-        ms_step = elapsed / args.steps * 1e3
-        value = rays / elapsed / 1e6
+        rays = float(r.item())
+    ms_step = elapsed / args.steps * 1e3
+    if st.ms_path >= lvl_ms:
+        kernel, launches = "k_path_leaf", st.path_launches
+        ach = path_flops / (st.ms_path * 1e-3) / 1e12 if st.ms_path > 0 else 0.0
+        traffic, src = pmc_traffic(name, kernel)
+        roof = {"bound": "valu", "achieved": round(ach, 2), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / VALU_PEAK_TFLOPS, 4), "traffic": traffic, "kernel": kernel,
+                "launches": int(launches), "avg_launch_us": round(st.ms_path * 1e3 / max(1, launches), 2),
+                "flop_per_launch": int(path_flops / max(1, launches)),
+                "note": "single-leaf BVH: paths run to completion in registers; FP32 VALU, not HBM, bounds it"}
+    else:
+        kernel, launches = "k_trace_level", lvl_launches
         ach = (lvl_bytes / (lvl_ms * 1e-3) / 1e9) if lvl_ms > 0 else 0.0
+        traffic, src = pmc_traffic(name, kernel)
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
+                "launches": int(launches), "avg_launch_us": round(lvl_ms * 1e3 / max(1, launches), 2),
+                "bytes_per_launch": int(lvl_bytes / max(1, launches))}
+    if src:
+        roof["traffic_source"] = src
+    out = {
+        "scene": name,
+        "value": round(rays / elapsed / 1e6, 2),
+        "ms_per_frame": round(ms_step, 2),
+        "rays_per_frame": int(rays / args.steps),
+        "batch_paths": st.batch_paths,
+        "roofline": roof,
+        "trace": {"visits_per_ray": round(st.visits / max(1, st.rays), 2),
+                  "instrumented_frame_ms": None if instrumented_ms is None else round(instrumented_ms, 2),
+                  "ms_path": round(st.ms_path, 1), "ms_trace": round(st.ms_trace, 1),
+                  "ms_shade": round(st.ms_shade, 1), "ms_root": round(st.ms_root, 1),
+                  "ms_scan": round(st.ms_scan, 1), "ms_levels": round(lvl_ms, 1),
+                  "levels": [{"level": l, "ms": round(st.ms_level[l], 2), "visits": int(st.level_visits[l]),
+                              "leaf_visits": int(st.level_leaf_visits[l]), "items": int(st.level_items[l]),
+                              "Gvisits_per_s": round(st.level_visits[l] / max(st.ms_level[l], 1e-9) / 1e6, 2)}
+                             for l in range(1, st.n_levels) if st.level_launches[l] > 0]},
+    }
+    return out, scene
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import ptrace
+    dist = None
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    ctx = ptrace.Context(local)
+
+    head, head_scene = run_workload(args.scene, args, ctx, rank, world, dev, dist)
+    others = []
+    for name in [s for s in args.configs.split(",") if s and s != args.scene]:
+        o, _ = run_workload(name, args, ctx, rank, world, dev, dist)
+        others.append(o)
+    if rank == 0:
         out = {
             "metric": f"Mrays/sec at {args.width}x{args.height}, {args.spp} spp, {args.bounces} bounces",
-            "value": round(value, 2),
+            "value": head["value"],
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 2),
+            "ms_per_step": head["ms_per_frame"],
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -161,28 +253,16 @@ def main():
             "data": f"scene {args.scene}.dae (reference media, flattened fixture); rays sampled with Philox seed {args.seed}",
             "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.spp}spp {args.bounces} bounces",
                        "scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
-                       "max_bounces": args.bounces, "batch_paths": st.batch_paths,
+                       "max_bounces": args.bounces, "batch_paths": head["batch_paths"],
                        "parallelism": f"tiles{args.tile}x{world}"},
-            "ms_per_frame": round(ms_step, 2),
-            "rays_per_frame": int(rays / args.steps),
-            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "k_trace_level", "launches": int(launches),
-                         "avg_launch_us": round(lvl_ms * 1e3 / max(1, launches), 2),
-                         "bytes_per_launch": int(lvl_bytes / max(1, launches))},
-            "trace": {"visits_per_ray": round(st.visits / max(1, st.rays), 2),
-                      "instrumented_frame_ms": None if args.stats_in_timed else round(instrumented_ms, 2),
-                      "ms_trace": round(st.ms_trace, 1), "ms_shade": round(st.ms_shade, 1),
-                      "ms_root": round(st.ms_root, 1), "ms_scan": round(st.ms_scan, 1),
-                      "ms_levels": round(lvl_ms, 1),
-                      "algorithmic_GBps_traversal": round(trace_bytes / max(st.ms_trace, 1e-9) / 1e6, 1),
-                      "levels": [{"level": l, "ms": round(st.ms_level[l], 2), "visits": int(st.level_visits[l]),
-                                  "leaf_visits": int(st.level_leaf_visits[l]), "items": int(st.level_items[l]),
-                                  "Gvisits_per_s": round(st.level_visits[l] / max(st.ms_level[l], 1e-9) / 1e6, 2)}
-                                 for l in range(1, st.n_levels)]},
+            "ms_per_frame": head["ms_per_frame"],
+            "rays_per_frame": head["rays_per_frame"],
+            "roofline": head["roofline"],
+            "trace": head["trace"],
+            "configs": others,
         }
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(scene.desc(), args)
+            out["cpu_baseline"] = cpu_baseline(head_scene.desc(), args)
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:

@@ -42,11 +42,10 @@ struct ShadeArgs {
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 __device__ __forceinline__ f3 xyz(float4 a) { return mk(a.x, a.y, a.z); }
 
-__global__ __launch_bounds__(TPB) void k_camera(ShadeArgs S) {
-  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
-  if (p >= S.N) return;
+// Camera ray of path p (pixel g = pix_of[p % npix], sample sample_base + p / npix).
+__device__ __forceinline__ f3 camera_dir(const ShadeArgs& S, uint32_t p, uint32_t& g) {
   const uint32_t q = p % S.npix, j = p / S.npix;
-  const uint32_t g = S.pix_of[q];
+  g = S.pix_of[q];
   const uint32_t row = g / (uint32_t)S.width, col = g - row * (uint32_t)S.width;
   const uint32_t s = S.sample_base + j;
   const u4 u = rng(S.seed, g, s, 0, 0);
@@ -62,7 +61,14 @@ __global__ __launch_bounds__(TPB) void k_camera(ShadeArgs S) {
   kz = kz / len;
   const f3 L = ld3(S.cam.left), U = ld3(S.cam.up), K = ld3(S.cam.look_at);
   f3 dir = mk(kx * L.x + ky * U.x + kz * K.x, kx * L.y + ky * U.y + kz * K.y, kx * L.z + ky * U.z + kz * K.z);
-  dir = normalize(dir);
+  return normalize(dir);
+}
+
+__global__ __launch_bounds__(TPB) void k_camera(ShadeArgs S) {
+  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
+  if (p >= S.N) return;
+  uint32_t g;
+  const f3 dir = camera_dir(S, p, g);
   S.ray[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], dir.x);
   S.ray[RSTRIDE * p + 1] = rec_r1(dir.y, dir.z, __builtin_inff());
   S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
@@ -71,37 +77,44 @@ __global__ __launch_bounds__(TPB) void k_camera(ShadeArgs S) {
   S.ps2[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
-__global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
-  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
-  if (p >= S.N) return;
-  const float4 s0 = S.ps0[p];
-  uint32_t flags = __float_as_uint(s0.w);
-  if ((flags & (F_EXT | F_SHADOW)) == 0) return;
-  f3 T = xyz(s0);
-  const float4 s1 = S.ps1[p];
-  f3 L = xyz(s1);
-  const uint32_t g = __float_as_uint(s1.w);
-  const uint32_t sidx = S.sample_base + p / S.npix;
+// Path state between vertices (ps0/ps1/ps2 in memory, registers in k_path_leaf).
+struct PathState {
+  f3 T;            // throughput
+  uint32_t flags;  // F_* | vertex << 8
+  f3 L;            // radiance gathered so far
+  uint32_t g;      // pixel
+};
+struct RayV {
+  f3 o, d;
+  float tmax;
+};
 
+// One path vertex (restated from cu:380-664, see header): resolves the shadow
+// ray of the previous vertex (C added when unoccluded), shades the extension
+// hit (prim != PT_PRIM_NONE at distance t along ext), and produces the next
+// extension ray and/or shadow ray with its pending contribution C.
+__device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, PathState& st, const f3 o,
+                                             const f3 d, uint32_t prim, float t, bool shadow_clear, f3& C,
+                                             bool& new_ext, RayV& ext, bool& new_sh, RayV& shr) {
+  const uint32_t flags = st.flags;
+  f3 T = st.T;
+  f3 L = st.L;
+  const uint32_t g = st.g;
   // 1. resolve the shadow ray of the previous vertex
   if (flags & F_SHADOW) {
-    if (__float_as_uint(S.ray[RSTRIDE * (S.N + p) + 1].z) == PT_PRIM_NONE) L = L + xyz(S.ps2[p]);
+    if (shadow_clear) L = L + C;
   }
-  bool new_ext = false, new_sh = false;
-  f3 o_new = mk(0, 0, 0), d_new = mk(0, 0, 1), sh_o = mk(0, 0, 0), sh_d = mk(0, 0, 1), C = mk(0, 0, 0);
+  new_ext = false;
+  new_sh = false;
+  f3 o_new = mk(0, 0, 0), d_new = mk(0, 0, 1), sh_o = mk(0, 0, 0), sh_d = mk(0, 0, 1);
+  C = mk(0, 0, 0);
   float sh_tmax = -1.0f;
   uint32_t spec = flags & F_SPEC;
   const uint32_t vtx = (flags >> 8) & 0xffu;
 
   // 2. shade the hit of the extension ray
   if (flags & F_EXT) {
-    const float4 r1 = S.ray[RSTRIDE * p + 1];
-    const uint32_t prim = __float_as_uint(r1.z);
     if (prim != PT_PRIM_NONE) {
-      const float t = r1.w;
-      const float4 r0 = S.ray[RSTRIDE * p];
-      const f3 o = xyz(r0);
-      const f3 d = mk(r0.w, r1.x, r1.y);
       const f3 P = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
       const float4* Q = S.prims + (size_t)prim * 6;
       const float4 q0 = Q[0];
@@ -236,22 +249,146 @@ __global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
     }
   }
 
-  const uint32_t fout = spec | (new_ext ? F_EXT : 0u) | (new_sh ? F_SHADOW : 0u) | ((vtx + 1u) << 8);
-  S.ps0[p] = make_float4(T.x, T.y, T.z, __uint_as_float(fout));
-  S.ps1[p] = make_float4(L.x, L.y, L.z, __uint_as_float(g));
+  st.T = T;
+  st.L = L;
+  st.flags = spec | (new_ext ? F_EXT : 0u) | (new_sh ? F_SHADOW : 0u) | ((vtx + 1u) << 8);
+  ext.o = o_new;
+  ext.d = d_new;
+  ext.tmax = __builtin_inff();
+  shr.o = sh_o;
+  shr.d = sh_d;
+  shr.tmax = sh_tmax;
+}
+
+__global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
+  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
+  if (p >= S.N) return;
+  const float4 s0 = S.ps0[p];
+  const uint32_t flags = __float_as_uint(s0.w);
+  if ((flags & (F_EXT | F_SHADOW)) == 0) return;
+  const float4 s1 = S.ps1[p];
+  PathState st{xyz(s0), flags, xyz(s1), __float_as_uint(s1.w)};
+  const uint32_t sidx = S.sample_base + p / S.npix;
+  bool clear = false;
+  f3 C = mk(0, 0, 0);
+  if (flags & F_SHADOW) {
+    clear = __float_as_uint(S.ray[RSTRIDE * (S.N + p) + 1].z) == PT_PRIM_NONE;
+    if (clear) C = xyz(S.ps2[p]);
+  }
+  uint32_t prim = PT_PRIM_NONE;
+  float t = 0.0f;
+  f3 o = mk(0, 0, 0), d = mk(0, 0, 1);
+  if (flags & F_EXT) {
+    const float4 r1 = S.ray[RSTRIDE * p + 1];
+    prim = __float_as_uint(r1.z);
+    if (prim != PT_PRIM_NONE) {
+      t = r1.w;
+      const float4 r0 = S.ray[RSTRIDE * p];
+      o = xyz(r0);
+      d = mk(r0.w, r1.x, r1.y);
+    }
+  }
+  bool new_ext, new_sh;
+  RayV ext, shr;
+  shade_vertex(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
+  S.ps0[p] = make_float4(st.T.x, st.T.y, st.T.z, __uint_as_float(st.flags));
+  S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(st.g));
   if (new_sh) S.ps2[p] = make_float4(C.x, C.y, C.z, 0.0f);
   if (new_ext) {
-    S.ray[RSTRIDE * p] = make_float4(o_new.x, o_new.y, o_new.z, d_new.x);
-    S.ray[RSTRIDE * p + 1] = rec_r1(d_new.y, d_new.z, __builtin_inff());
+    S.ray[RSTRIDE * p] = make_float4(ext.o.x, ext.o.y, ext.o.z, ext.d.x);
+    S.ray[RSTRIDE * p + 1] = rec_r1(ext.d.y, ext.d.z, __builtin_inff());
   } else {
     S.ray[RSTRIDE * p + 1] = rec_r1(0.f, 0.f, -1.0f);
   }
   if (new_sh) {
-    S.ray[RSTRIDE * (S.N + p)] = make_float4(sh_o.x, sh_o.y, sh_o.z, sh_d.x);
-    S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(sh_d.y, sh_d.z, sh_tmax);
+    S.ray[RSTRIDE * (S.N + p)] = make_float4(shr.o.x, shr.o.y, shr.o.z, shr.d.x);
+    S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(shr.d.y, shr.d.z, shr.tmax);
   } else {
     S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
   }
+}
+
+// ---- scenes whose BVH root is a leaf -----------------------------------------
+// With a single-leaf tree every traversal pass is the root pass: each ray tests
+// all primitives of the leaf and nothing is queued, so the pass/shade wavefront
+// collapses into one kernel that carries each path through all of its vertices
+// in registers (no ray records, hit words or path state in HBM).  Closest hits
+// use the same primitive tests and tie rule as the leaf code of
+// process_item (trace.hip); results are bit-identical to the wavefront path.
+__device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, int pcount, const RayV& r,
+                                             uint32_t& prim, float& t) {
+  float bt = r.tmax;
+  int bp = -1;
+  const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * 6);
+  for (int k = 0; k < pcount; ++k, P += 6) {
+    const float4 q0 = f4(P[0]), q1 = f4(P[1]);
+    float tt;
+    if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE)
+      tt = sphere_test(r.o, r.d, q0, q1);
+    else
+      tt = tri_test(r.o, r.d, q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), bt);
+    if (tt >= 0.0f && (tt < bt || (tt == bt && bp < 0))) {
+      bt = tt;
+      bp = pstart + k;
+    }
+  }
+  prim = bp < 0 ? PT_PRIM_NONE : (uint32_t)bp;
+  t = bt;
+}
+
+// any primitive at t in [0, tmax]
+__device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, int pcount, const RayV& r) {
+  const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * 6);
+  bool hit = false;
+  for (int k = 0; k < pcount; ++k, P += 6) {
+    const float4 q0 = f4(P[0]), q1 = f4(P[1]);
+    float tt;
+    if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE)
+      tt = sphere_test(r.o, r.d, q0, q1);
+    else
+      tt = tri_test(r.o, r.d, q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), r.tmax);
+    hit = hit || (tt >= 0.0f && tt <= r.tmax);
+    if (!__any(!hit)) break;  // every active lane is occluded
+  }
+  return hit;
+}
+
+__global__ __launch_bounds__(TPB) void k_path_leaf(ShadeArgs S, int pstart, int pcount, int passes,
+                                                   unsigned long long* __restrict__ rcount) {
+  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
+  uint32_t nrays = 0;
+  if (p < S.N) {
+    PathState st;
+    const f3 dir = camera_dir(S, p, st.g);
+    st.T = mk(1.0f, 1.0f, 1.0f);
+    st.L = mk(0.0f, 0.0f, 0.0f);
+    st.flags = F_EXT | (1u << 8);
+    RayV ext{ld3(S.cam.origin), dir, __builtin_inff()}, shr{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
+    f3 C = mk(0, 0, 0);
+    const uint32_t sidx = S.sample_base + p / S.npix;
+    for (int pass = 0; pass < passes && (st.flags & (F_EXT | F_SHADOW)); ++pass) {
+      uint32_t prim = PT_PRIM_NONE;
+      float t = 0.0f;
+      if (st.flags & F_EXT) {
+        leaf_closest(S.prims, pstart, pcount, ext, prim, t);
+        nrays++;
+      }
+      bool clear = false;
+      if (st.flags & F_SHADOW) {
+        clear = !leaf_occluded(S.prims, pstart, pcount, shr);
+        nrays++;
+      }
+      bool new_ext, new_sh;
+      RayV e2, s2;
+      shade_vertex(S, sidx, st, ext.o, ext.d, prim, t, clear, C, new_ext, e2, new_sh, s2);
+      if (new_ext) ext = e2;
+      if (new_sh) shr = s2;
+    }
+    S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(st.g));
+  }
+  // rays traced (R): one fire-and-forget atomic per wave into its lane's counter
+  const uint32_t w = wave_sum(nrays);
+  if ((threadIdx.x & 63) == 0 && w) atomicAdd(rcount + (size_t)(blockIdx.x & (NLANE - 1)) * 16, (unsigned long long)w);
 }
 
 // Sum each owned pixel's samples of this batch into the accumulation buffer,

@@ -84,7 +84,7 @@ struct pt_ctx {
   hipEvent_t ev[8] = {};
 
   // kernel timing with a pool of events, read back once per render
-  enum { K_CAM, K_ROOT, K_SCAN, K_LEVEL, K_SHADE, K_ACCUM };
+  enum { K_CAM, K_ROOT, K_SCAN, K_LEVEL, K_SHADE, K_ACCUM, K_PATH };
   struct Mark {
     int cls, level;
     size_t e0, e1;
@@ -280,6 +280,10 @@ static void collect_marks(pt_ctx* c) {
           c->stats.level_launches[m.level]++;
         }
         c->stats.ms_trace += ms;
+        break;
+      case pt_ctx::K_PATH:
+        c->stats.ms_path += ms;
+        c->stats.path_launches++;
         break;
       default:
         c->stats.ms_shade += ms;
@@ -542,9 +546,17 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.N = N;
     S.sample_base = (uint32_t)(P->sample_offset + done);
     const dim3 grid((N + TPB - 1) / TPB);
-    c->launch(pt_ctx::K_CAM, 0, k_camera, grid, dim3(TPB), S);
     const int passes = P->max_bounces + 2;
-    for (int pass = 0; pass < passes; ++pass) {
+    if (c->root_leaf) {
+      // single-leaf tree: every path runs to completion in one kernel
+      const pt_node& root = c->nodes_host[0];
+      c->launch(pt_ctx::K_PATH, 0, k_path_leaf, grid, dim3(TPB), S, root.prim_start, root.prim_count, passes,
+                c->d_rcount);
+      c->stats.passes += passes;
+    } else {
+      c->launch(pt_ctx::K_CAM, 0, k_camera, grid, dim3(TPB), S);
+    }
+    for (int pass = 0; pass < passes && !c->root_leaf; ++pass) {
       // pass 0: camera rays only; last pass: shadow rays only
       const uint32_t r0 = (pass == passes - 1) ? N : 0;
       const uint32_t r1 = (pass == 0) ? N : 2 * N;

@@ -33,6 +33,7 @@ PT_FLAG_NO_EMISSION = 0x2
 PT_FLAG_STATS = 0x4
 PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION = 0, 1, 2, 3
 PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT = 0, 1, 2
+PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1
 
 
 class pt_prim(C.Structure):
@@ -90,7 +91,8 @@ class pt_stats(C.Structure):
                 ("ms_level", C.c_double * 16), ("level_launches", C.c_uint64 * 16),
                 ("level_visits", C.c_uint64 * 16), ("level_leaf_visits", C.c_uint64 * 16),
                 ("level_items", C.c_uint64 * 16), ("root_launches", C.c_uint64),
-                ("peak_queue_entries", C.c_uint64), ("n_levels", C.c_int32), ("batch_paths", C.c_int32)]
+                ("peak_queue_entries", C.c_uint64), ("n_levels", C.c_int32), ("batch_paths", C.c_int32),
+                ("ms_path", C.c_double), ("path_launches", C.c_uint64)]
 
 
 # every symbol include/pt_api.h declares (tests check the library exports them)

@@ -257,6 +257,8 @@ typedef struct pt_stats {
   uint64_t peak_queue_entries;
   int32_t n_levels;
   int32_t batch_paths;
+  double ms_path;     /* k_path_leaf: whole paths of single-leaf scenes     */
+  uint64_t path_launches;
 } pt_stats;
 int pt_get_stats(pt_ctx* ctx, pt_stats* out);
 int pt_reset_stats(pt_ctx* ctx);
