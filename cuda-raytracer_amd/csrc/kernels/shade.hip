@@ -37,6 +37,8 @@ struct ShadeArgs {
   uint32_t N, npix, sample_base, seed;
   int width, height, max_bounces;
   uint32_t flags;
+  TraceArgs A;                   // fused root pass (camera/shade push into the root's target queues)
+  unsigned long long* rcount;    // rays entering the traversal (RCOUNT_SLOTS counters)
 };
 
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -260,9 +262,11 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
   shr.tmax = sh_tmax;
 }
 
-__global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
-  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
-  if (p >= S.N) return;
+// Shade path p: read its state, hit words and rays, run shade_vertex, write
+// the new state and ray records.  Returns the new rays in registers.
+__device__ __forceinline__ void shade_slot(const ShadeArgs& S, uint32_t p, bool& new_ext, RayV& ext, bool& new_sh,
+                                           RayV& shr) {
+  new_ext = new_sh = false;
   const float4 s0 = S.ps0[p];
   const uint32_t flags = __float_as_uint(s0.w);
   if ((flags & (F_EXT | F_SHADOW)) == 0) return;
@@ -288,8 +292,6 @@ __global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
       d = mk(r0.w, r1.x, r1.y);
     }
   }
-  bool new_ext, new_sh;
-  RayV ext, shr;
   shade_vertex(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
   S.ps0[p] = make_float4(st.T.x, st.T.y, st.T.z, __uint_as_float(st.flags));
   S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(st.g));
@@ -306,6 +308,67 @@ __global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
   } else {
     S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
   }
+}
+
+__global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
+  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
+  if (p >= S.N) return;
+  bool new_ext, new_sh;
+  RayV ext, shr;
+  shade_slot(S, p, new_ext, ext, new_sh, shr);
+}
+
+// One fire-and-forget atomic per workgroup: rays that enter the traversal.
+__device__ __forceinline__ void count_rays(unsigned long long* rcount, uint32_t v, uint32_t* sh4) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh4[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = sh4[0] + sh4[1] + sh4[2] + sh4[3];
+    if (t) atomicAdd(rcount + (size_t)(blockIdx.x & (RCOUNT_SLOTS - 1)) * 16, (unsigned long long)t);
+  }
+}
+
+// Fused root pass: the new rays never take the trip through HBM and back to
+// be tested against the root -- the producing kernel tests them against the
+// root's NC target boxes (4 children, or 16 grandchildren when level 1 is
+// skipped) and pushes their ids into those queues (lane = workgroup & 7).
+template <int NC>
+__global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
+  __shared__ uint32_t sh[NC * 8 + 4];
+  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
+  const bool live = p < S.N;
+  uint32_t id[1] = {p};
+  f3 o[1] = {ld3(S.cam.origin)}, d[1] = {mk(0.f, 0.f, 1.f)};
+  float tm[1] = {__builtin_inff()};
+  bool valid[1] = {live};
+  if (live) {
+    uint32_t g;
+    d[0] = camera_dir(S, p, g);
+    S.ray[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], d[0].x);
+    S.ray[RSTRIDE * p + 1] = rec_r1(d[0].y, d[0].z, __builtin_inff());
+    S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
+    S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
+    S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
+    S.ps2[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  push_children<1, NC>(S.A, (const CPTR(pt_node))S.A.nodes, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, 1, sh);
+  count_rays(S.rcount, live ? 1u : 0u, sh + NC * 8);
+}
+
+template <int NC>
+__global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
+  __shared__ uint32_t sh[NC * 8 + 4];
+  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
+  bool new_ext = false, new_sh = false;
+  RayV ext{mk(0, 0, 0), mk(0, 0, 1), -1.0f}, shr{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
+  if (p < S.N) shade_slot(S, p, new_ext, ext, new_sh, shr);
+  uint32_t id[2] = {p, S.N + p};
+  f3 o[2] = {ext.o, shr.o}, d[2] = {ext.d, shr.d};
+  float tm[2] = {__builtin_inff(), shr.tmax};
+  bool valid[2] = {new_ext, new_sh};
+  push_children<2, NC>(S.A, (const CPTR(pt_node))S.A.nodes, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, 2, sh);
+  count_rays(S.rcount, (new_ext ? 1u : 0u) + (new_sh ? 1u : 0u), sh + NC * 8);
 }
 
 // ---- scenes whose BVH root is a leaf -----------------------------------------
@@ -388,7 +451,8 @@ __global__ __launch_bounds__(TPB) void k_path_leaf(ShadeArgs S, int pstart, int 
   }
   // rays traced (R): one fire-and-forget atomic per wave into its lane's counter
   const uint32_t w = wave_sum(nrays);
-  if ((threadIdx.x & 63) == 0 && w) atomicAdd(rcount + (size_t)(blockIdx.x & (NLANE - 1)) * 16, (unsigned long long)w);
+  if ((threadIdx.x & 63) == 0 && w)
+    atomicAdd(rcount + (size_t)((blockIdx.x * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16, (unsigned long long)w);
 }
 
 // Sum each owned pixel's samples of this batch into the accumulation buffer,

@@ -31,7 +31,8 @@ constexpr int NLANE = 8;          // queue lanes (one per XCD)
 constexpr int CSTRIDE = 32;       // u32 per queue counter: each (node, lane) counter owns a 128-B line
 constexpr uint32_t MODE_WAVE = 0, MODE_BLOCK = 1;
 constexpr uint32_t BLOCK_MODE_RAYS_PER_PAIR = 512;  // level mode threshold (mean rays per queue lane)
-constexpr int LEVEL_GRID = 2048;  // workgroups of the per-level grid-stride kernel (8 per CU)
+constexpr int LEVEL_GRID = 2048;
+constexpr int RCOUNT_SLOTS = 64;  // ray counters (u64, 128 B apart), indexed by workgroup & 63  // workgroups of the per-level grid-stride kernel (8 per CU)
 
 // device statistics slots (unsigned long long)
 enum {

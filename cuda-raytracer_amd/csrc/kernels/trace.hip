@@ -125,6 +125,82 @@ __device__ __forceinline__ const CPTR(pt_node) child_slot(const TraceArgs& A, co
   return (const CPTR(pt_node))(A.nodes + nd->child[c >> 2]);
 }
 
+// Block-wide push of R rays per thread into the queues of NC children (or
+// grandchildren) of node nd in queue lane `lane`: slab tests, wave64 ballot
+// compaction, one atomic slot reservation per child for the whole workgroup,
+// cross-wave offsets through LDS (sh: NC * 8 u32).  Every thread of the
+// workgroup must call it (two barriers); rays with valid[j] false push nothing,
+// ray groups j >= nj (uniform) are skipped.
+template <int R, int NC>
+__device__ __forceinline__ void push_children(const TraceArgs& A, const CPTR(pt_node) nd, int lane,
+                                              const uint32_t (&id)[R], const f3 (&o)[R], const f3 (&d)[R],
+                                              const float (&tmax)[R], const bool (&valid)[R], int nj,
+                                              uint32_t* sh) {
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  uint32_t bits[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    bits[j] = 0;
+    if (j >= nj) continue;
+    // |d| components below 1e-20 are clamped so 1/d stays finite: the FMA slab
+    // form t = b*inv - o*inv would turn an axis-parallel ray (inv = inf) lying
+    // inside a slab into inf - inf = NaN and wrongly miss the box
+    f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
+                __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
+    f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
+    uint32_t b = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      int k;
+      const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
+      bool h = box_hit(cn->bmin_x[k], cn->bmax_x[k], cn->bmin_y[k], cn->bmax_y[k], cn->bmin_z[k], cn->bmax_z[k],
+                       oi, inv, tmax[j]);
+      b |= (valid[j] && h) ? (1u << c) : 0u;
+    }
+    bits[j] = b;
+  }
+  // per-wave counts per child -> LDS sh[c*4 + wave]; bases -> sh[NC*4 + c*4 + wave]
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    uint32_t wc = 0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) wc += (uint32_t)__popcll(__ballot((bits[j] >> c) & 1u));
+    if ((tid & 63) == 0) sh[c * 4 + wave] = wc;
+  }
+  __syncthreads();
+  if (tid < NC) {
+    const int c = tid;
+    int k;
+    const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
+    const int child = cn->child[k];
+    uint32_t w0 = sh[c * 4 + 0], w1 = sh[c * 4 + 1], w2 = sh[c * 4 + 2], w3 = sh[c * 4 + 3];
+    uint32_t tot = w0 + w1 + w2 + w3;
+    uint32_t b = 0;
+    if (child >= 0 && tot) b = atomicAdd(A.cnt + cnt_idx(child, lane), tot);
+    sh[NC * 4 + c * 4 + 0] = b;
+    sh[NC * 4 + c * 4 + 1] = b + w0;
+    sh[NC * 4 + c * 4 + 2] = b + w0 + w1;
+    sh[NC * 4 + c * 4 + 3] = b + w0 + w1 + w2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    int k;
+    const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
+    const int child = cn->child[k];
+    if (child < 0) continue;
+    uint32_t off = sh[NC * 4 + c * 4 + wave] + A.qoff[(size_t)child * NLANE + lane];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const bool h = (bits[j] >> c) & 1u;
+      const unsigned long long m = __ballot(h);
+      if (h) A.q[off + mbcnt64(m)] = id[j];
+      off += (uint32_t)__popcll(m);
+    }
+  }
+}
+
 template <bool IMPLICIT, int NC = 4>
 __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, uint32_t base, int n, int lane,
                                              uint32_t* sh) {
@@ -216,67 +292,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
   }
 
   // ---------------- interior: NC child boxes, compaction, push ----------------
-  uint32_t bits[RPT];
-#pragma unroll
-  for (int j = 0; j < RPT; ++j) {
-    bits[j] = 0;
-    if (j >= nj) continue;
-    // |d| components below 1e-20 are clamped so 1/d stays finite: the FMA slab
-    // form t = b*inv - o*inv would turn an axis-parallel ray (inv = inf) lying
-    // inside a slab into inf - inf = NaN and wrongly miss the box
-    f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
-                __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
-    f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
-    uint32_t b = 0;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      int k;
-      const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
-      bool h = box_hit(cn->bmin_x[k], cn->bmax_x[k], cn->bmin_y[k], cn->bmax_y[k], cn->bmin_z[k], cn->bmax_z[k],
-                       oi, inv, tmax[j]);
-      b |= (valid[j] && h) ? (1u << c) : 0u;
-    }
-    bits[j] = b;
-  }
-  // per-wave counts per child -> LDS sh[c*4 + wave]; bases -> sh[NC*4 + c*4 + wave]
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    uint32_t wc = 0;
-#pragma unroll
-    for (int j = 0; j < RPT; ++j) wc += (uint32_t)__popcll(__ballot((bits[j] >> c) & 1u));
-    if ((tid & 63) == 0) sh[c * 4 + wave] = wc;
-  }
-  __syncthreads();
-  if (tid < NC) {
-    const int c = tid;
-    int k;
-    const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
-    const int child = cn->child[k];
-    uint32_t w0 = sh[c * 4 + 0], w1 = sh[c * 4 + 1], w2 = sh[c * 4 + 2], w3 = sh[c * 4 + 3];
-    uint32_t tot = w0 + w1 + w2 + w3;
-    uint32_t b = 0;
-    if (child >= 0 && tot) b = atomicAdd(A.cnt + cnt_idx(child, lane), tot);
-    sh[NC * 4 + c * 4 + 0] = b;
-    sh[NC * 4 + c * 4 + 1] = b + w0;
-    sh[NC * 4 + c * 4 + 2] = b + w0 + w1;
-    sh[NC * 4 + c * 4 + 3] = b + w0 + w1 + w2;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    int k;
-    const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
-    const int child = cn->child[k];
-    if (child < 0) continue;
-    uint32_t off = sh[NC * 4 + c * 4 + wave] + A.qoff[(size_t)child * NLANE + lane];
-#pragma unroll
-    for (int j = 0; j < RPT; ++j) {
-      const bool h = (bits[j] >> c) & 1u;
-      const unsigned long long m = __ballot(h);
-      if (h) A.q[off + mbcnt64(m)] = id[j];
-      off += (uint32_t)__popcll(m);
-    }
-  }
+  push_children<RPT, NC>(A, nd, lane, id, o, d, tmax, valid, nj, sh);
   return nvalid;
 }
 
@@ -299,7 +315,7 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, uint32_t r0, ui
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t t = sh[NC * 8] + sh[NC * 8 + 1] + sh[NC * 8 + 2] + sh[NC * 8 + 3];
-    if (t) atomicAdd(rcount + (size_t)lane * 16, (unsigned long long)t);
+    if (t) atomicAdd(rcount + (size_t)(item & (RCOUNT_SLOTS - 1)) * 16, (unsigned long long)t);
   }
 }
 

@@ -69,7 +69,7 @@ struct pt_ctx {
   uint32_t* d_iprefix = nullptr;
   uint32_t* d_nitems = nullptr;  // one per level
   uint32_t* d_icnt = nullptr;
-  unsigned long long* d_rcount = nullptr;  // valid root rays, one 128-B line per lane
+  unsigned long long* d_rcount = nullptr;  // valid root rays: RCOUNT_SLOTS counters, one 128-B line each
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
 
@@ -224,17 +224,11 @@ static TraceArgs trace_args(pt_ctx* c) {
   return A;
 }
 
-// One breadth-first traversal pass over ray slots [r0, r1).
-static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
-  if (r1 <= r0) return PT_OK;
+// The per-level part of a traversal pass: { k_scan_level ; k_trace_level } for
+// every level below the root's targets (the root pass itself is k_trace_root
+// or fused into k_camera_push / k_shade_push).
+static int trace_levels(pt_ctx* c) {
   TraceArgs A = trace_args(c);
-  const uint32_t items = (r1 - r0 + TILE - 1) / TILE;
-  // the (node, lane) counters are zero here: each level's scan re-zeroes them
-  // after taking its snapshot (pt_load_scene zeroes them once)
-  if (c->skip_l1)
-    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<16>, dim3(items), dim3(TPB), A, r0, r1, c->d_rcount);
-  else
-    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<4>, dim3(items), dim3(TPB), A, r0, r1, c->d_rcount);
   const size_t lanecap = c->qcap / NLANE;
   for (int l = c->skip_l1 ? 2 : 1; l < c->n_levels; ++l) {
     LevelArgs L;
@@ -257,6 +251,25 @@ static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
   HIPCHK(c, hipGetLastError());
   c->stats.passes++;
   return PT_OK;
+}
+
+// One breadth-first traversal pass over ray slots [r0, r1) (pt_intersect).
+static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
+  if (r1 <= r0) return PT_OK;
+  TraceArgs A = trace_args(c);
+  const uint32_t items = (r1 - r0 + TILE - 1) / TILE;
+  // the (node, lane) counters are zero here: each level's scan re-zeroes them
+  // after taking its snapshot (pt_load_scene zeroes them once)
+  if (c->skip_l1)
+    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<16>, dim3(items), dim3(TPB), A, r0, r1, c->d_rcount);
+  else
+    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<4>, dim3(items), dim3(TPB), A, r0, r1, c->d_rcount);
+  if (c->root_leaf) {
+    HIPCHK(c, hipGetLastError());
+    c->stats.passes++;
+    return PT_OK;
+  }
+  return trace_levels(c);
 }
 
 // Fold the recorded kernel intervals into the stats (after the stream is idle).
@@ -297,13 +310,13 @@ static void collect_marks(pt_ctx* c) {
 static int read_device_stats(pt_ctx* c) {
   unsigned long long st[STAT_COUNT];
   uint32_t e = 0;
-  unsigned long long rl[NLANE * 16];
+  unsigned long long rl[RCOUNT_SLOTS * 16];
   HIPCHK(c, hipMemcpyAsync(st, c->d_stats, sizeof(st), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(rl, c->d_rcount, sizeof(rl), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   unsigned long long R = 0;
-  for (int s = 0; s < NLANE; ++s) R += rl[s * 16];
+  for (int s = 0; s < RCOUNT_SLOTS; ++s) R += rl[s * 16];
   c->stats.rays = R;
   c->stats.visits = st[STAT_V] + R;
   st[STAT_LV0] += R;
@@ -356,13 +369,13 @@ int pt_create(pt_ctx** out, int device) {
   }
   for (auto& e : c->ev) hipEventCreate(&e);
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
-      hipMalloc((void**)&c->d_rcount, NLANE * 16 * 8) != hipSuccess ||
+      hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_err, 4) != hipSuccess) {
     delete c;
     return PT_E_HIP;
   }
   hipMemset(c->d_stats, 0, STAT_COUNT * 8);
-  hipMemset(c->d_rcount, 0, NLANE * 16 * 8);
+  hipMemset(c->d_rcount, 0, RCOUNT_SLOTS * 16 * 8);
   hipMemset(c->d_err, 0, 4);
   *out = c;
   return PT_OK;
@@ -458,7 +471,7 @@ int pt_reset_stats(pt_ctx* c) {
   if (!c) return PT_E_INVALID;
   hipSetDevice(c->device);
   HIPCHK(c, hipMemset(c->d_stats, 0, STAT_COUNT * 8));
-  HIPCHK(c, hipMemset(c->d_rcount, 0, NLANE * 16 * 8));
+  HIPCHK(c, hipMemset(c->d_rcount, 0, RCOUNT_SLOTS * 16 * 8));
   memset(&c->stats, 0, sizeof(c->stats));
   return PT_OK;
 }
@@ -537,6 +550,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   S.height = P->height;
   S.max_bounces = P->max_bounces;
   S.flags = P->flags;
+  S.A = trace_args(c);
+  S.rcount = c->d_rcount;
 
   hipEvent_t t0 = c->ev[6], t1 = c->ev[7];
   HIPCHK(c, hipEventRecord(t0, c->stream));
@@ -554,14 +569,22 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
                 c->d_rcount);
       c->stats.passes += passes;
     } else {
-      c->launch(pt_ctx::K_CAM, 0, k_camera, grid, dim3(TPB), S);
-    }
-    for (int pass = 0; pass < passes && !c->root_leaf; ++pass) {
-      // pass 0: camera rays only; last pass: shadow rays only
-      const uint32_t r0 = (pass == passes - 1) ? N : 0;
-      const uint32_t r1 = (pass == 0) ? N : 2 * N;
-      if ((rc = trace_pass(c, r0, r1))) return rc;
-      c->launch(pt_ctx::K_SHADE, 0, k_shade, grid, dim3(TPB), S);
+      // camera rays enter the root's target queues directly; each pass traces
+      // the levels below, then shading pushes the next rays (none after the
+      // last pass: its shade only resolves the final shadow rays)
+      if (c->skip_l1)
+        c->launch(pt_ctx::K_CAM, 0, k_camera_push<16>, grid, dim3(TPB), S);
+      else
+        c->launch(pt_ctx::K_CAM, 0, k_camera_push<4>, grid, dim3(TPB), S);
+      for (int pass = 0; pass < passes; ++pass) {
+        if ((rc = trace_levels(c))) return rc;
+        if (pass == passes - 1)
+          c->launch(pt_ctx::K_SHADE, 0, k_shade, grid, dim3(TPB), S);
+        else if (c->skip_l1)
+          c->launch(pt_ctx::K_SHADE, 0, k_shade_push<16>, grid, dim3(TPB), S);
+        else
+          c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4>, grid, dim3(TPB), S);
+      }
     }
     c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_ps1,
               c->d_accum, npix, sb);

@@ -2,6 +2,7 @@
 """Summarise rocprofv3 --pmc passes per kernel (and per traversal level).
 
   python scripts/pmc_summary.py <run_counter_collection.csv>... [--levels L]
+                                 [--json OUT --config "what was run"]
 
 FETCH_SIZE and WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE counts 128-B
 memory-side requests at 64 B (MI355X_MICROARCH.md, HBM section), so the
@@ -20,13 +21,16 @@ def short(name):
 
 def main():
     args = sys.argv[1:]
-    levels = 0
-    if "--levels" in args:
-        i = args.index("--levels")
-        levels = int(args[i + 1])
-        del args[i:i + 2]
+    opts = {}
+    for o in ("--levels", "--json", "--config"):
+        if o in args:
+            i = args.index(o)
+            opts[o] = args[i + 1]
+            del args[i:i + 2]
+    levels = int(opts.get("--levels", 0))
     agg = defaultdict(lambda: defaultdict(float))  # key -> counter -> value
     ndisp = defaultdict(set)
+    per_file = defaultdict(dict)  # key -> path -> dispatch ids
     for path in args:
         rows = []
         with open(path) as f:
@@ -54,11 +58,30 @@ def main():
             for key in keys:
                 agg[key][c] += v
                 ndisp[key].add((path, d))
+                per_file[key].setdefault(path, set()).add(d)
     counters = sorted({c for a in agg.values() for c in a})
     print(f"{'kernel':22s} {'disp':>5s} " + " ".join(f"{c[:16]:>16s}" for c in counters))
     for key in sorted(agg, key=lambda k: (k.split("[")[0], k)):
         a = agg[key]
         print(f"{key:22s} {len(ndisp[key]):5d} " + " ".join(f"{a.get(c, 0):16.4g}" for c in counters))
+    if "--json" in opts:
+        import json
+        ker = {}
+        for key, a in agg.items():
+            n = max(len(v) for v in per_file[key].values())
+            e = {"dispatches": n}
+            if "READ_GB" in a and "WRITE_GB" in a:
+                e["read_bytes_per_launch"] = int(a["READ_GB"] * 1e9 / n)
+                e["write_bytes_per_launch"] = int(a["WRITE_GB"] * 1e9 / n)
+                e["hbm_bytes_per_launch"] = e["read_bytes_per_launch"] + e["write_bytes_per_launch"]
+            for c, v in a.items():
+                if c not in ("READ_GB", "WRITE_GB"):
+                    e[c] = v
+            ker[key] = e
+        with open(opts["--json"], "w") as f:
+            json.dump({"config": opts.get("--config", ""), "files": [str(p) for p in args],
+                       "correction": "read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE; KiB -> bytes",
+                       "kernels": ker}, f, indent=1)
 
 
 if __name__ == "__main__":
