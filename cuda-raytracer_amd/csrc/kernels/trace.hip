@@ -68,6 +68,45 @@ __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q
   return t == 0.0f ? 0.0f : t;
 }
 
+// Two independent triangle tests at once on packed fp32 (v_pk_mul_f32 /
+// v_pk_add_f32): element i is exactly tri_test(o[i], d[i], q..., tbest[i])
+// (same operations in the same order, so the same bits), written without
+// branches so both halves share every instruction.  Used for two rays against
+// one triangle (leaf loops) or one ray against two triangles (k_path_leaf).
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct f3x2 {
+  f2v x, y, z;
+};
+__device__ __forceinline__ f2v sp(float a) { return f2v{a, a}; }
+__device__ __forceinline__ f3x2 sp3(float a, float b, float c) { return f3x2{sp(a), sp(b), sp(c)}; }
+__device__ __forceinline__ f3x2 pair3(f3 a, f3 b) { return f3x2{f2v{a.x, b.x}, f2v{a.y, b.y}, f2v{a.z, b.z}}; }
+
+__device__ __forceinline__ f2v edge_side2(const f3x2& N, const f3x2& P, const f3x2& v, const f3x2& e) {
+  const f2v vx = P.x - v.x, vy = P.y - v.y, vz = P.z - v.z;
+  const f2v cx = e.y * vz - e.z * vy, cy = e.z * vx - e.x * vz, cz = e.x * vy - e.y * vx;
+  return N.x * cx + N.y * cy + N.z * cz;
+}
+
+// N: normal, pd: plane offset, v0..v2: vertices, e0..e2: edges (pt_prim layout)
+__device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const f3x2& N, f2v pd, const f3x2& v0,
+                                         const f3x2& v1, const f3x2& v2, const f3x2& e0, const f3x2& e1,
+                                         const f3x2& e2, f2v tbest) {
+  const f2v ndd = N.x * d.x + N.y * d.y + N.z * d.z;
+  const f2v t = (pd - (N.x * o.x + N.y * o.y + N.z * o.z)) / ndd;
+  const f3x2 P{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z};
+  const f2v s0 = edge_side2(N, P, v0, e0);
+  const f2v s1 = edge_side2(N, P, v1, e1);
+  const f2v s2 = edge_side2(N, P, v2, e2);
+  f2v r;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const bool miss = fabsf(ndd[i]) < 1e-6f || t[i] < 0.0f || t[i] > tbest[i] || s0[i] < 0.0f || s1[i] < 0.0f ||
+                      s2[i] < 0.0f;
+    r[i] = miss ? -1.0f : (t[i] == 0.0f ? 0.0f : t[i]);
+  }
+  return r;
+}
+
 // Ray-sphere (the reference has none: spheres are reinterpret_cast to
 // triangles at cu:1760).  Nearest root with t >= 0; d must be unit length.
 __device__ __forceinline__ float sphere_test(const f3 o, const f3 d, const float4 q0, const float4 q1) {
@@ -267,13 +306,21 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
         }
       } else {
         const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
+        const f3x2 N = sp3(q3.x, q3.y, q3.z), v0 = sp3(q0.x, q0.y, q0.z), v1 = sp3(q1.x, q1.y, q1.z),
+                   v2 = sp3(q2.x, q2.y, q2.z), e0 = sp3(q4.x, q4.y, q4.z), e1 = sp3(q5.x, q5.y, q5.z),
+                   e2 = sp3(q2.w, q3.w, q4.w);
 #pragma unroll
-        for (int j = 0; j < RPT; ++j) {
+        for (int j = 0; j < RPT; j += 2) {
           if (j >= nj) break;
-          float t = tri_test(o[j], d[j], q0, q1, q2, q3, q4, q5, bt[j]);
-          if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
-            bt[j] = t;
-            bp[j] = pstart + k;
+          const f2v t2 = tri_test2(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
+                                   e2, f2v{bt[j], bt[j + 1]});
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const float t = t2[i];
+            if (valid[j + i] && t >= 0.0f && (t < bt[j + i] || (t == bt[j + i] && bp[j + i] < 0))) {
+              bt[j + i] = t;
+              bp[j + i] = pstart + k;
+            }
           }
         }
       }
@@ -374,13 +421,21 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
         }
       } else {
         const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
+        const f3x2 N = sp3(q3.x, q3.y, q3.z), v0 = sp3(q0.x, q0.y, q0.z), v1 = sp3(q1.x, q1.y, q1.z),
+                   v2 = sp3(q2.x, q2.y, q2.z), e0 = sp3(q4.x, q4.y, q4.z), e1 = sp3(q5.x, q5.y, q5.z),
+                   e2 = sp3(q2.w, q3.w, q4.w);
 #pragma unroll
-        for (int j = 0; j < RPTW; ++j) {
+        for (int j = 0; j < RPTW; j += 2) {
           if (j >= nj) break;
-          float t = tri_test(o[j], d[j], q0, q1, q2, q3, q4, q5, bt[j]);
-          if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
-            bt[j] = t;
-            bp[j] = pstart + k;
+          const f2v t2 = tri_test2(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
+                                   e2, f2v{bt[j], bt[j + 1]});
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const float t = t2[i];
+            if (valid[j + i] && t >= 0.0f && (t < bt[j + i] || (t == bt[j + i] && bp[j + i] < 0))) {
+              bt[j + i] = t;
+              bp[j + i] = pstart + k;
+            }
           }
         }
       }
