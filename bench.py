@@ -5,8 +5,9 @@ tracer at 1024x1024, 256 spp, 8 bounces (BASELINE.json metric), on N GPUs.
 The headline workload is BASELINE.json configs[1]:
 the diffuse Cornell box CBempty.dae.  The same JSON line carries the other
 single-GPU configs of the metric (config 3: CBspheres, glass + mirror; config
-4: CBbunny, 28,588 triangles, deep wide BVH) measured the same way in the same
-run, under "configs".
+4: CBbunny, 28,588 triangles, deep wide BVH, and the ~100k-triangle dragon
+proxy of cuda-raytracer_amd/scenes.py) measured the same way in the same run,
+under "configs".
 
 A step is one full frame: every rank renders its interleaved 32x32 tiles of the
 1024x1024 image at 256 spp (strong scaling: the frame is fixed, ranks split it),
@@ -54,7 +55,7 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scene", default="CBempty", help="headline scene (configs[1] = CBempty)")
-    p.add_argument("--configs", default="CBspheres,CBbunny",
+    p.add_argument("--configs", default="CBspheres,CBbunny,dragon_proxy",
                    help="other single-GPU configs measured in the same run ('' = none)")
     p.add_argument("--width", type=int, default=1024)
     p.add_argument("--height", type=int, default=1024)
@@ -128,7 +129,8 @@ def run_workload(name, args, ctx, rank, world, dev, dist):
     import torch
     import ptrace
     import ptdist
-    scene = ptrace.ArrayScene.load(ROOT / "tests" / "golden" / "scenes" / f"{name}.npz")
+    import scenes
+    scene = scenes.load(name)
     ctx.load_scene(scene)
     desc = scene.desc()
 
@@ -250,7 +252,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"scene {args.scene}.dae (reference media, flattened fixture); rays sampled with Philox seed {args.seed}",
+            "data": f"scene {args.scene} (reference media, flattened fixture); rays sampled with Philox seed {args.seed}",
             "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.spp}spp {args.bounces} bounces",
                        "scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
                        "max_bounces": args.bounces, "batch_paths": head["batch_paths"],

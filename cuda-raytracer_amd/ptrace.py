@@ -95,9 +95,16 @@ class pt_stats(C.Structure):
                 ("ms_path", C.c_double), ("path_launches", C.c_uint64)]
 
 
+class pt_mesh_desc(C.Structure):
+    _fields_ = [("n_tris", C.c_int32), ("positions", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)),
+                ("tri_bsdf", C.POINTER(C.c_int32)), ("n_spheres", C.c_int32), ("spheres", C.POINTER(C.c_float)),
+                ("sphere_bsdf", C.POINTER(C.c_int32)), ("n_bsdfs", C.c_int32), ("bsdfs", C.POINTER(pt_bsdf)),
+                ("light", C.POINTER(pt_light)), ("camera", C.POINTER(pt_camera))]
+
+
 # every symbol include/pt_api.h declares (tests check the library exports them)
 API_SYMBOLS = [
-    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_free", "pt_scene_get_desc",
+    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_free", "pt_scene_get_desc",
     "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
     "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect",
@@ -123,6 +130,7 @@ def _load():
         "pt_scene_load_dae": (C.c_int, [C.c_char_p, C.POINTER(P), C.c_char_p, SZ]),
         "pt_scene_from_triangles": (C.c_int, [C.POINTER(C.c_float), I32, C.POINTER(pt_bsdf),
                                               C.POINTER(pt_light), C.POINTER(pt_camera), C.POINTER(P)]),
+        "pt_scene_from_mesh": (C.c_int, [C.POINTER(pt_mesh_desc), C.POINTER(P)]),
         "pt_scene_free": (None, [P]),
         "pt_scene_get_desc": (C.c_int, [P, C.POINTER(pt_scene_desc)]),
         "pt_scene_level_counts": (C.c_int, [P, C.POINTER(I32), I32, C.POINTER(I32)]),
@@ -187,6 +195,45 @@ class Scene:
                                          C.byref(camera) if camera else None, C.byref(h))
         if rc != PT_OK:
             raise PTError(rc, "pt_scene_from_triangles failed")
+        return cls(h)
+
+    @classmethod
+    def from_mesh(cls, positions, bsdfs, normals=None, tri_bsdf=None, spheres=None, sphere_bsdf=None,
+                  light=None, camera=None):
+        """General flattened input (pt_scene_from_mesh): triangles (n, 9),
+        optional vertex normals (n, 9), per-triangle bsdf ids, spheres (m, 4)
+        and a list of pt_bsdf."""
+        keep = []
+
+        def arr(a, dt, k):
+            if a is None:
+                return None
+            a = np.ascontiguousarray(a, dtype=dt).reshape(-1, k) if k else np.ascontiguousarray(a, dtype=dt)
+            keep.append(a)
+            return a
+
+        pos = arr(positions, np.float32, 9)
+        nrm = arr(normals, np.float32, 9)
+        tb = arr(tri_bsdf, np.int32, 0)
+        sph = arr(spheres, np.float32, 4)
+        sb = arr(sphere_bsdf, np.int32, 0)
+        bt = (pt_bsdf * len(bsdfs))(*bsdfs)
+        m = pt_mesh_desc()
+        m.n_tris = 0 if pos is None else len(pos)
+        m.positions = _ptr(pos, C.c_float) if pos is not None else None
+        m.normals = _ptr(nrm, C.c_float) if nrm is not None else None
+        m.tri_bsdf = _ptr(tb, C.c_int32) if tb is not None else None
+        m.n_spheres = 0 if sph is None else len(sph)
+        m.spheres = _ptr(sph, C.c_float) if sph is not None else None
+        m.sphere_bsdf = _ptr(sb, C.c_int32) if sb is not None else None
+        m.n_bsdfs = len(bsdfs)
+        m.bsdfs = C.cast(bt, C.POINTER(pt_bsdf))
+        m.light = C.pointer(light) if light is not None else None
+        m.camera = C.pointer(camera) if camera is not None else None
+        h = C.c_void_p()
+        rc = LIB.pt_scene_from_mesh(C.byref(m), C.byref(h))
+        if rc != PT_OK:
+            raise PTError(rc, "pt_scene_from_mesh failed")
         return cls(h)
 
     def __del__(self):

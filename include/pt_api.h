@@ -171,6 +171,25 @@ int pt_scene_load_dae(const char* path, pt_scene** out, char* errbuf, size_t err
  * triangles use bsdf 0; positions are n_tris*9 floats. */
 int pt_scene_from_triangles(const float* positions, int32_t n_tris, const pt_bsdf* bsdf0,
                             const pt_light* light, const pt_camera* camera, pt_scene** out);
+/* General flattened input (the scene-flattening step of SURVEY §8(f) row 2
+ * for callers that already hold meshes, e.g. the Scotty3D loader or a
+ * synthetic workload): a triangle soup with optional vertex normals and
+ * per-triangle bsdf ids, optional spheres, a bsdf table, one light and a
+ * camera.  Built with the same reference BVH (max leaf 32) as .dae scenes. */
+typedef struct pt_mesh_desc {
+  int32_t n_tris;
+  const float* positions;   /* n_tris * 9: v0, v1, v2                        */
+  const float* normals;     /* n_tris * 9 vertex normals, or NULL (face normal) */
+  const int32_t* tri_bsdf;  /* n_tris bsdf ids, or NULL (all 0)              */
+  int32_t n_spheres;
+  const float* spheres;     /* n_spheres * 4: centre, radius                 */
+  const int32_t* sphere_bsdf; /* n_spheres bsdf ids, or NULL (all 0)          */
+  int32_t n_bsdfs;
+  const pt_bsdf* bsdfs;     /* n_bsdfs >= 1                                   */
+  const pt_light* light;    /* NULL: no light                                 */
+  const pt_camera* camera;  /* NULL: default                                  */
+} pt_mesh_desc;
+int pt_scene_from_mesh(const pt_mesh_desc* mesh, pt_scene** out);
 void pt_scene_free(pt_scene* s);
 /* Borrowed view of the flattened arrays (valid until pt_scene_free). */
 int pt_scene_get_desc(const pt_scene* s, pt_scene_desc* out);

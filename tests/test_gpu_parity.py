@@ -103,6 +103,26 @@ def test_render_bit_exact(gpu_ctx, name, flags):
     assert o[..., :3].mean() > 0.01
 
 
+def test_dragon_proxy_parity(gpu_ctx):
+    """~100k triangles, 9 levels: closest hits and a small render bit-exact."""
+    import scenes
+    sc = scenes.dragon_proxy()
+    d = sc.desc()
+    gpu_ctx.load_scene(sc)
+    rays = np.concatenate([camera_rays(d, 20000, seed=27), interior_rays(d, 20000, seed=28)])
+    g = gpu_ctx.intersect(rays)
+    o = pyoracle.intersect(d, rays, use_bvh=True)
+    assert (o != ptrace.PT_HIT_NONE).sum() > 1000
+    assert np.array_equal(g, o)
+    W = H = 32
+    gpu_ctx.clear()
+    gpu_ctx.render(W, H, 2, max_bounces=8, seed=15618)
+    gi = gpu_ctx.get_image()
+    oi, _ = pyoracle.image(d, W, H, 2, max_bounces=8, seed=15618)
+    mx, l2, ok = _images_equal(gi, oi)
+    assert mx == 0.0, f"not bit-exact: max |diff| {mx}, rel L2 {l2}"
+
+
 def test_batching_and_progressive_invariance(gpu_ctx):
     sc = load_fixture("CBbunny")
     gpu_ctx.load_scene(sc)
