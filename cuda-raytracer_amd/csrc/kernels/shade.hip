@@ -416,7 +416,8 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
   return hit;
 }
 
-__global__ __launch_bounds__(TPB) void k_path_leaf(ShadeArgs S, int pstart, int pcount, int passes,
+// 6 waves per SIMD (<= 80 VGPRs, no spills): +2 % over the unconstrained 87
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_path_leaf(ShadeArgs S, int pstart, int pcount, int passes,
                                                    unsigned long long* __restrict__ rcount) {
   const uint32_t p = blockIdx.x * TPB + threadIdx.x;
   uint32_t nrays = 0;
