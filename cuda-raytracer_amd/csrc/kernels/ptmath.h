@@ -54,6 +54,12 @@ __device__ __forceinline__ u4 rng(uint32_t seed, uint32_t pixel, uint32_t sample
   return philox(u4{pixel, sample, vertex * 2u + call, 0x50540000u}, seed, 0x2545F491u);
 }
 
+// The second NEE sample of a vertex under the reference schedule: its own
+// stream (last counter word 'PT'+1), so it never aliases another vertex's.
+__device__ __forceinline__ u4 rng_nee2(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t vertex) {
+  return philox(u4{pixel, sample, vertex * 2u, 0x50540001u}, seed, 0x2545F491u);
+}
+
 // sin and cos of 2*pi*u for u in [0,1): quadrant reduction on u (exact), then
 // Taylor polynomials on [0, pi/2).  Max abs error < 2e-7.
 __device__ __forceinline__ void sincos2pi(float u, float* s, float* c) {

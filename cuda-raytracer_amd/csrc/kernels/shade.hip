@@ -20,14 +20,17 @@ namespace pt {
 constexpr uint32_t F_EXT = 1u;     // extension ray pending in slot p
 constexpr uint32_t F_SHADOW = 2u;  // shadow ray pending in slot N + p
 constexpr uint32_t F_SPEC = 4u;    // last scattering was specular
+constexpr uint32_t F_SHADOW2 = 8u; // second shadow ray pending in slot 2N + p (reference schedule)
+__device__ __forceinline__ uint32_t sh_bit(int s) { return s ? F_SHADOW2 : F_SHADOW; }
 constexpr float INV_PI = 0.318309886183790671f;
 constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
 
 struct ShadeArgs {
-  float4* ray;  // ray records (trace.h): ext ray of path p in slot p, shadow ray in slot N + p
+  float4* ray;  // ray records (trace.h): ext ray of path p in slot p, shadow ray s in slot (1+s)N + p
   float4* ps0;  // T.xyz, flags | vertex << 8
   float4* ps1;  // L.xyz, pixel
   float4* ps2;  // pending shadow contribution
+  float4* ps3;  // pending contribution of the second shadow ray (PT_FLAG_REF_SCHEDULE)
   const float4* __restrict__ prims;
   const pt_prim_shading* __restrict__ shading;
   const pt_bsdf* __restrict__ bsdfs;
@@ -66,19 +69,6 @@ __device__ __forceinline__ f3 camera_dir(const ShadeArgs& S, uint32_t p, uint32_
   return normalize(dir);
 }
 
-__global__ __launch_bounds__(TPB) void k_camera(ShadeArgs S) {
-  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
-  if (p >= S.N) return;
-  uint32_t g;
-  const f3 dir = camera_dir(S, p, g);
-  S.ray[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], dir.x);
-  S.ray[RSTRIDE * p + 1] = rec_r1(dir.y, dir.z, __builtin_inff());
-  S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
-  S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
-  S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
-  S.ps2[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-}
-
 // Path state between vertices (ps0/ps1/ps2 in memory, registers in k_path_leaf).
 struct PathState {
   f3 T;            // throughput
@@ -91,26 +81,80 @@ struct RayV {
   float tmax;
 };
 
-// One path vertex (restated from cu:380-664, see header): resolves the shadow
-// ray of the previous vertex (C added when unoccluded), shades the extension
-// hit (prim != PT_PRIM_NONE at distance t along ext), and produces the next
-// extension ray and/or shadow ray with its pending contribution C.
+// One NEE sample toward the scene light (kernelDirectLightRays, cu:380-481)
+// from the shading point pt with normal n; (ux, uy) pick the point on an area
+// light.  weight < 0: unweighted (the default schedule); otherwise the
+// reference schedule's per-sample weight (cu:2515-2533).
+__device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const f3 alb, const f3 n, const f3 pt,
+                                           float ux, float uy, float weight, f3& C, RayV& r) {
+  if (S.light.type == PT_LIGHT_AREA) {
+    const float sx = ux - 0.5f, sy = uy - 0.5f;
+    const f3 pos = ld3(S.light.position), dx = ld3(S.light.dim_x), dy = ld3(S.light.dim_y);
+    const f3 lpt = mk(pos.x + sx * dx.x + sy * dy.x, pos.y + sx * dx.y + sy * dy.y, pos.z + sx * dx.z + sy * dy.z);
+    const f3 dv = lpt - pt;
+    const float sq = dot(dv, dv);
+    const float dist = sqrtf(sq);
+    const f3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+    const float cosl = dot(w, ld3(S.light.direction));
+    const float cosn = dot(n, w);
+    if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
+      const float pdf = sq / (S.light.area * -cosl);
+      float scale = (cosn / pdf) * INV_PI;
+      if (weight >= 0.0f) scale = scale * weight;
+      C = mulv(mulv(T, alb), ld3(S.light.radiance)) * scale;
+      r.o = pt;
+      r.d = w;
+      r.tmax = dist - EPS;
+      return true;
+    }
+  } else if (S.light.type == PT_LIGHT_POINT) {
+    const f3 dv = ld3(S.light.position) - pt;
+    const float sq = dot(dv, dv);
+    const float dist = sqrtf(sq);
+    const f3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+    const float cosn = dot(n, w);
+    if (dist > 1e-2f && cosn > 0.0f) {
+      float scale = cosn * INV_PI;
+      if (weight >= 0.0f) scale = scale * weight;
+      C = mulv(mulv(T, alb), ld3(S.light.radiance)) * scale;
+      r.o = pt;
+      r.d = w;
+      r.tmax = dist - EPS;
+      return true;
+    }
+  }
+  return false;
+}
+
+// One path vertex (restated from cu:380-664, see header): resolves the NSH
+// shadow rays of the previous vertex (C[s] added when unoccluded), shades the
+// extension hit (prim != PT_PRIM_NONE at distance t along ext), and produces
+// the next extension ray and/or shadow rays with their pending contributions.
+// NSH = 2 only under PT_FLAG_REF_SCHEDULE (NEE samples 2, 2, 1 per vertex).
+template <int NSH>
 __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, PathState& st, const f3 o,
-                                             const f3 d, uint32_t prim, float t, bool shadow_clear, f3& C,
-                                             bool& new_ext, RayV& ext, bool& new_sh, RayV& shr) {
+                                             const f3 d, uint32_t prim, float t, const bool (&clear)[NSH],
+                                             f3 (&C)[NSH], bool& new_ext, RayV& ext, bool (&new_sh)[NSH],
+                                             RayV (&shr)[NSH]) {
   const uint32_t flags = st.flags;
   f3 T = st.T;
   f3 L = st.L;
   const uint32_t g = st.g;
-  // 1. resolve the shadow ray of the previous vertex
-  if (flags & F_SHADOW) {
-    if (shadow_clear) L = L + C;
-  }
+  // 1. resolve the shadow rays of the previous vertex
+#pragma unroll
+  for (int s = 0; s < NSH; ++s)
+    if ((flags & sh_bit(s)) && clear[s]) L = L + C[s];
+  // reference quirk (i): a path whose extension ray misses contributes
+  // nothing (kernelUpdateSSImage writes 0 for an invalid intersection, cu:679-698)
+  if ((S.flags & PT_FLAG_REF_DROP_ON_MISS) && (flags & F_EXT) && prim == PT_PRIM_NONE) L = mk(0.f, 0.f, 0.f);
   new_ext = false;
-  new_sh = false;
-  f3 o_new = mk(0, 0, 0), d_new = mk(0, 0, 1), sh_o = mk(0, 0, 0), sh_d = mk(0, 0, 1);
-  C = mk(0, 0, 0);
-  float sh_tmax = -1.0f;
+  f3 o_new = mk(0, 0, 0), d_new = mk(0, 0, 1);
+#pragma unroll
+  for (int s = 0; s < NSH; ++s) {
+    new_sh[s] = false;
+    C[s] = mk(0, 0, 0);
+    shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
+  }
   uint32_t spec = flags & F_SPEC;
   const uint32_t vtx = (flags >> 8) & 0xffu;
 
@@ -145,44 +189,33 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           L = L + mulv(T, ld3(B.albedo));
       } else {
         const u4 u = rng(S.seed, g, sidx, vtx, 0);
-        const f3 guide = (fabsf(n.x) < 0.9f) ? mk(1.0f, 0.0f, 0.0f) : mk(0.0f, 1.0f, 0.0f);
-        const f3 dpdu = normalize(cross(guide, n));
-        const f3 dpdv = cross(n, dpdu);
+        f3 dpdu, dpdv;
+        if (S.flags & PT_FLAG_REF_GUIDE) {
+          // reference quirk (ii): cu:572-574 (NaN when n is (0,-1,0))
+          const f3 guide = (n.y < 1e-4f) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+          dpdu = normalize(cross(guide, n));
+          dpdv = normalize(cross(dpdu, n));
+        } else {
+          const f3 guide = (fabsf(n.x) < 0.9f) ? mk(1.0f, 0.0f, 0.0f) : mk(0.0f, 1.0f, 0.0f);
+          dpdu = normalize(cross(guide, n));
+          dpdv = cross(n, dpdu);
+        }
         if (B.type == PT_BSDF_DIFFUSE) {
           const f3 alb = ld3(B.albedo);
-          // next-event estimation toward the scene light (cu:380-481)
-          if (S.light.type == PT_LIGHT_AREA) {
-            const float sx = u01(u.x) - 0.5f, sy = u01(u.y) - 0.5f;
-            const f3 pos = ld3(S.light.position), dx = ld3(S.light.dim_x), dy = ld3(S.light.dim_y);
-            const f3 lpt = mk(pos.x + sx * dx.x + sy * dy.x, pos.y + sx * dx.y + sy * dy.y,
-                              pos.z + sx * dx.z + sy * dy.z);
-            const f3 dv = lpt - pt;
-            const float sq = dot(dv, dv);
-            const float dist = sqrtf(sq);
-            const f3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
-            const float cosl = dot(w, ld3(S.light.direction));
-            const float cosn = dot(n, w);
-            if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
-              const float pdf = sq / (S.light.area * -cosl);
-              const float scale = (cosn / pdf) * INV_PI;
-              C = mulv(mulv(T, alb), ld3(S.light.radiance)) * scale;
-              new_sh = true;
-              sh_o = pt;
-              sh_d = w;
-              sh_tmax = dist - EPS;
-            }
-          } else if (S.light.type == PT_LIGHT_POINT) {
-            const f3 dv = ld3(S.light.position) - pt;
-            const float sq = dot(dv, dv);
-            const float dist = sqrtf(sq);
-            const f3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
-            const float cosn = dot(n, w);
-            if (dist > 1e-2f && cosn > 0.0f) {
-              C = mulv(mulv(T, alb), ld3(S.light.radiance)) * (cosn * INV_PI);
-              new_sh = true;
-              sh_o = pt;
-              sh_d = w;
-              sh_tmax = dist - EPS;
+          // next-event estimation toward the scene light (cu:380-481); the
+          // reference schedule takes 2, 2, 1 samples at vertices 1, 2, 3
+          const int nee = (NSH == 2 && vtx <= 2u) ? 2 : 1;
+#pragma unroll
+          for (int s = 0; s < NSH; ++s) {
+            if (s < nee) {
+              float ux = u01(u.x), uy = u01(u.y);
+              if (s == 1) {
+                const u4 v = rng_nee2(S.seed, g, sidx, vtx);
+                ux = u01(v.x);
+                uy = u01(v.y);
+              }
+              const float weight = NSH == 2 ? (nee == 2 ? 0.5f : 1.0f) : -1.0f;
+              new_sh[s] = nee_sample(S, T, alb, n, pt, ux, uy, weight, C[s], shr[s]);
             }
           }
           // BSDF sample
@@ -253,31 +286,39 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
 
   st.T = T;
   st.L = L;
-  st.flags = spec | (new_ext ? F_EXT : 0u) | (new_sh ? F_SHADOW : 0u) | ((vtx + 1u) << 8);
+  uint32_t fl = spec | (new_ext ? F_EXT : 0u) | ((vtx + 1u) << 8);
+#pragma unroll
+  for (int s = 0; s < NSH; ++s) fl |= new_sh[s] ? sh_bit(s) : 0u;
+  st.flags = fl;
   ext.o = o_new;
   ext.d = d_new;
   ext.tmax = __builtin_inff();
-  shr.o = sh_o;
-  shr.d = sh_d;
-  shr.tmax = sh_tmax;
 }
 
 // Shade path p: read its state, hit words and rays, run shade_vertex, write
 // the new state and ray records.  Returns the new rays in registers.
-__device__ __forceinline__ void shade_slot(const ShadeArgs& S, uint32_t p, bool& new_ext, RayV& ext, bool& new_sh,
-                                           RayV& shr) {
-  new_ext = new_sh = false;
+template <int NSH>
+__device__ __forceinline__ void shade_slot(const ShadeArgs& S, uint32_t p, bool& new_ext, RayV& ext,
+                                           bool (&new_sh)[NSH], RayV (&shr)[NSH]) {
+  new_ext = false;
+#pragma unroll
+  for (int s = 0; s < NSH; ++s) new_sh[s] = false;
   const float4 s0 = S.ps0[p];
   const uint32_t flags = __float_as_uint(s0.w);
-  if ((flags & (F_EXT | F_SHADOW)) == 0) return;
+  if ((flags & (F_EXT | F_SHADOW | F_SHADOW2)) == 0) return;
   const float4 s1 = S.ps1[p];
   PathState st{xyz(s0), flags, xyz(s1), __float_as_uint(s1.w)};
   const uint32_t sidx = S.sample_base + p / S.npix;
-  bool clear = false;
-  f3 C = mk(0, 0, 0);
-  if (flags & F_SHADOW) {
-    clear = __float_as_uint(S.ray[RSTRIDE * (S.N + p) + 1].z) == PT_PRIM_NONE;
-    if (clear) C = xyz(S.ps2[p]);
+  bool clear[NSH];
+  f3 C[NSH];
+#pragma unroll
+  for (int s = 0; s < NSH; ++s) {
+    clear[s] = false;
+    C[s] = mk(0, 0, 0);
+    if (flags & sh_bit(s)) {
+      clear[s] = __float_as_uint(S.ray[RSTRIDE * ((1 + s) * S.N + p) + 1].z) == PT_PRIM_NONE;
+      if (clear[s]) C[s] = xyz(s ? S.ps3[p] : S.ps2[p]);
+    }
   }
   uint32_t prim = PT_PRIM_NONE;
   float t = 0.0f;
@@ -292,30 +333,35 @@ __device__ __forceinline__ void shade_slot(const ShadeArgs& S, uint32_t p, bool&
       d = mk(r0.w, r1.x, r1.y);
     }
   }
-  shade_vertex(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
+  shade_vertex<NSH>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
   S.ps0[p] = make_float4(st.T.x, st.T.y, st.T.z, __uint_as_float(st.flags));
   S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(st.g));
-  if (new_sh) S.ps2[p] = make_float4(C.x, C.y, C.z, 0.0f);
   if (new_ext) {
     S.ray[RSTRIDE * p] = make_float4(ext.o.x, ext.o.y, ext.o.z, ext.d.x);
     S.ray[RSTRIDE * p + 1] = rec_r1(ext.d.y, ext.d.z, __builtin_inff());
   } else {
     S.ray[RSTRIDE * p + 1] = rec_r1(0.f, 0.f, -1.0f);
   }
-  if (new_sh) {
-    S.ray[RSTRIDE * (S.N + p)] = make_float4(shr.o.x, shr.o.y, shr.o.z, shr.d.x);
-    S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(shr.d.y, shr.d.z, shr.tmax);
-  } else {
-    S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
+#pragma unroll
+  for (int s = 0; s < NSH; ++s) {
+    const size_t slot = (size_t)(1 + s) * S.N + p;
+    if (new_sh[s]) {
+      (s ? S.ps3 : S.ps2)[p] = make_float4(C[s].x, C[s].y, C[s].z, 0.0f);
+      S.ray[RSTRIDE * slot] = make_float4(shr[s].o.x, shr[s].o.y, shr[s].o.z, shr[s].d.x);
+      S.ray[RSTRIDE * slot + 1] = rec_r1(shr[s].d.y, shr[s].d.z, shr[s].tmax);
+    } else {
+      S.ray[RSTRIDE * slot + 1] = rec_r1(0.f, 0.f, -1.0f);
+    }
   }
 }
 
+template <int NSH>
 __global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
   const uint32_t p = blockIdx.x * TPB + threadIdx.x;
   if (p >= S.N) return;
-  bool new_ext, new_sh;
-  RayV ext, shr;
-  shade_slot(S, p, new_ext, ext, new_sh, shr);
+  bool new_ext, new_sh[NSH];
+  RayV ext, shr[NSH];
+  shade_slot<NSH>(S, p, new_ext, ext, new_sh, shr);
 }
 
 // One fire-and-forget atomic per workgroup: rays that enter the traversal.
@@ -333,7 +379,7 @@ __device__ __forceinline__ void count_rays(unsigned long long* rcount, uint32_t 
 // be tested against the root -- the producing kernel tests them against the
 // root's NC target boxes (4 children, or 16 grandchildren when level 1 is
 // skipped) and pushes their ids into those queues (lane = workgroup & 7).
-template <int NC>
+template <int NC, int NSH>
 __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
   __shared__ uint32_t sh[NC * 8 + 4];
   const uint32_t p = blockIdx.x * TPB + threadIdx.x;
@@ -347,28 +393,49 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
     d[0] = camera_dir(S, p, g);
     S.ray[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], d[0].x);
     S.ray[RSTRIDE * p + 1] = rec_r1(d[0].y, d[0].z, __builtin_inff());
-    S.ray[RSTRIDE * (S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
+#pragma unroll
+    for (int s = 0; s < NSH; ++s) S.ray[RSTRIDE * ((size_t)(1 + s) * S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
     S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
     S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
-    S.ps2[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
   push_children<1, NC>(S.A, (const CPTR(pt_node))S.A.nodes, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, 1, sh);
   count_rays(S.rcount, live ? 1u : 0u, sh + NC * 8);
 }
 
-template <int NC>
+template <int NC, int NSH>
 __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t sh[NC * 8 + 4];
   const uint32_t p = blockIdx.x * TPB + threadIdx.x;
-  bool new_ext = false, new_sh = false;
-  RayV ext{mk(0, 0, 0), mk(0, 0, 1), -1.0f}, shr{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
-  if (p < S.N) shade_slot(S, p, new_ext, ext, new_sh, shr);
-  uint32_t id[2] = {p, S.N + p};
-  f3 o[2] = {ext.o, shr.o}, d[2] = {ext.d, shr.d};
-  float tm[2] = {__builtin_inff(), shr.tmax};
-  bool valid[2] = {new_ext, new_sh};
-  push_children<2, NC>(S.A, (const CPTR(pt_node))S.A.nodes, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, 2, sh);
-  count_rays(S.rcount, (new_ext ? 1u : 0u) + (new_sh ? 1u : 0u), sh + NC * 8);
+  bool new_ext = false, new_sh[NSH];
+  RayV ext{mk(0, 0, 0), mk(0, 0, 1), -1.0f}, shr[NSH];
+#pragma unroll
+  for (int s = 0; s < NSH; ++s) {
+    new_sh[s] = false;
+    shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
+  }
+  if (p < S.N) shade_slot<NSH>(S, p, new_ext, ext, new_sh, shr);
+  uint32_t id[1 + NSH];
+  f3 o[1 + NSH], d[1 + NSH];
+  float tm[1 + NSH];
+  bool valid[1 + NSH];
+  id[0] = p;
+  o[0] = ext.o;
+  d[0] = ext.d;
+  tm[0] = __builtin_inff();
+  valid[0] = new_ext;
+  uint32_t n = new_ext ? 1u : 0u;
+#pragma unroll
+  for (int s = 0; s < NSH; ++s) {
+    id[1 + s] = (1 + s) * S.N + p;
+    o[1 + s] = shr[s].o;
+    d[1 + s] = shr[s].d;
+    tm[1 + s] = shr[s].tmax;
+    valid[1 + s] = new_sh[s];
+    n += new_sh[s] ? 1u : 0u;
+  }
+  push_children<1 + NSH, NC>(S.A, (const CPTR(pt_node))S.A.nodes, blockIdx.x & (NLANE - 1), id, o, d, tm, valid,
+                             1 + NSH, sh);
+  count_rays(S.rcount, n, sh + NC * 8);
 }
 
 // ---- scenes whose BVH root is a leaf -----------------------------------------
@@ -417,8 +484,9 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
 }
 
 // 6 waves per SIMD (<= 80 VGPRs, no spills): +2 % over the unconstrained 87
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_path_leaf(ShadeArgs S, int pstart, int pcount, int passes,
-                                                   unsigned long long* __restrict__ rcount) {
+template <int NSH>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_path_leaf(
+    ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount) {
   const uint32_t p = blockIdx.x * TPB + threadIdx.x;
   uint32_t nrays = 0;
   if (p < S.N) {
@@ -427,33 +495,45 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     st.T = mk(1.0f, 1.0f, 1.0f);
     st.L = mk(0.0f, 0.0f, 0.0f);
     st.flags = F_EXT | (1u << 8);
-    RayV ext{ld3(S.cam.origin), dir, __builtin_inff()}, shr{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
-    f3 C = mk(0, 0, 0);
+    RayV ext{ld3(S.cam.origin), dir, __builtin_inff()}, shr[NSH];
+    f3 C[NSH];
+#pragma unroll
+    for (int s = 0; s < NSH; ++s) {
+      shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
+      C[s] = mk(0, 0, 0);
+    }
     const uint32_t sidx = S.sample_base + p / S.npix;
-    for (int pass = 0; pass < passes && (st.flags & (F_EXT | F_SHADOW)); ++pass) {
+    for (int pass = 0; pass < passes && (st.flags & (F_EXT | F_SHADOW | F_SHADOW2)); ++pass) {
       uint32_t prim = PT_PRIM_NONE;
       float t = 0.0f;
       if (st.flags & F_EXT) {
         leaf_closest(S.prims, pstart, pcount, ext, prim, t);
         nrays++;
       }
-      bool clear = false;
-      if (st.flags & F_SHADOW) {
-        clear = !leaf_occluded(S.prims, pstart, pcount, shr);
-        nrays++;
+      bool clear[NSH];
+#pragma unroll
+      for (int s = 0; s < NSH; ++s) {
+        clear[s] = false;
+        if (st.flags & sh_bit(s)) {
+          clear[s] = !leaf_occluded(S.prims, pstart, pcount, shr[s]);
+          nrays++;
+        }
       }
-      bool new_ext, new_sh;
-      RayV e2, s2;
-      shade_vertex(S, sidx, st, ext.o, ext.d, prim, t, clear, C, new_ext, e2, new_sh, s2);
+      bool new_ext, new_sh[NSH];
+      RayV e2, s2[NSH];
+      shade_vertex<NSH>(S, sidx, st, ext.o, ext.d, prim, t, clear, C, new_ext, e2, new_sh, s2);
       if (new_ext) ext = e2;
-      if (new_sh) shr = s2;
+#pragma unroll
+      for (int s = 0; s < NSH; ++s)
+        if (new_sh[s]) shr[s] = s2[s];
     }
     S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(st.g));
   }
   // rays traced (R): one fire-and-forget atomic per wave into its lane's counter
   const uint32_t w = wave_sum(nrays);
   if ((threadIdx.x & 63) == 0 && w)
-    atomicAdd(rcount + (size_t)((blockIdx.x * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16, (unsigned long long)w);
+    atomicAdd(rcount + (size_t)((blockIdx.x * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16,
+              (unsigned long long)w);
 }
 
 // Sum each owned pixel's samples of this batch into the accumulation buffer,

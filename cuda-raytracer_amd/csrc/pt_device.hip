@@ -59,9 +59,10 @@ struct pt_ctx {
   pt_bsdf* d_bsdfs = nullptr;
 
   // wavefront buffers (sized for N paths = 2N ray slots)
-  uint32_t cap_paths = 0;
+  uint32_t cap_paths = 0;  // paths the buffers hold
+  uint32_t cap_spp = 0;    // ray slots per path they hold (2, or 3 under the reference schedule)
   float4* d_ray = nullptr;  // 2N ray records (trace.h), RSTRIDE float4 each
-  float4 *d_ps0 = nullptr, *d_ps1 = nullptr, *d_ps2 = nullptr;
+  float4 *d_ps0 = nullptr, *d_ps1 = nullptr, *d_ps2 = nullptr, *d_ps3 = nullptr;
   uint32_t* d_q = nullptr;
   size_t qcap = 0;  // entries per parity half
   uint32_t* d_cnt = nullptr;
@@ -144,7 +145,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ray,
-                  c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_q,      c->d_cnt,
+                  c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,      c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err,
                   c->d_pix_of, c->d_accum};
   for (void* p : ptrs)
@@ -155,38 +156,52 @@ static void free_all(pt_ctx* c) {
 static constexpr size_t QFACTOR = 24;
 // Paths in flight per batch.  Large batches amortise the per-level launches
 // (deep levels hold few rays per pass); queue offsets are u32, so both parity
-// halves (2 x QFACTOR x 2N ids) must stay below 2^32.
+// halves (2 x QFACTOR x slots ids) must stay below 2^32.
 static constexpr uint32_t DEFAULT_BATCH_PATHS = 32u << 20;
-static constexpr uint32_t MAX_BATCH_PATHS = (uint32_t)((1ull << 32) / (2 * QFACTOR * 2)) & ~4095u;
+static uint32_t max_batch_paths(uint32_t slots_per_path) {
+  return (uint32_t)((1ull << 32) / (2 * QFACTOR * slots_per_path)) & ~4095u;
+}
 
-static int ensure_paths(pt_ctx* c, uint32_t N) {
-  if (N <= c->cap_paths) return PT_OK;
-  const size_t slots = 2 * (size_t)N;
+// Per-lane capacity of each root target queue for N paths with spp ray slots
+// per path: the root kernel (pt_intersect) pushes <= TILE rays per workgroup
+// and lane = item & 7; the fused producers (k_camera_push / k_shade_push)
+// push <= spp * TPB rays per workgroup with lane = workgroup & 7.
+static size_t root_per_lane(size_t N, size_t spp) {
+  const size_t items = (N * spp + TILE - 1) / TILE;
+  const size_t blocks = (N + TPB - 1) / TPB;
+  return std::max((items + NLANE - 1) / NLANE * TILE, (blocks + NLANE - 1) / NLANE * TPB * spp);
+}
+
+static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
+  if (N <= c->cap_paths && spp <= c->cap_spp) return PT_OK;
+  N = std::max(N, c->cap_paths);
+  spp = std::max(spp, c->cap_spp);
+  const size_t slots = (size_t)spp * N;
   int rc;
   if ((rc = dalloc(c, &c->d_ray, slots * RSTRIDE))) return rc;
   if ((rc = dalloc(c, &c->d_ps0, N))) return rc;
   if ((rc = dalloc(c, &c->d_ps1, N))) return rc;
   if ((rc = dalloc(c, &c->d_ps2, N))) return rc;
-  // every root target needs ceil(items/8)*TILE slots per lane (see
+  if (spp > 2 && (rc = dalloc(c, &c->d_ps3, N))) return rc;
+  // every root target needs root_per_lane slots per lane (<= 16 targets, see
   // set_root_child_offsets); deeper levels need at most 4x the visits of the
   // level above, which QFACTOR covers for the scenes measured (peak_queue_entries)
-  const size_t items = (slots + TILE - 1) / TILE;
-  const size_t root_need = (size_t)NLANE * 16 * ((items + NLANE - 1) / NLANE * TILE);  // <= 16 root targets
-  c->qcap = std::max(QFACTOR * slots, 2 * root_need);
+  const size_t root_need = (size_t)NLANE * 16 * root_per_lane(N, spp);
+  // a single-leaf tree queues nothing (k_path_leaf / the root pass only)
+  c->qcap = c->root_leaf ? NLANE * 64 : std::max(QFACTOR * slots, root_need);
   c->qcap = (c->qcap + NLANE * 64 - 1) / (NLANE * 64) * (NLANE * 64);
+  if (2 * c->qcap >= (1ull << 32)) return fail(c, PT_E_UNSUPPORTED, "batch too large for u32 queue offsets");
   if ((rc = dalloc(c, &c->d_q, 2 * c->qcap))) return rc;
   c->cap_paths = N;
+  c->cap_spp = spp;
   return PT_OK;
 }
 
-// Queue offsets of the root's children: root item k belongs to lane k % 8, so
-// lane s sees at most ceil(items/8) * TILE rays; child jj of the root gets that
-// many slots in lane s of the odd-parity half.
+// Queue offsets of the root's targets: each gets root_per_lane slots in every
+// lane of the half its level uses (level 1: odd half, level 2: even half).
 static int set_root_child_offsets(pt_ctx* c) {
   if (c->root_leaf) return PT_OK;
-  const size_t slots = 2 * (size_t)c->cap_paths;
-  const size_t items = (slots + TILE - 1) / TILE;
-  const size_t per_lane = (items + NLANE - 1) / NLANE * TILE;
+  const size_t per_lane = root_per_lane(c->cap_paths, c->cap_spp);
   const size_t lanecap = c->qcap / NLANE;
   const pt_node& root = c->nodes_host[0];
   // targets: the root's children (level 1, odd half) or, when level 1 is
@@ -448,6 +463,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   c->camera = s->camera;
   c->have_scene = true;
   c->cap_paths = 0;  // force re-derivation of root queue offsets
+  c->cap_spp = 0;
   return PT_OK;
 }
 
@@ -518,14 +534,19 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     return PT_OK;
   }
   // batch: spp_b samples of every owned pixel
+  // the reference schedule (cu:2499-2533) casts up to two shadow rays per vertex
+  const bool ref_sched = (P->flags & PT_FLAG_REF_SCHEDULE) != 0;
+  const uint32_t nsh = ref_sched ? 2u : 1u;
+  const int max_bounces = ref_sched ? 2 : P->max_bounces;
   uint32_t target = P->batch_paths > 0 ? (uint32_t)P->batch_paths : DEFAULT_BATCH_PATHS;
-  target = std::min<uint32_t>(target, MAX_BATCH_PATHS);
+  target = std::min<uint32_t>(target, max_batch_paths(1 + nsh));
   uint32_t spp_b = std::max<uint32_t>(1, target / npix);
   spp_b = std::min<uint32_t>(spp_b, (uint32_t)P->spp);
   const uint32_t Nmax = npix * spp_b;
-  if ((size_t)npix > MAX_BATCH_PATHS) return fail(c, PT_E_UNSUPPORTED, "more owned pixels than one batch holds");
-  const bool realloc = Nmax > c->cap_paths;
-  if ((rc = ensure_paths(c, Nmax))) return rc;
+  if ((size_t)npix > max_batch_paths(1 + nsh))
+    return fail(c, PT_E_UNSUPPORTED, "more owned pixels than one batch holds");
+  const bool realloc = Nmax > c->cap_paths || 1 + nsh > c->cap_spp;
+  if ((rc = ensure_paths(c, Nmax, 1 + nsh))) return rc;
   if (realloc && (rc = set_root_child_offsets(c))) return rc;
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
   c->timing = (P->flags & PT_FLAG_STATS) != 0;
@@ -538,6 +559,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   S.ps0 = c->d_ps0;
   S.ps1 = c->d_ps1;
   S.ps2 = c->d_ps2;
+  S.ps3 = c->d_ps3;
   S.prims = c->d_prims;
   S.shading = c->d_shading;
   S.bsdfs = c->d_bsdfs;
@@ -548,7 +570,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   S.seed = P->seed;
   S.width = P->width;
   S.height = P->height;
-  S.max_bounces = P->max_bounces;
+  S.max_bounces = max_bounces;
   S.flags = P->flags;
   S.A = trace_args(c);
   S.rcount = c->d_rcount;
@@ -561,29 +583,35 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.N = N;
     S.sample_base = (uint32_t)(P->sample_offset + done);
     const dim3 grid((N + TPB - 1) / TPB);
-    const int passes = P->max_bounces + 2;
+    const int passes = max_bounces + 2;
     if (c->root_leaf) {
       // single-leaf tree: every path runs to completion in one kernel
       const pt_node& root = c->nodes_host[0];
-      c->launch(pt_ctx::K_PATH, 0, k_path_leaf, grid, dim3(TPB), S, root.prim_start, root.prim_count, passes,
-                c->d_rcount);
+      if (nsh == 2)
+        c->launch(pt_ctx::K_PATH, 0, k_path_leaf<2>, grid, dim3(TPB), S, root.prim_start, root.prim_count, passes,
+                  c->d_rcount);
+      else
+        c->launch(pt_ctx::K_PATH, 0, k_path_leaf<1>, grid, dim3(TPB), S, root.prim_start, root.prim_count, passes,
+                  c->d_rcount);
       c->stats.passes += passes;
     } else {
       // camera rays enter the root's target queues directly; each pass traces
       // the levels below, then shading pushes the next rays (none after the
       // last pass: its shade only resolves the final shadow rays)
-      if (c->skip_l1)
-        c->launch(pt_ctx::K_CAM, 0, k_camera_push<16>, grid, dim3(TPB), S);
-      else
-        c->launch(pt_ctx::K_CAM, 0, k_camera_push<4>, grid, dim3(TPB), S);
+      const int nc = c->skip_l1 ? 16 : 4;
+      if (nc == 16 && nsh == 1) c->launch(pt_ctx::K_CAM, 0, k_camera_push<16, 1>, grid, dim3(TPB), S);
+      if (nc == 16 && nsh == 2) c->launch(pt_ctx::K_CAM, 0, k_camera_push<16, 2>, grid, dim3(TPB), S);
+      if (nc == 4 && nsh == 1) c->launch(pt_ctx::K_CAM, 0, k_camera_push<4, 1>, grid, dim3(TPB), S);
+      if (nc == 4 && nsh == 2) c->launch(pt_ctx::K_CAM, 0, k_camera_push<4, 2>, grid, dim3(TPB), S);
       for (int pass = 0; pass < passes; ++pass) {
         if ((rc = trace_levels(c))) return rc;
-        if (pass == passes - 1)
-          c->launch(pt_ctx::K_SHADE, 0, k_shade, grid, dim3(TPB), S);
-        else if (c->skip_l1)
-          c->launch(pt_ctx::K_SHADE, 0, k_shade_push<16>, grid, dim3(TPB), S);
-        else
-          c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4>, grid, dim3(TPB), S);
+        const bool last = pass == passes - 1;
+        if (last && nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade<1>, grid, dim3(TPB), S);
+        if (last && nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade<2>, grid, dim3(TPB), S);
+        if (!last && nc == 16 && nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<16, 1>, grid, dim3(TPB), S);
+        if (!last && nc == 16 && nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<16, 2>, grid, dim3(TPB), S);
+        if (!last && nc == 4 && nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4, 1>, grid, dim3(TPB), S);
+        if (!last && nc == 4 && nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4, 2>, grid, dim3(TPB), S);
       }
     }
     c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_ps1,
@@ -647,8 +675,8 @@ int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) {
   hipSetDevice(c->device);
   int rc;
   const uint32_t N = ((uint32_t)n + 1) / 2;
-  const bool realloc = N > c->cap_paths;
-  if ((rc = ensure_paths(c, N))) return rc;
+  const bool realloc = N > c->cap_paths || 2 > c->cap_spp;
+  if ((rc = ensure_paths(c, N, 2))) return rc;
   if (realloc && (rc = set_root_child_offsets(c))) return rc;
   float4* d_in = nullptr;
   HIPCHK(c, hipMalloc((void**)&d_in, (size_t)n * 32));  // rays in, then hit keys out

@@ -31,6 +31,9 @@ PT_HIT_NONE = 0xFFFFFFFFFFFFFFFF
 PT_FLAG_COSINE_DIFFUSE = 0x1
 PT_FLAG_NO_EMISSION = 0x2
 PT_FLAG_STATS = 0x4
+PT_FLAG_REF_DROP_ON_MISS = 0x8   # reference quirk (i)
+PT_FLAG_REF_GUIDE = 0x10         # reference quirk (ii)
+PT_FLAG_REF_SCHEDULE = 0x20      # reference quirk (vi): 2 bounces, NEE 2/2/1 weighted 0.5/0.5/1
 PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION = 0, 1, 2, 3
 PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT = 0, 1, 2
 PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1

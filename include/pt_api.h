@@ -218,6 +218,16 @@ int pt_set_camera(pt_ctx* ctx, const pt_camera* camera);
 #define PT_FLAG_NO_EMISSION 0x2u    /* do not count emissive surfaces (REAL_TIME,
                                        cudaRenderer.h:76, cu:1242-1246)        */
 #define PT_FLAG_STATS 0x4u          /* collect R/V counters and per-pass timing  */
+/* Reference-quirk modes (SURVEY §8(a) parity decisions; default off, the CPU
+ * oracle implements each the same way):                                     */
+#define PT_FLAG_REF_DROP_ON_MISS 0x8u /* (i) a path whose extension ray misses
+                                         contributes 0 (cu:679-698)          */
+#define PT_FLAG_REF_GUIDE 0x10u       /* (ii) the reference's local frame,
+                                         cu:572-574 (NaN for n = (0,-1,0))   */
+#define PT_FLAG_REF_SCHEDULE 0x20u    /* (vi) renderFrame's schedule, cu:2499-2533:
+                                         2 bounces, NEE samples 2, 2, 1 at
+                                         vertices 1, 2, 3 weighted 0.5, 0.5, 1;
+                                         max_bounces is ignored              */
 
 typedef struct pt_render_params {
   int32_t width, height;

@@ -77,6 +77,10 @@ static inline float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.
 static inline u4 rng(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t vertex, uint32_t call) {
   return philox(pixel, sample, vertex * 2u + call, 0x50540000u, seed, 0x2545F491u);
 }
+/* second NEE sample of a vertex under the reference schedule: own stream */
+static inline u4 rng_nee2(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t vertex) {
+  return philox(pixel, sample, vertex * 2u, 0x50540001u, seed, 0x2545F491u);
+}
 void pto_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t* out) {
   u4 r = philox(c0, c1, c2, c3, k0, k1);
   memcpy(out, r.v, 16);
@@ -283,9 +287,54 @@ static uint64_t trace(const job_t* J, v3 o, v3 d, float tmax) {
 }
 
 /* Radiance of sample s of pixel g: the per-path state machine of k_shade. */
+/* One NEE sample toward the scene light, kernelDirectLightRays cu:380-481.
+ * weight < 0: unweighted (default schedule); else the reference schedule's
+ * per-sample weight (cu:2515-2533). */
+static int nee_sample(const pt_scene_desc* S, v3 T, v3 alb, v3 n, v3 pt, float ux, float uy, float weight, v3* C,
+                      v3* sw, float* stmax) {
+  const float INV_PI = 0.318309886183790671f, EPS = 1e-3f;
+  if (S->light.type == PT_LIGHT_AREA) {
+    float sx = ux - 0.5f, sy = uy - 0.5f;
+    v3 pos = ld3(S->light.position), dx = ld3(S->light.dim_x), dy = ld3(S->light.dim_y);
+    v3 lpt = mk(pos.x + sx * dx.x + sy * dy.x, pos.y + sx * dx.y + sy * dy.y, pos.z + sx * dx.z + sy * dy.z);
+    v3 dv = sub(lpt, pt);
+    float sq = dot(dv, dv);
+    float dist = sqrtf(sq);
+    v3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+    float cosl = dot(w, ld3(S->light.direction));
+    float cosn = dot(n, w);
+    if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
+      float pdf = sq / (S->light.area * -cosl);
+      float scale = (cosn / pdf) * INV_PI;
+      if (weight >= 0.0f) scale = scale * weight;
+      *C = scl(mulv(mulv(T, alb), ld3(S->light.radiance)), scale);
+      *sw = w;
+      *stmax = dist - EPS;
+      return 1;
+    }
+  } else if (S->light.type == PT_LIGHT_POINT) {
+    v3 dv = sub(ld3(S->light.position), pt);
+    float sq = dot(dv, dv);
+    float dist = sqrtf(sq);
+    v3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+    float cosn = dot(n, w);
+    if (dist > 1e-2f && cosn > 0.0f) {
+      float scale = cosn * INV_PI;
+      if (weight >= 0.0f) scale = scale * weight;
+      *C = scl(mulv(mulv(T, alb), ld3(S->light.radiance)), scale);
+      *sw = w;
+      *stmax = dist - EPS;
+      return 1;
+    }
+  }
+  return 0;
+}
+
 static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays) {
   const pt_scene_desc* S = J->S;
-  const float INV_PI = 0.318309886183790671f, EPS = 1e-3f;
+  const float EPS = 1e-3f;
+  const int ref_sched = (J->flags & PT_FLAG_REF_SCHEDULE) != 0;
+  const int max_bounces = ref_sched ? 2 : J->max_bounces;
   uint32_t row = g / (uint32_t)J->W, col = g - row * (uint32_t)J->W;
   u4 u = rng(J->seed, g, s, 0, 0);
   /* camera ray, cu:338-354 */
@@ -306,7 +355,12 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
   for (uint32_t vtx = 1;; ++vtx) {
     uint64_t h = trace(J, o, d, INFINITY);
     (*nrays)++;
-    if (h == PT_HIT_NONE) break;
+    if (h == PT_HIT_NONE) {
+      /* reference quirk (i): kernelUpdateSSImage writes 0 for a path whose
+       * intersection became invalid (cu:679-698) */
+      if (J->flags & PT_FLAG_REF_DROP_ON_MISS) L = mk(0.0f, 0.0f, 0.0f);
+      break;
+    }
     uint32_t tb = (uint32_t)(h >> 32), prim = (uint32_t)h;
     float t;
     memcpy(&t, &tb, 4);
@@ -336,45 +390,33 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
       break;
     }
     u4 r = rng(J->seed, g, s, vtx, 0);
-    v3 guide = (fabsf(n.x) < 0.9f) ? mk(1.0f, 0.0f, 0.0f) : mk(0.0f, 1.0f, 0.0f);
-    v3 dpdu = nrm(cross(guide, n));
-    v3 dpdv = cross(n, dpdu);
+    v3 dpdu, dpdv;
+    if (J->flags & PT_FLAG_REF_GUIDE) { /* reference quirk (ii), cu:572-574 */
+      v3 guide = (n.y < 1e-4f) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+      dpdu = nrm(cross(guide, n));
+      dpdv = nrm(cross(dpdu, n));
+    } else {
+      v3 guide = (fabsf(n.x) < 0.9f) ? mk(1.0f, 0.0f, 0.0f) : mk(0.0f, 1.0f, 0.0f);
+      dpdu = nrm(cross(guide, n));
+      dpdv = cross(n, dpdu);
+    }
     v3 dn, on;
     if (Bs->type == PT_BSDF_DIFFUSE) {
       v3 alb = ld3(Bs->albedo);
-      int have_sh = 0;
-      v3 C = mk(0, 0, 0), sw = mk(0, 0, 1);
-      float stmax = -1.0f;
-      if (S->light.type == PT_LIGHT_AREA) {
-        float sx = u01(r.v[0]) - 0.5f, sy = u01(r.v[1]) - 0.5f;
-        v3 pos = ld3(S->light.position), dx = ld3(S->light.dim_x), dy = ld3(S->light.dim_y);
-        v3 lpt = mk(pos.x + sx * dx.x + sy * dy.x, pos.y + sx * dx.y + sy * dy.y, pos.z + sx * dx.z + sy * dy.z);
-        v3 dv = sub(lpt, pt);
-        float sq = dot(dv, dv);
-        float dist = sqrtf(sq);
-        v3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
-        float cosl = dot(w, ld3(S->light.direction));
-        float cosn = dot(n, w);
-        if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
-          float pdf = sq / (S->light.area * -cosl);
-          float scale = (cosn / pdf) * INV_PI;
-          C = scl(mulv(mulv(T, alb), ld3(S->light.radiance)), scale);
-          have_sh = 1;
-          sw = w;
-          stmax = dist - EPS;
+      /* NEE: one sample, or 2, 2, 1 at vertices 1, 2, 3 (reference schedule) */
+      const int nee = (ref_sched && vtx <= 2u) ? 2 : 1;
+      int have_sh[2] = {0, 0};
+      v3 C[2] = {{0, 0, 0}, {0, 0, 0}}, sw[2] = {{0, 0, 1}, {0, 0, 1}};
+      float stmax[2] = {-1.0f, -1.0f};
+      for (int k = 0; k < nee; ++k) {
+        float ux = u01(r.v[0]), uy = u01(r.v[1]);
+        if (k == 1) {
+          u4 r2 = rng_nee2(J->seed, g, s, vtx);
+          ux = u01(r2.v[0]);
+          uy = u01(r2.v[1]);
         }
-      } else if (S->light.type == PT_LIGHT_POINT) {
-        v3 dv = sub(ld3(S->light.position), pt);
-        float sq = dot(dv, dv);
-        float dist = sqrtf(sq);
-        v3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
-        float cosn = dot(n, w);
-        if (dist > 1e-2f && cosn > 0.0f) {
-          C = scl(mulv(mulv(T, alb), ld3(S->light.radiance)), cosn * INV_PI);
-          have_sh = 1;
-          sw = w;
-          stmax = dist - EPS;
-        }
+        float weight = ref_sched ? (nee == 2 ? 0.5f : 1.0f) : -1.0f;
+        have_sh[k] = nee_sample(S, T, alb, n, pt, ux, uy, weight, &C[k], &sw[k], &stmax[k]);
       }
       float x, y, z, sn, cs;
       sincos2pi(u01(r.v[3]), &sn, &cs);
@@ -399,10 +441,11 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
       }
       on = add(pt, scl(n, EPS));
       spec = 0;
-      if (have_sh) {
-        uint64_t hs = trace(J, pt, sw, stmax);
+      for (int k = 0; k < nee; ++k) {
+        if (!have_sh[k]) continue;
+        uint64_t hs = trace(J, pt, sw[k], stmax[k]);
         (*nrays)++;
-        if (hs == PT_HIT_NONE) L = add(L, C);
+        if (hs == PT_HIT_NONE) L = add(L, C[k]);
       }
     } else if (Bs->type == PT_BSDF_MIRROR) {
       float dd = dot(d, n);
@@ -439,7 +482,7 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
       }
       spec = 1;
     }
-    if (!(vtx <= (uint32_t)J->max_bounces && (T.x > 0.0f || T.y > 0.0f || T.z > 0.0f))) break;
+    if (!(vtx <= (uint32_t)max_bounces && (T.x > 0.0f || T.y > 0.0f || T.z > 0.0f))) break;
     o = on;
     d = dn;
   }

@@ -78,6 +78,12 @@ def test_tie_break_lowest_prim(gpu_ctx):
 
 
 def _images_equal(gimg, oimg):
+    # NaN pixels (PT_FLAG_REF_GUIDE reproduces the reference's NaN frame)
+    # must be NaN on both sides; they count as equal
+    gn, on = np.isnan(gimg[..., :3]), np.isnan(oimg[..., :3])
+    assert np.array_equal(gn, on), "NaN pixels differ"
+    gimg = np.where(gn, 0.0, gimg[..., :3])
+    oimg = np.where(on, 0.0, oimg[..., :3])
     diff = np.abs(gimg[..., :3] - oimg[..., :3])
     ref = np.abs(oimg[..., :3])
     l2 = np.linalg.norm(diff) / max(np.linalg.norm(ref), 1e-30)
@@ -85,8 +91,15 @@ def _images_equal(gimg, oimg):
     return float(diff.max()), float(l2), float(frac_ok)
 
 
+REF = ptrace.PT_FLAG_REF_SCHEDULE | ptrace.PT_FLAG_REF_DROP_ON_MISS
+
+
 @pytest.mark.parametrize("name,flags", [("CBbunny", 0), ("CBspheres", 0), ("CBgems", 0), ("CBempty", 0),
-                                        ("CBcoil", ptrace.PT_FLAG_COSINE_DIFFUSE)])
+                                        ("CBcoil", ptrace.PT_FLAG_COSINE_DIFFUSE),
+                                        # reference-quirk modes (SURVEY §8(a) parity decisions)
+                                        ("CBbunny", REF), ("CBempty", REF | ptrace.PT_FLAG_NO_EMISSION),
+                                        ("CBspheres", REF), ("CBcoil", ptrace.PT_FLAG_REF_GUIDE),
+                                        ("CBempty", ptrace.PT_FLAG_REF_GUIDE)])
 def test_render_bit_exact(gpu_ctx, name, flags):
     sc = load_fixture(name)
     d = sc.desc()
@@ -157,14 +170,15 @@ def test_tile_sharding_union(gpu_ctx):
     assert np.array_equal(sum(p[..., :3] for p in parts), full[..., :3])
 
 
-def test_ray_count_matches_oracle(gpu_ctx):
-    sc = load_fixture("CBbunny")
+@pytest.mark.parametrize("name,flags", [("CBbunny", 0), ("CBempty", 0), ("CBbunny", REF), ("CBempty", REF)])
+def test_ray_count_matches_oracle(gpu_ctx, name, flags):
+    sc = load_fixture(name)
     d = sc.desc()
     gpu_ctx.load_scene(sc)
     gpu_ctx.reset_stats()
     gpu_ctx.clear()
-    gpu_ctx.render(32, 32, 2, max_bounces=8)
+    gpu_ctx.render(32, 32, 2, max_bounces=8, flags=flags)
     st = gpu_ctx.stats()
-    _, rays = pyoracle.render(d, 32, 32, 2, max_bounces=8)
+    _, rays = pyoracle.render(d, 32, 32, 2, max_bounces=8, flags=flags)
     assert st.rays == rays
     assert st.visits >= st.rays

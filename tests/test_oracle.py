@@ -68,3 +68,21 @@ def test_golden_render_regression():
     sums, rays = pyoracle.render(d, 16, 16, 2, max_bounces=8, seed=15618)
     assert int(g["rays"]) == rays
     assert np.array_equal(g["sums"], sums)
+
+
+def test_oracle_quirk_modes():
+    """Reference-quirk modes of the oracle (SURVEY §8(a) parity decisions)."""
+    d = load_fixture("CBempty").desc()
+    W = H = 12
+    base, r0 = pyoracle.render(d, W, H, 1, max_bounces=8, threads=4)
+    drop, r1 = pyoracle.render(d, W, H, 1, max_bounces=8, threads=4, flags=ptrace.PT_FLAG_REF_DROP_ON_MISS)
+    # (i): a sample either keeps its radiance or (its path escaped) is dropped
+    same = np.all(drop[..., :3] == base[..., :3], axis=-1)
+    zero = np.all(drop[..., :3] == 0.0, axis=-1)
+    assert np.all(same | zero) and r1 == r0 and zero.sum() > 0
+    # (vi): 2 bounces with NEE samples 2, 2, 1; max_bounces is ignored
+    a, ra = pyoracle.render(d, W, H, 1, max_bounces=8, threads=4, flags=ptrace.PT_FLAG_REF_SCHEDULE)
+    b, rb = pyoracle.render(d, W, H, 1, max_bounces=1, threads=4, flags=ptrace.PT_FLAG_REF_SCHEDULE)
+    assert np.array_equal(a, b) and ra == rb
+    assert ra <= W * H * (3 + 5)  # 3 extension rays + 2 + 2 + 1 shadow rays per path at most
+    assert not np.array_equal(a, base)
