@@ -1,0 +1,61 @@
+// Post-process kernels (gfx950): the reference's display filter.
+//
+//   kernelMedianFilter   src/cudaRenderer.cu:773-842   -> k_median3
+//
+// Per channel the reference removes the maximum of the 3x3 neighbourhood
+// three times (setting it to 0) and keeps the fourth maximum; out-of-frame
+// neighbours are 1.0.  The selection is restated literally (max search from
+// 0.0 with >=, last index wins) so NaN and tie cases match too.
+#include "trace.h"
+
+namespace pt {
+
+__device__ __forceinline__ float ref_median_channel(float (&v)[9]) {
+  float out = 0.0f;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    int im = 0;
+    float m = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      if (v[j] >= m) {
+        m = v[j];
+        im = j;
+      }
+    }
+    if (it < 3) {
+#pragma unroll
+      for (int j = 0; j < 9; ++j)
+        if (j == im) v[j] = 0.0f;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 9; ++j)
+        if (j == im) out = v[j];
+    }
+  }
+  return out;
+}
+
+__global__ __launch_bounds__(TPB) void k_median3(const float4* __restrict__ in, float4* __restrict__ out, int w,
+                                                 int h) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= w * h) return;
+  const int r = i / w, col = i - r * w;
+  float R[9], G[9], B[9];
+  int k = 0;
+#pragma unroll
+  for (int dr = -1; dr <= 1; ++dr) {
+#pragma unroll
+    for (int dc = -1; dc <= 1; ++dc, ++k) {
+      const int rr = r + dr, cc = col + dc;
+      float4 v = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+      if (rr >= 0 && rr < h && cc >= 0 && cc < w) v = in[rr * w + cc];
+      R[k] = v.x;
+      G[k] = v.y;
+      B[k] = v.z;
+    }
+  }
+  out[i] = make_float4(ref_median_channel(R), ref_median_channel(G), ref_median_channel(B), 1.0f);
+}
+
+}  // namespace pt

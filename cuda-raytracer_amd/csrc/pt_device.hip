@@ -26,6 +26,7 @@
 
 #include "kernels/trace.hip"
 #include "kernels/shade.hip"
+#include "kernels/post.hip"
 
 using namespace pt;
 
@@ -657,6 +658,41 @@ int pt_get_image(pt_ctx* c, float* rgba, size_t n_floats) {
     px[3] = 1.0f;
   }
   return PT_OK;
+}
+
+int pt_median_filter(pt_ctx* c, const float* rgba_in, float* rgba_out, int32_t width, int32_t height) {
+  if (!c || !rgba_in || !rgba_out || width <= 0 || height <= 0) return PT_E_INVALID;
+  hipSetDevice(c->device);
+  const size_t n = (size_t)width * height;
+  float4 *d_in = nullptr, *d_out = nullptr;
+  HIPCHK(c, hipMalloc((void**)&d_in, n * sizeof(float4)));
+  if (hipMalloc((void**)&d_out, n * sizeof(float4)) != hipSuccess) {
+    hipFree(d_in);
+    return fail(c, PT_E_HIP, "pt_median_filter: out of device memory");
+  }
+  int rc = PT_OK;
+  if (hipMemcpyAsync(d_in, rgba_in, n * sizeof(float4), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    rc = fail(c, PT_E_HIP, "pt_median_filter: copy in");
+  if (!rc) {
+    hipLaunchKernelGGL(k_median3, dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, c->stream, d_in, d_out, width,
+                       height);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(rgba_out, d_out, n * sizeof(float4), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+      rc = fail(c, PT_E_HIP, "pt_median_filter: kernel / copy out");
+  }
+  hipFree(d_in);
+  hipFree(d_out);
+  return rc;
+}
+
+int pt_get_display_image(pt_ctx* c, float* rgba, size_t n_floats) {
+  if (!c || !rgba) return PT_E_INVALID;
+  if (c->fb_nranks != 1) return fail(c, PT_E_INVALID, "display image needs the whole frame (nranks == 1)");
+  int rc = pt_get_image(c, rgba, n_floats);
+  if (rc) return rc;
+  if (c->samples < PT_POST_PROCESS_THRESHOLD) rc = pt_median_filter(c, rgba, rgba, c->fb_w, c->fb_h);
+  return rc;
 }
 
 int pt_owned_pixels(pt_ctx* c, int32_t* n_pixels, int32_t* pixel_index, size_t max_idx, void** device_sums) {

@@ -37,6 +37,7 @@ PT_FLAG_REF_SCHEDULE = 0x20      # reference quirk (vi): 2 bounces, NEE 2/2/1 we
 PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION = 0, 1, 2, 3
 PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT = 0, 1, 2
 PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1
+PT_POST_PROCESS_THRESHOLD = 32
 
 
 class pt_prim(C.Structure):
@@ -111,7 +112,8 @@ API_SYMBOLS = [
     "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
     "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect",
-    "pt_get_stats", "pt_reset_stats",
+    "pt_get_stats", "pt_reset_stats", "pt_median_filter", "pt_get_display_image", "pt_tonemap",
+    "pt_write_png", "pt_write_pfm",
 ]
 
 
@@ -135,6 +137,11 @@ def _load():
                                               C.POINTER(pt_light), C.POINTER(pt_camera), C.POINTER(P)]),
         "pt_scene_from_mesh": (C.c_int, [C.POINTER(pt_mesh_desc), C.POINTER(P)]),
         "pt_scene_free": (None, [P]),
+        "pt_median_filter": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_float), I32, I32]),
+        "pt_get_display_image": (C.c_int, [P, C.POINTER(C.c_float), SZ]),
+        "pt_tonemap": (C.c_int, [C.POINTER(C.c_float), I32, I32, C.c_float, C.c_float, C.POINTER(C.c_uint8)]),
+        "pt_write_png": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), I32, I32]),
+        "pt_write_pfm": (C.c_int, [C.c_char_p, C.POINTER(C.c_float), I32, I32]),
         "pt_scene_get_desc": (C.c_int, [P, C.POINTER(pt_scene_desc)]),
         "pt_scene_level_counts": (C.c_int, [P, C.POINTER(I32), I32, C.POINTER(I32)]),
         "pt_scene_sorted_to_input": (C.c_int, [P, C.POINTER(I32), I32]),
@@ -380,6 +387,20 @@ class Context:
         self._chk(LIB.pt_get_image(self.h, _ptr(img, C.c_float), img.size))
         return img
 
+    def get_display_image(self):
+        """What CudaRenderer::getImage shows: median-filtered below 32 spp."""
+        img = np.zeros((self.height, self.width, 4), dtype=np.float32)
+        self._chk(LIB.pt_get_display_image(self.h, _ptr(img, C.c_float), img.size))
+        return img
+
+    def median_filter(self, img):
+        """3x3 reference median filter of an (H, W, 4) float32 frame, on the GPU."""
+        img = np.ascontiguousarray(img, dtype=np.float32)
+        out = np.empty_like(img)
+        self._chk(LIB.pt_median_filter(self.h, _ptr(img, C.c_float), _ptr(out, C.c_float), img.shape[1],
+                                       img.shape[0]))
+        return out
+
     def owned_pixels(self):
         n = C.c_int32()
         self._chk(LIB.pt_owned_pixels(self.h, C.byref(n), None, 0, None))
@@ -423,3 +444,27 @@ def hit_prim(keys):
     p = (keys & np.uint64(0xFFFFFFFF)).astype(np.int64)
     p[keys == np.uint64(PT_HIT_NONE)] = -1
     return p
+
+
+def tonemap(img, gamma=2.2, level=1.0):
+    """Scotty3D toColor (image.h:168-185): (H, W, 4) float32 -> (H, W, 4) uint8."""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.zeros(img.shape, dtype=np.uint8)
+    rc = LIB.pt_tonemap(_ptr(img, C.c_float), img.shape[1], img.shape[0], gamma, level, _ptr(out, C.c_uint8))
+    if rc != PT_OK:
+        raise PTError(rc, "pt_tonemap")
+    return out
+
+
+def write_png(path, rgba8):
+    rgba8 = np.ascontiguousarray(rgba8, dtype=np.uint8)
+    rc = LIB.pt_write_png(str(path).encode(), _ptr(rgba8, C.c_uint8), rgba8.shape[1], rgba8.shape[0])
+    if rc != PT_OK:
+        raise PTError(rc, f"pt_write_png {path}")
+
+
+def write_pfm(path, img):
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    rc = LIB.pt_write_pfm(str(path).encode(), _ptr(img, C.c_float), img.shape[1], img.shape[0])
+    if rc != PT_OK:
+        raise PTError(rc, f"pt_write_pfm {path}")

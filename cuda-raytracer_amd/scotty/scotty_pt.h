@@ -209,7 +209,13 @@ class CudaRenderer {
     dev_.check(pt_render(dev_.get(), &p), "pt_render");
     samples_ += spp;
   }
-  const Image* getImage() {  // cu:1539
+  // cu:1539-1569: the median-filtered frame below 32 accumulated samples
+  // (POST_PROCESS_THRESHOLD), the accumulated frame afterwards
+  const Image* getImage() {
+    dev_.check(pt_get_display_image(dev_.get(), image_.data.data(), image_.data.size()), "pt_get_display_image");
+    return &image_;
+  }
+  const Image* getAccumulatedImage() {
     dev_.check(pt_get_image(dev_.get(), image_.data.data(), image_.data.size()), "pt_get_image");
     return &image_;
   }
@@ -264,14 +270,19 @@ class PathTracer {
     const float* p = &img_->data[((size_t)y * img_->width + x) * 4];
     return Vector3D(p[0], p[1], p[2]);
   }
-  // PFM (float RGB, bottom-up rows: the framebuffer's own order)
+  // pathtracer.cpp:577-591 writes a tonemapped PNG; ".pfm" keeps the floats
   void save_image(const std::string& filename) const {
     if (!img_) throw Error(PT_E_INVALID, "save_image before start_raytracing");
-    FILE* f = fopen(filename.c_str(), "wb");
-    if (!f) throw Error(PT_E_IO, "save_image: cannot open " + filename);
-    fprintf(f, "PF\n%d %d\n-1.0\n", img_->width, img_->height);
-    for (size_t i = 0; i < (size_t)img_->width * img_->height; ++i) fwrite(&img_->data[i * 4], 4, 3, f);
-    fclose(f);
+    const bool pfm = filename.size() >= 4 && filename.compare(filename.size() - 4, 4, ".pfm") == 0;
+    int rc;
+    if (pfm) {
+      rc = pt_write_pfm(filename.c_str(), img_->data.data(), img_->width, img_->height);
+    } else {
+      std::vector<uint8_t> rgba8((size_t)img_->width * img_->height * 4);
+      rc = pt_tonemap(img_->data.data(), img_->width, img_->height, 2.2f, 1.0f, rgba8.data());
+      if (!rc) rc = pt_write_png(filename.c_str(), rgba8.data(), img_->width, img_->height);
+    }
+    if (rc) throw Error(rc, "save_image: cannot write " + filename);
   }
   CudaRenderer& renderer() { return r_; }
 

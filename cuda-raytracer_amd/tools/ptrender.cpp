@@ -2,7 +2,7 @@
 // (src/cudaMain.cpp:30-104 + display.cpp's GLUT loop): load a COLLADA scene,
 // render W x H at S spp on one GPU through the C ABI, write a PFM.
 //
-//   ptrender scene.dae [-w 1024] [-h 1024] [-s 256] [-m 8] [-o out.pfm] [-d device]
+//   ptrender scene.dae [-w 1024] [-h 1024] [-s 256] [-m 8] [-o out.png|out.pfm] [-d device]
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -12,7 +12,7 @@
 
 int main(int argc, char** argv) {
   if (argc < 2) {
-    std::cerr << "usage: ptrender scene.dae [-w W] [-h H] [-s spp] [-m bounces] [-o out.pfm] [-d device]\n";
+    std::cerr << "usage: ptrender scene.dae [-w W] [-h H] [-s spp] [-m bounces] [-o out.png|out.pfm] [-d device]\n";
     return 2;
   }
   int w = 512, h = 512, spp = 16, bounces = 8, dev = 0;

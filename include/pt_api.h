@@ -258,6 +258,29 @@ int pt_owned_pixels(pt_ctx* ctx, int32_t* n_pixels, int32_t* pixel_index, size_t
 /* Samples per pixel accumulated so far. */
 int pt_samples(pt_ctx* ctx, int32_t* spp);
 
+/* ---- post-process and output --------------------------
+ * 3x3 median filter of a width*height float RGBA frame on the device
+ * (kernelMedianFilter, cu:773-842): per channel the 4th largest of the 3x3
+ * neighbourhood, out-of-frame neighbours count as 1.0, alpha = 1.  In place
+ * is allowed (rgba_out == rgba_in). */
+int pt_median_filter(pt_ctx* ctx, const float* rgba_in, float* rgba_out, int32_t width, int32_t height);
+/* The frame CudaRenderer::getImage shows (cu:1539-1569): the median-filtered
+ * image while fewer than PT_POST_PROCESS_THRESHOLD samples are accumulated
+ * (cudaRenderer.h:70), the accumulated image afterwards.  Whole-frame
+ * contexts only (nranks == 1); ranks > 1 filter the gathered frame with
+ * pt_median_filter. */
+#define PT_POST_PROCESS_THRESHOLD 32
+int pt_get_display_image(pt_ctx* ctx, float* rgba, size_t n_floats);
+/* Scotty3D HDRImageBuffer::toColor (image.h:168-185): pow(c * sqrt(2^level),
+ * 1/gamma) per channel, clamped to [0,1] and scaled to 8 bits as
+ * ImageBuffer::update_pixel does (image.h:49-58); alpha 255.  Host function. */
+int pt_tonemap(const float* rgba, int32_t width, int32_t height, float gamma, float level, uint8_t* rgba8);
+/* Writers for frames in this ABI's layout (bottom-up rows): PNG (8-bit RGBA,
+ * stored deflate blocks, written top row first) and PFM (float RGB, whose
+ * scanlines run bottom-up like the frame). */
+int pt_write_png(const char* path, const uint8_t* rgba8, int32_t width, int32_t height);
+int pt_write_pfm(const char* path, const float* rgba, int32_t width, int32_t height);
+
 /* Closest-hit query through the breadth-first traversal.  rays: n records of
  * 8 floats (o.xyz, tmax, d.xyz, unused).  hits: n records of
  * (uint64) ((float bits of t) << 32 | sorted prim index), or

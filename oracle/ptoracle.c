@@ -578,3 +578,40 @@ void pto_sample(const pt_scene_desc* S, int W, int H, int max_bounces, uint32_t 
   out3[1] = l.y;
   out3[2] = l.z;
 }
+
+/* ---- display filter: kernelMedianFilter, cu:773-842 --------------------------
+ * Per channel: remove the maximum of the 3x3 neighbourhood three times (max
+ * search from 0.0 with >=, the last index wins, the removed value becomes 0)
+ * and keep the fourth; out-of-frame neighbours are 1.0; alpha 1. */
+void pto_median(const float* in, float* out, int w, int h) {
+  for (int r = 0; r < h; ++r)
+    for (int c = 0; c < w; ++c) {
+      float v[3][9];
+      int k = 0;
+      for (int dr = -1; dr <= 1; ++dr)
+        for (int dc = -1; dc <= 1; ++dc, ++k) {
+          int rr = r + dr, cc = c + dc;
+          for (int ch = 0; ch < 3; ++ch)
+            v[ch][k] = (rr >= 0 && rr < h && cc >= 0 && cc < w) ? in[((size_t)rr * w + cc) * 4 + ch] : 1.0f;
+        }
+      float* o = out + ((size_t)r * w + c) * 4;
+      for (int ch = 0; ch < 3; ++ch) {
+        float res = 0.0f;
+        for (int it = 0; it < 4; ++it) {
+          int im = 0;
+          float m = 0.0f;
+          for (int j = 0; j < 9; ++j)
+            if (v[ch][j] >= m) {
+              m = v[ch][j];
+              im = j;
+            }
+          if (it < 3)
+            v[ch][im] = 0.0f;
+          else
+            res = v[ch][im];
+        }
+        o[ch] = res;
+      }
+      o[3] = 1.0f;
+    }
+}

@@ -36,6 +36,8 @@ def _load():
     lib.pto_render.restype = C.c_uint64
     lib.pto_render.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_int, C.c_uint32,
                                C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
+    lib.pto_median.restype = None
+    lib.pto_median.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int, C.c_int]
     lib.pto_sample.restype = None
     lib.pto_sample.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32,
                                C.c_uint32, C.POINTER(C.c_float)]
@@ -98,3 +100,11 @@ def sincos2pi(u):
     s, c = C.c_float(), C.c_float()
     LIB.pto_sincos2pi(C.c_float(u), C.byref(s), C.byref(c))
     return s.value, c.value
+
+
+def median(img):
+    """kernelMedianFilter restated (cu:773-842) on an (H, W, 4) float32 frame."""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.zeros_like(img)
+    LIB.pto_median(_f(img), _f(out), img.shape[1], img.shape[0])
+    return out
