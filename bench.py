@@ -55,7 +55,7 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scene", default="CBempty", help="headline scene (configs[1] = CBempty)")
-    p.add_argument("--configs", default="CBspheres,CBbunny,dragon_proxy",
+    p.add_argument("--configs", default="CBspheres,CBbunny,dragon_proxy,dragon_proxy_lbvh",
                    help="other single-GPU configs measured in the same run ('' = none)")
     p.add_argument("--width", type=int, default=1024)
     p.add_argument("--height", type=int, default=1024)
@@ -130,7 +130,9 @@ def run_workload(name, args, ctx, rank, world, dev, dist):
     import ptrace
     import ptdist
     import scenes
+    tb = time.perf_counter()
     scene = scenes.load(name)
+    build_ms = (time.perf_counter() - tb) * 1e3  # scene assembly + BVH build (outside the timed frames)
     ctx.load_scene(scene)
     desc = scene.desc()
 
@@ -205,6 +207,9 @@ def run_workload(name, args, ctx, rank, world, dev, dist):
         "ms_per_frame": round(ms_step, 2),
         "rays_per_frame": int(rays / args.steps),
         "batch_paths": st.batch_paths,
+        "scene_build_ms": round(build_ms, 1),
+        "bvh": {"nodes": int(desc.n_nodes), "levels": int(desc.n_levels), "prims": int(desc.n_prims),
+                "gpu_build_ms": round(getattr(scene, "build_ms", 0.0), 2) or None},
         "roofline": roof,
         "trace": {"visits_per_ray": round(st.visits / max(1, st.rays), 2),
                   "instrumented_frame_ms": None if instrumented_ms is None else round(instrumented_ms, 2),

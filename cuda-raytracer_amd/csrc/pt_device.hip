@@ -62,6 +62,8 @@ struct pt_ctx {
   // wavefront buffers (sized for N paths = 2N ray slots)
   uint32_t cap_paths = 0;  // paths the buffers hold
   uint32_t cap_spp = 0;    // ray slots per path they hold (2, or 3 under the reference schedule)
+  size_t qfactor = 24;     // queue entries per ray slot and parity half (doubles on overflow)
+  size_t cap_qfactor = 0;
   float4* d_ray = nullptr;  // 2N ray records (trace.h), RSTRIDE float4 each
   float4 *d_ps0 = nullptr, *d_ps1 = nullptr, *d_ps2 = nullptr, *d_ps3 = nullptr;
   uint32_t* d_q = nullptr;
@@ -153,14 +155,16 @@ static void free_all(pt_ctx* c) {
     if (p) hipFree(p);
 }
 
-// Buffers for N paths (2N ray slots).  Queue halves hold QFACTOR * 2N ids.
-static constexpr size_t QFACTOR = 24;
+// Buffers for N paths (spp ray slots each).  Queue halves hold qfactor ids
+// per slot: 24 covers the measured scenes (peak_queue_entries); a level that
+// would overflow is abandoned on the device, the batch is re-run with twice
+// the factor (pathological overlap, e.g. random triangle soups).
 // Paths in flight per batch.  Large batches amortise the per-level launches
 // (deep levels hold few rays per pass); queue offsets are u32, so both parity
-// halves (2 x QFACTOR x slots ids) must stay below 2^32.
+// halves (2 x qfactor x slots ids) must stay below 2^32.
 static constexpr uint32_t DEFAULT_BATCH_PATHS = 32u << 20;
-static uint32_t max_batch_paths(uint32_t slots_per_path) {
-  return (uint32_t)((1ull << 32) / (2 * QFACTOR * slots_per_path)) & ~4095u;
+static uint32_t max_batch_paths(const pt_ctx* c, uint32_t slots_per_path) {
+  return (uint32_t)((1ull << 32) / (2 * c->qfactor * slots_per_path)) & ~4095u;
 }
 
 // Per-lane capacity of each root target queue for N paths with spp ray slots
@@ -174,7 +178,8 @@ static size_t root_per_lane(size_t N, size_t spp) {
 }
 
 static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
-  if (N <= c->cap_paths && spp <= c->cap_spp) return PT_OK;
+  if (N <= c->cap_paths && spp <= c->cap_spp && c->qfactor == c->cap_qfactor) return PT_OK;
+  if (c->qfactor != c->cap_qfactor) N = std::min(N, max_batch_paths(c, spp));
   N = std::max(N, c->cap_paths);
   spp = std::max(spp, c->cap_spp);
   const size_t slots = (size_t)spp * N;
@@ -186,15 +191,16 @@ static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
   if (spp > 2 && (rc = dalloc(c, &c->d_ps3, N))) return rc;
   // every root target needs root_per_lane slots per lane (<= 16 targets, see
   // set_root_child_offsets); deeper levels need at most 4x the visits of the
-  // level above, which QFACTOR covers for the scenes measured (peak_queue_entries)
+  // level above, which qfactor covers for the scenes measured (peak_queue_entries)
   const size_t root_need = (size_t)NLANE * 16 * root_per_lane(N, spp);
   // a single-leaf tree queues nothing (k_path_leaf / the root pass only)
-  c->qcap = c->root_leaf ? NLANE * 64 : std::max(QFACTOR * slots, root_need);
+  c->qcap = c->root_leaf ? NLANE * 64 : std::max(c->qfactor * slots, root_need);
   c->qcap = (c->qcap + NLANE * 64 - 1) / (NLANE * 64) * (NLANE * 64);
   if (2 * c->qcap >= (1ull << 32)) return fail(c, PT_E_UNSUPPORTED, "batch too large for u32 queue offsets");
   if ((rc = dalloc(c, &c->d_q, 2 * c->qcap))) return rc;
   c->cap_paths = N;
   c->cap_spp = spp;
+  c->cap_qfactor = c->qfactor;
   return PT_OK;
 }
 
@@ -220,11 +226,13 @@ static int set_root_child_offsets(pt_ctx* c) {
   }
   if (targets.size() * per_lane > lanecap) return fail(c, PT_E_OVERFLOW, "root queue capacity");
   const size_t half = c->skip_l1 ? 0 : c->qcap;
-  for (size_t jj = 0; jj < targets.size(); ++jj) {
-    uint32_t off[NLANE];
-    for (int s = 0; s < NLANE; ++s) off[s] = (uint32_t)(half + (size_t)s * lanecap + jj * per_lane);
-    HIPCHK(c, hipMemcpy(c->d_qoff + (size_t)targets[jj] * NLANE, off, sizeof(off), hipMemcpyHostToDevice));
-  }
+  // ordered on the context's (non-blocking) stream behind any work in flight
+  std::vector<uint32_t> off(targets.size() * NLANE);
+  for (size_t jj = 0; jj < targets.size(); ++jj)
+    for (int s = 0; s < NLANE; ++s) off[jj * NLANE + s] = (uint32_t)(half + (size_t)s * lanecap + jj * per_lane);
+  for (size_t jj = 0; jj < targets.size(); ++jj)
+    HIPCHK(c, hipMemcpyAsync(c->d_qoff + (size_t)targets[jj] * NLANE, &off[jj * NLANE], NLANE * 4,
+                             hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return PT_OK;
 }
@@ -539,48 +547,48 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   const bool ref_sched = (P->flags & PT_FLAG_REF_SCHEDULE) != 0;
   const uint32_t nsh = ref_sched ? 2u : 1u;
   const int max_bounces = ref_sched ? 2 : P->max_bounces;
-  uint32_t target = P->batch_paths > 0 ? (uint32_t)P->batch_paths : DEFAULT_BATCH_PATHS;
-  target = std::min<uint32_t>(target, max_batch_paths(1 + nsh));
-  uint32_t spp_b = std::max<uint32_t>(1, target / npix);
-  spp_b = std::min<uint32_t>(spp_b, (uint32_t)P->spp);
-  const uint32_t Nmax = npix * spp_b;
-  if ((size_t)npix > max_batch_paths(1 + nsh))
-    return fail(c, PT_E_UNSUPPORTED, "more owned pixels than one batch holds");
-  const bool realloc = Nmax > c->cap_paths || 1 + nsh > c->cap_spp;
-  if ((rc = ensure_paths(c, Nmax, 1 + nsh))) return rc;
-  if (realloc && (rc = set_root_child_offsets(c))) return rc;
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
   c->timing = (P->flags & PT_FLAG_STATS) != 0;
   const bool timed = c->timing;
-  (void)timed;
-  c->stats.batch_paths = (int32_t)Nmax;
-
-  ShadeArgs S;
-  S.ray = c->d_ray;
-  S.ps0 = c->d_ps0;
-  S.ps1 = c->d_ps1;
-  S.ps2 = c->d_ps2;
-  S.ps3 = c->d_ps3;
-  S.prims = c->d_prims;
-  S.shading = c->d_shading;
-  S.bsdfs = c->d_bsdfs;
-  S.pix_of = c->d_pix_of;
-  S.light = c->light;
-  S.cam = c->camera;
-  S.npix = npix;
-  S.seed = P->seed;
-  S.width = P->width;
-  S.height = P->height;
-  S.max_bounces = max_bounces;
-  S.flags = P->flags;
-  S.A = trace_args(c);
-  S.rcount = c->d_rcount;
 
   hipEvent_t t0 = c->ev[6], t1 = c->ev[7];
   HIPCHK(c, hipEventRecord(t0, c->stream));
+  bool first = true;
   for (int done = 0; done < P->spp;) {
+    // batch size under the current queue factor
+    const uint32_t cap = max_batch_paths(c, 1 + nsh);
+    if (npix > cap) return fail(c, PT_E_UNSUPPORTED, "more owned pixels than one batch holds");
+    uint32_t target = P->batch_paths > 0 ? (uint32_t)P->batch_paths : DEFAULT_BATCH_PATHS;
+    target = std::min<uint32_t>(target, cap);
+    const uint32_t spp_b = std::min<uint32_t>(std::max<uint32_t>(1, target / npix), (uint32_t)P->spp);
     const uint32_t sb = std::min<uint32_t>(spp_b, (uint32_t)(P->spp - done));
     const uint32_t N = npix * sb;
+    const bool realloc = N > c->cap_paths || 1 + nsh > c->cap_spp || c->qfactor != c->cap_qfactor;
+    if ((rc = ensure_paths(c, N, 1 + nsh))) return rc;
+    if (realloc && (rc = set_root_child_offsets(c))) return rc;
+    if (first) c->stats.batch_paths = (int32_t)N;
+    first = false;
+
+    ShadeArgs S;
+    S.ray = c->d_ray;
+    S.ps0 = c->d_ps0;
+    S.ps1 = c->d_ps1;
+    S.ps2 = c->d_ps2;
+    S.ps3 = c->d_ps3;
+    S.prims = c->d_prims;
+    S.shading = c->d_shading;
+    S.bsdfs = c->d_bsdfs;
+    S.pix_of = c->d_pix_of;
+    S.light = c->light;
+    S.cam = c->camera;
+    S.npix = npix;
+    S.seed = P->seed;
+    S.width = P->width;
+    S.height = P->height;
+    S.max_bounces = max_bounces;
+    S.flags = P->flags;
+    S.A = trace_args(c);
+    S.rcount = c->d_rcount;
     S.N = N;
     S.sample_base = (uint32_t)(P->sample_offset + done);
     const dim3 grid((N + TPB - 1) / TPB);
@@ -614,6 +622,18 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         if (!last && nc == 4 && nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4, 1>, grid, dim3(TPB), S);
         if (!last && nc == 4 && nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4, 2>, grid, dim3(TPB), S);
       }
+      // a level that overflowed its queue was abandoned: re-run the batch
+      // (nothing has been accumulated yet) with twice the queue factor
+      uint32_t e = 0;
+      HIPCHK(c, hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      if (e) {
+        if (max_batch_paths(c, 1 + nsh) / 2 < npix)
+          return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded (u32 queue offsets)");
+        c->qfactor *= 2;
+        HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+        continue;
+      }
     }
     c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_ps1,
               c->d_accum, npix, sb);
@@ -629,9 +649,6 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   if (timed) collect_marks(c);
   c->timing = false;
   c->samples += P->spp;
-  uint32_t e = 0;
-  HIPCHK(c, hipMemcpy(&e, c->d_err, 4, hipMemcpyDeviceToHost));
-  if (e) return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded; lower batch_paths");
   return PT_OK;
 }
 
@@ -716,16 +733,35 @@ int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) {
   if (realloc && (rc = set_root_child_offsets(c))) return rc;
   float4* d_in = nullptr;
   HIPCHK(c, hipMalloc((void**)&d_in, (size_t)n * 32));  // rays in, then hit keys out
-  HIPCHK(c, hipMemcpyAsync(d_in, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
-  hipLaunchKernelGGL(k_load_rays, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, d_in, c->d_ray,
-                     (uint32_t)n);
-  hipEventRecord(c->ev[6], c->stream);
-  rc = trace_pass(c, 0, (uint32_t)n);
-  hipEventRecord(c->ev[7], c->stream);
-  if (rc) {
-    hipFree(d_in);
-    return rc;
+  for (;;) {
+    HIPCHK(c, hipMemcpyAsync(d_in, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_load_rays, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, d_in, c->d_ray,
+                       (uint32_t)n);
+    hipEventRecord(c->ev[6], c->stream);
+    rc = trace_pass(c, 0, (uint32_t)n);
+    hipEventRecord(c->ev[7], c->stream);
+    if (rc) {
+      hipFree(d_in);
+      return rc;
+    }
+    uint32_t e = 0;  // (the context's stream is non-blocking: read the flag on it)
+    if (hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+      hipFree(d_in);
+      return fail(c, PT_E_HIP, "pt_intersect: error flag");
+    }
+    if (!e) break;
+    // a level overflowed its queue: twice the queue factor, trace again
+    if (2 * (2 * c->qfactor) * 2 * (size_t)N >= (1ull << 32)) {
+      hipFree(d_in);
+      return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded");
+    }
+    c->qfactor *= 2;
+    if ((rc = ensure_paths(c, N, 2)) || (rc = set_root_child_offsets(c))) {
+      hipFree(d_in);
+      return rc;
+    }
   }
   hipLaunchKernelGGL(k_store_hits, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, c->d_ray,
                      (unsigned long long*)d_in, (uint32_t)n);
@@ -735,9 +771,6 @@ int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) {
   hipEventElapsedTime(&ms, c->ev[6], c->ev[7]);
   c->stats.ms_total = ms;
   hipFree(d_in);
-  uint32_t e = 0;
-  HIPCHK(c, hipMemcpy(&e, c->d_err, 4, hipMemcpyDeviceToHost));
-  if (e) return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded");
   return PT_OK;
 }
 

@@ -269,6 +269,21 @@ float round_up(double v) {
 
 }  // namespace
 
+// BSDF table: one entry per scene object (cu:1694-1723)
+void flatten_bsdfs(Scene& S) {
+  S.dbsdfs.clear();
+  for (const Material& m : S.materials) {
+    pt_bsdf b{};
+    b.type = m.type;
+    for (int k = 0; k < 3; ++k) {
+      b.albedo[k] = m.albedo[k];
+      b.transmittance[k] = m.trans[k];
+    }
+    b.ior = m.ior;
+    S.dbsdfs.push_back(b);
+  }
+}
+
 void build_bvh_and_flatten(Scene& S, size_t max_leaf) {
   const int n = (int)S.prims.size();
   BuildCtx C;
@@ -347,18 +362,7 @@ void build_bvh_and_flatten(Scene& S, size_t max_leaf) {
     }
   }
 
-  // BSDF table: one entry per scene object (cu:1694-1723)
-  S.dbsdfs.clear();
-  for (const Material& m : S.materials) {
-    pt_bsdf b{};
-    b.type = m.type;
-    for (int k = 0; k < 3; ++k) {
-      b.albedo[k] = m.albedo[k];
-      b.transmittance[k] = m.trans[k];
-    }
-    b.ior = m.ior;
-    S.dbsdfs.push_back(b);
-  }
+  flatten_bsdfs(S);
 
   // wide tree + DFS compress + BFS renumbering
   S.dnodes.clear();

@@ -7,6 +7,71 @@
 
 using ptscene::Scene;
 
+namespace ptscene {
+
+// pt_mesh_desc -> input-order Scene (prims, meshes, materials, light, camera)
+int scene_from_mesh(const pt_mesh_desc* md, Scene& S) {
+  if (!md || md->n_tris < 0 || md->n_spheres < 0 || md->n_tris + md->n_spheres <= 0 || md->n_bsdfs <= 0 ||
+      !md->bsdfs || (md->n_tris > 0 && !md->positions) || (md->n_spheres > 0 && !md->spheres))
+    return PT_E_INVALID;
+  for (int32_t t = 0; t < md->n_tris; ++t)
+    if (md->tri_bsdf && (md->tri_bsdf[t] < 0 || md->tri_bsdf[t] >= md->n_bsdfs)) return PT_E_INVALID;
+  for (int32_t t = 0; t < md->n_spheres; ++t)
+    if (md->sphere_bsdf && (md->sphere_bsdf[t] < 0 || md->sphere_bsdf[t] >= md->n_bsdfs)) return PT_E_INVALID;
+  ptscene::Mesh m;
+  for (int32_t t = 0; t < md->n_tris; ++t) {
+    const float* q = md->positions + (size_t)t * 9;
+    ptscene::V3 p[3];
+    for (int k = 0; k < 3; ++k) p[k] = ptscene::V3(q[k * 3 + 0], q[k * 3 + 1], q[k * 3 + 2]);
+    ptscene::V3 fn = ptscene::cross(p[1] - p[0], p[2] - p[0]);
+    const double len = fn.norm();
+    fn = len > 0 ? fn / len : ptscene::V3(0, 0, 1);
+    ptscene::Prim pr;
+    pr.kind = PT_PRIM_TRIANGLE;
+    pr.object = md->tri_bsdf ? md->tri_bsdf[t] : 0;
+    pr.mesh = 0;
+    for (int k = 0; k < 3; ++k) {
+      pr.v[k] = (int)m.positions.size();
+      m.positions.push_back(p[k]);
+      if (md->normals) {
+        const float* n = md->normals + (size_t)t * 9 + k * 3;
+        m.normals.push_back(ptscene::V3(n[0], n[1], n[2]));
+      } else {
+        m.normals.push_back(fn);
+      }
+    }
+    S.prims.push_back(pr);
+  }
+  S.meshes.push_back(std::move(m));
+  for (int32_t t = 0; t < md->n_spheres; ++t) {
+    const float* q = md->spheres + (size_t)t * 4;
+    ptscene::Prim pr;
+    pr.kind = PT_PRIM_SPHERE;
+    pr.object = md->sphere_bsdf ? md->sphere_bsdf[t] : 0;
+    pr.centre = ptscene::V3(q[0], q[1], q[2]);
+    pr.radius = q[3];
+    S.prims.push_back(pr);
+  }
+  for (int32_t b = 0; b < md->n_bsdfs; ++b) {
+    ptscene::Material mat;
+    mat.type = md->bsdfs[b].type;
+    for (int k = 0; k < 3; ++k) {
+      mat.albedo[k] = md->bsdfs[b].albedo[k];
+      mat.trans[k] = md->bsdfs[b].transmittance[k];
+    }
+    mat.ior = md->bsdfs[b].ior;
+    S.materials.push_back(mat);
+  }
+  if (md->light) S.light = *md->light;
+  if (md->camera) {
+    S.camera = *md->camera;
+    S.have_camera = true;
+  }
+  return PT_OK;
+}
+
+}  // namespace ptscene
+
 extern "C" {
 
 int pt_scene_load_dae(const char* path, pt_scene** out, char* errbuf, size_t errbuf_len) {
@@ -94,66 +159,14 @@ int pt_scene_from_triangles(const float* positions, int32_t n_tris, const pt_bsd
 int pt_scene_from_mesh(const pt_mesh_desc* md, pt_scene** out) {
   if (!out) return PT_E_INVALID;
   *out = nullptr;
-  if (!md || md->n_tris < 0 || md->n_spheres < 0 || md->n_tris + md->n_spheres <= 0 || md->n_bsdfs <= 0 ||
-      !md->bsdfs || (md->n_tris > 0 && !md->positions) || (md->n_spheres > 0 && !md->spheres))
-    return PT_E_INVALID;
-  for (int32_t t = 0; t < md->n_tris; ++t)
-    if (md->tri_bsdf && (md->tri_bsdf[t] < 0 || md->tri_bsdf[t] >= md->n_bsdfs)) return PT_E_INVALID;
-  for (int32_t t = 0; t < md->n_spheres; ++t)
-    if (md->sphere_bsdf && (md->sphere_bsdf[t] < 0 || md->sphere_bsdf[t] >= md->n_bsdfs)) return PT_E_INVALID;
   auto* sc = new pt_scene();
-  Scene& S = sc->s;
-  ptscene::Mesh m;
-  for (int32_t t = 0; t < md->n_tris; ++t) {
-    const float* q = md->positions + (size_t)t * 9;
-    ptscene::V3 p[3];
-    for (int k = 0; k < 3; ++k) p[k] = ptscene::V3(q[k * 3 + 0], q[k * 3 + 1], q[k * 3 + 2]);
-    ptscene::V3 fn = ptscene::cross(p[1] - p[0], p[2] - p[0]);
-    const double len = fn.norm();
-    fn = len > 0 ? fn / len : ptscene::V3(0, 0, 1);
-    ptscene::Prim pr;
-    pr.kind = PT_PRIM_TRIANGLE;
-    pr.object = md->tri_bsdf ? md->tri_bsdf[t] : 0;
-    pr.mesh = 0;
-    for (int k = 0; k < 3; ++k) {
-      pr.v[k] = (int)m.positions.size();
-      m.positions.push_back(p[k]);
-      if (md->normals) {
-        const float* n = md->normals + (size_t)t * 9 + k * 3;
-        m.normals.push_back(ptscene::V3(n[0], n[1], n[2]));
-      } else {
-        m.normals.push_back(fn);
-      }
-    }
-    S.prims.push_back(pr);
-  }
-  S.meshes.push_back(std::move(m));
-  for (int32_t t = 0; t < md->n_spheres; ++t) {
-    const float* q = md->spheres + (size_t)t * 4;
-    ptscene::Prim pr;
-    pr.kind = PT_PRIM_SPHERE;
-    pr.object = md->sphere_bsdf ? md->sphere_bsdf[t] : 0;
-    pr.centre = ptscene::V3(q[0], q[1], q[2]);
-    pr.radius = q[3];
-    S.prims.push_back(pr);
-  }
-  for (int32_t b = 0; b < md->n_bsdfs; ++b) {
-    ptscene::Material mat;
-    mat.type = md->bsdfs[b].type;
-    for (int k = 0; k < 3; ++k) {
-      mat.albedo[k] = md->bsdfs[b].albedo[k];
-      mat.trans[k] = md->bsdfs[b].transmittance[k];
-    }
-    mat.ior = md->bsdfs[b].ior;
-    S.materials.push_back(mat);
-  }
-  if (md->light) S.light = *md->light;
-  if (md->camera) {
-    S.camera = *md->camera;
-    S.have_camera = true;
+  int rc = ptscene::scene_from_mesh(md, sc->s);
+  if (rc) {
+    delete sc;
+    return rc;
   }
   try {
-    ptscene::build_bvh_and_flatten(S, 32);
+    ptscene::build_bvh_and_flatten(sc->s, 32);
   } catch (const std::exception&) {
     delete sc;
     return PT_E_INVALID;

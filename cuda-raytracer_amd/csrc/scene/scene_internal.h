@@ -126,6 +126,11 @@ struct Scene {
 // bvh_ref.cpp: restated BVHAccel / compactTree / compress + BFS flattening.
 void build_bvh_and_flatten(Scene& s, size_t max_leaf_size = 32);
 
+// scene_api.cpp: pt_mesh_desc -> input-order Scene; PT_OK or PT_E_INVALID
+int scene_from_mesh(const pt_mesh_desc* md, Scene& s);
+// bvh_ref.cpp: the bsdf table (one entry per scene object)
+void flatten_bsdfs(Scene& s);
+
 // dae.cpp
 bool load_dae(const std::string& path, Scene& s, std::string& err);
 

@@ -108,7 +108,7 @@ class pt_mesh_desc(C.Structure):
 
 # every symbol include/pt_api.h declares (tests check the library exports them)
 API_SYMBOLS = [
-    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_free", "pt_scene_get_desc",
+    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_build_gpu", "pt_scene_free", "pt_scene_get_desc",
     "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
     "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect",
@@ -136,6 +136,7 @@ def _load():
         "pt_scene_from_triangles": (C.c_int, [C.POINTER(C.c_float), I32, C.POINTER(pt_bsdf),
                                               C.POINTER(pt_light), C.POINTER(pt_camera), C.POINTER(P)]),
         "pt_scene_from_mesh": (C.c_int, [C.POINTER(pt_mesh_desc), C.POINTER(P)]),
+        "pt_scene_build_gpu": (C.c_int, [C.POINTER(pt_mesh_desc), I32, I32, C.POINTER(P), C.POINTER(C.c_double)]),
         "pt_scene_free": (None, [P]),
         "pt_median_filter": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_float), I32, I32]),
         "pt_get_display_image": (C.c_int, [P, C.POINTER(C.c_float), SZ]),
@@ -209,10 +210,11 @@ class Scene:
 
     @classmethod
     def from_mesh(cls, positions, bsdfs, normals=None, tri_bsdf=None, spheres=None, sphere_bsdf=None,
-                  light=None, camera=None):
+                  light=None, camera=None, gpu_device=None, max_leaf=8):
         """General flattened input (pt_scene_from_mesh): triangles (n, 9),
         optional vertex normals (n, 9), per-triangle bsdf ids, spheres (m, 4)
-        and a list of pt_bsdf."""
+        and a list of pt_bsdf.  gpu_device=k builds the BVH on GPU k
+        (pt_scene_build_gpu, wide leaves of <= max_leaf primitives)."""
         keep = []
 
         def arr(a, dt, k):
@@ -241,10 +243,17 @@ class Scene:
         m.light = C.pointer(light) if light is not None else None
         m.camera = C.pointer(camera) if camera is not None else None
         h = C.c_void_p()
-        rc = LIB.pt_scene_from_mesh(C.byref(m), C.byref(h))
+        if gpu_device is None:
+            rc = LIB.pt_scene_from_mesh(C.byref(m), C.byref(h))
+        else:
+            ms = C.c_double()
+            rc = LIB.pt_scene_build_gpu(C.byref(m), gpu_device, max_leaf, C.byref(h), C.byref(ms))
         if rc != PT_OK:
-            raise PTError(rc, "pt_scene_from_mesh failed")
-        return cls(h)
+            raise PTError(rc, "pt_scene_from_mesh failed" if gpu_device is None else "pt_scene_build_gpu failed")
+        sc = cls(h)
+        if gpu_device is not None:
+            sc.build_ms = ms.value
+        return sc
 
     def __del__(self):
         if getattr(self, "h", None) and self.h.value:

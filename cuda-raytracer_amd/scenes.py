@@ -7,8 +7,9 @@ deterministically from CBbunny.dae (flattened fixture tests/golden/scenes/
 CBbunny.npz): the Cornell box walls and area light once, three copies of the
 28,576-triangle bunny (scaled 0.6, rotated about y by 0/120/240 degrees, set
 side by side on the floor) and a tessellated mirror sphere (60 x 120 UV
-sphere, 13,920 triangles) under the light: 99,660 triangles in total, run
-through the same reference BVH build (pt_scene_from_mesh).
+sphere, 14,160 triangles) under the light: 99,900 triangles in total, run
+through the same reference BVH build (pt_scene_from_mesh) or, as
+"dragon_proxy_lbvh", through the GPU build (pt_scene_build_gpu).
 """
 import math
 from pathlib import Path
@@ -93,14 +94,18 @@ def dragon_proxy_arrays():
     return (np.concatenate(out_p), np.concatenate(out_n), np.concatenate(out_b), bsdfs, light, camera)
 
 
-def dragon_proxy():
-    """The ~100k-triangle config-4/5 scene as a ptrace.Scene."""
+def dragon_proxy(gpu_device=None, max_leaf=8):
+    """The ~100k-triangle config-4/5 scene as a ptrace.Scene: the reference's
+    host SAH build, or (gpu_device=k) the GPU linear BVH build."""
     pos, nrm, tb, bsdfs, light, camera = dragon_proxy_arrays()
-    return ptrace.Scene.from_mesh(pos, bsdfs, normals=nrm, tri_bsdf=tb, light=light, camera=camera)
+    return ptrace.Scene.from_mesh(pos, bsdfs, normals=nrm, tri_bsdf=tb, light=light, camera=camera,
+                                  gpu_device=gpu_device, max_leaf=max_leaf)
 
 
 def load(name):
     """A bench/test workload by name: a committed fixture or a synthetic scene."""
     if name == "dragon_proxy":
         return dragon_proxy()
+    if name == "dragon_proxy_lbvh":
+        return dragon_proxy(gpu_device=0)
     return ptrace.ArrayScene.load(FIXTURES / f"{name}.npz")

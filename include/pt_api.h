@@ -190,6 +190,12 @@ typedef struct pt_mesh_desc {
   const pt_camera* camera;  /* NULL: default                                  */
 } pt_mesh_desc;
 int pt_scene_from_mesh(const pt_mesh_desc* mesh, pt_scene** out);
+/* The same input built on GPU `device`: Morton-ordered
+ * linear BVH collapsed to the 4-wide, level-major layout (wide leaves hold
+ * <= max_leaf primitives; the reference's host SAH build, bvh.cpp:48-337, is
+ * pt_scene_from_mesh).  *build_ms (optional) receives the build's wall time. */
+int pt_scene_build_gpu(const pt_mesh_desc* mesh, int32_t device, int32_t max_leaf, pt_scene** out,
+                       double* build_ms);
 void pt_scene_free(pt_scene* s);
 /* Borrowed view of the flattened arrays (valid until pt_scene_free). */
 int pt_scene_get_desc(const pt_scene* s, pt_scene_desc* out);
