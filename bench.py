@@ -265,6 +265,8 @@ def main():
             "ms_per_frame": head["ms_per_frame"],
             "rays_per_frame": head["rays_per_frame"],
             "roofline": head["roofline"],
+            "scene_build_ms": head["scene_build_ms"],
+            "bvh": head["bvh"],
             "trace": head["trace"],
             "configs": others,
         }
