@@ -25,13 +25,22 @@ constexpr uint32_t PT_PRIM_NONE = 0xFFFFFFFFu;
 constexpr int TPB = 256;          // threads per workgroup (4 waves)
 constexpr int RPT = 4;            // rays per thread in a traversal item
 constexpr int TILE = TPB * RPT;   // rays per traversal item
-constexpr int RPTW = 4;           // rays per lane in a wave-sized item
+#ifndef PT_RPTW
+#define PT_RPTW 4
+#endif
+#ifndef PT_BLOCK_MODE_RAYS
+#define PT_BLOCK_MODE_RAYS 512
+#endif
+#ifndef PT_LEVEL_GRID
+#define PT_LEVEL_GRID 2048
+#endif
+constexpr int RPTW = PT_RPTW;     // rays per lane in a wave-sized item
 constexpr int WTILE = 64 * RPTW;  // rays per wave item (levels >= 1)
 constexpr int NLANE = 8;          // queue lanes (one per XCD)
 constexpr int CSTRIDE = 32;       // u32 per queue counter: each (node, lane) counter owns a 128-B line
 constexpr uint32_t MODE_WAVE = 0, MODE_BLOCK = 1;
-constexpr uint32_t BLOCK_MODE_RAYS_PER_PAIR = 512;  // level mode threshold (mean rays per queue lane)
-constexpr int LEVEL_GRID = 2048;
+constexpr uint32_t BLOCK_MODE_RAYS_PER_PAIR = PT_BLOCK_MODE_RAYS;  // level mode threshold (mean rays per queue lane)
+constexpr int LEVEL_GRID = PT_LEVEL_GRID;
 constexpr int RCOUNT_SLOTS = 64;  // ray counters (u64, 128 B apart), indexed by workgroup & 63  // workgroups of the per-level grid-stride kernel (8 per CU)
 
 // device statistics slots (unsigned long long)

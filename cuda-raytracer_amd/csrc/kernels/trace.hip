@@ -494,7 +494,10 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 // ---- per-level pass: every wave walks the items of its block's lane ----------------
 // Lane s's items are processed by blocks b with b % 8 == s (same XCD under the
 // observed round-robin placement: a speed hint only).
-__global__ __launch_bounds__(TPB) void k_trace_level(TraceArgs A, LevelArgs L) {
+#ifndef PT_LEVEL_ATTR
+#define PT_LEVEL_ATTR
+#endif
+__global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, LevelArgs L) {
   const int lane = blockIdx.x & (NLANE - 1);
   const uint32_t lid = lane_id();
   const uint32_t wave = threadIdx.x >> 6;
