@@ -32,7 +32,7 @@ constexpr int TILE = TPB * RPT;   // rays per traversal item
 #define PT_BLOCK_MODE_RAYS 512
 #endif
 #ifndef PT_LEVEL_GRID
-#define PT_LEVEL_GRID 2048
+#define PT_LEVEL_GRID 8192
 #endif
 constexpr int RPTW = PT_RPTW;     // rays per lane in a wave-sized item
 constexpr int WTILE = 64 * RPTW;  // rays per wave item (levels >= 1)
@@ -84,6 +84,7 @@ struct LevelArgs {
   uint32_t* nitems_w;
   const uint32_t* mode;  // MODE_WAVE / MODE_BLOCK, chosen by the scan
   uint32_t* mode_w;
+  uint32_t* next;        // [lane * CSTRIDE] item counters of the dynamic work fetch (zeroed by the scan)
 };
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {

@@ -38,8 +38,10 @@ namespace pt {
 // ---- primitive tests ----------------------------------------------------------
 
 // Reference triangle test intersectRayTriangle (cu:217-270) on precomputed
-// operands (pt_api.h pt_prim).  Returns t >= 0 or -1 on a miss.  t = -0 is
-// returned as +0 so that the {t bits, id} key orders correctly.
+// operands (pt_api.h pt_prim): plane hit, then the three edge-side tests, each
+// dot(m_k, P - v_k) with m_k = N x e_k (the reference's dot(N, cross(e_k,
+// P - v_k)) without its per-ray cross products).  Returns t >= 0 or -1 on a
+// miss.  t = -0 is returned as +0 so that the {t bits, id} key orders correctly.
 __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q0, const float4 q1,
                                           const float4 q2, const float4 q3, const float4 q4,
                                           const float4 q5, const float tbest) {
@@ -50,21 +52,12 @@ __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q
   // t > tbest cannot win (ties need t == tbest): skip the edge tests
   if (t < 0.0f || t > tbest) return -1.0f;
   f3 P = mk(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
-  // edge 0: cross(v1 - v0, P - v0)
-  f3 vp = mk(P.x - q0.x, P.y - q0.y, P.z - q0.z);
-  f3 e = mk(q4.x, q4.y, q4.z);
-  f3 C = cross(e, vp);
-  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
-  // edge 1: cross(v2 - v1, P - v1)
-  vp = mk(P.x - q1.x, P.y - q1.y, P.z - q1.z);
-  e = mk(q5.x, q5.y, q5.z);
-  C = cross(e, vp);
-  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
-  // edge 2: cross(v0 - v2, P - v2)
-  vp = mk(P.x - q2.x, P.y - q2.y, P.z - q2.z);
-  e = mk(q2.w, q3.w, q4.w);
-  C = cross(e, vp);
-  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
+  // edge 0 (v0 -> v1)
+  if (q2.w * (P.x - q0.x) + q3.w * (P.y - q0.y) + q4.w * (P.z - q0.z) < 0.0f) return -1.0f;
+  // edge 1 (v1 -> v2)
+  if (q4.x * (P.x - q1.x) + q4.y * (P.y - q1.y) + q4.z * (P.z - q1.z) < 0.0f) return -1.0f;
+  // edge 2 (v2 -> v0)
+  if (q5.x * (P.x - q2.x) + q5.y * (P.y - q2.y) + q5.z * (P.z - q2.z) < 0.0f) return -1.0f;
   return t == 0.0f ? 0.0f : t;
 }
 
@@ -81,22 +74,21 @@ __device__ __forceinline__ f2v sp(float a) { return f2v{a, a}; }
 __device__ __forceinline__ f3x2 sp3(float a, float b, float c) { return f3x2{sp(a), sp(b), sp(c)}; }
 __device__ __forceinline__ f3x2 pair3(f3 a, f3 b) { return f3x2{f2v{a.x, b.x}, f2v{a.y, b.y}, f2v{a.z, b.z}}; }
 
-__device__ __forceinline__ f2v edge_side2(const f3x2& N, const f3x2& P, const f3x2& v, const f3x2& e) {
-  const f2v vx = P.x - v.x, vy = P.y - v.y, vz = P.z - v.z;
-  const f2v cx = e.y * vz - e.z * vy, cy = e.z * vx - e.x * vz, cz = e.x * vy - e.y * vx;
-  return N.x * cx + N.y * cy + N.z * cz;
+// dot(m, P - v) on two lanes: the edge-side test
+__device__ __forceinline__ f2v edge_side2(const f3x2& P, const f3x2& v, const f3x2& m) {
+  return m.x * (P.x - v.x) + m.y * (P.y - v.y) + m.z * (P.z - v.z);
 }
 
-// N: normal, pd: plane offset, v0..v2: vertices, e0..e2: edges (pt_prim layout)
+// N: normal, pd: plane offset, v0..v2: vertices, m0..m2: edge normals (pt_prim layout)
 __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const f3x2& N, f2v pd, const f3x2& v0,
-                                         const f3x2& v1, const f3x2& v2, const f3x2& e0, const f3x2& e1,
-                                         const f3x2& e2, f2v tbest) {
+                                         const f3x2& v1, const f3x2& v2, const f3x2& m0, const f3x2& m1,
+                                         const f3x2& m2, f2v tbest) {
   const f2v ndd = N.x * d.x + N.y * d.y + N.z * d.z;
   const f2v t = (pd - (N.x * o.x + N.y * o.y + N.z * o.z)) / ndd;
   const f3x2 P{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z};
-  const f2v s0 = edge_side2(N, P, v0, e0);
-  const f2v s1 = edge_side2(N, P, v1, e1);
-  const f2v s2 = edge_side2(N, P, v2, e2);
+  const f2v s0 = edge_side2(P, v0, m0);
+  const f2v s1 = edge_side2(P, v1, m1);
+  const f2v s2 = edge_side2(P, v2, m2);
   f2v r;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -307,8 +299,8 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
       } else {
         const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
         const f3x2 N = sp3(q3.x, q3.y, q3.z), v0 = sp3(q0.x, q0.y, q0.z), v1 = sp3(q1.x, q1.y, q1.z),
-                   v2 = sp3(q2.x, q2.y, q2.z), e0 = sp3(q4.x, q4.y, q4.z), e1 = sp3(q5.x, q5.y, q5.z),
-                   e2 = sp3(q2.w, q3.w, q4.w);
+                   v2 = sp3(q2.x, q2.y, q2.z), e0 = sp3(q2.w, q3.w, q4.w), e1 = sp3(q4.x, q4.y, q4.z),
+                   e2 = sp3(q5.x, q5.y, q5.z);  // edge normals m0, m1, m2
 #pragma unroll
         for (int j = 0; j < RPT; j += 2) {
           if (j >= nj) break;
@@ -422,8 +414,8 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
       } else {
         const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
         const f3x2 N = sp3(q3.x, q3.y, q3.z), v0 = sp3(q0.x, q0.y, q0.z), v1 = sp3(q1.x, q1.y, q1.z),
-                   v2 = sp3(q2.x, q2.y, q2.z), e0 = sp3(q4.x, q4.y, q4.z), e1 = sp3(q5.x, q5.y, q5.z),
-                   e2 = sp3(q2.w, q3.w, q4.w);
+                   v2 = sp3(q2.x, q2.y, q2.z), e0 = sp3(q2.w, q3.w, q4.w), e1 = sp3(q4.x, q4.y, q4.z),
+                   e2 = sp3(q5.x, q5.y, q5.z);  // edge normals m0, m1, m2
 #pragma unroll
         for (int j = 0; j < RPTW; j += 2) {
           if (j >= nj) break;
@@ -509,7 +501,16 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
     __shared__ int s_node;
     __shared__ uint32_t s_base;
     __shared__ int s_n;
+#ifdef PT_DYN_ITEMS
+    __shared__ uint32_t s_m;
+    for (;;) {
+      if (threadIdx.x == 0) s_m = atomicAdd(L.next + lane * CSTRIDE, 1u);
+      __syncthreads();
+      const uint32_t m = s_m;
+      if (m >= M) break;
+#else
     for (uint32_t m = blockIdx.x / NLANE; m < M; m += gridDim.x / NLANE) {
+#endif
       if (wave == 0) {
         int lo = 0, hi = L.nl;
         while (hi - lo > 1) {
@@ -540,8 +541,16 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
     return;
   }
   // many nodes with few rays each: every wave walks its own 256-ray items
+#ifdef PT_DYN_ITEMS
+  for (;;) {
+    uint32_t m = 0;
+    if (lid == 0) m = atomicAdd(L.next + lane * CSTRIDE, 1u);
+    m = __builtin_amdgcn_readfirstlane(m);
+    if (m >= M) break;
+#else
   const uint32_t stride = (gridDim.x / NLANE) * (TPB / 64);
   for (uint32_t m = (blockIdx.x / NLANE) * (TPB / 64) + wave; m < M; m += stride) {
+#endif
     // 64-ary search for the node k with ep[k] <= m < ep[k+1]
     int lo = 0, hi = L.nl;
     while (hi - lo > 1) {
@@ -699,6 +708,7 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
     // (the rest of the pass is abandoned and the host reports PT_E_OVERFLOW)
     for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + L.nl] = ovf ? 0u : run[s];
     *L.mode_w = block_mode ? MODE_BLOCK : MODE_WAVE;
+    for (int s = 0; s < NLANE; ++s) L.next[s * CSTRIDE] = 0u;
     if (ovf) atomicOr(err, 1u);
     if (stats) {  // fire-and-forget atomics: no round trip on the critical path
       atomicAdd(stats + STAT_V, V);

@@ -311,13 +311,20 @@ __global__ void k_prim_records(const float* __restrict__ pos, const float* __res
     N[1] = e0[2] * v02[0] - e0[0] * v02[2];
     N[2] = e0[0] * v02[1] - e0[1] * v02[0];
     const float dN = N[0] * v[0][0] + N[1] * v[0][1] + N[2] * v[0][2];
+    float m[3][3];  // edge normals m_k = N x e_k (pt_api.h)
+    const float* ek[3] = {e0, e1, e2};
+    for (int k = 0; k < 3; ++k) {
+      m[k][0] = N[1] * ek[k][2] - N[2] * ek[k][1];
+      m[k][1] = N[2] * ek[k][0] - N[0] * ek[k][2];
+      m[k][2] = N[0] * ek[k][1] - N[1] * ek[k][0];
+    }
     float* q = d.q;
     q[0] = v[0][0]; q[1] = v[0][1]; q[2] = v[0][2]; q[3] = __uint_as_float(meta);
     q[4] = v[1][0]; q[5] = v[1][1]; q[6] = v[1][2]; q[7] = dN;
-    q[8] = v[2][0]; q[9] = v[2][1]; q[10] = v[2][2]; q[11] = e2[0];
-    q[12] = N[0]; q[13] = N[1]; q[14] = N[2]; q[15] = e2[1];
-    q[16] = e0[0]; q[17] = e0[1]; q[18] = e0[2]; q[19] = e2[2];
-    q[20] = e1[0]; q[21] = e1[1]; q[22] = e1[2]; q[23] = 0.f;
+    q[8] = v[2][0]; q[9] = v[2][1]; q[10] = v[2][2]; q[11] = m[0][0];
+    q[12] = N[0]; q[13] = N[1]; q[14] = N[2]; q[15] = m[0][1];
+    q[16] = m[1][0]; q[17] = m[1][1]; q[18] = m[1][2]; q[19] = m[0][2];
+    q[20] = m[2][0]; q[21] = m[2][1]; q[22] = m[2][2]; q[23] = 0.f;
     if (nrm) {
       const float* m = nrm + (size_t)src * 9;
       for (int k = 0; k < 3; ++k) {

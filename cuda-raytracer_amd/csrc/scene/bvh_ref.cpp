@@ -348,13 +348,22 @@ void build_bvh_and_flatten(Scene& S, size_t max_leaf) {
     N[1] = e0[2] * v02[0] - e0[0] * v02[2];
     N[2] = e0[0] * v02[1] - e0[1] * v02[0];
     float dN = N[0] * v[0][0] + N[1] * v[0][1] + N[2] * v[0][2];
+    // edge normals m_k = N x e_k (pt_api.h): dot(m_k, P - v_k) is the
+    // reference's dot(N, cross(e_k, P - v_k))
+    float en[3][3];
+    const float* ek[3] = {e0, e1, e2};
+    for (int k = 0; k < 3; ++k) {
+      en[k][0] = N[1] * ek[k][2] - N[2] * ek[k][1];
+      en[k][1] = N[2] * ek[k][0] - N[0] * ek[k][2];
+      en[k][2] = N[0] * ek[k][1] - N[1] * ek[k][0];
+    }
     float* q = d.q;
     q[0] = v[0][0]; q[1] = v[0][1]; q[2] = v[0][2]; memcpy(&q[3], &meta, 4);
     q[4] = v[1][0]; q[5] = v[1][1]; q[6] = v[1][2]; q[7] = dN;
-    q[8] = v[2][0]; q[9] = v[2][1]; q[10] = v[2][2]; q[11] = e2[0];
-    q[12] = N[0]; q[13] = N[1]; q[14] = N[2]; q[15] = e2[1];
-    q[16] = e0[0]; q[17] = e0[1]; q[18] = e0[2]; q[19] = e2[2];
-    q[20] = e1[0]; q[21] = e1[1]; q[22] = e1[2]; q[23] = 0.f;
+    q[8] = v[2][0]; q[9] = v[2][1]; q[10] = v[2][2]; q[11] = en[0][0];
+    q[12] = N[0]; q[13] = N[1]; q[14] = N[2]; q[15] = en[0][1];
+    q[16] = en[1][0]; q[17] = en[1][1]; q[18] = en[1][2]; q[19] = en[0][2];
+    q[20] = en[2][0]; q[21] = en[2][1]; q[22] = en[2][2]; q[23] = 0.f;
     for (int k = 0; k < 3; ++k) {
       sh.n0[k] = nn[0][k];
       sh.n1[k] = nn[1][k];

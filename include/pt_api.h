@@ -68,14 +68,16 @@ extern "C" {
 
 /* One intersectable primitive, 96 bytes = 6 x float4, in BVH-sorted order
  * (the order of BVHAccel::getSortedPrimitives(), bvh.cpp:384).  Triangles store
- * exactly the operands the reference triangle test derives (cu:217-270):
+ * the operands of the reference triangle test (cu:217-270) in the form the
+ * kernels evaluate it:
  *   q0 = v0.xyz, meta        q1 = v1.xyz, dN = dot(N, v0)
- *   q2 = v2.xyz, e2.x        q3 = N.xyz (= cross(v1-v0, v2-v0)), e2.y
- *   q4 = e0.xyz (= v1-v0), e2.z   q5 = e1.xyz (= v2-v1), 0
- * with e2 = v0-v2.  All derived values are fp32 computed from the fp32 vertices
- * with the reference's operation order, so the kernel's results are those of
- * the reference formula.  Spheres: q0 = centre.xyz, meta; q1.x = radius,
- * q1.y = radius^2; rest 0.                                                     */
+ *   q2 = v2.xyz, m0.x        q3 = N.xyz (= cross(v1-v0, v2-v0)), m0.y
+ *   q4 = m1.xyz, m0.z        q5 = m2.xyz, 0
+ * with edge normals m_k = cross(N, e_k) for e0 = v1-v0, e1 = v2-v1, e2 = v0-v2:
+ * the reference's edge test dot(N, cross(e_k, P - v_k)) < 0 is evaluated as
+ * dot(m_k, P - v_k) < 0 (the same quantity; it differs only in fp32 rounding).
+ * All derived values are fp32 computed from the fp32 vertices.  Spheres:
+ * q0 = centre.xyz, meta; q1.x = radius, q1.y = radius^2; rest 0.            */
 typedef struct pt_prim {
   float q[24];
 } pt_prim;

@@ -125,7 +125,9 @@ static void sincos2pi(float u, float* s, float* c) {
 void pto_sincos2pi(float u, float* s, float* c) { sincos2pi(u, s, c); }
 
 /* ---- primitive tests -------------------------------------------------------- */
-/* intersectRayTriangle, cu:217-270: plane hit then three edge sign tests. */
+/* intersectRayTriangle, cu:217-270: plane hit then three edge sign tests,
+ * dot(N, cross(e_k, P - v_k)) evaluated as dot(m_k, P - v_k) with the
+ * precomputed edge normals m_k = N x e_k (pt_api.h pt_prim layout). */
 static float pto_tri(v3 o, v3 d, const float* q) {
   v3 N = mk(q[12], q[13], q[14]);
   float ndd = N.x * d.x + N.y * d.y + N.z * d.z;
@@ -133,15 +135,9 @@ static float pto_tri(v3 o, v3 d, const float* q) {
   float t = (q[7] - (N.x * o.x + N.y * o.y + N.z * o.z)) / ndd;
   if (t < 0.0f) return -1.0f;
   v3 P = mk(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
-  v3 vp = mk(P.x - q[0], P.y - q[1], P.z - q[2]);
-  v3 C = cross(mk(q[16], q[17], q[18]), vp);
-  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
-  vp = mk(P.x - q[4], P.y - q[5], P.z - q[6]);
-  C = cross(mk(q[20], q[21], q[22]), vp);
-  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
-  vp = mk(P.x - q[8], P.y - q[9], P.z - q[10]);
-  C = cross(mk(q[11], q[15], q[19]), vp);
-  if (N.x * C.x + N.y * C.y + N.z * C.z < 0.0f) return -1.0f;
+  if (q[11] * (P.x - q[0]) + q[15] * (P.y - q[1]) + q[19] * (P.z - q[2]) < 0.0f) return -1.0f;
+  if (q[16] * (P.x - q[4]) + q[17] * (P.y - q[5]) + q[18] * (P.z - q[6]) < 0.0f) return -1.0f;
+  if (q[20] * (P.x - q[8]) + q[21] * (P.y - q[9]) + q[22] * (P.z - q[10]) < 0.0f) return -1.0f;
   return t == 0.0f ? 0.0f : t;
 }
 static float pto_sphere(v3 o, v3 d, const float* q) {
