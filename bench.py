@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--seed", type=int, default=15618)
+    p.add_argument("--config5", choices=["auto", "on", "off"], default="auto",
+                   help="also run BASELINE config 5 (dragon proxy, 2048x2048, 1024 spp, tiles over all ranks); "
+                        "auto = when n_gpus >= 8")
     p.add_argument("--stats-in-timed", action="store_true",
                    help="record per-kernel HIP events inside the timed steps (default: one extra instrumented frame)")
     return p.parse_args()
@@ -126,6 +129,7 @@ def root_leaf_flops(desc):
 
 
 def run_workload(name, args, ctx, rank, world, dev, dist):
+    """One workload (scene + args' frame shape) timed over args.steps frames."""
     import torch
     import ptrace
     import ptdist
@@ -243,6 +247,18 @@ def main():
     others = []
     for name in [s for s in args.configs.split(",") if s and s != args.scene]:
         o, _ = run_workload(name, args, ctx, rank, world, dev, dist)
+        o["config"] = f"{args.width}x{args.height} {args.spp}spp {args.bounces} bounces"
+        others.append(o)
+    if args.config5 == "on" or (args.config5 == "auto" and world >= 8):
+        # BASELINE config 5: the dragon proxy at 2048x2048, 1024 spp, the
+        # framebuffer tiled over all ranks and gathered over RCCL
+        import copy
+        a5 = copy.copy(args)
+        a5.width = a5.height = 2048
+        a5.spp = 1024
+        a5.steps, a5.warmup = 1, 1
+        o, _ = run_workload("dragon_proxy", a5, ctx, rank, world, dev, dist)
+        o["config"] = "config 5: 2048x2048 1024spp 8 bounces, tiles over all ranks + RCCL gather"
         others.append(o)
     if rank == 0:
         out = {
