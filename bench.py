@@ -245,7 +245,7 @@ def main():
 
     head, head_scene = run_workload(args.scene, args, ctx, rank, world, dev, dist)
     others = []
-    for name in [s for s in args.configs.split(",") if s and s != args.scene]:
+    for name in [s for s in args.configs.split(",") if s not in ("", "none", '""') and s != args.scene]:
         o, _ = run_workload(name, args, ctx, rank, world, dev, dist)
         o["config"] = f"{args.width}x{args.height} {args.spp}spp {args.bounces} bounces"
         others.append(o)

@@ -40,7 +40,8 @@ constexpr int NLANE = 8;          // queue lanes (one per XCD)
 constexpr int CSTRIDE = 32;       // u32 per queue counter: each (node, lane) counter owns a 128-B line
 constexpr uint32_t MODE_WAVE = 0, MODE_BLOCK = 1;
 constexpr uint32_t BLOCK_MODE_RAYS_PER_PAIR = PT_BLOCK_MODE_RAYS;  // level mode threshold (mean rays per queue lane)
-constexpr int LEVEL_GRID = PT_LEVEL_GRID;
+constexpr int LEVEL_GRID = PT_LEVEL_GRID;  // workgroups of the level kernel (32 per CU: the
+                                          // dispatcher's refill balances uneven items)
 constexpr int RCOUNT_SLOTS = 64;  // ray counters (u64, 128 B apart), indexed by workgroup & 63  // workgroups of the per-level grid-stride kernel (8 per CU)
 
 // device statistics slots (unsigned long long)
@@ -84,7 +85,6 @@ struct LevelArgs {
   uint32_t* nitems_w;
   const uint32_t* mode;  // MODE_WAVE / MODE_BLOCK, chosen by the scan
   uint32_t* mode_w;
-  uint32_t* next;        // [lane * CSTRIDE] item counters of the dynamic work fetch (zeroed by the scan)
 };
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {

@@ -501,16 +501,7 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
     __shared__ int s_node;
     __shared__ uint32_t s_base;
     __shared__ int s_n;
-#ifdef PT_DYN_ITEMS
-    __shared__ uint32_t s_m;
-    for (;;) {
-      if (threadIdx.x == 0) s_m = atomicAdd(L.next + lane * CSTRIDE, 1u);
-      __syncthreads();
-      const uint32_t m = s_m;
-      if (m >= M) break;
-#else
     for (uint32_t m = blockIdx.x / NLANE; m < M; m += gridDim.x / NLANE) {
-#endif
       if (wave == 0) {
         int lo = 0, hi = L.nl;
         while (hi - lo > 1) {
@@ -541,16 +532,8 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
     return;
   }
   // many nodes with few rays each: every wave walks its own 256-ray items
-#ifdef PT_DYN_ITEMS
-  for (;;) {
-    uint32_t m = 0;
-    if (lid == 0) m = atomicAdd(L.next + lane * CSTRIDE, 1u);
-    m = __builtin_amdgcn_readfirstlane(m);
-    if (m >= M) break;
-#else
   const uint32_t stride = (gridDim.x / NLANE) * (TPB / 64);
   for (uint32_t m = (blockIdx.x / NLANE) * (TPB / 64) + wave; m < M; m += stride) {
-#endif
     // 64-ary search for the node k with ep[k] <= m < ep[k+1]
     int lo = 0, hi = L.nl;
     while (hi - lo > 1) {
@@ -708,7 +691,6 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
     // (the rest of the pass is abandoned and the host reports PT_E_OVERFLOW)
     for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + L.nl] = ovf ? 0u : run[s];
     *L.mode_w = block_mode ? MODE_BLOCK : MODE_WAVE;
-    for (int s = 0; s < NLANE; ++s) L.next[s * CSTRIDE] = 0u;
     if (ovf) atomicOr(err, 1u);
     if (stats) {  // fire-and-forget atomics: no round trip on the critical path
       atomicAdd(stats + STAT_V, V);

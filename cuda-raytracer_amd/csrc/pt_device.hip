@@ -76,7 +76,6 @@ struct pt_ctx {
   unsigned long long* d_rcount = nullptr;  // valid root rays: RCOUNT_SLOTS counters, one 128-B line each
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
-  uint32_t* d_next = nullptr;  // per-lane item counters of the level kernel (NLANE x CSTRIDE)
 
   // framebuffer
   int fb_w = 0, fb_h = 0, fb_tile = 0, fb_rank = 0, fb_nranks = 0;
@@ -150,7 +149,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,      c->d_cnt,
-                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err, c->d_next,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err,
                   c->d_pix_of, c->d_accum};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -268,7 +267,6 @@ static int trace_levels(pt_ctx* c) {
     L.nitems_w = c->d_nitems + l;
     L.mode = c->d_nitems + c->n_levels + l;
     L.mode_w = c->d_nitems + c->n_levels + l;
-    L.next = c->d_next;
     const uint32_t out_base = (uint32_t)(((l + 1) & 1) ? c->qcap : 0);
     c->launch(pt_ctx::K_SCAN, l, k_scan_level, dim3(1), dim3(1024), A, L, (uint32_t)lanecap, out_base,
               c->d_stats, l, c->d_err);
@@ -396,12 +394,10 @@ int pt_create(pt_ctx** out, int device) {
   for (auto& e : c->ev) hipEventCreate(&e);
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
-      hipMalloc((void**)&c->d_err, 4) != hipSuccess ||
-      hipMalloc((void**)&c->d_next, NLANE * CSTRIDE * 4) != hipSuccess) {
+      hipMalloc((void**)&c->d_err, 4) != hipSuccess) {
     delete c;
     return PT_E_HIP;
   }
-  hipMemset(c->d_next, 0, NLANE * CSTRIDE * 4);
   hipMemset(c->d_stats, 0, STAT_COUNT * 8);
   hipMemset(c->d_rcount, 0, RCOUNT_SLOTS * 16 * 8);
   hipMemset(c->d_err, 0, 4);
