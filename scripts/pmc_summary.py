@@ -16,7 +16,11 @@ from collections import defaultdict
 
 
 def short(name):
-    return name.split("(")[0].replace("pt::", "")
+    """pt::k_shade_push<16, 1>(pt::ShadeArgs) -> k_shade_push"""
+    n = name.split("(")[0].replace("pt::", "")
+    if n.startswith("void "):
+        n = n[5:]
+    return n.split("<")[0].strip()
 
 
 def main():
