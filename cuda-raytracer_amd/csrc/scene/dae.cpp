@@ -448,6 +448,25 @@ struct Loader {
       c_pos = xform_point(T, V3(0, 0, 0), false);
       c_dir = xform_point(T, V3(0, 0, -1), false).unit();
       cam = true;
+      // optics (collada.cpp:440-462): xfov/yfov default 50/35 degrees, yfov
+      // from the aspect ratio when only xfov is given
+      if (XNode* persp = get_element(e_cam, "optics/technique_common/perspective")) {
+        XNode* xf = persp->child("xfov");
+        XNode* yf = persp->child("yfov");
+        S.cam_hfov = xf ? atof(xf->text.c_str()) : 50.0f;
+        S.cam_vfov = yf ? atof(yf->text.c_str()) : 35.0f;
+        if (!yf) {
+          XNode* ar = persp->child("aspect_ratio");
+          if (!ar) {
+            err = "incomplete perspective definition";
+            return false;
+          }
+          const float aspect = (float)atof(ar->text.c_str());
+          S.cam_vfov = 2 * (atan(tan((0.5 * S.cam_hfov) * M_PI / 180.0) / aspect) * 180.0 / M_PI);
+        }
+        S.have_optics = true;
+      }
+      S.cam_dir = c_dir;
     } else if (e_light) {
       PendingLight pl;
       if (!parse_light(e_light, pl.info)) return false;

@@ -1,5 +1,7 @@
 // pt_scene_* entry points of pt_api.h: the host-side input adapter that
 // CudaRenderer::loadScene implements inline (src/cudaRenderer.cu:1679-1842).
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <exception>
 
@@ -172,6 +174,71 @@ int pt_scene_from_mesh(const pt_mesh_desc* md, pt_scene** out) {
     return PT_E_INVALID;
   }
   *out = sc;
+  return PT_OK;
+}
+
+int pt_scene_camera_scotty(const pt_scene* sc, int32_t width, int32_t height, pt_camera* out) {
+  if (!sc || !out || width <= 0 || height <= 0) return PT_E_INVALID;
+  const Scene& S = sc->s;
+  if (!S.have_optics) return PT_E_UNSUPPORTED;
+  const double PI = 3.14159265358979323846;
+  auto rad = [&](double d) { return d * (PI / 180); };
+  auto deg = [&](double r) { return r * (180 / PI); };
+  // Camera::configure (camera.cpp:15-33)
+  double hfov = S.cam_hfov, vfov = S.cam_vfov;
+  const double ar1 = tan(rad(hfov) / 2) / tan(rad(vfov) / 2);
+  const double ar = (double)width / height;
+  if (ar1 < ar)
+    hfov = 2 * deg(atan(tan(rad(vfov) / 2) * ar));
+  else if (ar1 > ar)
+    vfov = 2 * deg(atan(tan(rad(hfov) / 2) / ar));
+  // scene bbox (DynamicScene::Scene::get_bbox: meshes and spheres)
+  ptscene::V3 lo(INFINITY, INFINITY, INFINITY), hi(-INFINITY, -INFINITY, -INFINITY);
+  auto grow = [&](const ptscene::V3& a, const ptscene::V3& b) {
+    lo = ptscene::V3(std::min(lo.x, a.x), std::min(lo.y, a.y), std::min(lo.z, a.z));
+    hi = ptscene::V3(std::max(hi.x, b.x), std::max(hi.y, b.y), std::max(hi.z, b.z));
+  };
+  for (const auto& m : S.meshes)  // Mesh::get_bbox: every vertex
+    for (const auto& v : m.positions) grow(v, v);
+  for (const auto& p : S.prims)  // Sphere::get_bbox: centre +- radius
+    if (p.kind == PT_PRIM_SPHERE) {
+      const ptscene::V3 r(p.radius, p.radius, p.radius);
+      grow(p.centre - r, p.centre + r);
+    }
+  if (!(lo.x <= hi.x)) return PT_E_INVALID;
+  const ptscene::V3 target = (lo + hi) * 0.5, extent = hi - lo;
+  const double canonical = extent.norm() / 2 * 1.5;  // application.cpp:397-402
+  double r = std::min(std::max(canonical * 2, canonical / 10.0), canonical * 20.0);
+  // Camera::place + compute_position (camera.cpp:35-46, 86-108)
+  const ptscene::V3& c = S.cam_dir;
+  double phi = acos(c.y), theta = atan2(c.x, c.z);
+  if (sin(phi) == 0) phi += 0.00001f;  // EPS_F
+  double sinPhi = sin(phi);
+  if (sinPhi == 0) {
+    phi += 0.00001f;
+    sinPhi = sin(phi);
+  }
+  const ptscene::V3 dir_to_cam(r * sinPhi * sin(theta), r * cos(phi), r * sinPhi * cos(theta));
+  const ptscene::V3 pos = target + dir_to_cam;
+  const ptscene::V3 upv(0, sinPhi > 0 ? 1 : -1, 0);
+  ptscene::V3 X = ptscene::cross(upv, dir_to_cam);
+  X = X / X.norm();
+  ptscene::V3 Y = ptscene::cross(dir_to_cam, X);
+  Y = Y / Y.norm();
+  const ptscene::V3 Z = dir_to_cam / dir_to_cam.norm();
+  // generate_ray(x, y): c2w * ((x-.5) 2 tan(hfov/2), (y-.5) 2 tan(vfov/2), -1).
+  // The kernels form d = kx*left + ky*up + kz*look_at with (kx, ky, kz) a
+  // multiple of (x-.5, .5-y, 1) (cu:338-354), so left/up carry the sensor
+  // extents and up is negated.
+  const double sx = 2 * tan(rad(hfov) / 2), sy = 2 * tan(rad(vfov) / 2);
+  const ptscene::V3 look = Z * -1.0, left = X * sx, up = Y * -sy;
+  const ptscene::V3* vv[4] = {&pos, &look, &left, &up};
+  float* dst[4] = {out->origin, out->look_at, out->left, out->up};
+  for (int k = 0; k < 4; ++k) {
+    dst[k][0] = (float)vv[k]->x;
+    dst[k][1] = (float)vv[k]->y;
+    dst[k][2] = (float)vv[k]->z;
+  }
   return PT_OK;
 }
 

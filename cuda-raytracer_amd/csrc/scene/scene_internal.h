@@ -112,6 +112,11 @@ struct Scene {
   pt_light light{};
   pt_camera camera{};
   bool have_camera = false;
+  // COLLADA camera optics + view direction, for the Scotty3D framing
+  // (collada.cpp:429-470 parse_camera, application.cpp:352-408)
+  bool have_optics = false;
+  double cam_hfov = 50.0, cam_vfov = 35.0;
+  V3 cam_dir;
 
   // flattened output
   std::vector<int32_t> sorted_to_input;

@@ -108,7 +108,7 @@ class pt_mesh_desc(C.Structure):
 
 # every symbol include/pt_api.h declares (tests check the library exports them)
 API_SYMBOLS = [
-    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_build_gpu", "pt_scene_free", "pt_scene_get_desc",
+    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_build_gpu", "pt_scene_camera_scotty", "pt_scene_free", "pt_scene_get_desc",
     "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
     "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect",
@@ -137,6 +137,7 @@ def _load():
                                               C.POINTER(pt_light), C.POINTER(pt_camera), C.POINTER(P)]),
         "pt_scene_from_mesh": (C.c_int, [C.POINTER(pt_mesh_desc), C.POINTER(P)]),
         "pt_scene_build_gpu": (C.c_int, [C.POINTER(pt_mesh_desc), I32, I32, C.POINTER(P), C.POINTER(C.c_double)]),
+        "pt_scene_camera_scotty": (C.c_int, [P, I32, I32, C.POINTER(pt_camera)]),
         "pt_scene_free": (None, [P]),
         "pt_median_filter": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_float), I32, I32]),
         "pt_get_display_image": (C.c_int, [P, C.POINTER(C.c_float), SZ]),
@@ -256,7 +257,8 @@ class Scene:
         return sc
 
     def __del__(self):
-        if getattr(self, "h", None) and self.h.value:
+        # LIB is None once the interpreter tears the module down
+        if getattr(self, "h", None) and self.h.value and LIB is not None:
             LIB.pt_scene_free(self.h)
             self.h = C.c_void_p()
 
@@ -267,6 +269,14 @@ class Scene:
             raise PTError(rc, "pt_scene_get_desc")
         d._owner = self  # the desc borrows the scene's arrays
         return d
+
+    def camera_scotty(self, width, height):
+        """The Scotty3D framing of the COLLADA camera (pt_scene_camera_scotty)."""
+        cam = pt_camera()
+        rc = LIB.pt_scene_camera_scotty(self.h, width, height, C.byref(cam))
+        if rc != PT_OK:
+            raise PTError(rc, "pt_scene_camera_scotty")
+        return cam
 
     def level_counts(self):
         counts = (C.c_int32 * 256)()
@@ -357,7 +367,7 @@ class Context:
         self.width = self.height = 0
 
     def close(self):
-        if self.h and self.h.value:
+        if getattr(self, "h", None) and self.h.value and LIB is not None:
             LIB.pt_destroy(self.h)
             self.h = C.c_void_p()
 

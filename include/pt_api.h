@@ -198,6 +198,15 @@ int pt_scene_from_mesh(const pt_mesh_desc* mesh, pt_scene** out);
  * pt_scene_from_mesh).  *build_ms (optional) receives the build's wall time. */
 int pt_scene_build_gpu(const pt_mesh_desc* mesh, int32_t device, int32_t max_leaf, pt_scene** out,
                        double* build_ms);
+/* The Scotty3D framing of a COLLADA scene's camera (SURVEY §8(a) parity
+ * decision vii, camera=scotty): Application::load places the camera at the
+ * scene bbox centroid + 3 x half the bbox diagonal along the COLLADA view
+ * direction, looking back at the centroid (application.cpp:395-408,
+ * camera.cpp:35-46, 86-108); Camera::configure fits hFov/vFov to width/height
+ * (camera.cpp:15-33); generate_ray(x, y) is the documented pinhole mapping
+ * (camera.h:71-81).  The result is a pt_camera for pt_set_camera (the kernels'
+ * camera model spans the same rays).  PT_E_UNSUPPORTED without COLLADA optics. */
+int pt_scene_camera_scotty(const pt_scene* s, int32_t width, int32_t height, pt_camera* out);
 void pt_scene_free(pt_scene* s);
 /* Borrowed view of the flattened arrays (valid until pt_scene_free). */
 int pt_scene_get_desc(const pt_scene* s, pt_scene_desc* out);

@@ -182,3 +182,20 @@ def test_ray_count_matches_oracle(gpu_ctx, name, flags):
     _, rays = pyoracle.render(d, 32, 32, 2, max_bounces=8, flags=flags)
     assert st.rays == rays
     assert st.visits >= st.rays
+
+
+def test_scotty_camera_render(gpu_ctx):
+    """camera=scotty framing (pt_scene_camera_scotty, fixture made from
+    CBbunny.dae at 64x48): the kernels render it bit-exactly like the oracle."""
+    from conftest import ROOT
+    sc = load_fixture("CBbunny")
+    cam = ptrace.pt_camera.from_buffer_copy(np.load(ROOT / "tests/golden/camera_scotty_CBbunny_64x48.npy").tobytes())
+    gpu_ctx.load_scene(sc)
+    gpu_ctx.set_camera(cam)
+    gpu_ctx.clear()
+    gpu_ctx.render(64, 48, 2, max_bounces=6)
+    g = gpu_ctx.get_image()
+    d = sc.desc()
+    d.camera = cam
+    o, _ = pyoracle.image(d, 64, 48, 2, max_bounces=6)
+    assert np.array_equal(g, o) and o[..., :3].mean() > 0.01

@@ -134,3 +134,26 @@ def test_dragon_proxy_deterministic():
             assert n.prim_count <= 32
             covered[n.prim_start:n.prim_start + n.prim_count] += 1
     assert (covered == 1).all()
+
+
+@pytest.mark.skipif(not REFERENCE_MEDIA.exists(), reason="reference media not present")
+def test_camera_scotty_framing():
+    """camera=scotty (SURVEY §8(a) vii): placed 3 half-diagonals from the bbox
+    centroid along the COLLADA view direction, looking back at it, with the
+    sensor extents of Camera::configure."""
+    import math
+    sc = ptrace.Scene.load_dae(REFERENCE_MEDIA / "advanced" / "CBbunny.dae")
+    cam = sc.camera_scotty(640, 480)
+    o, look = np.array(cam.origin, np.float64), np.array(cam.look_at, np.float64)
+    left, up = np.array(cam.left, np.float64), np.array(cam.up, np.float64)
+    assert abs(np.linalg.norm(look) - 1) < 1e-6
+    assert abs(look @ left) < 1e-6 and abs(look @ up) < 1e-6 and abs(left @ up) < 1e-5
+    # CBbunny: box [-1,1]x[0,1.5]x[-1,1] (+ bunny inside): centroid (0,0.75,0), half diagonal 1.5625
+    centroid = o + look * np.linalg.norm(o - np.array([0.0, 0.75, 0.0]))
+    assert np.allclose(centroid, [0.0, 0.75, 0.0], atol=1e-5)
+    r = np.linalg.norm(o - centroid)
+    assert abs(r - 2 * 1.5 * math.sqrt(4 + 2.25 + 4) / 2) < 1e-5
+    # sensor aspect follows the frame: |left| / |up| = 640 / 480
+    assert abs(np.linalg.norm(left) / np.linalg.norm(up) - 640 / 480) < 1e-5
+    with pytest.raises(ptrace.PTError):
+        ptrace.Scene.from_triangles(np.eye(3, dtype=np.float32).reshape(1, 9)).camera_scotty(64, 64)
