@@ -483,27 +483,76 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
   return hit;
 }
 
-// 6 waves per SIMD (<= 80 VGPRs, no spills): +2 % over the unconstrained 87
+// Path regeneration (persistent waves).  A wave of 64 independent paths would
+// run as long as its longest path (up to max_bounces + 2 vertices) while the
+// mean path has ~4: most lanes would sit idle.  Instead every lane whose path
+// has ended takes the next unstarted path from its wave's pool, and the wave
+// refills the pool from a global counter in chunks of PATH_CHUNK paths; the
+// grid is sized to the resident wave count, every wave exits once the counter
+// passes N and its lanes are idle.  Results do not depend on which lane runs a
+// path: random numbers are keyed by (pixel, sample, vertex) and each path
+// writes only its own slot ps1[p].
+#ifndef PT_PATH_CHUNK
+#define PT_PATH_CHUNK 256
+#endif
+constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
+
+#ifndef PT_PATH_WAVES
+#define PT_PATH_WAVES 6
+#endif
+// PT_PATH_WAVES waves per SIMD (6: <= 80 VGPRs)
 template <int NSH>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_path_leaf(
-    ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount) {
-  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
+    ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
+    uint32_t* __restrict__ work) {
+  const uint32_t lid = lane_id();
   uint32_t nrays = 0;
-  if (p < S.N) {
-    PathState st;
-    const f3 dir = camera_dir(S, p, st.g);
-    st.T = mk(1.0f, 1.0f, 1.0f);
-    st.L = mk(0.0f, 0.0f, 0.0f);
-    st.flags = F_EXT | (1u << 8);
-    RayV ext{ld3(S.cam.origin), dir, __builtin_inff()}, shr[NSH];
-    f3 C[NSH];
+  // wave-uniform pool [next, end) of unstarted paths; `drained`: the global
+  // counter has passed N
+  uint32_t next = 0, end = 0;
+  bool drained = false;
+  bool active = false;
+  uint32_t p = 0, sidx = 0;
+  PathState st{mk(0, 0, 0), 0u, mk(0, 0, 0), 0u};
+  RayV ext{mk(0, 0, 0), mk(0, 0, 1), -1.0f}, shr[NSH];
+  f3 C[NSH];
 #pragma unroll
-    for (int s = 0; s < NSH; ++s) {
-      shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
-      C[s] = mk(0, 0, 0);
+  for (int s = 0; s < NSH; ++s) {
+    shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
+    C[s] = mk(0, 0, 0);
+  }
+  for (;;) {
+    // ---- refill idle lanes from the pool (new paths start at their camera ray)
+    unsigned long long idle = __ballot(!active);
+    if (idle && next == end && !drained) {
+      uint32_t base = 0;
+      if (lid == 0) base = atomicAdd(work, PATH_CHUNK);
+      base = __builtin_amdgcn_readfirstlane(base);
+      drained = base >= S.N;
+      next = drained ? 0u : base;
+      end = drained ? 0u : min(base + PATH_CHUNK, S.N);
     }
-    const uint32_t sidx = S.sample_base + p / S.npix;
-    for (int pass = 0; pass < passes && (st.flags & (F_EXT | F_SHADOW | F_SHADOW2)); ++pass) {
+    if (idle && next < end) {
+      const uint32_t r = mbcnt64(idle);
+      const uint32_t avail = end - next;
+      if (!active && r < avail) {
+        p = next + r;
+        active = true;
+        const f3 dir = camera_dir(S, p, st.g);
+        st.T = mk(1.0f, 1.0f, 1.0f);
+        st.L = mk(0.0f, 0.0f, 0.0f);
+        st.flags = F_EXT | (1u << 8);
+        ext = RayV{ld3(S.cam.origin), dir, __builtin_inff()};
+        sidx = S.sample_base + p / S.npix;
+      }
+      next += min((uint32_t)__popcll(idle), avail);
+    }
+    if (!__any(active)) {
+      if (drained) break;
+      continue;  // (pool was empty: the next iteration grabs a chunk)
+    }
+    // ---- one vertex of every active path: leaf tests, then shade
+    if (active) {
       uint32_t prim = PT_PRIM_NONE;
       float t = 0.0f;
       if (st.flags & F_EXT) {
@@ -526,12 +575,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 #pragma unroll
       for (int s = 0; s < NSH; ++s)
         if (new_sh[s]) shr[s] = s2[s];
+      // vertices done = vtx - 1 (shade_vertex advanced it); the path ends
+      // after `passes` of them or when it has no ray left to trace
+      const uint32_t done = ((st.flags >> 8) & 0xffu) - 1u;
+      if (!(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || done >= (uint32_t)passes) {
+        S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(st.g));
+        active = false;
+      }
     }
-    S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(st.g));
   }
   // rays traced (R): one fire-and-forget atomic per wave into its lane's counter
   const uint32_t w = wave_sum(nrays);
-  if ((threadIdx.x & 63) == 0 && w)
+  if (lid == 0 && w)
     atomicAdd(rcount + (size_t)((blockIdx.x * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16,
               (unsigned long long)w);
 }

@@ -89,12 +89,16 @@ __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const f3x
   const f2v s0 = edge_side2(P, v0, m0);
   const f2v s1 = edge_side2(P, v1, m1);
   const f2v s2 = edge_side2(P, v2, m2);
+  // t + 0 maps -0 to +0 and leaves every other value unchanged (strict fp:
+  // the add is not folded away)
+  const f2v tz = t + sp(0.0f);
   f2v r;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const bool miss = fabsf(ndd[i]) < 1e-6f || t[i] < 0.0f || t[i] > tbest[i] || s0[i] < 0.0f || s1[i] < 0.0f ||
-                      s2[i] < 0.0f;
-    r[i] = miss ? -1.0f : (t[i] == 0.0f ? 0.0f : t[i]);
+    // non-short-circuit: every comparison is one v_cmp, combined on the SALU
+    const bool miss = (fabsf(ndd[i]) < 1e-6f) | (t[i] < 0.0f) | (t[i] > tbest[i]) | (s0[i] < 0.0f) |
+                      (s1[i] < 0.0f) | (s2[i] < 0.0f);
+    r[i] = miss ? -1.0f : tz[i];
   }
   return r;
 }

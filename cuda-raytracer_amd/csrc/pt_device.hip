@@ -76,6 +76,8 @@ struct pt_ctx {
   unsigned long long* d_rcount = nullptr;  // valid root rays: RCOUNT_SLOTS counters, one 128-B line each
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
+  uint32_t* d_work = nullptr;  // k_path_leaf path counter
+  int path_grid[2] = {0, 0};   // resident workgroups of k_path_leaf<1>, <2>
 
   // framebuffer
   int fb_w = 0, fb_h = 0, fb_tile = 0, fb_rank = 0, fb_nranks = 0;
@@ -149,7 +151,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,      c->d_cnt,
-                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err, c->d_work,
                   c->d_pix_of, c->d_accum};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -394,13 +396,22 @@ int pt_create(pt_ctx** out, int device) {
   for (auto& e : c->ev) hipEventCreate(&e);
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
-      hipMalloc((void**)&c->d_err, 4) != hipSuccess) {
+      hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, 4) != hipSuccess) {
     delete c;
     return PT_E_HIP;
   }
   hipMemset(c->d_stats, 0, STAT_COUNT * 8);
   hipMemset(c->d_rcount, 0, RCOUNT_SLOTS * 16 * 8);
   hipMemset(c->d_err, 0, 4);
+  // k_path_leaf runs persistent waves: one grid of exactly the resident workgroups
+  {
+    int ncu = 0, nb1 = 0, nb2 = 0;
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb1, k_path_leaf<1>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, k_path_leaf<2>, TPB, 0);
+    c->path_grid[0] = std::max(1, ncu * std::max(1, nb1));
+    c->path_grid[1] = std::max(1, ncu * std::max(1, nb2));
+  }
   *out = c;
   return PT_OK;
 }
@@ -596,12 +607,15 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     if (c->root_leaf) {
       // single-leaf tree: every path runs to completion in one kernel
       const pt_node& root = c->nodes_host[0];
+      // persistent waves: no more workgroups than paths in chunks of 64-lane waves
+      const uint32_t want = (N + 4 * PATH_CHUNK - 1) / (4 * PATH_CHUNK);
+      HIPCHK(c, hipMemsetAsync(c->d_work, 0, 4, c->stream));
       if (nsh == 2)
-        c->launch(pt_ctx::K_PATH, 0, k_path_leaf<2>, grid, dim3(TPB), S, root.prim_start, root.prim_count, passes,
-                  c->d_rcount);
+        c->launch(pt_ctx::K_PATH, 0, k_path_leaf<2>, dim3(std::min<uint32_t>(want, c->path_grid[1])), dim3(TPB), S,
+                  root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work);
       else
-        c->launch(pt_ctx::K_PATH, 0, k_path_leaf<1>, grid, dim3(TPB), S, root.prim_start, root.prim_count, passes,
-                  c->d_rcount);
+        c->launch(pt_ctx::K_PATH, 0, k_path_leaf<1>, dim3(std::min<uint32_t>(want, c->path_grid[0])), dim3(TPB), S,
+                  root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work);
       c->stats.passes += passes;
     } else {
       // camera rays enter the root's target queues directly; each pass traces
