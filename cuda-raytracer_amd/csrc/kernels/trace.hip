@@ -40,32 +40,37 @@ namespace pt {
 // Reference triangle test intersectRayTriangle (cu:217-270) on precomputed
 // operands (pt_api.h pt_prim): plane hit, then the three edge-side tests, each
 // dot(m_k, P - v_k) with m_k = N x e_k (the reference's dot(N, cross(e_k,
-// P - v_k)) without its per-ray cross products).  Returns t >= 0 or -1 on a
-// miss.  t = -0 is returned as +0 so that the {t bits, id} key orders correctly.
+// P - v_k)) without its per-ray cross products).  Dot products and P = o + t d
+// are FMA chains (what nvcc makes of the reference's expressions under its
+// default --fmad=true): dot(a, b) = fma(a.z, b.z, fma(a.y, b.y, a.x * b.x)).
+// Returns t >= 0 or -1 on a miss.  t = -0 is returned as +0 so that the
+// {t bits, id} key orders correctly.
+__device__ __forceinline__ float fdot(float ax, float ay, float az, float bx, float by, float bz) {
+  return __builtin_fmaf(az, bz, __builtin_fmaf(ay, by, ax * bx));
+}
 __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q0, const float4 q1,
                                           const float4 q2, const float4 q3, const float4 q4,
                                           const float4 q5, const float tbest) {
-  const f3 N = mk(q3.x, q3.y, q3.z);
-  float ndd = N.x * d.x + N.y * d.y + N.z * d.z;
+  float ndd = fdot(q3.x, q3.y, q3.z, d.x, d.y, d.z);
   if (fabsf(ndd) < 1e-6f) return -1.0f;
-  float t = (q1.w - (N.x * o.x + N.y * o.y + N.z * o.z)) / ndd;
+  float t = (q1.w - fdot(q3.x, q3.y, q3.z, o.x, o.y, o.z)) / ndd;
   // t > tbest cannot win (ties need t == tbest): skip the edge tests
   if (t < 0.0f || t > tbest) return -1.0f;
-  f3 P = mk(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
+  f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
   // edge 0 (v0 -> v1)
-  if (q2.w * (P.x - q0.x) + q3.w * (P.y - q0.y) + q4.w * (P.z - q0.z) < 0.0f) return -1.0f;
+  if (fdot(q2.w, q3.w, q4.w, P.x - q0.x, P.y - q0.y, P.z - q0.z) < 0.0f) return -1.0f;
   // edge 1 (v1 -> v2)
-  if (q4.x * (P.x - q1.x) + q4.y * (P.y - q1.y) + q4.z * (P.z - q1.z) < 0.0f) return -1.0f;
+  if (fdot(q4.x, q4.y, q4.z, P.x - q1.x, P.y - q1.y, P.z - q1.z) < 0.0f) return -1.0f;
   // edge 2 (v2 -> v0)
-  if (q5.x * (P.x - q2.x) + q5.y * (P.y - q2.y) + q5.z * (P.z - q2.z) < 0.0f) return -1.0f;
+  if (fdot(q5.x, q5.y, q5.z, P.x - q2.x, P.y - q2.y, P.z - q2.z) < 0.0f) return -1.0f;
   return t == 0.0f ? 0.0f : t;
 }
 
-// Two independent triangle tests at once on packed fp32 (v_pk_mul_f32 /
+// Two independent triangle tests at once on packed fp32 (v_pk_fma_f32 /
 // v_pk_add_f32): element i is exactly tri_test(o[i], d[i], q..., tbest[i])
 // (same operations in the same order, so the same bits), written without
 // branches so both halves share every instruction.  Used for two rays against
-// one triangle (leaf loops) or one ray against two triangles (k_path_leaf).
+// one triangle (leaf loops).
 typedef float f2v __attribute__((ext_vector_type(2)));
 struct f3x2 {
   f2v x, y, z;
@@ -73,19 +78,23 @@ struct f3x2 {
 __device__ __forceinline__ f2v sp(float a) { return f2v{a, a}; }
 __device__ __forceinline__ f3x2 sp3(float a, float b, float c) { return f3x2{sp(a), sp(b), sp(c)}; }
 __device__ __forceinline__ f3x2 pair3(f3 a, f3 b) { return f3x2{f2v{a.x, b.x}, f2v{a.y, b.y}, f2v{a.z, b.z}}; }
+__device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2v fdot2(const f3x2& a, const f3x2& b) {
+  return fma2(a.z, b.z, fma2(a.y, b.y, a.x * b.x));
+}
 
 // dot(m, P - v) on two lanes: the edge-side test
 __device__ __forceinline__ f2v edge_side2(const f3x2& P, const f3x2& v, const f3x2& m) {
-  return m.x * (P.x - v.x) + m.y * (P.y - v.y) + m.z * (P.z - v.z);
+  return fma2(m.z, P.z - v.z, fma2(m.y, P.y - v.y, m.x * (P.x - v.x)));
 }
 
 // N: normal, pd: plane offset, v0..v2: vertices, m0..m2: edge normals (pt_prim layout)
 __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const f3x2& N, f2v pd, const f3x2& v0,
                                          const f3x2& v1, const f3x2& v2, const f3x2& m0, const f3x2& m1,
                                          const f3x2& m2, f2v tbest) {
-  const f2v ndd = N.x * d.x + N.y * d.y + N.z * d.z;
-  const f2v t = (pd - (N.x * o.x + N.y * o.y + N.z * o.z)) / ndd;
-  const f3x2 P{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z};
+  const f2v ndd = fdot2(N, d);
+  const f2v t = (pd - fdot2(N, o)) / ndd;
+  const f3x2 P{fma2(t, d.x, o.x), fma2(t, d.y, o.y), fma2(t, d.z, o.z)};
   const f2v s0 = edge_side2(P, v0, m0);
   const f2v s1 = edge_side2(P, v1, m1);
   const f2v s2 = edge_side2(P, v2, m2);
@@ -107,9 +116,9 @@ __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const f3x
 // triangles at cu:1760).  Nearest root with t >= 0; d must be unit length.
 __device__ __forceinline__ float sphere_test(const f3 o, const f3 d, const float4 q0, const float4 q1) {
   f3 oc = mk(o.x - q0.x, o.y - q0.y, o.z - q0.z);
-  float b = oc.x * d.x + oc.y * d.y + oc.z * d.z;
-  float cc = (oc.x * oc.x + oc.y * oc.y + oc.z * oc.z) - q1.y;
-  float disc = b * b - cc;
+  float b = fdot(oc.x, oc.y, oc.z, d.x, d.y, d.z);
+  float cc = fdot(oc.x, oc.y, oc.z, oc.x, oc.y, oc.z) - q1.y;
+  float disc = __builtin_fmaf(b, b, -cc);
   if (disc < 0.0f) return -1.0f;
   float sq = sqrtf(disc);
   float t0 = -b - sq;

@@ -128,23 +128,27 @@ void pto_sincos2pi(float u, float* s, float* c) { sincos2pi(u, s, c); }
 /* intersectRayTriangle, cu:217-270: plane hit then three edge sign tests,
  * dot(N, cross(e_k, P - v_k)) evaluated as dot(m_k, P - v_k) with the
  * precomputed edge normals m_k = N x e_k (pt_api.h pt_prim layout). */
+/* dot products and P = o + t d as FMA chains, exactly as trace.hip:
+ * fdot(a, b) = fma(a.z, b.z, fma(a.y, b.y, a.x * b.x)) */
+static inline float fdot(float ax, float ay, float az, float bx, float by, float bz) {
+  return fmaf(az, bz, fmaf(ay, by, ax * bx));
+}
 static float pto_tri(v3 o, v3 d, const float* q) {
-  v3 N = mk(q[12], q[13], q[14]);
-  float ndd = N.x * d.x + N.y * d.y + N.z * d.z;
+  float ndd = fdot(q[12], q[13], q[14], d.x, d.y, d.z);
   if (fabsf(ndd) < 1e-6f) return -1.0f;
-  float t = (q[7] - (N.x * o.x + N.y * o.y + N.z * o.z)) / ndd;
+  float t = (q[7] - fdot(q[12], q[13], q[14], o.x, o.y, o.z)) / ndd;
   if (t < 0.0f) return -1.0f;
-  v3 P = mk(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
-  if (q[11] * (P.x - q[0]) + q[15] * (P.y - q[1]) + q[19] * (P.z - q[2]) < 0.0f) return -1.0f;
-  if (q[16] * (P.x - q[4]) + q[17] * (P.y - q[5]) + q[18] * (P.z - q[6]) < 0.0f) return -1.0f;
-  if (q[20] * (P.x - q[8]) + q[21] * (P.y - q[9]) + q[22] * (P.z - q[10]) < 0.0f) return -1.0f;
+  v3 P = mk(fmaf(t, d.x, o.x), fmaf(t, d.y, o.y), fmaf(t, d.z, o.z));
+  if (fdot(q[11], q[15], q[19], P.x - q[0], P.y - q[1], P.z - q[2]) < 0.0f) return -1.0f;
+  if (fdot(q[16], q[17], q[18], P.x - q[4], P.y - q[5], P.z - q[6]) < 0.0f) return -1.0f;
+  if (fdot(q[20], q[21], q[22], P.x - q[8], P.y - q[9], P.z - q[10]) < 0.0f) return -1.0f;
   return t == 0.0f ? 0.0f : t;
 }
 static float pto_sphere(v3 o, v3 d, const float* q) {
   v3 oc = mk(o.x - q[0], o.y - q[1], o.z - q[2]);
-  float b = oc.x * d.x + oc.y * d.y + oc.z * d.z;
-  float cc = (oc.x * oc.x + oc.y * oc.y + oc.z * oc.z) - q[5];
-  float disc = b * b - cc;
+  float b = fdot(oc.x, oc.y, oc.z, d.x, d.y, d.z);
+  float cc = fdot(oc.x, oc.y, oc.z, oc.x, oc.y, oc.z) - q[5];
+  float disc = fmaf(b, b, -cc);
   if (disc < 0.0f) return -1.0f;
   float sq = sqrtf(disc);
   float t0 = -b - sq, t1 = -b + sq;
