@@ -19,9 +19,12 @@ __device__ __forceinline__ f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y +
 __device__ __forceinline__ f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ f3 mulv(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// dot and cross products are FMA chains (nvcc's default contraction of the
+// reference's cuda_util.h expressions); the oracle spells them the same way
+__device__ __forceinline__ float dot(f3 a, f3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
-  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+  return mk(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
+            __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
 }
 __device__ __forceinline__ float length(f3 a) { return sqrtf(dot(a, a)); }
 // v * (1 / |v|)
