@@ -33,6 +33,22 @@ __device__ __forceinline__ f3 normalize(f3 a) {
   return a * inv;
 }
 
+// ---- division by a run-time constant -------------------------------------------
+// floor(n / d) = (n * m) >> s for every n < 2^30 (m, s from udiv_make): with
+// s = 30 + ceil(log2 d) and m = ceil(2^s / d), e = m d - 2^s < d, so n e < 2^s.
+struct udiv {
+  uint32_t m, s;
+};
+__host__ __device__ inline udiv udiv_make(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint32_t s = 30 + l;
+  return udiv{(uint32_t)(((1ull << s) + d - 1) / d), s};
+}
+__device__ __forceinline__ uint32_t udiv_q(uint32_t n, udiv d) {
+  return (uint32_t)(((unsigned long long)n * d.m) >> d.s);
+}
+
 // ---- Philox4x32-10 (Salmon et al., SC'11) ------------------------------------
 struct u4 {
   uint32_t x, y, z, w;

@@ -38,6 +38,7 @@ struct ShadeArgs {
   pt_light light;
   pt_camera cam;
   uint32_t N, npix, sample_base, seed;
+  udiv div_npix, div_width;  // p / npix, pixel / width (N and width * height < 2^30)
   int width, height, max_bounces;
   uint32_t flags;
   TraceArgs A;                   // fused root pass (camera/shade push into the root's target queues)
@@ -49,9 +50,9 @@ __device__ __forceinline__ f3 xyz(float4 a) { return mk(a.x, a.y, a.z); }
 
 // Camera ray of path p (pixel g = pix_of[p % npix], sample sample_base + p / npix).
 __device__ __forceinline__ f3 camera_dir(const ShadeArgs& S, uint32_t p, uint32_t& g) {
-  const uint32_t q = p % S.npix, j = p / S.npix;
+  const uint32_t j = udiv_q(p, S.div_npix), q = p - j * S.npix;
   g = S.pix_of[q];
-  const uint32_t row = g / (uint32_t)S.width, col = g - row * (uint32_t)S.width;
+  const uint32_t row = udiv_q(g, S.div_width), col = g - row * (uint32_t)S.width;
   const uint32_t s = S.sample_base + j;
   const u4 u = rng(S.seed, g, s, 0, 0);
   // cu:338-354: ss = (x + u, y + v); k = ((ss.y/W)-.5, -((ss.x/H)-.5), 1) / |k|
@@ -308,7 +309,7 @@ __device__ __forceinline__ void shade_slot(const ShadeArgs& S, uint32_t p, bool&
   if ((flags & (F_EXT | F_SHADOW | F_SHADOW2)) == 0) return;
   const float4 s1 = S.ps1[p];
   PathState st{xyz(s0), flags, xyz(s1), __float_as_uint(s1.w)};
-  const uint32_t sidx = S.sample_base + p / S.npix;
+  const uint32_t sidx = S.sample_base + udiv_q(p, S.div_npix);
   bool clear[NSH];
   f3 C[NSH];
 #pragma unroll
@@ -453,10 +454,13 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
   for (int k = 0; k < pcount; ++k, P += 6) {
     const float4 q0 = f4(P[0]), q1 = f4(P[1]);
     float tt;
-    if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE)
+    if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
       tt = sphere_test(r.o, r.d, q0, q1);
-    else
+    } else {
+      // (a tri_outside pre-test does not pay here: extension rays of one wave
+      // rarely all miss a plane, measured -7 % on CBempty)
       tt = tri_test(r.o, r.d, q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), bt);
+    }
     if (tt >= 0.0f && (tt < bt || (tt == bt && bp < 0))) {
       bt = tt;
       bp = pstart + k;
@@ -466,17 +470,23 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
   t = bt;
 }
 
-// any primitive at t in [0, tmax]
+// any primitive at t in [0, tmax]; triangles whose plane hit is certainly
+// outside [0, tmax] for every lane (tri_outside: shadow rays toward the light
+// mostly point away from the walls or end before them) cost no division
 __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, int pcount, const RayV& r) {
   const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * 6);
   bool hit = false;
   for (int k = 0; k < pcount; ++k, P += 6) {
     const float4 q0 = f4(P[0]), q1 = f4(P[1]);
-    float tt;
-    if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE)
+    float tt = -1.0f;
+    if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
       tt = sphere_test(r.o, r.d, q0, q1);
-    else
-      tt = tri_test(r.o, r.d, q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), r.tmax);
+    } else {
+      const float4 q3 = f4(P[3]);
+      const float ndd = fdot(q3.x, q3.y, q3.z, r.d.x, r.d.y, r.d.z);
+      const float num = q1.w - fdot(q3.x, q3.y, q3.z, r.o.x, r.o.y, r.o.z);
+      if (!tri_outside(ndd, num, r.tmax)) tt = tri_test(r.o, r.d, q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), r.tmax);
+    }
     hit = hit || (tt >= 0.0f && tt <= r.tmax);
     if (!__any(!hit)) break;  // every active lane is occluded
   }
@@ -543,7 +553,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
         st.L = mk(0.0f, 0.0f, 0.0f);
         st.flags = F_EXT | (1u << 8);
         ext = RayV{ld3(S.cam.origin), dir, __builtin_inff()};
-        sidx = S.sample_base + p / S.npix;
+        sidx = S.sample_base + udiv_q(p, S.div_npix);
       }
       next += min((uint32_t)__popcll(idle), avail);
     }

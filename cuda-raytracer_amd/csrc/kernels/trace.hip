@@ -66,6 +66,22 @@ __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q
   return t == 0.0f ? 0.0f : t;
 }
 
+// Division-free early rejection: true only when the plane hit of tri_test is
+// certainly outside [0, tmax] (its rounded t = num / ndd is < 0 or > tmax) or
+// |ndd| < 1e-6.  Lanes for which it is false run the exact test; a wave whose
+// lanes all reject skips the division and the edge tests.
+//  * signs differ, 2^-60 < |num|, |ndd| < 2^60: |q| > 2^-120, so t < 0;
+//  * same signs, tmax >= 2^-60: x = RN(RN(tmax |ndd|) (1 + 2^-20)) exceeds
+//    tmax |ndd| (1 + 2^-21), so |num| > x gives q > tmax (1 + 2^-21), which
+//    rounds above tmax (tmax = inf never rejects).
+__device__ __forceinline__ bool tri_outside(float ndd, float num, float tmax) {
+  const float an = fabsf(num), ad = fabsf(ndd);
+  const bool flat = ad < 1e-6f;
+  const bool behind = ((num < 0.0f) != (ndd < 0.0f)) & (an > 0x1p-60f) & (ad < 0x1p60f);
+  const bool beyond = ((num < 0.0f) == (ndd < 0.0f)) & (tmax >= 0x1p-60f) & (an > (tmax * ad) * (1.0f + 0x1p-20f));
+  return flat | behind | beyond;
+}
+
 // Two independent triangle tests at once on packed fp32 (v_pk_fma_f32 /
 // v_pk_add_f32): element i is exactly tri_test(o[i], d[i], q..., tbest[i])
 // (same operations in the same order, so the same bits), written without

@@ -530,6 +530,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   const int rank = P->rank;
   if (rank < 0 || rank >= nranks) return fail(c, PT_E_INVALID, "bad rank");
   const int tile = P->tile_size > 0 ? P->tile_size : 32;
+  if ((unsigned long long)P->width * P->height >= (1ull << 30))
+    return fail(c, PT_E_UNSUPPORTED, "image larger than 2^30 pixels");
   hipSetDevice(c->device);
   int rc;
   // framebuffer / owned pixels
@@ -593,6 +595,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.light = c->light;
     S.cam = c->camera;
     S.npix = npix;
+    S.div_npix = udiv_make(npix);
+    S.div_width = udiv_make((uint32_t)P->width);
     S.seed = P->seed;
     S.width = P->width;
     S.height = P->height;
