@@ -28,7 +28,7 @@ constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
 struct ShadeArgs {
   float4* ray;  // ray records (trace.h): ext ray of path p in slot p, shadow ray s in slot (1+s)N + p
   float4* ps0;  // T.xyz, flags | vertex << 8
-  float4* ps1;  // L.xyz, pixel
+  float4* ps1;  // L.xyz, path index P (wavefront slots) / pixel (k_path_leaf output)
   float4* ps2;  // pending shadow contribution
   float4* ps3;  // pending contribution of the second shadow ray (PT_FLAG_REF_SCHEDULE)
   const float4* __restrict__ prims;
@@ -42,6 +42,15 @@ struct ShadeArgs {
   int width, height, max_bounces;
   uint32_t flags;
   TraceArgs A;                   // fused root pass (camera/shade push into the root's target queues)
+  // path regeneration of the wavefront: the N slots run the M paths of a chunk
+  // (P = j * npix + q: sample j of owned pixel q); a slot whose path ends
+  // writes res[P] and starts the next unstarted path
+  float4* res;        // per-path radiance of the chunk
+  uint32_t M;         // paths in the chunk
+  // workgroup b runs the paths [range_start(b), range_start(b + 1)): a share of
+  // the chunk proportional to its slots (the last workgroup may be partial)
+  uint2* wstate;      // per workgroup: {next unstarted path, live slots after its last pass}
+  int passes;         // vertices per path at most (max_bounces + 2)
   unsigned long long* rcount;    // rays entering the traversal (RCOUNT_SLOTS counters)
 };
 
@@ -296,20 +305,34 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
   ext.tmax = __builtin_inff();
 }
 
-// Shade path p: read its state, hit words and rays, run shade_vertex, write
-// the new state and ray records.  Returns the new rays in registers.
+// Pixel and sample of path P of the chunk.
+__device__ __forceinline__ void path_pixel(const ShadeArgs& S, uint32_t P, uint32_t& g, uint32_t& sidx) {
+  const uint32_t j = udiv_q(P, S.div_npix);
+  g = S.pix_of[P - j * S.npix];
+  sidx = S.sample_base + j;
+}
+
+// Slot states returned by shade_slot
+constexpr int SLOT_FREE = 0, SLOT_LIVE = 1, SLOT_ENDED = 2;
+
+// Shade the path in slot p: read its state, hit words and rays, run
+// shade_vertex, write the new state and ray records.  Returns the new rays in
+// registers.  A path with nothing left to trace (or `passes` vertices done)
+// writes its radiance to res[P] and frees the slot.
 template <int NSH>
-__device__ __forceinline__ void shade_slot(const ShadeArgs& S, uint32_t p, bool& new_ext, RayV& ext,
-                                           bool (&new_sh)[NSH], RayV (&shr)[NSH]) {
+__device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& new_ext, RayV& ext,
+                                          bool (&new_sh)[NSH], RayV (&shr)[NSH]) {
   new_ext = false;
 #pragma unroll
   for (int s = 0; s < NSH; ++s) new_sh[s] = false;
   const float4 s0 = S.ps0[p];
   const uint32_t flags = __float_as_uint(s0.w);
-  if ((flags & (F_EXT | F_SHADOW | F_SHADOW2)) == 0) return;
+  if ((flags & (F_EXT | F_SHADOW | F_SHADOW2)) == 0) return SLOT_FREE;
   const float4 s1 = S.ps1[p];
-  PathState st{xyz(s0), flags, xyz(s1), __float_as_uint(s1.w)};
-  const uint32_t sidx = S.sample_base + udiv_q(p, S.div_npix);
+  const uint32_t P = __float_as_uint(s1.w);
+  PathState st{xyz(s0), flags, xyz(s1), 0u};
+  uint32_t sidx;
+  path_pixel(S, P, st.g, sidx);
   bool clear[NSH];
   f3 C[NSH];
 #pragma unroll
@@ -335,8 +358,19 @@ __device__ __forceinline__ void shade_slot(const ShadeArgs& S, uint32_t p, bool&
     }
   }
   shade_vertex<NSH>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
-  S.ps0[p] = make_float4(st.T.x, st.T.y, st.T.z, __uint_as_float(st.flags));
-  S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(st.g));
+  // (vertices done = vtx - 1: the last one resolves shadow rays only)
+  const bool ended =
+      !(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || ((st.flags >> 8) & 0xffu) - 1u >= (uint32_t)S.passes;
+  if (ended) {
+    new_ext = false;
+#pragma unroll
+    for (int s = 0; s < NSH; ++s) new_sh[s] = false;
+    S.res[P] = make_float4(st.L.x, st.L.y, st.L.z, 0.0f);
+    S.ps0[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+  } else {
+    S.ps0[p] = make_float4(st.T.x, st.T.y, st.T.z, __uint_as_float(st.flags));
+    S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(P));
+  }
   if (new_ext) {
     S.ray[RSTRIDE * p] = make_float4(ext.o.x, ext.o.y, ext.o.z, ext.d.x);
     S.ray[RSTRIDE * p + 1] = rec_r1(ext.d.y, ext.d.z, __builtin_inff());
@@ -354,15 +388,18 @@ __device__ __forceinline__ void shade_slot(const ShadeArgs& S, uint32_t p, bool&
       S.ray[RSTRIDE * slot + 1] = rec_r1(0.f, 0.f, -1.0f);
     }
   }
+  return ended ? SLOT_ENDED : SLOT_LIVE;
 }
 
-template <int NSH>
-__global__ __launch_bounds__(TPB) void k_shade(ShadeArgs S) {
-  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
-  if (p >= S.N) return;
-  bool new_ext, new_sh[NSH];
-  RayV ext, shr[NSH];
-  shade_slot<NSH>(S, p, new_ext, ext, new_sh, shr);
+// Start path P in slot p: state and camera ray (kernelPrimaryRays, cu:312-376).
+__device__ __forceinline__ f3 start_path(const ShadeArgs& S, uint32_t p, uint32_t P) {
+  uint32_t g;
+  const f3 d = camera_dir(S, P, g);
+  S.ray[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], d.x);
+  S.ray[RSTRIDE * p + 1] = rec_r1(d.y, d.z, __builtin_inff());
+  S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
+  S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
+  return d;
 }
 
 // One fire-and-forget atomic per workgroup: rays that enter the traversal.
@@ -376,37 +413,73 @@ __device__ __forceinline__ void count_rays(unsigned long long* rcount, uint32_t 
   }
 }
 
+__device__ __forceinline__ uint32_t range_start(const ShadeArgs& S, uint32_t b) {
+  const uint64_t first_slot = (uint64_t)b * TPB;
+  return first_slot >= S.N ? S.M : (uint32_t)(((uint64_t)S.M * first_slot) / S.N);
+}
+
 // Fused root pass: the new rays never take the trip through HBM and back to
 // be tested against the root -- the producing kernel tests them against the
 // root's NC target boxes (4 children, or 16 grandchildren when level 1 is
 // skipped) and pushes their ids into those queues (lane = workgroup & 7).
+//
+// Path regeneration without atomics: workgroup b owns a contiguous path range
+// of the chunk (consecutive pixels of one sample, range_start) and the same
+// 256 slots in every pass; it alone reads and writes its
+// wstate word, so starting paths needs no shared counter.
+// First fill: slot i of workgroup b starts path range_start(b) + i.
 template <int NC, int NSH>
 __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
   __shared__ uint32_t sh[NC * 8 + 4];
+  __shared__ uint32_t s_rng[2];
+  if (threadIdx.x < 2) s_rng[threadIdx.x] = range_start(S, blockIdx.x + threadIdx.x);
+  __syncthreads();
   const uint32_t p = blockIdx.x * TPB + threadIdx.x;
-  const bool live = p < S.N;
+  const uint32_t base = s_rng[0], end = s_rng[1];
+  const uint32_t slots = min((uint32_t)TPB, S.N - blockIdx.x * TPB);  // (the last workgroup may be partial)
+  const uint32_t n0 = end > base ? min(slots, end - base) : 0u;
+  const bool live = threadIdx.x < n0;
   uint32_t id[1] = {p};
   f3 o[1] = {ld3(S.cam.origin)}, d[1] = {mk(0.f, 0.f, 1.f)};
   float tm[1] = {__builtin_inff()};
   bool valid[1] = {live};
-  if (live) {
-    uint32_t g;
-    d[0] = camera_dir(S, p, g);
-    S.ray[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], d[0].x);
-    S.ray[RSTRIDE * p + 1] = rec_r1(d[0].y, d[0].z, __builtin_inff());
+  if (threadIdx.x == 0) S.wstate[blockIdx.x] = make_uint2(base + n0, n0);
+  if (p < S.N) {
 #pragma unroll
     for (int s = 0; s < NSH; ++s) S.ray[RSTRIDE * ((size_t)(1 + s) * S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
-    S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
-    S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
+    if (live) {
+      d[0] = start_path(S, p, base + threadIdx.x);
+    } else {
+      S.ps0[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+      S.ray[RSTRIDE * p + 1] = rec_r1(0.f, 0.f, -1.0f);
+    }
   }
   push_children<1, NC>(S.A, (const CPTR(pt_node))S.A.nodes, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, 1, sh);
   count_rays(S.rcount, live ? 1u : 0u, sh + NC * 8);
 }
 
+// One pass of shading with path regeneration: shade every live slot, then the
+// free slots (free before, or their path just ended) start the next paths of
+// the workgroup's range, and all new rays (extension, shadow, camera) are
+// pushed into the root's target queues.  A workgroup with no live slot and an
+// exhausted range returns at once (passes queued after the chunk ended).
 template <int NC, int NSH>
 __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t sh[NC * 8 + 4];
-  const uint32_t p = blockIdx.x * TPB + threadIdx.x;
+  __shared__ uint32_t s_free[4], s_live[4], s_next, s_end;
+  __shared__ int s_skip;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  if (tid == 0) {
+    const uint2 ws = S.wstate[blockIdx.x];
+    const uint32_t end = range_start(S, blockIdx.x + 1);
+    s_next = ws.x;
+    s_end = end;
+    s_skip = ws.y == 0 && ws.x >= end;
+  }
+  __syncthreads();
+  const uint32_t end = s_end;
+  if (s_skip) return;
+  const uint32_t p = blockIdx.x * TPB + tid;
   bool new_ext = false, new_sh[NSH];
   RayV ext{mk(0, 0, 0), mk(0, 0, 1), -1.0f}, shr[NSH];
 #pragma unroll
@@ -414,7 +487,31 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
     new_sh[s] = false;
     shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
   }
-  if (p < S.N) shade_slot<NSH>(S, p, new_ext, ext, new_sh, shr);
+  int state = SLOT_LIVE;
+  if (p < S.N) state = shade_slot<NSH>(S, p, new_ext, ext, new_sh, shr);
+  // ---- regeneration: free slots take the next paths of the range in rank order
+  const bool fr = p < S.N && state != SLOT_LIVE;
+  const unsigned long long mf = __ballot(fr), ml = __ballot(p < S.N && state == SLOT_LIVE);
+  if ((tid & 63) == 0) {
+    s_free[wave] = (uint32_t)__popcll(mf);
+    s_live[wave] = (uint32_t)__popcll(ml);
+  }
+  __syncthreads();
+  const uint32_t next = s_next;
+  const uint32_t avail = end > next ? end - next : 0u;
+  if (tid == 0) {
+    const uint32_t nf = s_free[0] + s_free[1] + s_free[2] + s_free[3];
+    const uint32_t take = min(nf, avail);
+    S.wstate[blockIdx.x] = make_uint2(next + take, s_live[0] + s_live[1] + s_live[2] + s_live[3] + take);
+  }
+  if (fr) {
+    uint32_t rank = mbcnt64(mf);
+    for (int w = 0; w < wave; ++w) rank += s_free[w];
+    if (rank < avail) {
+      ext = RayV{ld3(S.cam.origin), start_path(S, p, next + rank), __builtin_inff()};
+      new_ext = true;
+    }
+  }
   uint32_t id[1 + NSH];
   f3 o[1 + NSH], d[1 + NSH];
   float tm[1 + NSH];
@@ -437,6 +534,21 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
   push_children<1 + NSH, NC>(S.A, (const CPTR(pt_node))S.A.nodes, blockIdx.x & (NLANE - 1), id, o, d, tm, valid,
                              1 + NSH, sh);
   count_rays(S.rcount, n, sh + NC * 8);
+}
+
+// Live slots over all workgroups (the host polls it: 0 = the chunk is done).
+__global__ __launch_bounds__(1024) void k_live_sum(const uint2* __restrict__ wstate, uint32_t G, uint32_t* out) {
+  __shared__ uint32_t part[16];
+  uint32_t v = 0;
+  for (uint32_t b = threadIdx.x; b < G; b += 1024) v += wstate[b].y;
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < 16; ++w) t += part[w];
+    *out = t;
+  }
 }
 
 // ---- scenes whose BVH root is a leaf -----------------------------------------

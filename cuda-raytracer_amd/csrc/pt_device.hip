@@ -77,6 +77,13 @@ struct pt_ctx {
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
   uint32_t* d_work = nullptr;  // k_path_leaf path counter
+  float4* d_res = nullptr;     // per-path radiance of a chunk
+  size_t res_cap = 0;
+  uint2* d_wstate = nullptr;   // per shade workgroup {next path, live slots}
+  size_t wstate_cap = 0;
+  uint32_t* d_live = nullptr;  // live slots after a pass group (k_live_sum)
+  uint32_t* h_poll = nullptr;  // pinned: {live, err} x 2 poll slots
+  hipEvent_t ev_poll[2] = {};
   int path_grid[2] = {0, 0};   // resident workgroups of k_path_leaf<1>, <2>
 
   // framebuffer
@@ -151,7 +158,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,      c->d_cnt,
-                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err, c->d_work,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live,
                   c->d_pix_of, c->d_accum};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -165,6 +172,10 @@ static void free_all(pt_ctx* c) {
 // (deep levels hold few rays per pass); queue offsets are u32, so both parity
 // halves (2 x qfactor x slots ids) must stay below 2^32.
 static constexpr uint32_t DEFAULT_BATCH_PATHS = 32u << 20;
+// paths per chunk (per-path radiance buffer: 16 B each); POLL_GROUP passes
+// are queued between two reads of the finished-path count
+static constexpr uint32_t CHUNK_PATHS = 1u << 28;
+static constexpr int POLL_GROUP = 4;
 static uint32_t max_batch_paths(const pt_ctx* c, uint32_t slots_per_path) {
   return (uint32_t)((1ull << 32) / (2 * c->qfactor * slots_per_path)) & ~4095u;
 }
@@ -394,9 +405,12 @@ int pt_create(pt_ctx** out, int device) {
     return PT_E_HIP;
   }
   for (auto& e : c->ev) hipEventCreate(&e);
+  for (auto& e : c->ev_poll) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
-      hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, 4) != hipSuccess) {
+      hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, 4) != hipSuccess ||
+      hipMalloc((void**)&c->d_live, 4) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_poll, 16, hipHostMallocDefault) != hipSuccess) {
     delete c;
     return PT_E_HIP;
   }
@@ -424,6 +438,9 @@ void pt_destroy(pt_ctx* c) {
   for (auto& e : c->evpool) hipEventDestroy(e);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
+  for (auto& e : c->ev_poll)
+    if (e) hipEventDestroy(e);
+  if (c->h_poll) hipHostFree(c->h_poll);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -555,11 +572,11 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     c->samples += P->spp;
     return PT_OK;
   }
-  // batch: spp_b samples of every owned pixel
   // the reference schedule (cu:2499-2533) casts up to two shadow rays per vertex
   const bool ref_sched = (P->flags & PT_FLAG_REF_SCHEDULE) != 0;
   const uint32_t nsh = ref_sched ? 2u : 1u;
   const int max_bounces = ref_sched ? 2 : P->max_bounces;
+  const int passes = max_bounces + 2;  // vertices per path at most
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
   c->timing = (P->flags & PT_FLAG_STATS) != 0;
   const bool timed = c->timing;
@@ -567,27 +584,16 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   hipEvent_t t0 = c->ev[6], t1 = c->ev[7];
   HIPCHK(c, hipEventRecord(t0, c->stream));
   bool first = true;
+  // chunks of spp_c samples of every owned pixel: M = npix * spp_c paths, each
+  // path's radiance lands in res[j * npix + q] and is summed in sample order
   for (int done = 0; done < P->spp;) {
-    // batch size under the current queue factor
-    const uint32_t cap = max_batch_paths(c, 1 + nsh);
-    if (npix > cap) return fail(c, PT_E_UNSUPPORTED, "more owned pixels than one batch holds");
-    uint32_t target = P->batch_paths > 0 ? (uint32_t)P->batch_paths : DEFAULT_BATCH_PATHS;
-    target = std::min<uint32_t>(target, cap);
-    const uint32_t spp_b = std::min<uint32_t>(std::max<uint32_t>(1, target / npix), (uint32_t)P->spp);
-    const uint32_t sb = std::min<uint32_t>(spp_b, (uint32_t)(P->spp - done));
-    const uint32_t N = npix * sb;
-    const bool realloc = N > c->cap_paths || 1 + nsh > c->cap_spp || c->qfactor != c->cap_qfactor;
-    if ((rc = ensure_paths(c, N, 1 + nsh))) return rc;
-    if (realloc && (rc = set_root_child_offsets(c))) return rc;
-    if (first) c->stats.batch_paths = (int32_t)N;
-    first = false;
-
+    const uint32_t spp_c = std::min<uint32_t>(std::max<uint32_t>(1, CHUNK_PATHS / npix), (uint32_t)(P->spp - done));
+    const uint32_t M = npix * spp_c;
+    if ((size_t)M > c->res_cap) {
+      if ((rc = dalloc(c, &c->d_res, M))) return rc;
+      c->res_cap = M;
+    }
     ShadeArgs S;
-    S.ray = c->d_ray;
-    S.ps0 = c->d_ps0;
-    S.ps1 = c->d_ps1;
-    S.ps2 = c->d_ps2;
-    S.ps3 = c->d_ps3;
     S.prims = c->d_prims;
     S.shading = c->d_shading;
     S.bsdfs = c->d_bsdfs;
@@ -602,17 +608,20 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.height = P->height;
     S.max_bounces = max_bounces;
     S.flags = P->flags;
-    S.A = trace_args(c);
     S.rcount = c->d_rcount;
-    S.N = N;
     S.sample_base = (uint32_t)(P->sample_offset + done);
-    const dim3 grid((N + TPB - 1) / TPB);
-    const int passes = max_bounces + 2;
+    S.res = c->d_res;
+    S.M = M;
+    S.passes = passes;
     if (c->root_leaf) {
       // single-leaf tree: every path runs to completion in one kernel
+      // (persistent waves with path regeneration, output res[P])
       const pt_node& root = c->nodes_host[0];
-      // persistent waves: no more workgroups than paths in chunks of 64-lane waves
-      const uint32_t want = (N + 4 * PATH_CHUNK - 1) / (4 * PATH_CHUNK);
+      S.ray = nullptr;
+      S.ps0 = S.ps2 = S.ps3 = nullptr;
+      S.ps1 = c->d_res;
+      S.N = M;
+      const uint32_t want = (M + 4 * PATH_CHUNK - 1) / (4 * PATH_CHUNK);
       HIPCHK(c, hipMemsetAsync(c->d_work, 0, 4, c->stream));
       if (nsh == 2)
         c->launch(pt_ctx::K_PATH, 0, k_path_leaf<2>, dim3(std::min<uint32_t>(want, c->path_grid[1])), dim3(TPB), S,
@@ -621,42 +630,91 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         c->launch(pt_ctx::K_PATH, 0, k_path_leaf<1>, dim3(std::min<uint32_t>(want, c->path_grid[0])), dim3(TPB), S,
                   root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work);
       c->stats.passes += passes;
+      if (first) c->stats.batch_paths = (int32_t)M;
     } else {
-      // camera rays enter the root's target queues directly; each pass traces
-      // the levels below, then shading pushes the next rays (none after the
-      // last pass: its shade only resolves the final shadow rays)
+      // N path slots run the chunk's M paths: a slot whose path ends starts the
+      // next one in the same shade kernel, so every pass traces a full pool
+      const uint32_t cap = max_batch_paths(c, 1 + nsh);
+      uint32_t target = P->batch_paths > 0 ? (uint32_t)P->batch_paths : DEFAULT_BATCH_PATHS;
+      const uint32_t N = std::min<uint32_t>(std::min<uint32_t>(target, cap), M);
+      const bool realloc = N > c->cap_paths || 1 + nsh > c->cap_spp || c->qfactor != c->cap_qfactor;
+      if ((rc = ensure_paths(c, N, 1 + nsh))) return rc;
+      if (realloc && (rc = set_root_child_offsets(c))) return rc;
+      if (first) c->stats.batch_paths = (int32_t)N;
+      // (device buffers as (re)allocated by ensure_paths)
+      S.ray = c->d_ray;
+      S.ps0 = c->d_ps0;
+      S.ps1 = c->d_ps1;
+      S.ps2 = c->d_ps2;
+      S.ps3 = c->d_ps3;
+      S.N = N;
+      S.A = trace_args(c);
+      const dim3 grid((N + TPB - 1) / TPB);
+      // workgroup b of the shade grid runs its slots' share of the chunk
+      const uint32_t G = (N + TPB - 1) / TPB;
+      if (G > c->wstate_cap) {
+        if ((rc = dalloc(c, &c->d_wstate, G))) return rc;
+        c->wstate_cap = G;
+      }
+      S.wstate = c->d_wstate;
       const int nc = c->skip_l1 ? 16 : 4;
       if (nc == 16 && nsh == 1) c->launch(pt_ctx::K_CAM, 0, k_camera_push<16, 1>, grid, dim3(TPB), S);
       if (nc == 16 && nsh == 2) c->launch(pt_ctx::K_CAM, 0, k_camera_push<16, 2>, grid, dim3(TPB), S);
       if (nc == 4 && nsh == 1) c->launch(pt_ctx::K_CAM, 0, k_camera_push<4, 1>, grid, dim3(TPB), S);
       if (nc == 4 && nsh == 2) c->launch(pt_ctx::K_CAM, 0, k_camera_push<4, 2>, grid, dim3(TPB), S);
-      for (int pass = 0; pass < passes; ++pass) {
-        if ((rc = trace_levels(c))) return rc;
-        const bool last = pass == passes - 1;
-        if (last && nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade<1>, grid, dim3(TPB), S);
-        if (last && nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade<2>, grid, dim3(TPB), S);
-        if (!last && nc == 16 && nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<16, 1>, grid, dim3(TPB), S);
-        if (!last && nc == 16 && nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<16, 2>, grid, dim3(TPB), S);
-        if (!last && nc == 4 && nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4, 1>, grid, dim3(TPB), S);
-        if (!last && nc == 4 && nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4, 2>, grid, dim3(TPB), S);
+      // passes in groups of POLL_GROUP; the host reads the finished-path count
+      // of group g (pinned memory, event) while group g + 1 is already queued
+      auto enqueue_group = [&](int g) -> int {
+        for (int k = 0; k < POLL_GROUP; ++k) {
+          int r = trace_levels(c);
+          if (r) return r;
+          if (nc == 16 && nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<16, 1>, grid, dim3(TPB), S);
+          if (nc == 16 && nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<16, 2>, grid, dim3(TPB), S);
+          if (nc == 4 && nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4, 1>, grid, dim3(TPB), S);
+          if (nc == 4 && nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4, 2>, grid, dim3(TPB), S);
+        }
+        hipLaunchKernelGGL(k_live_sum, dim3(1), dim3(1024), 0, c->stream, (const uint2*)S.wstate, G, c->d_live);
+        HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1), c->d_live, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1) + 1, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev_poll[g & 1], c->stream));
+        return PT_OK;
+      };
+      // every path ends within `passes` passes of its start, and a workgroup
+      // starts a new path in every slot that ends; its range holds at most
+      // ceil(M / N) paths per slot
+      const int max_groups = (int)(((uint64_t)(M / N + 2) * passes) / POLL_GROUP + 3);
+      bool overflow = false, finished = false;
+      if ((rc = enqueue_group(0)) || (rc = enqueue_group(1))) return rc;
+      for (int g = 0; g < max_groups; ++g) {
+        HIPCHK(c, hipEventSynchronize(c->ev_poll[g & 1]));
+        const uint32_t nlive = c->h_poll[2 * (g & 1)], err = c->h_poll[2 * (g & 1) + 1];
+        if (err) {
+          overflow = true;
+          break;
+        }
+        if (nlive == 0) {
+          finished = true;
+          break;
+        }
+        if ((rc = enqueue_group(g + 2))) return rc;
       }
-      // a level that overflowed its queue was abandoned: re-run the batch
-      // (nothing has been accumulated yet) with twice the queue factor
-      uint32_t e = 0;
-      HIPCHK(c, hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      if (e) {
-        if (max_batch_paths(c, 1 + nsh) / 2 < npix)
+      if (overflow) {
+        // a level overflowed its queue (the pass was abandoned): re-run the
+        // chunk with twice the queue factor (nothing has been accumulated yet)
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (max_batch_paths(c, 1 + nsh) / 2 < 4096)
           return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded (u32 queue offsets)");
         c->qfactor *= 2;
         HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
         continue;
       }
+      if (!finished) return fail(c, PT_E_HIP, "paths did not finish within the pass bound");
     }
-    c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_ps1,
-              c->d_accum, npix, sb);
+    c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_res,
+              c->d_accum, npix, spp_c);
     HIPCHK(c, hipGetLastError());
-    done += (int)sb;
+    done += (int)spp_c;
+    first = false;
     c->stats.batches++;
   }
   HIPCHK(c, hipEventRecord(t1, c->stream));
