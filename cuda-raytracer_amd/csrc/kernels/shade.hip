@@ -42,6 +42,7 @@ struct ShadeArgs {
   int width, height, max_bounces;
   uint32_t flags;
   TraceArgs A;                   // fused root pass (camera/shade push into the root's target queues)
+  RootTable T;                   // its inline leaves and targets
   // path regeneration of the wavefront: the N slots run the M paths of a chunk
   // (P = j * npix + q: sample j of owned pixel q); a slot whose path ends
   // writes res[P] and starts the next unstarted path
@@ -371,19 +372,17 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
     S.ps0[p] = make_float4(st.T.x, st.T.y, st.T.z, __uint_as_float(st.flags));
     S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(P));
   }
-  if (new_ext) {
+  // new rays: r0 here, r1 (with the key of the inline leaves) in root_pass
+  if (new_ext)
     S.ray[RSTRIDE * p] = make_float4(ext.o.x, ext.o.y, ext.o.z, ext.d.x);
-    S.ray[RSTRIDE * p + 1] = rec_r1(ext.d.y, ext.d.z, __builtin_inff());
-  } else {
+  else
     S.ray[RSTRIDE * p + 1] = rec_r1(0.f, 0.f, -1.0f);
-  }
 #pragma unroll
   for (int s = 0; s < NSH; ++s) {
     const size_t slot = (size_t)(1 + s) * S.N + p;
     if (new_sh[s]) {
       (s ? S.ps3 : S.ps2)[p] = make_float4(C[s].x, C[s].y, C[s].z, 0.0f);
       S.ray[RSTRIDE * slot] = make_float4(shr[s].o.x, shr[s].o.y, shr[s].o.z, shr[s].d.x);
-      S.ray[RSTRIDE * slot + 1] = rec_r1(shr[s].d.y, shr[s].d.z, shr[s].tmax);
     } else {
       S.ray[RSTRIDE * slot + 1] = rec_r1(0.f, 0.f, -1.0f);
     }
@@ -395,8 +394,7 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
 __device__ __forceinline__ f3 start_path(const ShadeArgs& S, uint32_t p, uint32_t P) {
   uint32_t g;
   const f3 d = camera_dir(S, P, g);
-  S.ray[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], d.x);
-  S.ray[RSTRIDE * p + 1] = rec_r1(d.y, d.z, __builtin_inff());
+  S.ray[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], d.x);  // r1: root_pass
   S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
   S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
   return d;
@@ -428,9 +426,9 @@ __device__ __forceinline__ uint32_t range_start(const ShadeArgs& S, uint32_t b) 
 // 256 slots in every pass; it alone reads and writes its
 // wstate word, so starting paths needs no shared counter.
 // First fill: slot i of workgroup b starts path range_start(b) + i.
-template <int NC, int NSH>
+template <int NSH>
 __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
-  __shared__ uint32_t sh[NC * 8 + 4];
+  __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
   __shared__ uint32_t s_rng[2];
   if (threadIdx.x < 2) s_rng[threadIdx.x] = range_start(S, blockIdx.x + threadIdx.x);
   __syncthreads();
@@ -442,7 +440,7 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
   uint32_t id[1] = {p};
   f3 o[1] = {ld3(S.cam.origin)}, d[1] = {mk(0.f, 0.f, 1.f)};
   float tm[1] = {__builtin_inff()};
-  bool valid[1] = {live};
+  bool valid[1] = {live}, anyhit[1] = {false};
   if (threadIdx.x == 0) S.wstate[blockIdx.x] = make_uint2(base + n0, n0);
   if (p < S.N) {
 #pragma unroll
@@ -454,8 +452,8 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
       S.ray[RSTRIDE * p + 1] = rec_r1(0.f, 0.f, -1.0f);
     }
   }
-  push_children<1, NC>(S.A, (const CPTR(pt_node))S.A.nodes, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, 1, sh);
-  count_rays(S.rcount, live ? 1u : 0u, sh + NC * 8);
+  root_pass<1>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh);
+  count_rays(S.rcount, live ? 1u : 0u, sh + MAX_ROOT_TARGETS * 8);
 }
 
 // One pass of shading with path regeneration: shade every live slot, then the
@@ -463,9 +461,9 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
 // the workgroup's range, and all new rays (extension, shadow, camera) are
 // pushed into the root's target queues.  A workgroup with no live slot and an
 // exhausted range returns at once (passes queued after the chunk ended).
-template <int NC, int NSH>
+template <int NSH>
 __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
-  __shared__ uint32_t sh[NC * 8 + 4];
+  __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
   __shared__ uint32_t s_free[4], s_live[4], s_next, s_end;
   __shared__ int s_skip;
   const int tid = threadIdx.x, wave = tid >> 6;
@@ -515,12 +513,13 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
   uint32_t id[1 + NSH];
   f3 o[1 + NSH], d[1 + NSH];
   float tm[1 + NSH];
-  bool valid[1 + NSH];
+  bool valid[1 + NSH], anyhit[1 + NSH];
   id[0] = p;
   o[0] = ext.o;
   d[0] = ext.d;
   tm[0] = __builtin_inff();
   valid[0] = new_ext;
+  anyhit[0] = false;
   uint32_t n = new_ext ? 1u : 0u;
 #pragma unroll
   for (int s = 0; s < NSH; ++s) {
@@ -529,11 +528,11 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
     d[1 + s] = shr[s].d;
     tm[1 + s] = shr[s].tmax;
     valid[1 + s] = new_sh[s];
+    anyhit[1 + s] = true;
     n += new_sh[s] ? 1u : 0u;
   }
-  push_children<1 + NSH, NC>(S.A, (const CPTR(pt_node))S.A.nodes, blockIdx.x & (NLANE - 1), id, o, d, tm, valid,
-                             1 + NSH, sh);
-  count_rays(S.rcount, n, sh + NC * 8);
+  root_pass<1 + NSH>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh);
+  count_rays(S.rcount, n, sh + MAX_ROOT_TARGETS * 8);
 }
 
 // Live slots over all workgroups (the host polls it: 0 = the chunk is done).

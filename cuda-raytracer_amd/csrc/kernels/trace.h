@@ -73,6 +73,22 @@ __device__ __forceinline__ float4 rec_r1(float dy, float dz, float tmax) {
 
 __host__ __device__ inline size_t cnt_idx(int node, int lane) { return ((size_t)node * NLANE + lane) * CSTRIDE; }
 
+// The root pass (fused into the ray producers, or k_trace_root): small leaves
+// among the root's children / grandchildren are tested right there ("inline
+// leaves": their closest hit becomes the ray's initial key and tmax, and a
+// shadow ray occluded by one is never queued); every other ray is pushed into
+// the queues of the targets (nodes of one level, 1 or 2) whose boxes it hits.
+constexpr int MAX_ROOT_TARGETS = 16, MAX_INLINE_LEAVES = 4;
+struct RootTable {
+  int nt;                          // queue targets
+  int tnode[MAX_ROOT_TARGETS];     // target node ids
+  int tbox[MAX_ROOT_TARGETS];      // parent * 4 + slot: where the target's box is stored
+  int ni;                          // inline leaves
+  int ibox[MAX_INLINE_LEAVES];     // parent * 4 + slot of the leaf's box
+  int istart[MAX_INLINE_LEAVES];   // its primitives
+  int icount[MAX_INLINE_LEAVES];
+};
+
 struct LevelArgs {
   int first;  // first node id of the level
   int nl;     // nodes in the level

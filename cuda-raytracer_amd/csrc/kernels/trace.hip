@@ -168,36 +168,40 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// ---- one work item: up to TILE rays of one node's queue lane ---------------------
-// ids: implicit (root pass: base + i) or read from qin[base + i].
-// NC = 4: the node's children.  NC = 16 (root pass only): the node's
-// grandchildren, i.e. the first interior level is skipped -- every box is
-// conservative for its subtree, so testing a grandchild box directly never
-// drops a ray that would hit a primitive below it.
-template <int NC>
-__device__ __forceinline__ const CPTR(pt_node) child_slot(const TraceArgs& A, const CPTR(pt_node) nd, int c,
-                                                          int& k) {
-  if (NC == 4) {
+// ---- push targets ------------------------------------------------------------
+// A node's 4 children (level passes), or the root table's targets (root pass).
+struct ChildTargets {
+  const CPTR(pt_node) nd;
+  __device__ __forceinline__ int count() const { return 4; }
+  __device__ __forceinline__ const CPTR(pt_node) box(const TraceArgs&, int c, int& k) const {
     k = c;
     return nd;
   }
-  k = c & 3;
-  return (const CPTR(pt_node))(A.nodes + nd->child[c >> 2]);
-}
+  __device__ __forceinline__ int node(const TraceArgs&, int c) const { return nd->child[c]; }
+};
+struct TableTargets {
+  const RootTable& T;
+  __device__ __forceinline__ int count() const { return T.nt; }
+  __device__ __forceinline__ const CPTR(pt_node) box(const TraceArgs& A, int c, int& k) const {
+    k = T.tbox[c] & 3;
+    return (const CPTR(pt_node))(A.nodes + (T.tbox[c] >> 2));
+  }
+  __device__ __forceinline__ int node(const TraceArgs&, int c) const { return T.tnode[c]; }
+};
 
-// Block-wide push of R rays per thread into the queues of NC children (or
-// grandchildren) of node nd in queue lane `lane`: slab tests, wave64 ballot
-// compaction, one atomic slot reservation per child for the whole workgroup,
-// cross-wave offsets through LDS (sh: NC * 8 u32).  Every thread of the
-// workgroup must call it (two barriers); rays with valid[j] false push nothing,
-// ray groups j >= nj (uniform) are skipped.
-template <int R, int NC>
-__device__ __forceinline__ void push_children(const TraceArgs& A, const CPTR(pt_node) nd, int lane,
-                                              const uint32_t (&id)[R], const f3 (&o)[R], const f3 (&d)[R],
-                                              const float (&tmax)[R], const bool (&valid)[R], int nj,
-                                              uint32_t* sh) {
+// Block-wide push of R rays per thread into the queues of up to NC targets in
+// queue lane `lane`: slab tests, wave64 ballot compaction, one atomic slot
+// reservation per target for the whole workgroup, cross-wave offsets through
+// LDS (sh: NC * 8 u32).  Every thread of the workgroup must call it (two
+// barriers); rays with valid[j] false push nothing, ray groups j >= nj
+// (uniform) are skipped.
+template <int R, int NC, class Tg>
+__device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, int lane, const uint32_t (&id)[R],
+                                              const f3 (&o)[R], const f3 (&d)[R], const float (&tmax)[R],
+                                              const bool (&valid)[R], int nj, uint32_t* sh) {
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
+  const int nt = tg.count();
   uint32_t bits[R];
 #pragma unroll
   for (int j = 0; j < R; ++j) {
@@ -212,28 +216,28 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const CPTR(pt_
     uint32_t b = 0;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
+      if (c >= nt) break;
       int k;
-      const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
+      const CPTR(pt_node) cn = tg.box(A, c, k);
       bool h = box_hit(cn->bmin_x[k], cn->bmax_x[k], cn->bmin_y[k], cn->bmax_y[k], cn->bmin_z[k], cn->bmax_z[k],
                        oi, inv, tmax[j]);
       b |= (valid[j] && h) ? (1u << c) : 0u;
     }
     bits[j] = b;
   }
-  // per-wave counts per child -> LDS sh[c*4 + wave]; bases -> sh[NC*4 + c*4 + wave]
+  // per-wave counts per target -> LDS sh[c*4 + wave]; bases -> sh[NC*4 + c*4 + wave]
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
+    if (c >= nt) break;
     uint32_t wc = 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) wc += (uint32_t)__popcll(__ballot((bits[j] >> c) & 1u));
     if ((tid & 63) == 0) sh[c * 4 + wave] = wc;
   }
   __syncthreads();
-  if (tid < NC) {
+  if (tid < nt) {
     const int c = tid;
-    int k;
-    const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
-    const int child = cn->child[k];
+    const int child = tg.node(A, c);
     uint32_t w0 = sh[c * 4 + 0], w1 = sh[c * 4 + 1], w2 = sh[c * 4 + 2], w3 = sh[c * 4 + 3];
     uint32_t tot = w0 + w1 + w2 + w3;
     uint32_t b = 0;
@@ -246,9 +250,8 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const CPTR(pt_
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    int k;
-    const CPTR(pt_node) cn = child_slot<NC>(A, nd, c, k);
-    const int child = cn->child[k];
+    if (c >= nt) break;
+    const int child = tg.node(A, c);
     if (child < 0) continue;
     uint32_t off = sh[NC * 4 + c * 4 + wave] + A.qoff[(size_t)child * NLANE + lane];
 #pragma unroll
@@ -261,7 +264,60 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const CPTR(pt_
   }
 }
 
-template <bool IMPLICIT, int NC = 4>
+// Root pass of R rays per thread (every thread of the workgroup calls it):
+//  1. the inline leaves of the root table, when the ray enters their box:
+//     closest hit with the leaf rules of process_item (ties to the lowest
+//     primitive) -- it becomes the ray's initial key {prim, t} and its tmax;
+//  2. the record word r1 = {d.y, d.z, prim, t} of every valid ray is written
+//     here (the callers write r0 and the empty r1 of invalid slots);
+//  3. a shadow ray (anyhit) occluded by an inline leaf is done: not queued;
+//     the others are pushed into the targets' queues with the tightened tmax.
+template <int R>
+__device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T, int lane, const uint32_t (&id)[R],
+                                          const f3 (&o)[R], const f3 (&d)[R], const float (&tmax)[R],
+                                          const bool (&valid)[R], const bool (&anyhit)[R], uint32_t* sh) {
+  float tm[R];
+  bool pv[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    float bt = tmax[j];
+    int bp = -1;
+    if (T.ni > 0) {
+      const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
+                        __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
+      const f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
+      for (int i = 0; i < T.ni; ++i) {
+        const CPTR(pt_node) bn = (const CPTR(pt_node))(A.nodes + (T.ibox[i] >> 2));
+        const int k = T.ibox[i] & 3;
+        if (!valid[j] || !box_hit(bn->bmin_x[k], bn->bmax_x[k], bn->bmin_y[k], bn->bmax_y[k], bn->bmin_z[k],
+                                  bn->bmax_z[k], oi, inv, bt))
+          continue;
+        const int pstart = T.istart[i];
+        const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);
+        for (int kk = 0; kk < T.icount[i]; ++kk, P += 6) {
+          const float4 q0 = f4(P[0]), q1 = f4(P[1]);
+          float tt;
+          if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE)
+            tt = sphere_test(o[j], d[j], q0, q1);
+          else
+            tt = tri_test(o[j], d[j], q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), bt);
+          if (tt >= 0.0f && (tt < bt || (tt == bt && bp < 0))) {
+            bt = tt;
+            bp = pstart + kk;
+          }
+        }
+      }
+    }
+    if (valid[j])
+      A.ray[RSTRIDE * id[j] + 1] =
+          make_float4(d[j].y, d[j].z, __uint_as_float(bp >= 0 ? (uint32_t)bp : PT_PRIM_NONE), bt);
+    tm[j] = bt;
+    pv[j] = valid[j] && !(anyhit[j] && bp >= 0);
+  }
+  push_children<R, MAX_ROOT_TARGETS>(A, TableTargets{T}, lane, id, o, d, tm, pv, R, sh);
+}
+
+template <bool IMPLICIT>
 __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, uint32_t base, int n, int lane,
                                              uint32_t* sh) {
   const int tid = threadIdx.x;
@@ -360,29 +416,60 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
   }
 
   // ---------------- interior: NC child boxes, compaction, push ----------------
-  push_children<RPT, NC>(A, nd, lane, id, o, d, tmax, valid, nj, sh);
+  push_children<RPT, 4>(A, ChildTargets{nd}, lane, id, o, d, tmax, valid, nj, sh);
   return nvalid;
 }
 
-// ---- root pass (level 0): implicit queue = slots [r0, r1) ------------------------
-// NC = 16: rays go straight to the level-2 queues (host: skip_l1).
-template <int NC>
-__global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, uint32_t r0, uint32_t r1,
+// ---- root pass (level 0) of pt_intersect: implicit queue = slots [r0, r1) ------------
+// Single-leaf trees: the root leaf's primitives against every ray (process_item).
+// Otherwise root_pass: inline leaves, then the root table's targets.
+__global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, uint32_t r0, uint32_t r1,
                                                     unsigned long long* __restrict__ rcount) {
-  __shared__ uint32_t sh[NC * 8 + 4];
+  __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
   const uint32_t item = blockIdx.x;
   const uint32_t first = r0 + item * TILE;
   const int n = (int)min((uint32_t)TILE, r1 - first);
   const int lane = item & (NLANE - 1);
-  uint32_t v = process_item<true, NC>(A, 0, first, n, lane, sh);
+  uint32_t v = 0;
+  if (((const CPTR(pt_node))A.nodes)->prim_count > 0) {
+    v = process_item<true>(A, 0, first, n, lane, sh);
+  } else {
+    uint32_t id[RPT];
+    f3 o[RPT], d[RPT];
+    float tmax[RPT];
+    bool valid[RPT], anyhit[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int i = j * TPB + (int)threadIdx.x;
+      id[j] = first + (uint32_t)i;
+      o[j] = mk(0.f, 0.f, 0.f);
+      d[j] = mk(0.f, 0.f, 1.f);
+      tmax[j] = -1.0f;
+      valid[j] = false;
+      anyhit[j] = false;
+      if (i < n) {
+        const float4 b = A.ray[RSTRIDE * id[j] + 1];
+        if (b.w >= 0.0f) {
+          const float4 a = A.ray[RSTRIDE * id[j]];
+          o[j] = mk(a.x, a.y, a.z);
+          d[j] = mk(a.w, b.x, b.y);
+          tmax[j] = b.w;
+          valid[j] = true;
+          v++;
+        }
+      }
+    }
+    root_pass<RPT>(A, T, lane, id, o, d, tmax, valid, anyhit, sh);
+  }
   // valid-ray count (R of the roofline formula): one fire-and-forget atomic per
   // workgroup into this lane's counter line
   v = wave_sum(v);
   __syncthreads();
-  if ((threadIdx.x & 63) == 0) sh[NC * 8 + (threadIdx.x >> 6)] = v;
+  if ((threadIdx.x & 63) == 0) sh[MAX_ROOT_TARGETS * 8 + (threadIdx.x >> 6)] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t t = sh[NC * 8] + sh[NC * 8 + 1] + sh[NC * 8 + 2] + sh[NC * 8 + 3];
+    const uint32_t t = sh[MAX_ROOT_TARGETS * 8] + sh[MAX_ROOT_TARGETS * 8 + 1] + sh[MAX_ROOT_TARGETS * 8 + 2] +
+                       sh[MAX_ROOT_TARGETS * 8 + 3];
     if (t) atomicAdd(rcount + (size_t)(item & (RCOUNT_SLOTS - 1)) * 16, (unsigned long long)t);
   }
 }

@@ -51,6 +51,7 @@ struct pt_ctx {
   int max_level_nodes = 0;
   bool root_leaf = true;
   bool skip_l1 = false;  // root pass pushes straight into the level-2 queues
+  RootTable rt{};        // root pass: inline leaves and queue targets (build_root_table)
   std::vector<pt_node> nodes_host;
   pt_light light{};
   pt_camera camera{};
@@ -217,6 +218,53 @@ static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
   return PT_OK;
 }
 
+// The root pass's table.  Small leaves among the root's children (and, when
+// level 1 is skipped, grandchildren) are tested inline by the ray producers,
+// up to PT_INLINE_MAX primitives in all (default 32; 0 disables).  Level 1 is
+// skipped when every other child of the root is interior (PT_NO_SKIP_L1=1
+// disables it): the producers then test the grandchild boxes directly (boxes
+// are conservative for their subtrees, so no ray is lost).
+static void build_root_table(pt_ctx* c) {
+  RootTable& T = c->rt;
+  memset(&T, 0, sizeof(T));
+  c->skip_l1 = false;
+  if (c->root_leaf) return;
+  const char* e = getenv("PT_INLINE_MAX");
+  int budget = e ? atoi(e) : 32;
+  const std::vector<pt_node>& nd = c->nodes_host;
+  auto try_inline = [&](int parent, int k) {
+    const pt_node& leaf = nd[nd[parent].child[k]];
+    if (leaf.prim_count <= 0 || leaf.prim_count > budget || T.ni >= MAX_INLINE_LEAVES) return false;
+    T.ibox[T.ni] = parent * 4 + k;
+    T.istart[T.ni] = leaf.prim_start;
+    T.icount[T.ni] = leaf.prim_count;
+    T.ni++;
+    budget -= leaf.prim_count;
+    return true;
+  };
+  auto add_target = [&](int parent, int k) {
+    T.tbox[T.nt] = parent * 4 + k;
+    T.tnode[T.nt] = nd[parent].child[k];
+    T.nt++;
+  };
+  std::vector<int> rest;  // root slots neither empty nor inline
+  for (int k = 0; k < 4; ++k)
+    if (nd[0].child[k] >= 0 && !try_inline(0, k)) rest.push_back(k);
+  bool skip = c->n_levels >= 3 && !getenv("PT_NO_SKIP_L1") && !rest.empty();
+  for (int k : rest)
+    if (nd[nd[0].child[k]].prim_count > 0) skip = false;
+  for (int k : rest) {
+    if (!skip) {
+      add_target(0, k);
+      continue;
+    }
+    const int ch = nd[0].child[k];
+    for (int g = 0; g < 4; ++g)
+      if (nd[ch].child[g] >= 0 && !try_inline(ch, g)) add_target(ch, g);
+  }
+  c->skip_l1 = skip;
+}
+
 // Queue offsets of the root's targets: each gets root_per_lane slots in every
 // lane of the half its level uses (level 1: odd half, level 2: even half).
 static int set_root_child_offsets(pt_ctx* c) {
@@ -224,19 +272,9 @@ static int set_root_child_offsets(pt_ctx* c) {
   const size_t per_lane = root_per_lane(c->cap_paths, c->cap_spp);
   const size_t lanecap = c->qcap / NLANE;
   const pt_node& root = c->nodes_host[0];
-  // targets: the root's children (level 1, odd half) or, when level 1 is
-  // skipped, its grandchildren (level 2, even half)
-  std::vector<int> targets;
-  for (int k = 0; k < 4; ++k) {
-    if (root.child[k] < 0) continue;
-    if (!c->skip_l1) {
-      targets.push_back(root.child[k]);
-      continue;
-    }
-    const pt_node& ch = c->nodes_host[root.child[k]];
-    for (int g = 0; g < 4; ++g)
-      if (ch.child[g] >= 0) targets.push_back(ch.child[g]);
-  }
+  // targets: nodes of level 1 (odd half) or, when level 1 is skipped, of
+  // level 2 (even half)
+  std::vector<int> targets(c->rt.tnode, c->rt.tnode + c->rt.nt);
   if (targets.size() * per_lane > lanecap) return fail(c, PT_E_OVERFLOW, "root queue capacity");
   const size_t half = c->skip_l1 ? 0 : c->qcap;
   // ordered on the context's (non-blocking) stream behind any work in flight
@@ -297,10 +335,7 @@ static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
   const uint32_t items = (r1 - r0 + TILE - 1) / TILE;
   // the (node, lane) counters are zero here: each level's scan re-zeroes them
   // after taking its snapshot (pt_load_scene zeroes them once)
-  if (c->skip_l1)
-    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<16>, dim3(items), dim3(TPB), A, r0, r1, c->d_rcount);
-  else
-    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<4>, dim3(items), dim3(TPB), A, r0, r1, c->d_rcount);
+  c->launch(pt_ctx::K_ROOT, 0, k_trace_root, dim3(items), dim3(TPB), A, c->rt, r0, r1, c->d_rcount);
   if (c->root_leaf) {
     HIPCHK(c, hipGetLastError());
     c->stats.passes++;
@@ -460,13 +495,6 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     c->max_level_nodes = std::max(c->max_level_nodes, c->level_start[l + 1] - c->level_start[l]);
   c->nodes_host.assign(s->nodes, s->nodes + s->n_nodes);
   c->root_leaf = c->nodes_host[0].prim_count > 0;
-  // skip the first interior level when every child of the root is interior:
-  // the root pass tests the 16 grandchild boxes (PT_NO_SKIP_L1=1 disables it)
-  c->skip_l1 = !c->root_leaf && c->n_levels >= 3 && !getenv("PT_NO_SKIP_L1");
-  for (int k = 0; k < 4 && c->skip_l1; ++k) {
-    const int ch = c->nodes_host[0].child[k];
-    if (ch >= 0 && c->nodes_host[ch].prim_count > 0) c->skip_l1 = false;
-  }
   for (int i = 0; i < s->n_nodes; ++i) {
     const pt_node& nd = s->nodes[i];
     if (nd.prim_start < 0 || nd.prim_count < 0 || nd.prim_start + nd.prim_count > s->n_prims)
@@ -480,6 +508,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     memcpy(&meta, &s->prims[i].q[3], 4);
     if ((int)(meta & 0x0FFFFFFFu) >= s->n_bsdfs) return fail(c, PT_E_INVALID, "primitive bsdf out of range");
   }
+  build_root_table(c);
   if ((rc = dalloc(c, &c->d_nodes, s->n_nodes))) return rc;
   if ((rc = dalloc(c, &c->d_prims, (size_t)s->n_prims * 6))) return rc;
   if ((rc = dalloc(c, &c->d_shading, s->n_prims))) return rc;
@@ -649,6 +678,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       S.ps3 = c->d_ps3;
       S.N = N;
       S.A = trace_args(c);
+      S.T = c->rt;
       const dim3 grid((N + TPB - 1) / TPB);
       // workgroup b of the shade grid runs its slots' share of the chunk
       const uint32_t G = (N + TPB - 1) / TPB;
@@ -657,21 +687,16 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         c->wstate_cap = G;
       }
       S.wstate = c->d_wstate;
-      const int nc = c->skip_l1 ? 16 : 4;
-      if (nc == 16 && nsh == 1) c->launch(pt_ctx::K_CAM, 0, k_camera_push<16, 1>, grid, dim3(TPB), S);
-      if (nc == 16 && nsh == 2) c->launch(pt_ctx::K_CAM, 0, k_camera_push<16, 2>, grid, dim3(TPB), S);
-      if (nc == 4 && nsh == 1) c->launch(pt_ctx::K_CAM, 0, k_camera_push<4, 1>, grid, dim3(TPB), S);
-      if (nc == 4 && nsh == 2) c->launch(pt_ctx::K_CAM, 0, k_camera_push<4, 2>, grid, dim3(TPB), S);
+      if (nsh == 1) c->launch(pt_ctx::K_CAM, 0, k_camera_push<1>, grid, dim3(TPB), S);
+      if (nsh == 2) c->launch(pt_ctx::K_CAM, 0, k_camera_push<2>, grid, dim3(TPB), S);
       // passes in groups of POLL_GROUP; the host reads the finished-path count
       // of group g (pinned memory, event) while group g + 1 is already queued
       auto enqueue_group = [&](int g) -> int {
         for (int k = 0; k < POLL_GROUP; ++k) {
           int r = trace_levels(c);
           if (r) return r;
-          if (nc == 16 && nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<16, 1>, grid, dim3(TPB), S);
-          if (nc == 16 && nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<16, 2>, grid, dim3(TPB), S);
-          if (nc == 4 && nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4, 1>, grid, dim3(TPB), S);
-          if (nc == 4 && nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<4, 2>, grid, dim3(TPB), S);
+          if (nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<1>, grid, dim3(TPB), S);
+          if (nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<2>, grid, dim3(TPB), S);
         }
         hipLaunchKernelGGL(k_live_sum, dim3(1), dim3(1024), 0, c->stream, (const uint2*)S.wstate, G, c->d_live);
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1), c->d_live, 4, hipMemcpyDeviceToHost, c->stream));
