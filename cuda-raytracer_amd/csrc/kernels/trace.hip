@@ -602,8 +602,10 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 // ---- per-level pass: every wave walks the items of its block's lane ----------------
 // Lane s's items are processed by blocks b with b % 8 == s (same XCD under the
 // observed round-robin placement: a speed hint only).
+// 6 waves per SIMD (<= 80 VGPRs, no spills): +2-3 % over the unconstrained
+// 106 VGPRs (4 waves); 7 waves spill and lose 4 %
 #ifndef PT_LEVEL_ATTR
-#define PT_LEVEL_ATTR
+#define PT_LEVEL_ATTR __attribute__((amdgpu_waves_per_eu(6, 8)))
 #endif
 __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, LevelArgs L) {
   const int lane = blockIdx.x & (NLANE - 1);
