@@ -205,6 +205,23 @@ def run_workload(name, args, ctx, rank, world, dev, dist):
                 "bytes_per_launch": int(lvl_bytes / max(1, launches))}
     if src:
         roof["traffic_source"] = src
+    others = []
+    if st.shade_launches > 0:
+        # shading with the fused root pass: 96 B per shaded path
+        # vertex (hit 8 + path state 44 read + 44 write)
+        sbytes = 96 * st.shaded
+        ach = sbytes / (st.ms_shade_push * 1e-3) / 1e9 if st.ms_shade_push > 0 else 0.0
+        straffic, ssrc = pmc_traffic(name, "k_shade_push")
+        sroof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": straffic, "kernel": "k_shade_push",
+                 "launches": int(st.shade_launches),
+                 "avg_launch_us": round(st.ms_shade_push * 1e3 / max(1, st.shade_launches), 2),
+                 "bytes_per_launch": int(sbytes / max(1, st.shade_launches)), "shaded_vertices": int(st.shaded)}
+        if ssrc:
+            sroof["traffic_source"] = ssrc
+        if st.ms_shade_push > lvl_ms:  # the dominant kernel first
+            roof, sroof = sroof, roof
+        others.append(sroof)
     out = {
         "scene": name,
         "value": round(rays / elapsed / 1e6, 2),
@@ -215,10 +232,12 @@ def run_workload(name, args, ctx, rank, world, dev, dist):
         "bvh": {"nodes": int(desc.n_nodes), "levels": int(desc.n_levels), "prims": int(desc.n_prims),
                 "gpu_build_ms": round(getattr(scene, "build_ms", 0.0), 2) or None},
         "roofline": roof,
+        "roofline_other": others,
         "trace": {"visits_per_ray": round(st.visits / max(1, st.rays), 2),
                   "instrumented_frame_ms": None if instrumented_ms is None else round(instrumented_ms, 2),
                   "ms_path": round(st.ms_path, 1), "ms_trace": round(st.ms_trace, 1),
-                  "ms_shade": round(st.ms_shade, 1), "ms_root": round(st.ms_root, 1),
+                  "ms_shade": round(st.ms_shade, 1), "ms_shade_push": round(st.ms_shade_push, 1),
+                  "ms_root": round(st.ms_root, 1),
                   "ms_scan": round(st.ms_scan, 1), "ms_levels": round(lvl_ms, 1),
                   "levels": [{"level": l, "ms": round(st.ms_level[l], 2), "visits": int(st.level_visits[l]),
                               "leaf_visits": int(st.level_leaf_visits[l]), "items": int(st.level_items[l]),

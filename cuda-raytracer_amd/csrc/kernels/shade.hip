@@ -50,7 +50,7 @@ struct ShadeArgs {
   uint32_t M;         // paths in the chunk
   // workgroup b runs the paths [range_start(b), range_start(b + 1)): a share of
   // the chunk proportional to its slots (the last workgroup may be partial)
-  uint2* wstate;      // per workgroup: {next unstarted path, live slots after its last pass}
+  uint4* wstate;      // per workgroup: {next unstarted path, live slots after its last pass, vertices shaded, 0}
   int passes;         // vertices per path at most (max_bounces + 2)
   unsigned long long* rcount;    // rays entering the traversal (RCOUNT_SLOTS counters)
 };
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
   f3 o[1] = {ld3(S.cam.origin)}, d[1] = {mk(0.f, 0.f, 1.f)};
   float tm[1] = {__builtin_inff()};
   bool valid[1] = {live}, anyhit[1] = {false};
-  if (threadIdx.x == 0) S.wstate[blockIdx.x] = make_uint2(base + n0, n0);
+  if (threadIdx.x == 0) S.wstate[blockIdx.x] = make_uint4(base + n0, n0, 0u, 0u);
   if (p < S.N) {
 #pragma unroll
     for (int s = 0; s < NSH; ++s) S.ray[RSTRIDE * ((size_t)(1 + s) * S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
@@ -464,13 +464,14 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
 template <int NSH>
 __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
-  __shared__ uint32_t s_free[4], s_live[4], s_next, s_end;
+  __shared__ uint32_t s_free[4], s_live[4], s_busy[4], s_next, s_end, s_shaded;
   __shared__ int s_skip;
   const int tid = threadIdx.x, wave = tid >> 6;
   if (tid == 0) {
-    const uint2 ws = S.wstate[blockIdx.x];
+    const uint4 ws = S.wstate[blockIdx.x];
     const uint32_t end = range_start(S, blockIdx.x + 1);
     s_next = ws.x;
+    s_shaded = ws.z;
     s_end = end;
     s_skip = ws.y == 0 && ws.x >= end;
   }
@@ -489,10 +490,12 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
   if (p < S.N) state = shade_slot<NSH>(S, p, new_ext, ext, new_sh, shr);
   // ---- regeneration: free slots take the next paths of the range in rank order
   const bool fr = p < S.N && state != SLOT_LIVE;
-  const unsigned long long mf = __ballot(fr), ml = __ballot(p < S.N && state == SLOT_LIVE);
+  const unsigned long long mf = __ballot(fr), ml = __ballot(p < S.N && state == SLOT_LIVE),
+                           mb = __ballot(p < S.N && state != SLOT_FREE);
   if ((tid & 63) == 0) {
     s_free[wave] = (uint32_t)__popcll(mf);
     s_live[wave] = (uint32_t)__popcll(ml);
+    s_busy[wave] = (uint32_t)__popcll(mb);
   }
   __syncthreads();
   const uint32_t next = s_next;
@@ -500,7 +503,8 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
   if (tid == 0) {
     const uint32_t nf = s_free[0] + s_free[1] + s_free[2] + s_free[3];
     const uint32_t take = min(nf, avail);
-    S.wstate[blockIdx.x] = make_uint2(next + take, s_live[0] + s_live[1] + s_live[2] + s_live[3] + take);
+    S.wstate[blockIdx.x] = make_uint4(next + take, s_live[0] + s_live[1] + s_live[2] + s_live[3] + take,
+                                      s_shaded + s_busy[0] + s_busy[1] + s_busy[2] + s_busy[3], 0u);
   }
   if (fr) {
     uint32_t rank = mbcnt64(mf);
@@ -535,18 +539,32 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
   count_rays(S.rcount, n, sh + MAX_ROOT_TARGETS * 8);
 }
 
-// Live slots over all workgroups (the host polls it: 0 = the chunk is done).
-__global__ __launch_bounds__(1024) void k_live_sum(const uint2* __restrict__ wstate, uint32_t G, uint32_t* out) {
-  __shared__ uint32_t part[16];
-  uint32_t v = 0;
-  for (uint32_t b = threadIdx.x; b < G; b += 1024) v += wstate[b].y;
-  v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+// Live slots over all workgroups (the host polls it: 0 = the chunk is done);
+// with stats, also adds the chunk's shaded vertices to stats[STAT_SHADED].
+__global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wstate, uint32_t G, uint32_t* out,
+                                                   unsigned long long* stats) {
+  __shared__ unsigned long long part[2][16];
+  unsigned long long v = 0, sh = 0;
+  for (uint32_t b = threadIdx.x; b < G; b += 1024) {
+    const uint4 w = wstate[b];
+    v += w.y;
+    sh += w.z;
+  }
+  v = wave_sum64(v);
+  sh = wave_sum64(sh);
+  if ((threadIdx.x & 63) == 0) {
+    part[0][threadIdx.x >> 6] = v;
+    part[1][threadIdx.x >> 6] = sh;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < 16; ++w) t += part[w];
-    *out = t;
+    unsigned long long t = 0, u = 0;
+    for (int w = 0; w < 16; ++w) {
+      t += part[0][w];
+      u += part[1][w];
+    }
+    *out = (uint32_t)t;
+    if (stats) atomicAdd(stats + STAT_SHADED, u);
   }
 }
 

@@ -52,7 +52,8 @@ enum {
   STAT_LV0 = 8,     // 16 per-level visit counters
   STAT_LEAF0 = 24,  // 16 per-level leaf-visit counters
   STAT_ITEMS0 = 40, // 16 per-level item counters
-  STAT_COUNT = 56
+  STAT_SHADED = 56, // path vertices shaded by k_shade_push
+  STAT_COUNT = 64
 };
 
 struct TraceArgs {

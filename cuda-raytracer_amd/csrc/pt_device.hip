@@ -80,7 +80,7 @@ struct pt_ctx {
   uint32_t* d_work = nullptr;  // k_path_leaf path counter
   float4* d_res = nullptr;     // per-path radiance of a chunk
   size_t res_cap = 0;
-  uint2* d_wstate = nullptr;   // per shade workgroup {next path, live slots}
+  uint4* d_wstate = nullptr;   // per shade workgroup {next path, live slots, shaded vertices}
   size_t wstate_cap = 0;
   uint32_t* d_live = nullptr;  // live slots after a pass group (k_live_sum)
   uint32_t* h_poll = nullptr;  // pinned: {live, err} x 2 poll slots
@@ -370,6 +370,11 @@ static void collect_marks(pt_ctx* c) {
         c->stats.ms_path += ms;
         c->stats.path_launches++;
         break;
+      case pt_ctx::K_SHADE:
+        c->stats.ms_shade_push += ms;
+        c->stats.shade_launches++;
+        c->stats.ms_shade += ms;
+        break;
       default:
         c->stats.ms_shade += ms;
         break;
@@ -393,6 +398,7 @@ static int read_device_stats(pt_ctx* c) {
   c->stats.visits = st[STAT_V] + R;
   st[STAT_LV0] += R;
   c->stats.peak_queue_entries = st[STAT_PEAKQ];
+  c->stats.shaded = st[STAT_SHADED];
   for (int l = 0; l < 16; ++l) {
     c->stats.level_visits[l] = st[STAT_LV0 + l];
     c->stats.level_leaf_visits[l] = st[STAT_LEAF0 + l];
@@ -698,7 +704,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
           if (nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<1>, grid, dim3(TPB), S);
           if (nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<2>, grid, dim3(TPB), S);
         }
-        hipLaunchKernelGGL(k_live_sum, dim3(1), dim3(1024), 0, c->stream, (const uint2*)S.wstate, G, c->d_live);
+        hipLaunchKernelGGL(k_live_sum, dim3(1), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G, c->d_live,
+                           (unsigned long long*)nullptr);
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1), c->d_live, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1) + 1, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->ev_poll[g & 1], c->stream));
@@ -734,6 +741,9 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         continue;
       }
       if (!finished) return fail(c, PT_E_HIP, "paths did not finish within the pass bound");
+      if (timed)  // shaded vertices of the chunk (stats only)
+        hipLaunchKernelGGL(k_live_sum, dim3(1), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G, c->d_live,
+                           c->d_stats);
     }
     c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_res,
               c->d_accum, npix, spp_c);

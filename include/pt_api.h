@@ -328,6 +328,9 @@ typedef struct pt_stats {
   int32_t batch_paths;
   double ms_path;     /* k_path_leaf: whole paths of single-leaf scenes     */
   uint64_t path_launches;
+  uint64_t shaded;        /* path vertices shaded by k_shade_push             */
+  double ms_shade_push;   /* k_shade_push alone (part of ms_shade)            */
+  uint64_t shade_launches;
 } pt_stats;
 int pt_get_stats(pt_ctx* ctx, pt_stats* out);
 int pt_reset_stats(pt_ctx* ctx);
