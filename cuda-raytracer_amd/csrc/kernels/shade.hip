@@ -540,12 +540,15 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
 }
 
 // Live slots over all workgroups (the host polls it: 0 = the chunk is done);
-// with stats, also adds the chunk's shaded vertices to stats[STAT_SHADED].
-__global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wstate, uint32_t G, uint32_t* out,
-                                                   unsigned long long* stats) {
+// with stats, also the chunk's shaded vertices (stats[STAT_SHADED]).  A grid
+// of LIVE_SUM_BLOCKS workgroups, one atomic each into the zeroed out[0..2]
+// ({live, shaded lo, shaded hi} as one u32 and one u64).
+constexpr int LIVE_SUM_BLOCKS = 64;
+__global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wstate, uint32_t G, uint32_t* live,
+                                                   unsigned long long* shaded) {
   __shared__ unsigned long long part[2][16];
   unsigned long long v = 0, sh = 0;
-  for (uint32_t b = threadIdx.x; b < G; b += 1024) {
+  for (uint32_t b = blockIdx.x * 1024 + threadIdx.x; b < G; b += gridDim.x * 1024) {
     const uint4 w = wstate[b];
     v += w.y;
     sh += w.z;
@@ -563,8 +566,8 @@ __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wst
       t += part[0][w];
       u += part[1][w];
     }
-    *out = (uint32_t)t;
-    if (stats) atomicAdd(stats + STAT_SHADED, u);
+    if (t) atomicAdd(live, (uint32_t)t);
+    if (shaded && u) atomicAdd(shaded, u);
   }
 }
 

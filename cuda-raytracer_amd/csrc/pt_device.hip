@@ -707,8 +707,9 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
           if (nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<1>, grid, dim3(TPB), S);
           if (nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<2>, grid, dim3(TPB), S);
         }
-        hipLaunchKernelGGL(k_live_sum, dim3(1), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G, c->d_live,
-                           (unsigned long long*)nullptr);
+        HIPCHK(c, hipMemsetAsync(c->d_live, 0, 4, c->stream));
+        hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G,
+                           c->d_live, (unsigned long long*)nullptr);
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1), c->d_live, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1) + 1, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->ev_poll[g & 1], c->stream));
@@ -745,8 +746,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       }
       if (!finished) return fail(c, PT_E_HIP, "paths did not finish within the pass bound");
       if (timed)  // shaded vertices of the chunk (stats only)
-        hipLaunchKernelGGL(k_live_sum, dim3(1), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G, c->d_live,
-                           c->d_stats);
+        hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G,
+                           c->d_live, c->d_stats + STAT_SHADED);
     }
     c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_res,
               c->d_accum, npix, spp_c);
