@@ -62,8 +62,11 @@ struct TraceArgs {
   float4* ray;                       // ray records (RSTRIDE float4 each)
   uint32_t* cnt;                     // [node][lane] rays pushed into the node
   uint32_t* qoff;                    // [node][lane] absolute queue offset
-  uint32_t* q;                       // ray-id queues (two parity halves)
+  uint32_t* q;                       // ray-id queues of the root pass's targets (4 B ids)
+  float4* qe;                        // ray-entry queues of the levels below (two parity halves):
+                                     // QESTRIDE float4 per entry, {o, d.x}{d.y, d.z, id, tmax}
 };
+constexpr int QESTRIDE = 2;
 
 __device__ __forceinline__ unsigned long long* rec_key(float4* ray, uint32_t id) {
   return reinterpret_cast<unsigned long long*>(ray + (size_t)RSTRIDE * id + 1) + 1;
@@ -102,6 +105,8 @@ struct LevelArgs {
   uint32_t* nitems_w;
   const uint32_t* mode;  // MODE_WAVE / MODE_BLOCK, chosen by the scan
   uint32_t* mode_w;
+  int ids;      // 1: the level's queues hold ray ids, 0: ray entries
+  int out_ids;  // format of the queues it pushes into (the next level's ids)
 };
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {

@@ -168,6 +168,41 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// ---- queue entries ---------------------------------------------------------------
+// The root pass pushes 4-byte ray ids (its targets' queues are sized for the
+// worst case, every ray in every target).  Below that, queues hold 32-byte ray
+// entries {o, d.x}{d.y, d.z, id, tmax}: a level reads its rays as contiguous
+// entries (full lines) instead of gathering 32-byte records through ids
+// (a 64-128 B memory request each), and pushes copies to the children.  The
+// closest-hit key stays in the ray record (atomicMin through id); an entry's
+// tmax is the ray's tmax when it was pushed (conservative: it only shrinks).
+__device__ __forceinline__ void push_ray(const TraceArgs& A, bool entry, uint32_t e, uint32_t id, const f3 o,
+                                         const f3 d, float tmax) {
+  if (entry) {
+    A.qe[QESTRIDE * (size_t)e] = make_float4(o.x, o.y, o.z, d.x);
+    A.qe[QESTRIDE * (size_t)e + 1] = make_float4(d.y, d.z, __uint_as_float(id), tmax);
+  } else {
+    A.q[e] = id;
+  }
+}
+// Ray e of a level queue: an id (gather from the ray record) or an entry.
+__device__ __forceinline__ void load_ray(const TraceArgs& A, bool ids, uint32_t e, uint32_t& id, f3& o, f3& d,
+                                         float& tmax) {
+  if (ids) {
+    id = A.q[e];
+    const float4 a = A.ray[RSTRIDE * id], b = A.ray[RSTRIDE * id + 1];
+    o = mk(a.x, a.y, a.z);
+    d = mk(a.w, b.x, b.y);
+    tmax = b.w;
+  } else {
+    const float4 a = A.qe[QESTRIDE * (size_t)e], b = A.qe[QESTRIDE * (size_t)e + 1];
+    o = mk(a.x, a.y, a.z);
+    d = mk(a.w, b.x, b.y);
+    id = __float_as_uint(b.z);
+    tmax = b.w;
+  }
+}
+
 // ---- push targets ------------------------------------------------------------
 // A node's 4 children (level passes), or the root table's targets (root pass).
 struct ChildTargets {
@@ -198,7 +233,7 @@ struct TableTargets {
 template <int R, int NC, class Tg>
 __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, int lane, const uint32_t (&id)[R],
                                               const f3 (&o)[R], const f3 (&d)[R], const float (&tmax)[R],
-                                              const bool (&valid)[R], int nj, uint32_t* sh) {
+                                              const bool (&valid)[R], int nj, uint32_t* sh, bool entry) {
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int nt = tg.count();
@@ -258,7 +293,7 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
     for (int j = 0; j < R; ++j) {
       const bool h = (bits[j] >> c) & 1u;
       const unsigned long long m = __ballot(h);
-      if (h) A.q[off + mbcnt64(m)] = id[j];
+      if (h) push_ray(A, entry, off + mbcnt64(m), id[j], o[j], d[j], tmax[j]);
       off += (uint32_t)__popcll(m);
     }
   }
@@ -314,12 +349,12 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
     tm[j] = bt;
     pv[j] = valid[j] && !(anyhit[j] && bp >= 0);
   }
-  push_children<R, MAX_ROOT_TARGETS>(A, TableTargets{T}, lane, id, o, d, tm, pv, R, sh);
+  push_children<R, MAX_ROOT_TARGETS>(A, TableTargets{T}, lane, id, o, d, tm, pv, R, sh, false);
 }
 
 template <bool IMPLICIT>
 __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, uint32_t base, int n, int lane,
-                                             uint32_t* sh) {
+                                             uint32_t* sh, bool ids = true, bool out_ids = true) {
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   // node and primitive records are wave-uniform: read them through the
@@ -339,14 +374,18 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
     o[j] = mk(0.f, 0.f, 0.f);
     d[j] = mk(0.f, 0.f, 1.f);
     if (valid[j]) {
-      id[j] = IMPLICIT ? base + (uint32_t)i : A.q[base + i];
-      const float4 b = A.ray[RSTRIDE * id[j] + 1];
-      tmax[j] = b.w;
-      if (IMPLICIT) valid[j] = b.w >= 0.0f;
-      if (valid[j]) {
-        const float4 a = A.ray[RSTRIDE * id[j]];
-        o[j] = mk(a.x, a.y, a.z);
-        d[j] = mk(a.w, b.x, b.y);
+      if (IMPLICIT) {
+        id[j] = base + (uint32_t)i;
+        const float4 b = A.ray[RSTRIDE * id[j] + 1];
+        tmax[j] = b.w;
+        valid[j] = b.w >= 0.0f;
+        if (valid[j]) {
+          const float4 a = A.ray[RSTRIDE * id[j]];
+          o[j] = mk(a.x, a.y, a.z);
+          d[j] = mk(a.w, b.x, b.y);
+        }
+      } else {
+        load_ray(A, ids, base + (uint32_t)i, id[j], o[j], d[j], tmax[j]);
       }
     }
   }
@@ -416,7 +455,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
   }
 
   // ---------------- interior: NC child boxes, compaction, push ----------------
-  push_children<RPT, 4>(A, ChildTargets{nd}, lane, id, o, d, tmax, valid, nj, sh);
+  push_children<RPT, 4>(A, ChildTargets{nd}, lane, id, o, d, tmax, valid, nj, sh, !out_ids);
   return nvalid;
 }
 
@@ -478,7 +517,8 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, ui
 // Levels >= 1 are processed at wave granularity: no LDS, no workgroup barrier,
 // one returning atomic per wave per child.  Deep levels hold many nodes with a
 // few hundred rays each, where 1024-ray workgroup items would run mostly empty.
-__device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane) {
+__device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane, bool ids,
+                                             bool out_ids) {
   const uint32_t lid = lane_id();
   const CPTR(pt_node) nd = (const CPTR(pt_node))(A.nodes + node);
   uint32_t id[RPTW];
@@ -489,18 +529,11 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
   for (int j = 0; j < RPTW; ++j) {
     const int i = j * 64 + (int)lid;
     valid[j] = i < n;
-    id[j] = valid[j] ? A.q[base + i] : 0u;
-  }
-#pragma unroll
-  for (int j = 0; j < RPTW; ++j) {
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = make_float4(1.f, 0.f, 0.f, -1.f);
-    if (valid[j]) {
-      a = A.ray[RSTRIDE * id[j]];
-      b = A.ray[RSTRIDE * id[j] + 1];
-    }
-    o[j] = mk(a.x, a.y, a.z);
-    tmax[j] = b.w;
-    d[j] = mk(a.w, b.x, b.y);
+    id[j] = 0u;
+    o[j] = mk(0.f, 0.f, 0.f);
+    d[j] = mk(1.f, 0.f, 0.f);
+    tmax[j] = -1.0f;
+    if (valid[j]) load_ray(A, ids, base + (uint32_t)i, id[j], o[j], d[j], tmax[j]);
   }
   const int nj = (n + 63) >> 6;  // ray groups with at least one valid lane (uniform)
   const int pcount = nd->prim_count;
@@ -575,26 +608,33 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     }
     bits[j] = b;
   }
+  // per-child totals, then the (up to) four slot reservations at once, one per
+  // lane 0..3: a single atomic round trip per item instead of four in a row
+  uint32_t tot[4], qo[4];
+  int child[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    const int child = nd->child[c];
-    if (child < 0) continue;
-    unsigned long long m[RPTW];
-    uint32_t tot = 0;
+    child[c] = nd->child[c];
+    tot[c] = 0;
+#pragma unroll
+    for (int j = 0; j < RPTW; ++j) tot[c] += (uint32_t)__popcll(__ballot((bits[j] >> c) & 1u));
+    qo[c] = (child[c] >= 0 && tot[c]) ? A.qoff[(size_t)child[c] * NLANE + lane] : 0u;
+  }
+  uint32_t b = 0;
+  const int lc = (int)lid;
+  const int mych = lc == 0 ? child[0] : lc == 1 ? child[1] : lc == 2 ? child[2] : child[3];
+  const uint32_t myt = lc == 0 ? tot[0] : lc == 1 ? tot[1] : lc == 2 ? tot[2] : tot[3];
+  if (lc < 4 && mych >= 0 && myt) b = atomicAdd(A.cnt + cnt_idx(mych, lane), myt);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (child[c] < 0 || tot[c] == 0) continue;
+    uint32_t off = __builtin_amdgcn_readlane(b, c) + qo[c];
 #pragma unroll
     for (int j = 0; j < RPTW; ++j) {
-      m[j] = __ballot((bits[j] >> c) & 1u);
-      tot += (uint32_t)__popcll(m[j]);
-    }
-    if (tot == 0) continue;
-    uint32_t b = 0;
-    if (lid == 0) b = atomicAdd(A.cnt + cnt_idx(child, lane), tot);
-    b = __builtin_amdgcn_readfirstlane(b);
-    uint32_t off = b + A.qoff[(size_t)child * NLANE + lane];
-#pragma unroll
-    for (int j = 0; j < RPTW; ++j) {
-      if ((bits[j] >> c) & 1u) A.q[off + mbcnt64(m[j])] = id[j];
-      off += (uint32_t)__popcll(m[j]);
+      const bool h = (bits[j] >> c) & 1u;
+      const unsigned long long m = __ballot(h);
+      if (h) push_ray(A, !out_ids, off + mbcnt64(m), id[j], o[j], d[j], tmax[j]);
+      off += (uint32_t)__popcll(m);
     }
   }
 }
@@ -644,7 +684,7 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
       const uint32_t base = __builtin_amdgcn_readfirstlane(s_base);
       const int n = __builtin_amdgcn_readfirstlane(s_n);
       __syncthreads();
-      process_item<false>(A, node, base, n, lane, sh);
+      process_item<false>(A, node, base, n, lane, sh, L.ids != 0, L.out_ids != 0);
       __syncthreads();
     }
     return;
@@ -668,7 +708,8 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
     const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
     const uint32_t base = A.qoff[(size_t)node * NLANE + lane] + i * WTILE;
     const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
-    process_wave(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane);
+    process_wave(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane,
+                 L.ids != 0, L.out_ids != 0);
   }
 }
 

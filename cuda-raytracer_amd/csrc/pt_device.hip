@@ -63,12 +63,15 @@ struct pt_ctx {
   // wavefront buffers (sized for N paths = 2N ray slots)
   uint32_t cap_paths = 0;  // paths the buffers hold
   uint32_t cap_spp = 0;    // ray slots per path they hold (2, or 3 under the reference schedule)
-  size_t qfactor = 24;     // queue entries per ray slot and parity half (doubles on overflow)
+  size_t qfactor = 4;      // ray entries per ray slot and parity half (doubles on overflow)
   size_t cap_qfactor = 0;
   float4* d_ray = nullptr;  // 2N ray records (trace.h), RSTRIDE float4 each
   float4 *d_ps0 = nullptr, *d_ps1 = nullptr, *d_ps2 = nullptr, *d_ps3 = nullptr;
-  uint32_t* d_q = nullptr;
-  size_t qcap = 0;  // entries per parity half
+  uint32_t* d_q = nullptr;   // ray-id queues (two parity halves): the root's targets and the levels above entry_level
+  size_t qcap = 0;           // ids per parity half
+  int entry_level = 0;       // first level whose queues hold ray entries (build_root_table)
+  float4* d_qe = nullptr;    // ray-entry queues of the levels below the root's targets
+  size_t qecap = 0;          // entries per parity half
   uint32_t* d_cnt = nullptr;
   uint32_t* d_qoff = nullptr;
   uint32_t* d_iprefix = nullptr;
@@ -158,7 +161,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ray,
-                  c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,      c->d_cnt,
+                  c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live,
                   c->d_pix_of, c->d_accum};
   for (void* p : ptrs)
@@ -180,8 +183,22 @@ static constexpr uint32_t DEFAULT_BATCH_PATHS = 36u << 20;
 // are queued between two reads of the finished-path count
 static constexpr uint32_t CHUNK_PATHS = 1u << 28;
 static constexpr int POLL_GROUP = 4;
+// ray-id queues hold ID_FACTOR x qfactor ids per ray slot and parity half
+// (the entry queues qfactor entries of 32 B)
+static constexpr size_t ID_FACTOR = 6;
+// Ray entries below the root targets' level measured -3 % on CBbunny and
+// +1.5-4 % on the dragon proxy trees (the leaf-heavy levels are bound by the
+// leaf loop and the closest-hit atomics, not by the ray gathers): off by default.
+#ifndef PT_ENTRY_LEVEL_DEFAULT
+#define PT_ENTRY_LEVEL_DEFAULT 0
+#endif
+static constexpr int ENTRY_LEVEL_DEFAULT = PT_ENTRY_LEVEL_DEFAULT;
 static uint32_t max_batch_paths(const pt_ctx* c, uint32_t slots_per_path) {
-  return (uint32_t)((1ull << 32) / (2 * c->qfactor * slots_per_path)) & ~4095u;
+  // u32 entry offsets: both halves of the entry queues, and the root's id
+  // queues (<= 16 targets x every ray, see root_per_lane)
+  const uint64_t a = (1ull << 32) / (2 * ID_FACTOR * c->qfactor * slots_per_path);
+  const uint64_t b = (1ull << 32) / (20ull * slots_per_path);
+  return (uint32_t)std::min<uint64_t>(std::min(a, b), 0xFFFFFFFFull) & ~4095u;
 }
 
 // Per-lane capacity of each root target queue for N paths with spp ray slots
@@ -206,15 +223,22 @@ static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
   if ((rc = dalloc(c, &c->d_ps1, N))) return rc;
   if ((rc = dalloc(c, &c->d_ps2, N))) return rc;
   if (spp > 2 && (rc = dalloc(c, &c->d_ps3, N))) return rc;
-  // every root target needs root_per_lane slots per lane (<= 16 targets, see
-  // set_root_child_offsets); deeper levels need at most 4x the visits of the
-  // level above, which qfactor covers for the scenes measured (peak_queue_entries)
-  const size_t root_need = (size_t)NLANE * 16 * root_per_lane(N, spp);
+  // every root target needs root_per_lane ids per lane (see
+  // set_root_child_offsets); the levels below get ray entries: a level needs at
+  // most 4x the visits of the level above (the scan's allocation), which
+  // qfactor entries per ray slot cover for the scenes measured
+  // (peak_queue_entries; an overflowing level re-runs the chunk with 2x)
+  const size_t root_need = (size_t)NLANE * std::max(1, c->rt.nt) * root_per_lane(N, spp);
   // a single-leaf tree queues nothing (k_path_leaf / the root pass only)
-  c->qcap = c->root_leaf ? NLANE * 64 : std::max(c->qfactor * slots, root_need);
+  c->qcap = c->root_leaf ? NLANE * 64 : std::max(root_need, ID_FACTOR * c->qfactor * slots);
   c->qcap = (c->qcap + NLANE * 64 - 1) / (NLANE * 64) * (NLANE * 64);
-  if (2 * c->qcap >= (1ull << 32)) return fail(c, PT_E_UNSUPPORTED, "batch too large for u32 queue offsets");
+  const bool entries = !c->root_leaf && c->entry_level < c->n_levels;
+  c->qecap = entries ? c->qfactor * slots : NLANE * 64;
+  c->qecap = (c->qecap + NLANE * 64 - 1) / (NLANE * 64) * (NLANE * 64);
+  if (2 * c->qcap >= (1ull << 32) || 2 * c->qecap >= (1ull << 32))
+    return fail(c, PT_E_UNSUPPORTED, "batch too large for u32 queue offsets");
   if ((rc = dalloc(c, &c->d_q, 2 * c->qcap))) return rc;
+  if ((rc = dalloc(c, &c->d_qe, 2 * c->qecap * QESTRIDE))) return rc;
   c->cap_paths = N;
   c->cap_spp = spp;
   c->cap_qfactor = c->qfactor;
@@ -266,20 +290,23 @@ static void build_root_table(pt_ctx* c) {
       if (nd[ch].child[g] >= 0 && !try_inline(ch, g)) add_target(ch, g);
   }
   c->skip_l1 = skip;
+  // ray entries from PT_ENTRY_LEVEL levels below the root's targets on (0: ids only)
+  const char* el = getenv("PT_ENTRY_LEVEL");
+  const int eoff = el ? atoi(el) : ENTRY_LEVEL_DEFAULT;
+  c->entry_level = eoff > 0 ? (skip ? 2 : 1) + eoff : 1 << 20;
 }
 
-// Queue offsets of the root's targets: each gets root_per_lane slots in every
-// lane of the half its level uses (level 1: odd half, level 2: even half).
+// Queue offsets of the root's targets: each gets root_per_lane ids in every
+// lane of the id queue.
 static int set_root_child_offsets(pt_ctx* c) {
   if (c->root_leaf) return PT_OK;
   const size_t per_lane = root_per_lane(c->cap_paths, c->cap_spp);
   const size_t lanecap = c->qcap / NLANE;
   const pt_node& root = c->nodes_host[0];
-  // targets: nodes of level 1 (odd half) or, when level 1 is skipped, of
-  // level 2 (even half)
+  // targets: nodes of level 1 or, when level 1 is skipped, of level 2
   std::vector<int> targets(c->rt.tnode, c->rt.tnode + c->rt.nt);
   if (targets.size() * per_lane > lanecap) return fail(c, PT_E_OVERFLOW, "root queue capacity");
-  const size_t half = c->skip_l1 ? 0 : c->qcap;
+  const size_t half = c->skip_l1 ? 0 : c->qcap;  // the parity half of their level
   // ordered on the context's (non-blocking) stream behind any work in flight
   std::vector<uint32_t> off(targets.size() * NLANE);
   for (size_t jj = 0; jj < targets.size(); ++jj)
@@ -299,6 +326,7 @@ static TraceArgs trace_args(pt_ctx* c) {
   A.cnt = c->d_cnt;
   A.qoff = c->d_qoff;
   A.q = c->d_q;
+  A.qe = c->d_qe;
   return A;
 }
 
@@ -307,8 +335,8 @@ static TraceArgs trace_args(pt_ctx* c) {
 // or fused into k_camera_push / k_shade_push).
 static int trace_levels(pt_ctx* c) {
   TraceArgs A = trace_args(c);
-  const size_t lanecap = c->qcap / NLANE;
-  for (int l = c->skip_l1 ? 2 : 1; l < c->n_levels; ++l) {
+  const int l0 = c->skip_l1 ? 2 : 1;  // the root targets' level: its queues hold ids
+  for (int l = l0; l < c->n_levels; ++l) {
     LevelArgs L;
     L.first = c->level_start[l];
     L.nl = c->level_start[l + 1] - c->level_start[l];
@@ -321,7 +349,11 @@ static int trace_levels(pt_ctx* c) {
     L.nitems_w = c->d_nitems + l;
     L.mode = c->d_nitems + c->n_levels + l;
     L.mode_w = c->d_nitems + c->n_levels + l;
-    const uint32_t out_base = (uint32_t)(((l + 1) & 1) ? c->qcap : 0);
+    // levels above entry_level take ray ids, the others ray entries
+    L.ids = l < c->entry_level;
+    L.out_ids = l + 1 < c->entry_level;
+    const size_t lanecap = (L.out_ids ? c->qcap : c->qecap) / NLANE;
+    const uint32_t out_base = (uint32_t)(((l + 1) & 1) ? (L.out_ids ? c->qcap : c->qecap) : 0);
     c->launch(pt_ctx::K_SCAN, l, k_scan_level, dim3(1), dim3(1024), A, L, (uint32_t)lanecap, out_base,
               c->d_stats, l, c->d_err);
     c->launch(pt_ctx::K_LEVEL, l, k_trace_level, dim3(LEVEL_GRID), dim3(TPB), A, L);
@@ -868,7 +900,7 @@ int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) {
     }
     if (!e) break;
     // a level overflowed its queue: twice the queue factor, trace again
-    if (2 * (2 * c->qfactor) * 2 * (size_t)N >= (1ull << 32)) {
+    if (2 * ID_FACTOR * (2 * c->qfactor) * 2 * (size_t)N >= (1ull << 32)) {
       hipFree(d_in);
       return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded");
     }
