@@ -372,17 +372,14 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
     S.ps0[p] = make_float4(st.T.x, st.T.y, st.T.z, __uint_as_float(st.flags));
     S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(P));
   }
-  // new rays: r0 here, r1 (with the key of the inline leaves) in root_pass
-  if (new_ext)
-    S.ray[RSTRIDE * p] = make_float4(ext.o.x, ext.o.y, ext.o.z, ext.d.x);
-  else
-    S.ray[RSTRIDE * p + 1] = rec_r1(0.f, 0.f, -1.0f);
+  // new rays: their records are written by root_pass (with the key of the
+  // inline leaves); empty slots get an empty r1 here
+  if (!new_ext) S.ray[RSTRIDE * p + 1] = rec_r1(0.f, 0.f, -1.0f);
 #pragma unroll
   for (int s = 0; s < NSH; ++s) {
     const size_t slot = (size_t)(1 + s) * S.N + p;
     if (new_sh[s]) {
       (s ? S.ps3 : S.ps2)[p] = make_float4(C[s].x, C[s].y, C[s].z, 0.0f);
-      S.ray[RSTRIDE * slot] = make_float4(shr[s].o.x, shr[s].o.y, shr[s].o.z, shr[s].d.x);
     } else {
       S.ray[RSTRIDE * slot + 1] = rec_r1(0.f, 0.f, -1.0f);
     }
@@ -394,7 +391,7 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
 __device__ __forceinline__ f3 start_path(const ShadeArgs& S, uint32_t p, uint32_t P) {
   uint32_t g;
   const f3 d = camera_dir(S, P, g);
-  S.ray[RSTRIDE * p] = make_float4(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], d.x);  // r1: root_pass
+  // (the ray record is written by root_pass)
   S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
   S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
   return d;

@@ -303,8 +303,8 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 //  1. the inline leaves of the root table, when the ray enters their box:
 //     closest hit with the leaf rules of process_item (ties to the lowest
 //     primitive) -- it becomes the ray's initial key {prim, t} and its tmax;
-//  2. the record word r1 = {d.y, d.z, prim, t} of every valid ray is written
-//     here (the callers write r0 and the empty r1 of invalid slots);
+//  2. the record {o, d.x}{d.y, d.z, prim, t} of every valid ray is written
+//     here (the callers write the empty r1 of invalid slots);
 //  3. a shadow ray (anyhit) occluded by an inline leaf is done: not queued;
 //     the others are pushed into the targets' queues with the tightened tmax.
 template <int R>
@@ -343,9 +343,11 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
         }
       }
     }
-    if (valid[j])
+    if (valid[j]) {  // the whole 32-B record at once (one full half line per ray)
+      A.ray[RSTRIDE * id[j]] = make_float4(o[j].x, o[j].y, o[j].z, d[j].x);
       A.ray[RSTRIDE * id[j] + 1] =
           make_float4(d[j].y, d[j].z, __uint_as_float(bp >= 0 ? (uint32_t)bp : PT_PRIM_NONE), bt);
+    }
     tm[j] = bt;
     pv[j] = valid[j] && !(anyhit[j] && bp >= 0);
   }

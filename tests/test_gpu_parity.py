@@ -56,6 +56,27 @@ def test_level_skip_off_matches(gpu_ctx, name, monkeypatch):
     assert np.array_equal(g_skip, pyoracle.intersect(d, rays, use_bvh=True))
 
 
+@pytest.mark.parametrize("env", [("PT_ENTRY_LEVEL", "1"), ("PT_ENTRY_LEVEL", "2"), ("PT_INLINE_MAX", "0")])
+def test_schedule_options_match(gpu_ctx, env, monkeypatch):
+    """Ray-entry queues below the root targets (PT_ENTRY_LEVEL) and the root
+    pass without inline leaves (PT_INLINE_MAX=0) give the same closest hits and
+    the same image as the default schedule."""
+    sc = load_fixture("CBbunny")
+    d = sc.desc()
+    rays = np.concatenate([camera_rays(d, 20000, seed=27), interior_rays(d, 20000, seed=28)])
+    monkeypatch.setenv(*env)
+    gpu_ctx.load_scene(sc)
+    g = gpu_ctx.intersect(rays)
+    gpu_ctx.clear()
+    gpu_ctx.render(32, 32, 2, max_bounces=6, seed=15618)
+    img = gpu_ctx.get_image()
+    monkeypatch.delenv(env[0])
+    gpu_ctx.load_scene(sc)
+    assert np.array_equal(g, pyoracle.intersect(d, rays, use_bvh=True))
+    o, _ = pyoracle.image(d, 32, 32, 2, max_bounces=6, seed=15618)
+    assert np.array_equal(img, o)
+
+
 def test_tie_break_lowest_prim(gpu_ctx):
     # two identical triangles: every hit must report the lower sorted index
     tri = np.array([[-1, -1, 0, 1, -1, 0, 0, 1, 0]] * 2, np.float32)
