@@ -24,6 +24,7 @@ constexpr uint32_t F_SHADOW2 = 8u; // second shadow ray pending in slot 2N + p (
 __device__ __forceinline__ uint32_t sh_bit(int s) { return s ? F_SHADOW2 : F_SHADOW; }
 constexpr float INV_PI = 0.318309886183790671f;
 constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
+constexpr int SHADE_REC = 5;  // float4 per hit-shading record (ShadeArgs::shade)
 
 struct ShadeArgs {
   float4* ray;  // ray records (trace.h): ext ray of path p in slot p, shadow ray s in slot (1+s)N + p
@@ -32,7 +33,11 @@ struct ShadeArgs {
   float4* ps2;  // pending shadow contribution
   float4* ps3;  // pending contribution of the second shadow ray (PT_FLAG_REF_SCHEDULE)
   const float4* __restrict__ prims;
-  const pt_prim_shading* __restrict__ shading;
+  // per-primitive hit-shading record, 5 float4 (80 B, two 64-B sectors):
+  // {A, meta}{B, n0.x}{C, n0.y}{n0.z, n1}{n2, 0} -- vertices and vertex
+  // normals of a triangle (a sphere: {centre, meta}), built by pt_load_scene
+  // from pt_prim + pt_prim_shading so a hit gathers 80 B instead of 96
+  const float4* __restrict__ shade;
   const pt_bsdf* __restrict__ bsdfs;
   const uint32_t* __restrict__ pix_of;
   pt_light light;
@@ -173,7 +178,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
   if (flags & F_EXT) {
     if (prim != PT_PRIM_NONE) {
       const f3 P = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
-      const float4* Q = S.prims + (size_t)prim * 6;
+      const float4* Q = S.shade + (size_t)prim * SHADE_REC;
       const float4 q0 = Q[0];
       const uint32_t meta = __float_as_uint(q0.w);
       f3 ns;
@@ -181,13 +186,13 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
         ns = normalize(mk(P.x - q0.x, P.y - q0.y, P.z - q0.z));
       } else {
         // barycentric shading normal (cu:1213-1221)
-        const f3 A = xyz(q0), B = xyz(Q[1]), Cv = xyz(Q[2]);
-        const pt_prim_shading sh = S.shading[prim];
+        const float4 q1 = Q[1], q2 = Q[2], q3 = Q[3], q4 = Q[4];
+        const f3 A = xyz(q0), B = xyz(q1), Cv = xyz(q2);
         float total = length(cross(A - B, B - Cv));
         float bC = length(cross(A - P, B - P)) / total;
         float bA = length(cross(B - P, Cv - P)) / total;
         float bB = length(cross(Cv - P, A - P)) / total;
-        f3 n0 = ld3(sh.n0), n1 = ld3(sh.n1), n2 = ld3(sh.n2);
+        f3 n0 = mk(q1.w, q2.w, q3.x), n1 = mk(q3.y, q3.z, q3.w), n2 = mk(q4.x, q4.y, q4.z);
         ns = normalize(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y,
                           bA * n0.z + bB * n1.z + bC * n2.z));
       }

@@ -334,7 +334,15 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
           float tt;
           if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE)
             tt = sphere_test(o[j], d[j], q0, q1);
-          else
+          else if (anyhit[j]) {
+            // shadow rays: division-free pre-test (they mostly point away from
+            // the walls or end before them, see tri_outside)
+            const float4 q3 = f4(P[3]);
+            const float ndd = fdot(q3.x, q3.y, q3.z, d[j].x, d[j].y, d[j].z);
+            const float num = q1.w - fdot(q3.x, q3.y, q3.z, o[j].x, o[j].y, o[j].z);
+            tt = -1.0f;
+            if (!tri_outside(ndd, num, bt)) tt = tri_test(o[j], d[j], q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), bt);
+          } else
             tt = tri_test(o[j], d[j], q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), bt);
           if (tt >= 0.0f && (tt < bt || (tt == bt && bp < 0))) {
             bt = tt;

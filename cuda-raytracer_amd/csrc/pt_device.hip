@@ -57,7 +57,7 @@ struct pt_ctx {
   pt_camera camera{};
   pt_node* d_nodes = nullptr;
   float4* d_prims = nullptr;
-  pt_prim_shading* d_shading = nullptr;
+  float4* d_shade = nullptr;  // hit-shading records (SHADE_REC float4 per primitive)
   pt_bsdf* d_bsdfs = nullptr;
 
   // wavefront buffers (sized for N paths = 2N ray slots)
@@ -160,7 +160,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 }
 
 static void free_all(pt_ctx* c) {
-  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shading, c->d_bsdfs,   c->d_ray,
+  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shade, c->d_bsdfs,   c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live,
                   c->d_pix_of, c->d_accum};
@@ -552,7 +552,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   build_root_table(c);
   if ((rc = dalloc(c, &c->d_nodes, s->n_nodes))) return rc;
   if ((rc = dalloc(c, &c->d_prims, (size_t)s->n_prims * 6))) return rc;
-  if ((rc = dalloc(c, &c->d_shading, s->n_prims))) return rc;
+  if ((rc = dalloc(c, &c->d_shade, (size_t)s->n_prims * SHADE_REC))) return rc;
   if ((rc = dalloc(c, &c->d_bsdfs, std::max(1, s->n_bsdfs)))) return rc;
   if ((rc = dalloc(c, &c->d_cnt, (size_t)s->n_nodes * NLANE * CSTRIDE))) return rc;
   if ((rc = dalloc(c, &c->d_qoff, (size_t)s->n_nodes * NLANE))) return rc;
@@ -561,7 +561,21 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   if ((rc = dalloc(c, &c->d_nitems, 2 * std::max(1, s->n_levels) + NLANE))) return rc;
   HIPCHK(c, hipMemcpy(c->d_nodes, s->nodes, sizeof(pt_node) * s->n_nodes, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_prims, s->prims, sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->d_shading, s->shading, sizeof(pt_prim_shading) * s->n_prims, hipMemcpyHostToDevice));
+  {
+    // {A, meta}{B, n0.x}{C, n0.y}{n0.z, n1}{n2, 0} (shade.hip ShadeArgs::shade)
+    std::vector<float4> rec((size_t)s->n_prims * SHADE_REC);
+    for (int i = 0; i < s->n_prims; ++i) {
+      const float* q = s->prims[i].q;
+      const float *n0 = s->shading[i].n0, *n1 = s->shading[i].n1, *n2 = s->shading[i].n2;
+      float4* r = &rec[(size_t)i * SHADE_REC];
+      r[0] = make_float4(q[0], q[1], q[2], q[3]);
+      r[1] = make_float4(q[4], q[5], q[6], n0[0]);
+      r[2] = make_float4(q[8], q[9], q[10], n0[1]);
+      r[3] = make_float4(n0[2], n1[0], n1[1], n1[2]);
+      r[4] = make_float4(n2[0], n2[1], n2[2], 0.0f);
+    }
+    HIPCHK(c, hipMemcpy(c->d_shade, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice));
+  }
   if (s->n_bsdfs > 0)
     HIPCHK(c, hipMemcpy(c->d_bsdfs, s->bsdfs, sizeof(pt_bsdf) * s->n_bsdfs, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemset(c->d_cnt, 0, (size_t)s->n_nodes * NLANE * CSTRIDE * 4));
@@ -665,7 +679,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     }
     ShadeArgs S;
     S.prims = c->d_prims;
-    S.shading = c->d_shading;
+    S.shade = c->d_shade;
     S.bsdfs = c->d_bsdfs;
     S.pix_of = c->d_pix_of;
     S.light = c->light;
