@@ -641,10 +641,12 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
 #endif
 constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 
+// 7 waves per SIMD (72 VGPRs, ~20 spilled around the shading code): +2.3 %
+// over 6 waves (80 VGPRs, no spills) on CBempty and CBspheres; 8 waves (64
+// VGPRs, ~60 spilled) lose 10 %
 #ifndef PT_PATH_WAVES
-#define PT_PATH_WAVES 6
+#define PT_PATH_WAVES 7
 #endif
-// PT_PATH_WAVES waves per SIMD (6: <= 80 VGPRs)
 template <int NSH>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
