@@ -53,9 +53,11 @@ struct ShadeArgs {
   // writes res[P] and starts the next unstarted path
   float4* res;        // per-path radiance of the chunk
   uint32_t M;         // paths in the chunk
-  // workgroup b runs the paths [range_start(b), range_start(b + 1)): a share of
-  // the chunk proportional to its slots (the last workgroup may be partial)
-  uint4* wstate;      // per workgroup: {next unstarted path, live slots after its last pass, vertices shaded, 0}
+  // paths are handed out in blocks of POOL_BLOCK consecutive paths (one sample
+  // of 256 owned pixels): block c comes from dispenser c % POOLS
+  uint4* wstate;      // per workgroup: {next, end} of its current block, live slots after its last pass,
+                      // vertices shaded
+  uint32_t* pool;     // POOLS dispensers, CSTRIDE apart (block counters)
   int passes;         // vertices per path at most (max_bounces + 2)
   unsigned long long* rcount;    // rays entering the traversal (RCOUNT_SLOTS counters)
 };
@@ -413,29 +415,49 @@ __device__ __forceinline__ void count_rays(unsigned long long* rcount, uint32_t 
   }
 }
 
-__device__ __forceinline__ uint32_t range_start(const ShadeArgs& S, uint32_t b) {
-  const uint64_t first_slot = (uint64_t)b * TPB;
-  return first_slot >= S.N ? S.M : (uint32_t)(((uint64_t)S.M * first_slot) / S.N);
+// ---- path blocks -------------------------------------------------------------
+// Block c = paths [POOL_BLOCK c, min(POOL_BLOCK (c + 1), M)); dispenser s hands
+// out blocks s, s + POOLS, s + 2 POOLS, ... (its counter v -> block s + POOLS v).
+// The first fill gives workgroup b block b; afterwards a workgroup takes one new
+// block whenever its current one cannot fill its free slots (one atomic per
+// POOL_BLOCK paths, spread over POOLS counters), so every workgroup keeps its
+// slots busy until the whole chunk is handed out: no workgroup runs out of
+// paths early while others still hold many (a static split of the chunk by
+// pixel region leaves a long tail: regions differ in mean path length).
+constexpr uint32_t POOL_BLOCK = TPB, POOLS = 64;
+__device__ __forceinline__ uint32_t pool_limit(uint32_t nblocks, uint32_t s) {
+  return nblocks > s ? (nblocks - s + POOLS - 1) / POOLS : 0u;
+}
+// Wave 0 of a workgroup: claim one block, trying dispenser (b + k) % POOLS in
+// order among those not yet exhausted (all 64 peeked at once, one lane each).
+// Returns the block index, or -1 when every dispenser is exhausted (or lost
+// the race for its last block).
+__device__ __forceinline__ int claim_block(const ShadeArgs& S, uint32_t nblocks) {
+  const uint32_t ln = lane_id();
+  const uint32_t sd = (blockIdx.x + ln) & (POOLS - 1);
+  const bool open =
+      __hip_atomic_load(S.pool + (size_t)sd * CSTRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+      pool_limit(nblocks, sd);
+  const unsigned long long mo = __ballot(open);
+  if (!mo) return -1;
+  const uint32_t k = (uint32_t)__builtin_ctzll(mo);
+  int c = -1;
+  if (ln == k) {
+    const uint32_t v = atomicAdd(S.pool + (size_t)sd * CSTRIDE, 1u);
+    if (v < pool_limit(nblocks, sd)) c = (int)(sd + POOLS * v);
+  }
+  return __builtin_amdgcn_readlane(c, k);
 }
 
 // Fused root pass: the new rays never take the trip through HBM and back to
 // be tested against the root -- the producing kernel tests them against the
-// root's NC target boxes (4 children, or 16 grandchildren when level 1 is
-// skipped) and pushes their ids into those queues (lane = workgroup & 7).
-//
-// Path regeneration without atomics: workgroup b owns a contiguous path range
-// of the chunk (consecutive pixels of one sample, range_start) and the same
-// 256 slots in every pass; it alone reads and writes its
-// wstate word, so starting paths needs no shared counter.
-// First fill: slot i of workgroup b starts path range_start(b) + i.
+// root's targets and pushes their ids into those queues (lane = workgroup & 7).
+// First fill: workgroup b runs block b, slot i its path i.
 template <int NSH>
 __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
-  __shared__ uint32_t s_rng[2];
-  if (threadIdx.x < 2) s_rng[threadIdx.x] = range_start(S, blockIdx.x + threadIdx.x);
-  __syncthreads();
   const uint32_t p = blockIdx.x * TPB + threadIdx.x;
-  const uint32_t base = s_rng[0], end = s_rng[1];
+  const uint32_t base = blockIdx.x * POOL_BLOCK, end = min(S.M, base + POOL_BLOCK);
   const uint32_t slots = min((uint32_t)TPB, S.N - blockIdx.x * TPB);  // (the last workgroup may be partial)
   const uint32_t n0 = end > base ? min(slots, end - base) : 0u;
   const bool live = threadIdx.x < n0;
@@ -443,7 +465,7 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
   f3 o[1] = {ld3(S.cam.origin)}, d[1] = {mk(0.f, 0.f, 1.f)};
   float tm[1] = {__builtin_inff()};
   bool valid[1] = {live}, anyhit[1] = {false};
-  if (threadIdx.x == 0) S.wstate[blockIdx.x] = make_uint4(base + n0, n0, 0u, 0u);
+  if (threadIdx.x == 0) S.wstate[blockIdx.x] = make_uint4(base + n0, end, n0, 0u);
   if (p < S.N) {
 #pragma unroll
     for (int s = 0; s < NSH; ++s) S.ray[RSTRIDE * ((size_t)(1 + s) * S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
@@ -460,26 +482,37 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
 
 // One pass of shading with path regeneration: shade every live slot, then the
 // free slots (free before, or their path just ended) start the next paths of
-// the workgroup's range, and all new rays (extension, shadow, camera) are
-// pushed into the root's target queues.  A workgroup with no live slot and an
-// exhausted range returns at once (passes queued after the chunk ended).
+// the workgroup's block (and of a newly claimed block when it runs short), and
+// all new rays (extension, shadow, camera) are pushed into the root's target
+// queues.  A workgroup with no live slot and nothing left to start returns at
+// once (passes queued after the chunk ended).
 template <int NSH>
 __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
-  __shared__ uint32_t s_free[4], s_live[4], s_busy[4], s_next, s_end, s_shaded;
+  __shared__ uint32_t s_free[4], s_live[4], s_busy[4], s_next, s_end, s_shaded, s_nb, s_nbn;
   __shared__ int s_skip;
   const int tid = threadIdx.x, wave = tid >> 6;
+  const uint32_t nblocks = (S.M + POOL_BLOCK - 1) / POOL_BLOCK;
   if (tid == 0) {
     const uint4 ws = S.wstate[blockIdx.x];
-    const uint32_t end = range_start(S, blockIdx.x + 1);
     s_next = ws.x;
-    s_shaded = ws.z;
-    s_end = end;
-    s_skip = ws.y == 0 && ws.x >= end;
+    s_end = ws.y;
+    s_shaded = ws.w;
+    s_skip = ws.z == 0 && ws.x >= ws.y;  // idle: unless a dispenser is still open (below)
   }
   __syncthreads();
-  const uint32_t end = s_end;
-  if (s_skip) return;
+  if (s_skip) {  // (uniform: every thread has read it before the barrier below)
+    __syncthreads();
+    if (wave == 0) {
+      const uint32_t sd = lane_id();
+      const bool open = __hip_atomic_load(S.pool + (size_t)sd * CSTRIDE, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) < pool_limit(nblocks, sd);
+      if (tid == 0) s_skip = 0;
+      if (__ballot(open) == 0 && tid == 0) s_skip = 1;
+    }
+    __syncthreads();
+    if (s_skip) return;
+  }
   const uint32_t p = blockIdx.x * TPB + tid;
   bool new_ext = false, new_sh[NSH];
   RayV ext{mk(0, 0, 0), mk(0, 0, 1), -1.0f}, shr[NSH];
@@ -490,7 +523,8 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
   }
   int state = SLOT_LIVE;
   if (p < S.N) state = shade_slot<NSH>(S, p, new_ext, ext, new_sh, shr);
-  // ---- regeneration: free slots take the next paths of the range in rank order
+  // ---- regeneration: free slots take the next paths in rank order, from the
+  // current block and then from a newly claimed one
   const bool fr = p < S.N && state != SLOT_LIVE;
   const unsigned long long mf = __ballot(fr), ml = __ballot(p < S.N && state == SLOT_LIVE),
                            mb = __ballot(p < S.N && state != SLOT_FREE);
@@ -500,19 +534,36 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
     s_busy[wave] = (uint32_t)__popcll(mb);
   }
   __syncthreads();
-  const uint32_t next = s_next;
+  const uint32_t nf = s_free[0] + s_free[1] + s_free[2] + s_free[3];
+  const uint32_t next = s_next, end = s_end;
   const uint32_t avail = end > next ? end - next : 0u;
-  if (tid == 0) {
-    const uint32_t nf = s_free[0] + s_free[1] + s_free[2] + s_free[3];
-    const uint32_t take = min(nf, avail);
-    S.wstate[blockIdx.x] = make_uint4(next + take, s_live[0] + s_live[1] + s_live[2] + s_live[3] + take,
-                                      s_shaded + s_busy[0] + s_busy[1] + s_busy[2] + s_busy[3], 0u);
+  const uint32_t t1 = min(nf, avail);
+  if (wave == 0) {
+    // (nf <= 256 = POOL_BLOCK: one new block always covers the rest)
+    int c = -1;
+    if (nf > t1) c = claim_block(S, nblocks);
+    if (tid == 0) {
+      uint32_t nb = 0, nbn = 0, nnext = next + t1, nend = end;
+      if (c >= 0) {
+        nb = (uint32_t)c * POOL_BLOCK;
+        const uint32_t nbend = min(S.M, nb + POOL_BLOCK);
+        nbn = min(nf - t1, nbend - nb);
+        nnext = nb + nbn;
+        nend = nbend;
+      }
+      s_nb = nb;
+      s_nbn = nbn;
+      S.wstate[blockIdx.x] = make_uint4(nnext, nend, s_live[0] + s_live[1] + s_live[2] + s_live[3] + t1 + nbn,
+                                        s_shaded + s_busy[0] + s_busy[1] + s_busy[2] + s_busy[3]);
+    }
   }
+  __syncthreads();
   if (fr) {
     uint32_t rank = mbcnt64(mf);
     for (int w = 0; w < wave; ++w) rank += s_free[w];
-    if (rank < avail) {
-      ext = RayV{ld3(S.cam.origin), start_path(S, p, next + rank), __builtin_inff()};
+    const int P = rank < t1 ? (int)(next + rank) : (rank - t1 < s_nbn ? (int)(s_nb + rank - t1) : -1);
+    if (P >= 0) {
+      ext = RayV{ld3(S.cam.origin), start_path(S, p, (uint32_t)P), __builtin_inff()};
       new_ext = true;
     }
   }
@@ -541,19 +592,23 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
   count_rays(S.rcount, n, sh + MAX_ROOT_TARGETS * 8);
 }
 
-// Live slots over all workgroups (the host polls it: 0 = the chunk is done);
-// with stats, also the chunk's shaded vertices (stats[STAT_SHADED]).  A grid
-// of LIVE_SUM_BLOCKS workgroups, one atomic each into the zeroed out[0..2]
-// ({live, shaded lo, shaded hi} as one u32 and one u64).
+// Work left (the host polls it: 0 = the chunk is done): live slots over all
+// workgroups plus the blocks no dispenser has handed out yet; with stats, also
+// the chunk's shaded vertices (stats[STAT_SHADED]).  A grid of LIVE_SUM_BLOCKS
+// workgroups, one atomic each into the zeroed *live.
 constexpr int LIVE_SUM_BLOCKS = 64;
-__global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wstate, uint32_t G, uint32_t* live,
-                                                   unsigned long long* shaded) {
+__global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wstate, uint32_t G, const uint32_t* pool,
+                                                   uint32_t nblocks, uint32_t* live, unsigned long long* shaded) {
   __shared__ unsigned long long part[2][16];
   unsigned long long v = 0, sh = 0;
   for (uint32_t b = blockIdx.x * 1024 + threadIdx.x; b < G; b += gridDim.x * 1024) {
     const uint4 w = wstate[b];
-    v += w.y;
-    sh += w.z;
+    v += w.z;
+    sh += w.w;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < POOLS) {
+    const uint32_t lim = pool_limit(nblocks, threadIdx.x), c = pool[(size_t)threadIdx.x * CSTRIDE];
+    v += c < lim ? lim - c : 0u;
   }
   v = wave_sum64(v);
   sh = wave_sum64(sh);

@@ -83,7 +83,8 @@ struct pt_ctx {
   uint32_t* d_work = nullptr;  // k_path_leaf path counter
   float4* d_res = nullptr;     // per-path radiance of a chunk
   size_t res_cap = 0;
-  uint4* d_wstate = nullptr;   // per shade workgroup {next path, live slots, shaded vertices}
+  uint4* d_wstate = nullptr;   // per shade workgroup {block next, block end, live slots, shaded vertices}
+  uint32_t* d_pool = nullptr;  // POOLS path-block dispensers, CSTRIDE apart
   size_t wstate_cap = 0;
   uint32_t* d_live = nullptr;  // live slots after a pass group (k_live_sum)
   uint32_t* h_poll = nullptr;  // pinned: {live, err} x 2 poll slots
@@ -162,7 +163,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shade, c->d_bsdfs,   c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
-                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live, c->d_pool,
                   c->d_pix_of, c->d_accum};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -486,6 +487,7 @@ int pt_create(pt_ctx** out, int device) {
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, 4) != hipSuccess ||
       hipMalloc((void**)&c->d_live, 4) != hipSuccess ||
+      hipMalloc((void**)&c->d_pool, POOLS * CSTRIDE * 4) != hipSuccess ||
       hipHostMalloc((void**)&c->h_poll, 16, hipHostMallocDefault) != hipSuccess) {
     delete c;
     return PT_E_HIP;
@@ -742,6 +744,15 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         c->wstate_cap = G;
       }
       S.wstate = c->d_wstate;
+      S.pool = c->d_pool;
+      // dispensers: the first fill runs blocks 0 .. G-1 (workgroup b block b)
+      const uint32_t nblocks = (M + POOL_BLOCK - 1) / POOL_BLOCK;
+      {
+        std::vector<uint32_t> init((size_t)POOLS * CSTRIDE, 0u);
+        for (uint32_t k = 0; k < POOLS; ++k) init[(size_t)k * CSTRIDE] = G > k ? (G - k + POOLS - 1) / POOLS : 0u;
+        HIPCHK(c, hipMemcpyAsync(c->d_pool, init.data(), init.size() * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // (init is a host temporary)
+      }
       if (nsh == 1) c->launch(pt_ctx::K_CAM, 0, k_camera_push<1>, grid, dim3(TPB), S);
       if (nsh == 2) c->launch(pt_ctx::K_CAM, 0, k_camera_push<2>, grid, dim3(TPB), S);
       // passes in groups of POLL_GROUP; the host reads the finished-path count
@@ -755,15 +766,15 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         }
         HIPCHK(c, hipMemsetAsync(c->d_live, 0, 4, c->stream));
         hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G,
-                           c->d_live, (unsigned long long*)nullptr);
+                           (const uint32_t*)c->d_pool, nblocks, c->d_live, (unsigned long long*)nullptr);
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1), c->d_live, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1) + 1, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->ev_poll[g & 1], c->stream));
         return PT_OK;
       };
-      // every path ends within `passes` passes of its start, and a workgroup
-      // starts a new path in every slot that ends; its range holds at most
-      // ceil(M / N) paths per slot
+      // every path ends within `passes` passes of its start, and while blocks
+      // remain every free slot starts a path: at most (M / N + 2) rounds of
+      // `passes` passes
       const int max_groups = (int)(((uint64_t)(M / N + 2) * passes) / POLL_GROUP + 3);
       bool overflow = false, finished = false;
       if ((rc = enqueue_group(0)) || (rc = enqueue_group(1))) return rc;
@@ -793,7 +804,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       if (!finished) return fail(c, PT_E_HIP, "paths did not finish within the pass bound");
       if (timed)  // shaded vertices of the chunk (stats only)
         hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G,
-                           c->d_live, c->d_stats + STAT_SHADED);
+                           (const uint32_t*)c->d_pool, nblocks, c->d_live, c->d_stats + STAT_SHADED);
     }
     c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_res,
               c->d_accum, npix, spp_c);
