@@ -34,7 +34,7 @@ struct ShadeArgs {
   float4* ps3;  // pending contribution of the second shadow ray (PT_FLAG_REF_SCHEDULE)
   const float4* __restrict__ prims;
   // per-primitive hit-shading record, 5 float4 (80 B, two 64-B sectors):
-  // {A, meta}{B, n0.x}{C, n0.y}{n0.z, n1}{n2, 0} -- vertices and vertex
+  // {A, meta}{B, n0.x}{C, n0.y}{n0.z, n1}{n2, flat} -- vertices and vertex
   // normals of a triangle (a sphere: {centre, meta}), built by pt_load_scene
   // from pt_prim + pt_prim_shading so a hit gathers 80 B instead of 96
   const float4* __restrict__ shade;
@@ -112,12 +112,14 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
     const f3 dv = lpt - pt;
     const float sq = dot(dv, dv);
     const float dist = sqrtf(sq);
-    const f3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+    const float inv = 1.0f / dist;
+    const f3 w = mk(dv.x * inv, dv.y * inv, dv.z * inv);
     const float cosl = dot(w, ld3(S.light.direction));
     const float cosn = dot(n, w);
     if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
-      const float pdf = sq / (S.light.area * -cosl);
-      float scale = (cosn / pdf) * INV_PI;
+      // cosn / pdf with pdf = sq / (area * -cosl) (solid-angle pdf of the
+      // light sample), as one division
+      float scale = ((cosn * (S.light.area * -cosl)) / sq) * INV_PI;
       if (weight >= 0.0f) scale = scale * weight;
       C = mulv(mulv(T, alb), ld3(S.light.radiance)) * scale;
       r.o = pt;
@@ -129,7 +131,8 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
     const f3 dv = ld3(S.light.position) - pt;
     const float sq = dot(dv, dv);
     const float dist = sqrtf(sq);
-    const f3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+    const float inv = 1.0f / dist;
+    const f3 w = mk(dv.x * inv, dv.y * inv, dv.z * inv);
     const float cosn = dot(n, w);
     if (dist > 1e-2f && cosn > 0.0f) {
       float scale = cosn * INV_PI;
@@ -187,16 +190,22 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
       if ((meta >> 28) == PT_PRIM_SPHERE) {
         ns = normalize(mk(P.x - q0.x, P.y - q0.y, P.z - q0.z));
       } else {
-        // barycentric shading normal (cu:1213-1221)
         const float4 q1 = Q[1], q2 = Q[2], q3 = Q[3], q4 = Q[4];
-        const f3 A = xyz(q0), B = xyz(q1), Cv = xyz(q2);
-        float total = length(cross(A - B, B - Cv));
-        float bC = length(cross(A - P, B - P)) / total;
-        float bA = length(cross(B - P, Cv - P)) / total;
-        float bB = length(cross(Cv - P, A - P)) / total;
-        f3 n0 = mk(q1.w, q2.w, q3.x), n1 = mk(q3.y, q3.z, q3.w), n2 = mk(q4.x, q4.y, q4.z);
-        ns = normalize(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y,
-                          bA * n0.z + bB * n1.z + bC * n2.z));
+        const f3 n0 = mk(q1.w, q2.w, q3.x), n1 = mk(q3.y, q3.z, q3.w), n2 = mk(q4.x, q4.y, q4.z);
+        if (q4.w != 0.0f) {
+          // flat triangle (n0 == n1 == n2): the barycentric blend is a
+          // positive multiple of n0, so its normalisation is normalize(n0)
+          ns = normalize(n0);
+        } else {
+          // barycentric shading normal (cu:1213-1221)
+          const f3 A = xyz(q0), B = xyz(q1), Cv = xyz(q2);
+          float total = length(cross(A - B, B - Cv));
+          float bC = length(cross(A - P, B - P)) / total;
+          float bA = length(cross(B - P, Cv - P)) / total;
+          float bB = length(cross(Cv - P, A - P)) / total;
+          ns = normalize(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y,
+                            bA * n0.z + bB * n1.z + bC * n2.z));
+        }
       }
       const bool front = dot(ns, d) < 0.0f;
       const f3 n = front ? ns : mk(-ns.x, -ns.y, -ns.z);  // faces the incoming ray (cu:1222)

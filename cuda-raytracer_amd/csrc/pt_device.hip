@@ -564,7 +564,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   HIPCHK(c, hipMemcpy(c->d_nodes, s->nodes, sizeof(pt_node) * s->n_nodes, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_prims, s->prims, sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));
   {
-    // {A, meta}{B, n0.x}{C, n0.y}{n0.z, n1}{n2, 0} (shade.hip ShadeArgs::shade)
+    // {A, meta}{B, n0.x}{C, n0.y}{n0.z, n1}{n2, flat} (shade.hip ShadeArgs::shade)
     std::vector<float4> rec((size_t)s->n_prims * SHADE_REC);
     for (int i = 0; i < s->n_prims; ++i) {
       const float* q = s->prims[i].q;
@@ -574,7 +574,10 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
       r[1] = make_float4(q[4], q[5], q[6], n0[0]);
       r[2] = make_float4(q[8], q[9], q[10], n0[1]);
       r[3] = make_float4(n0[2], n1[0], n1[1], n1[2]);
-      r[4] = make_float4(n2[0], n2[1], n2[2], 0.0f);
+      // flat: identical vertex normals (the shading normal is normalize(n0))
+      const bool flat = n0[0] == n1[0] && n0[1] == n1[1] && n0[2] == n1[2] && n1[0] == n2[0] && n1[1] == n2[1] &&
+                        n1[2] == n2[2];
+      r[4] = make_float4(n2[0], n2[1], n2[2], flat ? 1.0f : 0.0f);
     }
     HIPCHK(c, hipMemcpy(c->d_shade, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice));
   }

@@ -303,12 +303,13 @@ static int nee_sample(const pt_scene_desc* S, v3 T, v3 alb, v3 n, v3 pt, float u
     v3 dv = sub(lpt, pt);
     float sq = dot(dv, dv);
     float dist = sqrtf(sq);
-    v3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+    float inv = 1.0f / dist;
+    v3 w = mk(dv.x * inv, dv.y * inv, dv.z * inv);
     float cosl = dot(w, ld3(S->light.direction));
     float cosn = dot(n, w);
     if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
-      float pdf = sq / (S->light.area * -cosl);
-      float scale = (cosn / pdf) * INV_PI;
+      /* cosn / pdf, pdf = sq / (area * -cosl), as one division */
+      float scale = ((cosn * (S->light.area * -cosl)) / sq) * INV_PI;
       if (weight >= 0.0f) scale = scale * weight;
       *C = scl(mulv(mulv(T, alb), ld3(S->light.radiance)), scale);
       *sw = w;
@@ -319,7 +320,8 @@ static int nee_sample(const pt_scene_desc* S, v3 T, v3 alb, v3 n, v3 pt, float u
     v3 dv = sub(ld3(S->light.position), pt);
     float sq = dot(dv, dv);
     float dist = sqrtf(sq);
-    v3 w = mk(dv.x / dist, dv.y / dist, dv.z / dist);
+    float inv = 1.0f / dist;
+    v3 w = mk(dv.x * inv, dv.y * inv, dv.z * inv);
     float cosn = dot(n, w);
     if (dist > 1e-2f && cosn > 0.0f) {
       float scale = cosn * INV_PI;
@@ -374,15 +376,21 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
     v3 ns;
     if ((meta >> 28) == PT_PRIM_SPHERE) {
       ns = nrm(mk(P.x - q[0], P.y - q[1], P.z - q[2]));
-    } else { /* barycentric shading normal, cu:1213-1221 */
-      v3 A = mk(q[0], q[1], q[2]), B = mk(q[4], q[5], q[6]), Cv = mk(q[8], q[9], q[10]);
+    } else {
       const pt_prim_shading* sh = &S->shading[prim];
-      float total = len3(cross(sub(A, B), sub(B, Cv)));
-      float bC = len3(cross(sub(A, P), sub(B, P))) / total;
-      float bA = len3(cross(sub(B, P), sub(Cv, P))) / total;
-      float bB = len3(cross(sub(Cv, P), sub(A, P))) / total;
       v3 n0 = ld3(sh->n0), n1 = ld3(sh->n1), n2 = ld3(sh->n2);
-      ns = nrm(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y, bA * n0.z + bB * n1.z + bC * n2.z));
+      if (n0.x == n1.x && n0.y == n1.y && n0.z == n1.z && n1.x == n2.x && n1.y == n2.y && n1.z == n2.z) {
+        /* flat triangle: the barycentric blend is a positive multiple of n0 */
+        ns = nrm(n0);
+      } else { /* barycentric shading normal, cu:1213-1221 */
+        v3 A = mk(q[0], q[1], q[2]), B = mk(q[4], q[5], q[6]), Cv = mk(q[8], q[9], q[10]);
+        float total = len3(cross(sub(A, B), sub(B, Cv)));
+        float bC = len3(cross(sub(A, P), sub(B, P))) / total;
+        float bA = len3(cross(sub(B, P), sub(Cv, P))) / total;
+        float bB = len3(cross(sub(Cv, P), sub(A, P))) / total;
+        ns = nrm(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y,
+                    bA * n0.z + bB * n1.z + bC * n2.z));
+      }
     }
     int front = dot(ns, d) < 0.0f;
     v3 n = front ? ns : mk(-ns.x, -ns.y, -ns.z);
