@@ -208,18 +208,22 @@ __device__ __forceinline__ void load_ray(const TraceArgs& A, bool ids, uint32_t 
 struct ChildTargets {
   const CPTR(pt_node) nd;
   __device__ __forceinline__ int count() const { return 4; }
-  __device__ __forceinline__ const CPTR(pt_node) box(const TraceArgs&, int c, int& k) const {
-    k = c;
-    return nd;
+  __device__ __forceinline__ void box(const TraceArgs&, int c, float (&b)[6]) const {
+    b[0] = nd->bmin_x[c];
+    b[1] = nd->bmax_x[c];
+    b[2] = nd->bmin_y[c];
+    b[3] = nd->bmax_y[c];
+    b[4] = nd->bmin_z[c];
+    b[5] = nd->bmax_z[c];
   }
   __device__ __forceinline__ int node(const TraceArgs&, int c) const { return nd->child[c]; }
 };
 struct TableTargets {
   const RootTable& T;
   __device__ __forceinline__ int count() const { return T.nt; }
-  __device__ __forceinline__ const CPTR(pt_node) box(const TraceArgs& A, int c, int& k) const {
-    k = T.tbox[c] & 3;
-    return (const CPTR(pt_node))(A.nodes + (T.tbox[c] >> 2));
+  __device__ __forceinline__ void box(const TraceArgs&, int c, float (&b)[6]) const {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) b[i] = T.tb[i][c];
   }
   __device__ __forceinline__ int node(const TraceArgs&, int c) const { return T.tnode[c]; }
 };
@@ -252,10 +256,9 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       if (c >= nt) break;
-      int k;
-      const CPTR(pt_node) cn = tg.box(A, c, k);
-      bool h = box_hit(cn->bmin_x[k], cn->bmax_x[k], cn->bmin_y[k], cn->bmax_y[k], cn->bmin_z[k], cn->bmax_z[k],
-                       oi, inv, tmax[j]);
+      float bx[6];
+      tg.box(A, c, bx);
+      bool h = box_hit(bx[0], bx[1], bx[2], bx[3], bx[4], bx[5], oi, inv, tmax[j]);
       b |= (valid[j] && h) ? (1u << c) : 0u;
     }
     bits[j] = b;
@@ -322,10 +325,8 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
                         __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
       const f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
       for (int i = 0; i < T.ni; ++i) {
-        const CPTR(pt_node) bn = (const CPTR(pt_node))(A.nodes + (T.ibox[i] >> 2));
-        const int k = T.ibox[i] & 3;
-        if (!valid[j] || !box_hit(bn->bmin_x[k], bn->bmax_x[k], bn->bmin_y[k], bn->bmax_y[k], bn->bmin_z[k],
-                                  bn->bmax_z[k], oi, inv, bt))
+        if (!valid[j] || !box_hit(T.ib[0][i], T.ib[1][i], T.ib[2][i], T.ib[3][i], T.ib[4][i], T.ib[5][i], oi, inv,
+                                  bt))
           continue;
         const int pstart = T.istart[i];
         const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);

@@ -252,6 +252,16 @@ static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
 // skipped when every other child of the root is interior (PT_NO_SKIP_L1=1
 // disables it): the producers then test the grandchild boxes directly (boxes
 // are conservative for their subtrees, so no ray is lost).
+template <int W>
+static void box_row(float (&b)[6][W], int i, const pt_node& parent, int k) {
+  b[0][i] = parent.bmin_x[k];
+  b[1][i] = parent.bmax_x[k];
+  b[2][i] = parent.bmin_y[k];
+  b[3][i] = parent.bmax_y[k];
+  b[4][i] = parent.bmin_z[k];
+  b[5][i] = parent.bmax_z[k];
+}
+
 static void build_root_table(pt_ctx* c) {
   RootTable& T = c->rt;
   memset(&T, 0, sizeof(T));
@@ -264,6 +274,7 @@ static void build_root_table(pt_ctx* c) {
     const pt_node& leaf = nd[nd[parent].child[k]];
     if (leaf.prim_count <= 0 || leaf.prim_count > budget || T.ni >= MAX_INLINE_LEAVES) return false;
     T.ibox[T.ni] = parent * 4 + k;
+    box_row(T.ib, T.ni, nd[parent], k);
     T.istart[T.ni] = leaf.prim_start;
     T.icount[T.ni] = leaf.prim_count;
     T.ni++;
@@ -272,6 +283,7 @@ static void build_root_table(pt_ctx* c) {
   };
   auto add_target = [&](int parent, int k) {
     T.tbox[T.nt] = parent * 4 + k;
+    box_row(T.tb, T.nt, nd[parent], k);
     T.tnode[T.nt] = nd[parent].child[k];
     T.nt++;
   };
