@@ -489,6 +489,9 @@ int pt_create(pt_ctx** out, int device) {
   if (device < 0 || device >= n) return PT_E_INVALID;
   pt_ctx* c = new pt_ctx();
   c->device = device;
+  // initial queue factor (doubles whenever a level overflows; PT_QFACTOR=1
+  // exercises that path in the tests)
+  if (const char* q = getenv("PT_QFACTOR")) c->qfactor = std::max(1, atoi(q));
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return PT_E_HIP;
@@ -635,6 +638,7 @@ int pt_get_stats(pt_ctx* c, pt_stats* out) {
   hipSetDevice(c->device);
   int rc = read_device_stats(c);
   c->stats.n_levels = c->n_levels;
+  c->stats.queue_factor = (int32_t)c->qfactor;
   *out = c->stats;
   return rc == PT_E_OVERFLOW ? PT_OK : rc;
 }

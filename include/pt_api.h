@@ -331,6 +331,8 @@ typedef struct pt_stats {
   uint64_t shaded;        /* path vertices shaded by k_shade_push             */
   double ms_shade_push;   /* k_shade_push alone (part of ms_shade)            */
   uint64_t shade_launches;
+  int32_t queue_factor;   /* current queue factor (grows when a level overflows) */
+  int32_t pad_;
 } pt_stats;
 int pt_get_stats(pt_ctx* ctx, pt_stats* out);
 int pt_reset_stats(pt_ctx* ctx);

@@ -77,6 +77,33 @@ def test_schedule_options_match(gpu_ctx, env, monkeypatch):
     assert np.array_equal(img, o)
 
 
+def test_queue_overflow_rerun(monkeypatch):
+    """A context started with the smallest queue factor (PT_QFACTOR=1) on a
+    soup of large overlapping triangles overflows a level queue, abandons the
+    pass and re-runs it with twice the capacity (pt_intersect and pt_render):
+    hits and image still equal the oracle's."""
+    rng = np.random.default_rng(11)
+    c = rng.random((3000, 1, 3), dtype=np.float32)
+    tris = (c + 0.6 * (rng.random((3000, 3, 3), dtype=np.float32) - 0.5)).reshape(-1, 9)
+    sc = ptrace.Scene.from_triangles(tris)
+    d = sc.desc()
+    monkeypatch.setenv("PT_QFACTOR", "1")
+    ctx = ptrace.Context(0)
+    monkeypatch.delenv("PT_QFACTOR")
+    try:
+        ctx.load_scene(sc)
+        rays = interior_rays(d, 50000, seed=41)
+        g = ctx.intersect(rays)
+        assert np.array_equal(g, pyoracle.intersect(d, rays, use_bvh=True))
+        assert (g != ptrace.PT_HIT_NONE).sum() > 10000
+        assert ctx.stats().queue_factor > 1  # the overflow path did run
+        ctx.render(32, 32, 2, max_bounces=4, seed=15618)
+        o, _ = pyoracle.image(d, 32, 32, 2, max_bounces=4, seed=15618)
+        assert np.array_equal(ctx.get_image(), o)
+    finally:
+        ctx.close()
+
+
 def test_tie_break_lowest_prim(gpu_ctx):
     # two identical triangles: every hit must report the lower sorted index
     tri = np.array([[-1, -1, 0, 1, -1, 0, 0, 1, 0]] * 2, np.float32)
