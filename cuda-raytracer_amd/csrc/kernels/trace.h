@@ -65,9 +65,24 @@ struct TraceArgs {
   uint32_t* q;                       // ray-id queues of the root pass's targets (4 B ids)
   float4* qe;                        // ray-entry queues of the levels below (two parity halves):
                                      // QESTRIDE float4 per entry, {o, d.x}{d.y, d.z, id, tmax}
+  uint32_t shadow_base;              // ray slots >= shadow_base are shadow rays (any hit ends them);
+                                     // 0xFFFFFFFF: every ray wants its closest hit (pt_intersect)
 };
 constexpr int QESTRIDE = 2;
 
+// A leaf's hit {t, prim} for ray id.  Closest-hit rays: atomicMin on the
+// record's key (its t is the tmax of every later box test).  Shadow rays only
+// need to know that something blocks them: a plain store of {prim, t = -1}
+// marks the ray occluded (prim != PT_PRIM_NONE) and fails every later box
+// test (tmax < 0), so an occluded shadow ray leaves the traversal at once.
+__device__ __forceinline__ unsigned long long* rec_key(float4* ray, uint32_t id);
+__device__ __forceinline__ void report_hit(float4* ray, uint32_t shadow_base, uint32_t id, float t, uint32_t prim) {
+  if (id >= shadow_base) {
+    *rec_key(ray, id) = ((unsigned long long)__float_as_uint(-1.0f) << 32) | (unsigned long long)prim;
+  } else {
+    atomicMin(rec_key(ray, id), ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)prim);
+  }
+}
 __device__ __forceinline__ unsigned long long* rec_key(float4* ray, uint32_t id) {
   return reinterpret_cast<unsigned long long*>(ray + (size_t)RSTRIDE * id + 1) + 1;
 }

@@ -454,13 +454,9 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
     }
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
-      if (valid[j] && bp[j] >= 0) {
-        unsigned long long key =
-            ((unsigned long long)__float_as_uint(bt[j]) << 32) | (unsigned long long)(uint32_t)bp[j];
-        // the record's {prim, t} word: later box tests of this ray read the
-        // tightened t as their tmax
-        atomicMin(rec_key(A.ray, id[j]), key);
-      }
+      // the record's {prim, t} word: later box tests of this ray read the
+      // tightened t as their tmax (a shadow ray: occluded, done)
+      if (valid[j] && bp[j] >= 0) report_hit(A.ray, A.shadow_base, id[j], bt[j], (uint32_t)bp[j]);
     }
     return nvalid;
   }
@@ -594,11 +590,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     }
 #pragma unroll
     for (int j = 0; j < RPTW; ++j) {
-      if (valid[j] && bp[j] >= 0) {
-        unsigned long long key =
-            ((unsigned long long)__float_as_uint(bt[j]) << 32) | (unsigned long long)(uint32_t)bp[j];
-        atomicMin(rec_key(A.ray, id[j]), key);
-      }
+      if (valid[j] && bp[j] >= 0) report_hit(A.ray, A.shadow_base, id[j], bt[j], (uint32_t)bp[j]);
     }
     return;
   }

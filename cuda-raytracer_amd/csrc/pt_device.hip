@@ -70,6 +70,7 @@ struct pt_ctx {
   uint32_t* d_q = nullptr;   // ray-id queues (two parity halves): the root's targets and the levels above entry_level
   size_t qcap = 0;           // ids per parity half
   int entry_level = 0;       // first level whose queues hold ray entries (build_root_table)
+  uint32_t shadow_base = 0xFFFFFFFFu;  // ray slots >= it are shadow rays (pt_render sets N; pt_intersect none)
   float4* d_qe = nullptr;    // ray-entry queues of the levels below the root's targets
   size_t qecap = 0;          // entries per parity half
   uint32_t* d_cnt = nullptr;
@@ -340,6 +341,7 @@ static TraceArgs trace_args(pt_ctx* c) {
   A.qoff = c->d_qoff;
   A.q = c->d_q;
   A.qe = c->d_qe;
+  A.shadow_base = c->shadow_base;
   return A;
 }
 
@@ -753,6 +755,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       S.ps2 = c->d_ps2;
       S.ps3 = c->d_ps3;
       S.N = N;
+      c->shadow_base = N;  // slots >= N hold shadow rays
       S.A = trace_args(c);
       S.T = c->rt;
       const dim3 grid((N + TPB - 1) / TPB);
@@ -918,6 +921,7 @@ int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) {
   if (n == 0) return PT_OK;
   hipSetDevice(c->device);
   int rc;
+  c->shadow_base = 0xFFFFFFFFu;  // every ray wants its closest hit
   const uint32_t N = ((uint32_t)n + 1) / 2;
   const bool realloc = N > c->cap_paths || 2 > c->cap_spp;
   if ((rc = ensure_paths(c, N, 2))) return rc;
