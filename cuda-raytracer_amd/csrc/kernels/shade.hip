@@ -705,11 +705,12 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
 #endif
 constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 
-// 7 waves per SIMD (72 VGPRs, ~20 spilled around the shading code): +2.3 %
-// over 6 waves (80 VGPRs, no spills) on CBempty and CBspheres; 8 waves (64
-// VGPRs, ~60 spilled) lose 10 %
+// 6 waves per SIMD (80 VGPRs, no spills).  7 waves (72 VGPRs) run within
+// 0.6 % of it but spill ~20 VGPRs around the shading code, which turns into
+// ~35 GB of scratch write-back per 1024^2 x 256 spp frame (PMC WRITE_SIZE);
+// 8 waves spill ~60 and lose 10 %.
 #ifndef PT_PATH_WAVES
-#define PT_PATH_WAVES 7
+#define PT_PATH_WAVES 6
 #endif
 template <int NSH>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
@@ -722,7 +723,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
   uint32_t next = 0, end = 0;
   bool drained = false;
   bool active = false;
-  uint32_t p = 0, sidx = 0;
+  uint32_t p = 0;
   PathState st{mk(0, 0, 0), 0u, mk(0, 0, 0), 0u};
   RayV ext{mk(0, 0, 0), mk(0, 0, 1), -1.0f}, shr[NSH];
   f3 C[NSH];
@@ -753,7 +754,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
         st.L = mk(0.0f, 0.0f, 0.0f);
         st.flags = F_EXT | (1u << 8);
         ext = RayV{ld3(S.cam.origin), dir, __builtin_inff()};
-        sidx = S.sample_base + udiv_q(p, S.div_npix);
       }
       next += min((uint32_t)__popcll(idle), avail);
     }
@@ -766,7 +766,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       uint32_t prim = PT_PRIM_NONE;
       float t = 0.0f;
       if (st.flags & F_EXT) {
-        leaf_closest(S.prims, pstart, pcount, ext, prim, t);
+        // (extension rays have tmax = inf: not carried across iterations)
+        leaf_closest(S.prims, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t);
         nrays++;
       }
       bool clear[NSH];
@@ -780,7 +781,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       }
       bool new_ext, new_sh[NSH];
       RayV e2, s2[NSH];
-      shade_vertex<NSH>(S, sidx, st, ext.o, ext.d, prim, t, clear, C, new_ext, e2, new_sh, s2);
+      // (the sample index is recomputed, not carried: one register less)
+      shade_vertex<NSH>(S, S.sample_base + udiv_q(p, S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
+                        new_sh, s2);
       if (new_ext) ext = e2;
 #pragma unroll
       for (int s = 0; s < NSH; ++s)
