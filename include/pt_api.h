@@ -252,7 +252,8 @@ typedef struct pt_render_params {
   int32_t max_bounces; /* indirect (BSDF-sampled) rays per path; vertices = +1 */
   uint32_t seed;       /* Philox key; reference seed 15618 (samplers.cu_inl:8) */
   int32_t sample_offset; /* index of the first sample (progressive rendering) */
-  int32_t batch_paths; /* paths in flight per wavefront batch; 0 = auto       */
+  int32_t batch_paths; /* wavefront path pool: path slots in flight (each slot
+                          runs path after path); 0 = auto (36 Mi)            */
   int32_t tile_size;   /* framebuffer tile edge for sharding (0 = 32)          */
   int32_t rank, nranks; /* this context renders tiles t with t % nranks == rank */
   uint32_t flags;
