@@ -389,17 +389,12 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
     S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(P));
   }
   // new rays: their records are written by root_pass (with the key of the
-  // inline leaves); empty slots get an empty r1 here
-  if (!new_ext) S.ray[RSTRIDE * p + 1] = rec_r1(0.f, 0.f, -1.0f);
+  // inline leaves).  A slot without a new ray keeps its stale record: only
+  // the path's flags say which records the next shade reads, and nothing
+  // else reads a record that was not queued (no 16-B "empty" partial writes)
 #pragma unroll
-  for (int s = 0; s < NSH; ++s) {
-    const size_t slot = (size_t)(1 + s) * S.N + p;
-    if (new_sh[s]) {
-      (s ? S.ps3 : S.ps2)[p] = make_float4(C[s].x, C[s].y, C[s].z, 0.0f);
-    } else {
-      S.ray[RSTRIDE * slot + 1] = rec_r1(0.f, 0.f, -1.0f);
-    }
-  }
+  for (int s = 0; s < NSH; ++s)
+    if (new_sh[s]) (s ? S.ps3 : S.ps2)[p] = make_float4(C[s].x, C[s].y, C[s].z, 0.0f);
   return ended ? SLOT_ENDED : SLOT_LIVE;
 }
 
@@ -476,14 +471,12 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
   bool valid[1] = {live}, anyhit[1] = {false};
   if (threadIdx.x == 0) S.wstate[blockIdx.x] = make_uint4(base + n0, end, n0, 0u);
   if (p < S.N) {
-#pragma unroll
-    for (int s = 0; s < NSH; ++s) S.ray[RSTRIDE * ((size_t)(1 + s) * S.N + p) + 1] = rec_r1(0.f, 0.f, -1.0f);
-    if (live) {
+    // (records are written by root_pass for the rays it receives; a path's
+    // flags say which of its records are meaningful)
+    if (live)
       d[0] = start_path(S, p, base + threadIdx.x);
-    } else {
+    else
       S.ps0[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
-      S.ray[RSTRIDE * p + 1] = rec_r1(0.f, 0.f, -1.0f);
-    }
   }
   root_pass<1>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh);
   count_rays(S.rcount, live ? 1u : 0u, sh + MAX_ROOT_TARGETS * 8);
