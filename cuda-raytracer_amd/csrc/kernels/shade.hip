@@ -383,7 +383,7 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
 #pragma unroll
     for (int s = 0; s < NSH; ++s) new_sh[s] = false;
     S.res[P] = make_float4(st.L.x, st.L.y, st.L.z, 0.0f);
-    S.ps0[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+    // (the caller frees the slot -- ps0 flags 0 -- unless it starts a new path)
   } else {
     S.ps0[p] = make_float4(st.T.x, st.T.y, st.T.z, __uint_as_float(st.flags));
     S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(P));
@@ -567,6 +567,8 @@ __global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
     if (P >= 0) {
       ext = RayV{ld3(S.cam.origin), start_path(S, p, (uint32_t)P), __builtin_inff()};
       new_ext = true;
+    } else if (state == SLOT_ENDED) {
+      S.ps0[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));  // the slot stays free
     }
   }
   uint32_t id[1 + NSH];
