@@ -31,8 +31,10 @@ constexpr int TILE = TPB * RPT;   // rays per traversal item
 #ifndef PT_BLOCK_MODE_RAYS
 #define PT_BLOCK_MODE_RAYS 512
 #endif
+// level-kernel workgroups: 16384 (vs 8192: dragon proxy levels -4 %; 2048
+// -15 %, 32768 within noise)
 #ifndef PT_LEVEL_GRID
-#define PT_LEVEL_GRID 8192
+#define PT_LEVEL_GRID 16384
 #endif
 constexpr int RPTW = PT_RPTW;     // rays per lane in a wave-sized item
 constexpr int WTILE = 64 * RPTW;  // rays per wave item (levels >= 1)
