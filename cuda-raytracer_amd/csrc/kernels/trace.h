@@ -42,9 +42,9 @@ constexpr int NLANE = 8;          // queue lanes (one per XCD)
 constexpr int CSTRIDE = 32;       // u32 per queue counter: each (node, lane) counter owns a 128-B line
 constexpr uint32_t MODE_WAVE = 0, MODE_BLOCK = 1;
 constexpr uint32_t BLOCK_MODE_RAYS_PER_PAIR = PT_BLOCK_MODE_RAYS;  // level mode threshold (mean rays per queue lane)
-constexpr int LEVEL_GRID = PT_LEVEL_GRID;  // workgroups of the level kernel (32 per CU: the
+constexpr int LEVEL_GRID = PT_LEVEL_GRID;  // workgroups of the level kernel (64 per CU: the
                                           // dispatcher's refill balances uneven items)
-constexpr int RCOUNT_SLOTS = 64;  // ray counters (u64, 128 B apart), indexed by workgroup & 63  // workgroups of the per-level grid-stride kernel (8 per CU)
+constexpr int RCOUNT_SLOTS = 64;  // ray counters (u64, 128 B apart), indexed by workgroup & 63
 
 // device statistics slots (unsigned long long)
 enum {
