@@ -53,11 +53,21 @@ __device__ __forceinline__ uint32_t udiv_q(uint32_t n, udiv d) {
 struct u4 {
   uint32_t x, y, z, w;
 };
+// M64: each 32x32 -> 64-bit product as one v_mad_u64_u32 instead of
+// v_mul_hi_u32 + v_mul_lo_u32 (same bits; faster, but 4 more VGPRs live)
+template <bool M64 = false>
 __device__ __forceinline__ u4 philox(u4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-    uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    uint32_t hi0, lo0, hi1, lo1;
+    if constexpr (M64) {
+      const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+      hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+      hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    } else {
+      hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+      hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    }
     c = u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -68,15 +78,17 @@ __device__ __forceinline__ u4 philox(u4 c, uint32_t k0, uint32_t k1) {
 __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
 
 // Random numbers of one path vertex.  counter = (pixel, sample, 2*vertex+call, 'PT')
+template <bool M64 = false>
 __device__ __forceinline__ u4 rng(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t vertex,
                                   uint32_t call) {
-  return philox(u4{pixel, sample, vertex * 2u + call, 0x50540000u}, seed, 0x2545F491u);
+  return philox<M64>(u4{pixel, sample, vertex * 2u + call, 0x50540000u}, seed, 0x2545F491u);
 }
 
 // The second NEE sample of a vertex under the reference schedule: its own
 // stream (last counter word 'PT'+1), so it never aliases another vertex's.
+template <bool M64 = false>
 __device__ __forceinline__ u4 rng_nee2(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t vertex) {
-  return philox(u4{pixel, sample, vertex * 2u, 0x50540001u}, seed, 0x2545F491u);
+  return philox<M64>(u4{pixel, sample, vertex * 2u, 0x50540001u}, seed, 0x2545F491u);
 }
 
 // sin and cos of 2*pi*u for u in [0,1): quadrant reduction on u (exact), then

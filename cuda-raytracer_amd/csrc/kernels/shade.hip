@@ -152,7 +152,7 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
 // extension hit (prim != PT_PRIM_NONE at distance t along ext), and produces
 // the next extension ray and/or shadow rays with their pending contributions.
 // NSH = 2 only under PT_FLAG_REF_SCHEDULE (NEE samples 2, 2, 1 per vertex).
-template <int NSH>
+template <int NSH, bool M64 = false>
 __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, PathState& st, const f3 o,
                                              const f3 d, uint32_t prim, float t, const bool (&clear)[NSH],
                                              f3 (&C)[NSH], bool& new_ext, RayV& ext, bool (&new_sh)[NSH],
@@ -215,7 +215,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
         if (!(S.flags & PT_FLAG_NO_EMISSION) && (vtx == 1u || spec))
           L = L + mulv(T, ld3(B.albedo));
       } else {
-        const u4 u = rng(S.seed, g, sidx, vtx, 0);
+        const u4 u = rng<M64>(S.seed, g, sidx, vtx, 0);
         f3 dpdu, dpdv;
         if (S.flags & PT_FLAG_REF_GUIDE) {
           // reference quirk (ii): cu:572-574 (NaN when n is (0,-1,0))
@@ -237,7 +237,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
             if (s < nee) {
               float ux = u01(u.x), uy = u01(u.y);
               if (s == 1) {
-                const u4 v = rng_nee2(S.seed, g, sidx, vtx);
+                const u4 v = rng_nee2<M64>(S.seed, g, sidx, vtx);
                 ux = u01(v.x);
                 uy = u01(v.y);
               }
@@ -291,7 +291,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
             const float c = front ? cosi : cost;
             const float m = 1.0f - c;
             const float F = r0 + (1.0f - r0) * (((m * m) * (m * m)) * m);
-            const u4 u2 = rng(S.seed, g, sidx, vtx, 1);
+            const u4 u2 = rng<M64>(S.seed, g, sidx, vtx, 1);
             refl = u01(u2.x) < F;
           }
           if (refl) {
@@ -488,8 +488,11 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
 // all new rays (extension, shadow, camera) are pushed into the root's target
 // queues.  A workgroup with no live slot and nothing left to start returns at
 // once (passes queued after the chunk ended).
+#ifndef PT_SHADE_ATTR
+#define PT_SHADE_ATTR
+#endif
 template <int NSH>
-__global__ __launch_bounds__(TPB) void k_shade_push(ShadeArgs S) {
+__global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
   __shared__ uint32_t s_free[4], s_live[4], s_busy[4], s_next, s_end, s_shaded, s_nb, s_nbn;
   __shared__ int s_skip;
@@ -695,6 +698,9 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
 // passes N and its lanes are idle.  Results do not depend on which lane runs a
 // path: random numbers are keyed by (pixel, sample, vertex) and each path
 // writes only its own slot ps1[p].
+#ifndef PT_PATH_MAD64
+#define PT_PATH_MAD64 true  // Philox products as v_mad_u64_u32 (CBempty +1.4 %; k_shade_push would lose its 7th wave)
+#endif
 #ifndef PT_PATH_CHUNK
 #define PT_PATH_CHUNK 256
 #endif
@@ -777,7 +783,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       bool new_ext, new_sh[NSH];
       RayV e2, s2[NSH];
       // (the sample index is recomputed, not carried: one register less)
-      shade_vertex<NSH>(S, S.sample_base + udiv_q(p, S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
+      shade_vertex<NSH, PT_PATH_MAD64>(S, S.sample_base + udiv_q(p, S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
                         new_sh, s2);
       if (new_ext) ext = e2;
 #pragma unroll
