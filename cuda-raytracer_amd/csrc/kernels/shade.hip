@@ -184,13 +184,14 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
     if (prim != PT_PRIM_NONE) {
       const f3 P = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
       const float4* Q = S.shade + (size_t)prim * SHADE_REC;
-      const float4 q0 = Q[0];
+      // the whole record in one round trip (a sphere needs only q0)
+      const float4 q0 = Q[0], q1 = Q[1], q2 = Q[2], q3 = Q[3], q4 = Q[4];
+      asm volatile("" ::"v"(q0.w), "v"(q1.x), "v"(q2.x), "v"(q3.x), "v"(q4.w));
       const uint32_t meta = __float_as_uint(q0.w);
       f3 ns;
       if ((meta >> 28) == PT_PRIM_SPHERE) {
         ns = normalize(mk(P.x - q0.x, P.y - q0.y, P.z - q0.z));
       } else {
-        const float4 q1 = Q[1], q2 = Q[2], q3 = Q[3], q4 = Q[4];
         const f3 n0 = mk(q1.w, q2.w, q3.x), n1 = mk(q3.y, q3.z, q3.w), n2 = mk(q4.x, q4.y, q4.z);
         if (q4.w != 0.0f) {
           // flat triangle (n0 == n1 == n2): the barycentric blend is a
@@ -342,10 +343,26 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
   new_ext = false;
 #pragma unroll
   for (int s = 0; s < NSH; ++s) new_sh[s] = false;
+  // every word the slot may need is loaded at once (one memory round trip
+  // instead of three dependent ones: flags, then records, then the ray and the
+  // pending contributions); words the flags do not cover are stale and only
+  // pass through selects
   const float4 s0 = S.ps0[p];
+  const float4 s1 = S.ps1[p];
+  const float4 r0 = S.ray[RSTRIDE * p], r1 = S.ray[RSTRIDE * p + 1];
+  float4 hs[NSH], cs[NSH];
+#pragma unroll
+  for (int s = 0; s < NSH; ++s) {
+    hs[s] = S.ray[RSTRIDE * ((1 + s) * S.N + p) + 1];
+    cs[s] = (s ? S.ps3 : S.ps2)[p];
+  }
+  // (the compiler would sink each load into the branch that uses it, i.e.
+  // behind the previous load's wait: pin them all here)
+  asm volatile("" ::"v"(s0.w), "v"(s1.w), "v"(r0.x), "v"(r1.x));
+#pragma unroll
+  for (int s = 0; s < NSH; ++s) asm volatile("" ::"v"(hs[s].z), "v"(cs[s].x));
   const uint32_t flags = __float_as_uint(s0.w);
   if ((flags & (F_EXT | F_SHADOW | F_SHADOW2)) == 0) return SLOT_FREE;
-  const float4 s1 = S.ps1[p];
   const uint32_t P = __float_as_uint(s1.w);
   PathState st{xyz(s0), flags, xyz(s1), 0u};
   uint32_t sidx;
@@ -354,26 +371,13 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
   f3 C[NSH];
 #pragma unroll
   for (int s = 0; s < NSH; ++s) {
-    clear[s] = false;
-    C[s] = mk(0, 0, 0);
-    if (flags & sh_bit(s)) {
-      clear[s] = __float_as_uint(S.ray[RSTRIDE * ((1 + s) * S.N + p) + 1].z) == PT_PRIM_NONE;
-      if (clear[s]) C[s] = xyz(s ? S.ps3[p] : S.ps2[p]);
-    }
+    clear[s] = (flags & sh_bit(s)) && __float_as_uint(hs[s].z) == PT_PRIM_NONE;
+    C[s] = clear[s] ? xyz(cs[s]) : mk(0, 0, 0);
   }
-  uint32_t prim = PT_PRIM_NONE;
-  float t = 0.0f;
-  f3 o = mk(0, 0, 0), d = mk(0, 0, 1);
-  if (flags & F_EXT) {
-    const float4 r1 = S.ray[RSTRIDE * p + 1];
-    prim = __float_as_uint(r1.z);
-    if (prim != PT_PRIM_NONE) {
-      t = r1.w;
-      const float4 r0 = S.ray[RSTRIDE * p];
-      o = xyz(r0);
-      d = mk(r0.w, r1.x, r1.y);
-    }
-  }
+  const bool ext_hit = (flags & F_EXT) && __float_as_uint(r1.z) != PT_PRIM_NONE;
+  const uint32_t prim = (flags & F_EXT) ? __float_as_uint(r1.z) : PT_PRIM_NONE;
+  const float t = ext_hit ? r1.w : 0.0f;
+  const f3 o = ext_hit ? xyz(r0) : mk(0, 0, 0), d = ext_hit ? mk(r0.w, r1.x, r1.y) : mk(0, 0, 1);
   shade_vertex<NSH>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
   // (vertices done = vtx - 1: the last one resolves shadow rays only)
   const bool ended =
@@ -488,8 +492,11 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
 // all new rays (extension, shadow, camera) are pushed into the root's target
 // queues.  A workgroup with no live slot and nothing left to start returns at
 // once (passes queued after the chunk ended).
+// 7 waves/SIMD (72 VGPRs, a few spills): with the slot's loads issued
+// together (shade_slot) the kernel needs 74 and would drop to 6 waves;
+// 6 waves: CBbunny shade 101 -> 105 ms
 #ifndef PT_SHADE_ATTR
-#define PT_SHADE_ATTR
+#define PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(7, 8)))
 #endif
 template <int NSH>
 __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
