@@ -28,6 +28,10 @@
 #include "kernels/shade.hip"
 #include "kernels/post.hip"
 
+// k_shade_push lives in pt_shade.hip (its own compile flags)
+hipError_t pt_launch_shade_push(int nsh, unsigned grid, hipStream_t stream, hipEvent_t e0, hipEvent_t e1,
+                                const void* S);
+
 using namespace pt;
 
 namespace {
@@ -783,8 +787,12 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         for (int k = 0; k < POLL_GROUP; ++k) {
           int r = trace_levels(c);
           if (r) return r;
-          if (nsh == 1) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<1>, grid, dim3(TPB), S);
-          if (nsh == 2) c->launch(pt_ctx::K_SHADE, 0, k_shade_push<2>, grid, dim3(TPB), S);
+          if (c->timing) {
+            const auto e = c->pair(pt_ctx::K_SHADE, 0);
+            HIPCHK(c, pt_launch_shade_push(nsh, grid.x, c->stream, e.first, e.second, &S));
+          } else {
+            HIPCHK(c, pt_launch_shade_push(nsh, grid.x, c->stream, nullptr, nullptr, &S));
+          }
         }
         HIPCHK(c, hipMemsetAsync(c->d_live, 0, 4, c->stream));
         hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G,
