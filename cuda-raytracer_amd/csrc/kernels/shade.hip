@@ -492,9 +492,9 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
 // all new rays (extension, shadow, camera) are pushed into the root's target
 // queues.  A workgroup with no live slot and nothing left to start returns at
 // once (passes queued after the chunk ended).
-// 7 waves/SIMD (72 VGPRs, a few spills): with the slot's loads issued
-// together (shade_slot) the kernel needs 74 and would drop to 6 waves;
-// 6 waves: CBbunny shade 101 -> 105 ms
+// at least 7 waves/SIMD (built without SLP vectorisation, pt_shade.hip, it
+// needs 64 VGPRs and runs 8; with SLP it needed 74, i.e. 6 waves:
+// CBbunny shade 101 -> 105 ms)
 #ifndef PT_SHADE_ATTR
 #define PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(7, 8)))
 #endif
