@@ -2,12 +2,21 @@
 // CudaRenderer::loadScene implements inline (src/cudaRenderer.cu:1679-1842).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 
 #include "scene_internal.h"
 
 using ptscene::Scene;
+
+// Leaf size of the host SAH build: the reference's 32 (BVHAccel(prims, 32));
+// PT_MAX_LEAF overrides it for experiments (hits do not depend on the tree).
+static size_t host_max_leaf() {
+  const char* e = getenv("PT_MAX_LEAF");
+  const long v = e ? atol(e) : 0;
+  return v > 0 ? (size_t)v : 32;
+}
 
 namespace ptscene {
 
@@ -88,7 +97,7 @@ int pt_scene_load_dae(const char* path, pt_scene** out, char* errbuf, size_t err
       err = "scene has no primitives";
       ok = false;
     }
-    if (ok) ptscene::build_bvh_and_flatten(sc->s, 32);
+    if (ok) ptscene::build_bvh_and_flatten(sc->s, host_max_leaf());
   } catch (const std::exception& e) {
     err = e.what();
     ok = false;
@@ -149,7 +158,7 @@ int pt_scene_from_triangles(const float* positions, int32_t n_tris, const pt_bsd
     S.have_camera = true;
   }
   try {
-    ptscene::build_bvh_and_flatten(S, 32);
+    ptscene::build_bvh_and_flatten(S, host_max_leaf());
   } catch (const std::exception&) {
     delete sc;
     return PT_E_INVALID;
@@ -168,7 +177,7 @@ int pt_scene_from_mesh(const pt_mesh_desc* md, pt_scene** out) {
     return rc;
   }
   try {
-    ptscene::build_bvh_and_flatten(sc->s, 32);
+    ptscene::build_bvh_and_flatten(sc->s, host_max_leaf());
   } catch (const std::exception&) {
     delete sc;
     return PT_E_INVALID;
