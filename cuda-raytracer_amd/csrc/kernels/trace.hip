@@ -725,9 +725,15 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
 //     child's queue lane with capacity = the parent's count in that lane (the
 //     reference's wOffset + i*rayCount, cu:922 and cu:1384, without the
 //     single-warp scan and the D2H of maxBlocks, cu:2237).
+// Each thread owns SCAN_NPT consecutive nodes of a chunk of 1024 * SCAN_NPT:
+// their counter loads are issued together, and a level that fits one chunk
+// (all but the widest) keeps its counts in registers between the passes.
+constexpr int SCAN_NPT = 2;
 __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, uint32_t lanecap,
                                                      uint32_t out_parity_base, unsigned long long* stats,
                                                      int level, uint32_t* err) {
+  static_assert((TILE & (TILE - 1)) == 0 && (WTILE & (WTILE - 1)) == 0, "item sizes are powers of two");
+  constexpr int CH = 1024 * SCAN_NPT;
   __shared__ uint32_t wsum[16][16];
   __shared__ uint32_t run[16];
   __shared__ uint32_t ctot[16];
@@ -735,23 +741,42 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
   const int tid = threadIdx.x;
   const int wave = tid >> 6, ln = tid & 63;
   const size_t row = (size_t)L.maxln + 1;
+  const bool one = L.nl <= CH;
   if (tid < 16) run[tid] = 0;
 
   // pass 1: snapshot + zero the counters, totals for the mode decision
+  uint32_t cnt[SCAN_NPT][NLANE];
   unsigned long long v = 0, pairs = 0, leafv = 0;
-  for (int k = tid; k < L.nl; k += 1024) {
-    const int node = L.first + k;
-    const bool leaf = A.nodes[node].prim_count > 0;
+  for (int chunk = 0; chunk < L.nl; chunk += CH) {
+    bool leaf[SCAN_NPT];
 #pragma unroll
-    for (int s = 0; s < NLANE; ++s) {
-      const uint32_t c = A.cnt[cnt_idx(node, s)];
-      L.icnt_w[s * row + k] = c;
-      v += c;
-      pairs += c ? 1 : 0;
-      if (leaf) leafv += c;
+    for (int i = 0; i < SCAN_NPT; ++i) {
+      const int k = chunk + tid * SCAN_NPT + i;
+      leaf[i] = false;
+#pragma unroll
+      for (int s = 0; s < NLANE; ++s) cnt[i][s] = 0u;
+      if (k < L.nl) {
+        const int node = L.first + k;
+        leaf[i] = A.nodes[node].prim_count > 0;
+#pragma unroll
+        for (int s = 0; s < NLANE; ++s) cnt[i][s] = A.cnt[cnt_idx(node, s)];
+      }
     }
 #pragma unroll
-    for (int s = 0; s < NLANE; ++s) A.cnt[cnt_idx(node, s)] = 0u;
+    for (int i = 0; i < SCAN_NPT; ++i) {
+      const int k = chunk + tid * SCAN_NPT + i;
+      if (k >= L.nl) continue;
+      const int node = L.first + k;
+#pragma unroll
+      for (int s = 0; s < NLANE; ++s) {
+        const uint32_t c = cnt[i][s];
+        L.icnt_w[s * row + k] = c;
+        v += c;
+        pairs += c ? 1 : 0;
+        if (leaf[i]) leafv += c;
+        A.cnt[cnt_idx(node, s)] = 0u;
+      }
+    }
   }
   v = wave_sum64(v);
   pairs = wave_sum64(pairs);
@@ -773,68 +798,92 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
   // atomic contention), wave items otherwise
   const bool block_mode = V >= (unsigned long long)BLOCK_MODE_RAYS_PER_PAIR * (PAIRS ? PAIRS : 1ull);
   const uint32_t itile = block_mode ? TILE : WTILE;
+  const uint32_t ishift = (uint32_t)__builtin_ctz(itile);
 
-  // pass 2: items and child capacities, block exclusive scan of 16 values
-  for (int chunk = 0; chunk < L.nl; chunk += 1024) {
-    const int k = chunk + tid;
-    const bool act = k < L.nl;
-    const int node = L.first + k;
-    int nch = 0;
-    int child[4] = {-1, -1, -1, -1};
-    if (act && A.nodes[node].prim_count == 0) {
+  // pass 2: items and child capacities (16 values per node: items per lane,
+  // child capacity per lane), thread-sequential over its nodes, then a block
+  // exclusive scan of the thread totals
+  for (int chunk = 0; chunk < L.nl; chunk += CH) {
+    int child[SCAN_NPT][4];
+    uint32_t nch[SCAN_NPT];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        child[c] = A.nodes[node].child[c];
-        nch += child[c] >= 0;
-      }
-    }
-    uint32_t vv[16], cnt8[NLANE];
+    for (int i = 0; i < SCAN_NPT; ++i) {
+      const int k = chunk + tid * SCAN_NPT + i;
+      nch[i] = 0;
 #pragma unroll
-    for (int s = 0; s < NLANE; ++s) {
-      const uint32_t c = act ? L.icnt_w[s * row + k] : 0u;
-      cnt8[s] = c;
-      vv[s] = (c + itile - 1) / itile;  // items
-      vv[8 + s] = c * (uint32_t)nch;    // child capacity
-    }
-    uint32_t incl[16];
+      for (int c = 0; c < 4; ++c) child[i][c] = -1;
+      if (k < L.nl && A.nodes[L.first + k].prim_count == 0) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      uint32_t x = vv[q];
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off, 64);
-        if (ln >= off) x += y;
-      }
-      incl[q] = x;
-      if (ln == 63) wsum[wave][q] = x;
-    }
-    __syncthreads();
-    if (tid < 16) {
-      uint32_t acc = 0;
-      for (int w = 0; w < 16; ++w) {
-        const uint32_t t = wsum[w][tid];
-        wsum[w][tid] = acc;
-        acc += t;
-      }
-      ctot[tid] = acc;
-    }
-    __syncthreads();
-    uint32_t ex[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) ex[q] = run[q] + wsum[wave][q] + incl[q] - vv[q];
-    if (act) {
-#pragma unroll
-      for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + k] = ex[s];
-      uint32_t jj = 0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (child[c] >= 0) {
-#pragma unroll
-          for (int s = 0; s < NLANE; ++s)
-            A.qoff[(size_t)child[c] * NLANE + s] =
-                out_parity_base + (uint32_t)s * lanecap + ex[8 + s] + jj * cnt8[s];
-          jj++;
+        for (int c = 0; c < 4; ++c) {
+          child[i][c] = A.nodes[L.first + k].child[c];
+          nch[i] += child[i][c] >= 0 ? 1u : 0u;
         }
+      }
+      if (!one) {
+#pragma unroll
+        for (int s = 0; s < NLANE; ++s) cnt[i][s] = k < L.nl ? L.icnt_w[s * row + k] : 0u;
+      }
+    }
+    // two halves of 8 values each (items per lane, then child capacity per
+    // lane): half the registers of one 16-value scan
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t tv[NLANE];
+#pragma unroll
+      for (int s = 0; s < NLANE; ++s) {
+        tv[s] = 0;
+#pragma unroll
+        for (int i = 0; i < SCAN_NPT; ++i)
+          tv[s] += h == 0 ? (cnt[i][s] + itile - 1) >> ishift : cnt[i][s] * nch[i];
+      }
+      uint32_t ex[NLANE];
+#pragma unroll
+      for (int s = 0; s < NLANE; ++s) {
+        uint32_t x = tv[s];
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const uint32_t y = __shfl_up(x, off, 64);
+          if (ln >= off) x += y;
+        }
+        ex[s] = x - tv[s];
+        if (ln == 63) wsum[wave][8 * h + s] = x;
+      }
+      __syncthreads();
+      if (tid < NLANE) {
+        uint32_t acc = 0;
+        for (int w = 0; w < 16; ++w) {
+          const uint32_t t = wsum[w][8 * h + tid];
+          wsum[w][8 * h + tid] = acc;
+          acc += t;
+        }
+        ctot[8 * h + tid] = acc;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < NLANE; ++s) ex[s] += run[8 * h + s] + wsum[wave][8 * h + s];
+#pragma unroll
+      for (int i = 0; i < SCAN_NPT; ++i) {
+        const int k = chunk + tid * SCAN_NPT + i;
+        if (k < L.nl) {
+          if (h == 0) {
+#pragma unroll
+            for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + k] = ex[s];
+          } else {
+            uint32_t jj = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              if (child[i][c] >= 0) {
+#pragma unroll
+                for (int s = 0; s < NLANE; ++s)
+                  A.qoff[(size_t)child[i][c] * NLANE + s] =
+                      out_parity_base + (uint32_t)s * lanecap + ex[s] + jj * cnt[i][s];
+                jj++;
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < NLANE; ++s) ex[s] += h == 0 ? (cnt[i][s] + itile - 1) >> ishift : cnt[i][s] * nch[i];
       }
     }
     __syncthreads();
