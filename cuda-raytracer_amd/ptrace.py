@@ -213,7 +213,7 @@ class Scene:
 
     @classmethod
     def from_mesh(cls, positions, bsdfs, normals=None, tri_bsdf=None, spheres=None, sphere_bsdf=None,
-                  light=None, camera=None, gpu_device=None, max_leaf=8):
+                  light=None, camera=None, gpu_device=None, max_leaf=32):
         """General flattened input (pt_scene_from_mesh): triangles (n, 9),
         optional vertex normals (n, 9), per-triangle bsdf ids, spheres (m, 4)
         and a list of pt_bsdf.  gpu_device=k builds the BVH on GPU k

@@ -48,7 +48,7 @@ def _check_layout(sc, max_leaf):
     assert (covered == 1).all()
 
 
-@pytest.mark.parametrize("max_leaf", [4, 8])
+@pytest.mark.parametrize("max_leaf", [4, 8, 32])
 def test_gpu_build_dragon_proxy(gpu_ctx, max_leaf):
     t = time.perf_counter()
     host = scenes.dragon_proxy()
@@ -63,7 +63,7 @@ def test_gpu_build_dragon_proxy(gpu_ctx, max_leaf):
     inv_h = np.empty_like(perm_h)
     inv_h[perm_h] = np.arange(len(perm_h))
     assert np.array_equal(pg.view(np.uint32), ph[inv_h[perm_g]].view(np.uint32))
-    if max_leaf == 8:
+    if max_leaf >= 8:
         _check_layout(sc, max_leaf)
     gpu_ctx.load_scene(sc)
     rays = np.concatenate([camera_rays(d, 20000, seed=37), interior_rays(d, 20000, seed=38)])
