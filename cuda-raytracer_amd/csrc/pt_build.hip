@@ -203,24 +203,42 @@ __device__ __forceinline__ int2 node_range(int v, int n, const int2* __restrict_
   return v >= n - 1 ? make_int2(v - (n - 1), v - (n - 1)) : range[v];
 }
 
-// the wide children (binary node ids) of binary node v; 0 for a wide leaf
+// the wide children (binary node ids) of binary node v; 0 for a wide leaf.
+// Greedy collapse: starting from v's two children, the child with the largest
+// box surface area that is still an internal node of more than max_leaf
+// primitives is replaced by its two children until there are 4 (a Morton tree
+// is often unbalanced: the fixed two-level collapse leaves 3-child nodes).
+__device__ __forceinline__ float box_area(const Box& b) {
+  const float x = b.hi[0] - b.lo[0], y = b.hi[1] - b.lo[1], z = b.hi[2] - b.lo[2];
+  return x * y + y * z + z * x;
+}
 __device__ __forceinline__ int wide_children(int v, int n, int max_leaf, const int2* __restrict__ child,
-                                             const int2* __restrict__ range, int (&out)[4]) {
+                                             const int2* __restrict__ range, const Box* __restrict__ nbox,
+                                             int (&out)[4]) {
   const int2 r = node_range(v, n, range);
   if (v >= n - 1 || r.y - r.x + 1 <= max_leaf) return 0;
-  int m = 0;
   const int2 c = child[v];
-  const int cc[2] = {c.x, c.y};
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int u = cc[h];
-    const int2 ru = node_range(u, n, range);
-    if (u < n - 1 && ru.y - ru.x + 1 > max_leaf) {
-      out[m++] = child[u].x;
-      out[m++] = child[u].y;
-    } else {
-      out[m++] = u;
+  out[0] = c.x;
+  out[1] = c.y;
+  int m = 2;
+  while (m < 4) {
+    int best = -1;
+    float ba = -1.0f;
+    for (int j = 0; j < m; ++j) {
+      const int u = out[j];
+      if (u >= n - 1) continue;
+      const int2 ru = range[u];
+      if (ru.y - ru.x + 1 <= max_leaf) continue;
+      const float a = box_area(nbox[u]);
+      if (a > ba) {
+        ba = a;
+        best = j;
+      }
     }
+    if (best < 0) break;
+    const int2 cu = child[out[best]];
+    out[best] = cu.x;
+    out[m++] = cu.y;
   }
   return m;
 }
@@ -228,11 +246,11 @@ __device__ __forceinline__ int wide_children(int v, int n, int max_leaf, const i
 // 6a. children per frontier node
 __global__ void k_wide_count(const int* __restrict__ front, int m, int n, int max_leaf,
                              const int2* __restrict__ child, const int2* __restrict__ range,
-                             uint32_t* __restrict__ cnt) {
+                             const Box* __restrict__ nbox, uint32_t* __restrict__ cnt) {
   const int f = blockIdx.x * TPB + threadIdx.x;
   if (f >= m) return;
   int out[4];
-  cnt[f] = (uint32_t)wide_children(front[f], n, max_leaf, child, range, out);
+  cnt[f] = (uint32_t)wide_children(front[f], n, max_leaf, child, range, nbox, out);
 }
 
 // 6b. write the level's pt_node records and the next frontier
@@ -244,7 +262,7 @@ __global__ void k_wide_emit(const int* __restrict__ front, int m, int n, int max
   if (f >= m) return;
   const int v = front[f];
   int out[4];
-  const int k = wide_children(v, n, max_leaf, child, range, out);
+  const int k = wide_children(v, n, max_leaf, child, range, nbox, out);
   pt_node d;
   d.level = level;
   d.ref_id = v;
@@ -436,7 +454,8 @@ static int build_on_device(const pt_mesh_desc* md, int max_leaf, ptscene::Scene&
     if (level > 1000) return PT_E_INVALID;
     const dim3 gm((m + TPB - 1) / TPB);
     BCHK(hipMemsetAsync(d_cnt + m, 0, 4, st));
-    hipLaunchKernelGGL(k_wide_count, gm, dim3(TPB), 0, st, d_front, m, n, max_leaf, d_child, d_range, d_cnt);
+    hipLaunchKernelGGL(k_wide_count, gm, dim3(TPB), 0, st, d_front, m, n, max_leaf, d_child, d_range, d_nbox,
+                       d_cnt);
     BCHK(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_cnt, d_off, m + 1, st));
     uint32_t next_m = 0;
     BCHK(hipMemcpyAsync(&next_m, d_off + m, 4, hipMemcpyDeviceToHost, st));
