@@ -1,5 +1,5 @@
-// GPU BVH build: linear BVH on the device, collapsed to
-// the reference's 4-wide, level-major node layout.
+// GPU BVH build: a binary BVH built on the device,
+// collapsed to the reference's 4-wide, level-major node layout.
 //
 // The reference builds on the host (bvh.cpp:48-337: per-node full re-sorts on
 // three axes and a 12-bucket SAH, O(n log^2 n), 0.84 s for CBbunny) and then
@@ -7,8 +7,11 @@
 //   1. primitive boxes and centroids             k_prim_bounds
 //   2. centroid bounds (ordered-int atomics)     k_reduce_bounds
 //   3. 63-bit Morton codes, radix sort           k_morton + hipcub
-//   4. binary radix tree (Karras 2012)           k_karras
-//   5. node boxes bottom-up (arrival counters)   k_bottom_up
+//   4. binary tree: PLOC agglomerative clustering (default, k_ploc_*: mutual
+//      nearest neighbours by union box area in a Morton-order window, then a
+//      depth-first renumbering of the primitives), or the radix tree of
+//      Karras 2012 (PT_GPU_BVH=lbvh; k_karras)
+//   5. node boxes: made by the merges (PLOC) or bottom-up (k_bottom_up)
 //   6. 4-wide collapse, one kernel per level:    k_wide_count / scan / k_wide_emit
 //      a node with <= max_leaf primitives is a leaf; otherwise its wide
 //      children are its binary grandchildren (binary children that are
@@ -25,6 +28,7 @@
 
 #include <cfloat>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -367,6 +371,140 @@ __global__ void k_prim_records(const float* __restrict__ pos, const float* __res
   shading[i] = sh;
 }
 
+// ---- 4'-5'. PLOC: parallel locally-ordered clustering (Meister & Bittner,
+// TVCG 2018) instead of the radix tree.  Clusters start as the primitives in
+// Morton order; in every iteration each cluster finds its nearest neighbour
+// (smallest union box area) among the PLOC_R clusters on either side, mutual
+// nearest neighbours merge into a new internal node, and the cluster list is
+// compacted (order kept).  Pairs compare by (area, lower position, higher
+// position), a strict total order, so the globally closest pair is always
+// mutual and every iteration merges at least once.  Internal node ids count
+// down from n - 2 in creation order (the root, created last, is 0); leaves
+// are n - 1 + Morton position until k_ploc_remap renumbers them to the
+// final depth-first primitive order, in which every node covers a contiguous
+// range (as the radix tree's nodes do).
+#ifndef PT_PLOC_R
+#define PT_PLOC_R 16
+#endif
+constexpr int PLOC_R = PT_PLOC_R;  // search window radius
+
+__device__ __forceinline__ float union_area(const Box& a, const Box& b) {
+  const float x = fmaxf(a.hi[0], b.hi[0]) - fminf(a.lo[0], b.lo[0]);
+  const float y = fmaxf(a.hi[1], b.hi[1]) - fminf(a.lo[1], b.lo[1]);
+  const float z = fmaxf(a.hi[2], b.hi[2]) - fminf(a.lo[2], b.lo[2]);
+  return x * y + y * z + z * x;
+}
+
+__global__ void k_ploc_init(const Box* __restrict__ pbox, const uint32_t* __restrict__ sorted, int n,
+                            int* __restrict__ clus, Box* __restrict__ nbox) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  clus[i] = n - 1 + i;
+  nbox[n - 1 + i] = pbox[sorted[i]];
+}
+
+__global__ void k_ploc_nn(const int* __restrict__ clus, int m, const Box* __restrict__ nbox, int* __restrict__ nn) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= m) return;
+  const Box bi = nbox[clus[i]];
+  int best = -1;
+  float ba = FLT_MAX;
+  const int j0 = max(0, i - PLOC_R), j1 = min(m - 1, i + PLOC_R);
+  // candidates in increasing position: for equal areas the first one found
+  // has the smaller (lower, higher) position pair, so strict < keeps it
+  for (int j = j0; j <= j1; ++j) {
+    if (j == i) continue;
+    const float a = union_area(bi, nbox[clus[j]]);
+    if (a < ba || best < 0) {
+      ba = a;
+      best = j;
+    }
+  }
+  nn[i] = best;
+}
+
+__global__ void k_ploc_flags(const int* __restrict__ nn, int m, uint32_t* __restrict__ lead,
+                             uint32_t* __restrict__ keep) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= m) return;
+  const int j = nn[i];
+  const bool mutual = nn[j] == i;
+  lead[i] = mutual && i < j;
+  keep[i] = !mutual || i < j;
+}
+
+__device__ __forceinline__ uint32_t subtree_prims(int v, int n, const uint32_t* __restrict__ cnt) {
+  return v >= n - 1 ? 1u : cnt[v];
+}
+
+// merges (new node id idbase - rank) and compaction; the last thread writes
+// {clusters left, merges}
+__global__ void k_ploc_merge(const int* __restrict__ clus, const int* __restrict__ nn, int m, int n,
+                             const uint32_t* __restrict__ lead, const uint32_t* __restrict__ lrank,
+                             const uint32_t* __restrict__ keep, const uint32_t* __restrict__ kpos, int idbase,
+                             int2* __restrict__ child, Box* __restrict__ nbox, uint32_t* __restrict__ cnt,
+                             int* __restrict__ clus2, uint32_t* __restrict__ totals) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= m) return;
+  if (i == m - 1) {
+    totals[0] = kpos[i] + keep[i];
+    totals[1] = lrank[i] + lead[i];
+  }
+  if (!keep[i]) return;
+  int c = clus[i];
+  if (lead[i]) {
+    const int a = c, b = clus[nn[i]];
+    const int p = idbase - (int)lrank[i];
+    child[p] = make_int2(a, b);
+    const Box x = nbox[a], y = nbox[b];
+    Box u;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      u.lo[k] = fminf(x.lo[k], y.lo[k]);
+      u.hi[k] = fmaxf(x.hi[k], y.hi[k]);
+    }
+    nbox[p] = u;
+    cnt[p] = subtree_prims(a, n, cnt) + subtree_prims(b, n, cnt);
+    c = p;
+  }
+  clus2[kpos[i]] = c;
+}
+
+// depth-first primitive offsets, top-down over the nodes of one iteration
+// (ids [lo, hi]; their parents were made in later iterations)
+__global__ void k_ploc_offsets(int lo, int hi, int n, const int2* __restrict__ child,
+                               const uint32_t* __restrict__ cnt, uint32_t* __restrict__ start,
+                               int2* __restrict__ range, uint32_t* __restrict__ pos) {
+  const int p = lo + blockIdx.x * TPB + threadIdx.x;
+  if (p > hi) return;
+  const uint32_t s = start[p];
+  range[p] = make_int2((int)s, (int)(s + cnt[p] - 1));
+  const int2 c = child[p];
+  const uint32_t ca = subtree_prims(c.x, n, cnt);
+  if (c.x >= n - 1) pos[c.x - (n - 1)] = s;
+  else start[c.x] = s;
+  if (c.y >= n - 1) pos[c.y - (n - 1)] = s + ca;
+  else start[c.y] = s + ca;
+}
+
+// leaves renumbered to their depth-first position: child links, leaf boxes
+// (into nbox2) and the final primitive order
+__global__ void k_ploc_remap(int n, int2* __restrict__ child, const uint32_t* __restrict__ pos,
+                             const Box* __restrict__ nbox, Box* __restrict__ nbox2,
+                             const uint32_t* __restrict__ sorted, uint32_t* __restrict__ sorted2) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  if (i < n - 1) {
+    int2 c = child[i];
+    if (c.x >= n - 1) c.x = n - 1 + (int)pos[c.x - (n - 1)];
+    if (c.y >= n - 1) c.y = n - 1 + (int)pos[c.y - (n - 1)];
+    child[i] = c;
+  }
+  if (i < n) {
+    nbox2[n - 1 + pos[i]] = nbox[n - 1 + i];
+    sorted2[pos[i]] = sorted[i];
+  }
+}
+
 struct DevBuf {
   std::vector<void*> ptrs;
   ~DevBuf() {
@@ -433,11 +571,61 @@ static int build_on_device(const pt_mesh_desc* md, int max_leaf, ptscene::Scene&
   void* d_tmp = B.alloc<uint8_t>(tmp_bytes);
   if (!d_tmp) return PT_E_HIP;
   BCHK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp_bytes, d_key, d_key2, d_idx, d_idx2, n, 0, 63, st));
-  if (n > 1)
-    hipLaunchKernelGGL(k_karras, dim3((n - 1 + TPB - 1) / TPB), dim3(TPB), 0, st, d_key2, n, d_child, d_range,
-                       d_parent);
-  hipLaunchKernelGGL(k_bottom_up, g, dim3(TPB), 0, st, d_pbox, d_idx2, n, d_child, d_parent, d_nbox, d_arr);
-  hipLaunchKernelGGL(k_prim_records, g, dim3(TPB), 0, st, d_pos, d_nrm, d_tb, n_tris, d_sph, d_sb, d_idx2, n,
+  // binary tree: PLOC (default) or the radix tree (PT_GPU_BVH=lbvh)
+  const char* gb = getenv("PT_GPU_BVH");
+  const bool ploc = n > 1 && !(gb && strcmp(gb, "lbvh") == 0);
+  uint32_t* d_sorted = d_idx2;  // final primitive order
+  if (ploc) {
+    int *d_clus = B.alloc<int>(n), *d_clus2 = B.alloc<int>(n), *d_nn = B.alloc<int>(n);
+    uint32_t *d_lead = B.alloc<uint32_t>(n), *d_lrank = B.alloc<uint32_t>(n), *d_keep = B.alloc<uint32_t>(n),
+             *d_kpos = B.alloc<uint32_t>(n), *d_pcnt = B.alloc<uint32_t>(n), *d_start = B.alloc<uint32_t>(n),
+             *d_ppos = B.alloc<uint32_t>(n), *d_sorted2 = B.alloc<uint32_t>(n), *d_tot = B.alloc<uint32_t>(2);
+    Box* d_nbox2 = B.alloc<Box>(2 * (size_t)n);
+    size_t sb = 0;
+    BCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, d_lead, d_lrank, n, st));
+    void* d_pscan = B.alloc<uint8_t>(sb);
+    if (!d_clus || !d_clus2 || !d_nn || !d_lead || !d_lrank || !d_keep || !d_kpos || !d_pcnt || !d_start ||
+        !d_ppos || !d_sorted2 || !d_tot || !d_nbox2 || !d_pscan)
+      return PT_E_HIP;
+    hipLaunchKernelGGL(k_ploc_init, g, dim3(TPB), 0, st, d_pbox, d_idx2, n, d_clus, d_nbox);
+    std::vector<std::pair<int, int>> made_ranges;  // internal ids made per iteration
+    int m = n, made = 0;
+    while (m > 1) {
+      const dim3 gm((m + TPB - 1) / TPB);
+      hipLaunchKernelGGL(k_ploc_nn, gm, dim3(TPB), 0, st, d_clus, m, d_nbox, d_nn);
+      hipLaunchKernelGGL(k_ploc_flags, gm, dim3(TPB), 0, st, d_nn, m, d_lead, d_keep);
+      BCHK(hipcub::DeviceScan::ExclusiveSum(d_pscan, sb, d_lead, d_lrank, m, st));
+      BCHK(hipcub::DeviceScan::ExclusiveSum(d_pscan, sb, d_keep, d_kpos, m, st));
+      const int idbase = n - 2 - made;
+      hipLaunchKernelGGL(k_ploc_merge, gm, dim3(TPB), 0, st, d_clus, d_nn, m, n, d_lead, d_lrank, d_keep, d_kpos,
+                         idbase, d_child, d_nbox, d_pcnt, d_clus2, d_tot);
+      uint32_t tot[2] = {0, 0};
+      BCHK(hipMemcpyAsync(tot, d_tot, 8, hipMemcpyDeviceToHost, st));
+      BCHK(hipStreamSynchronize(st));
+      BCHK(hipGetLastError());
+      if (tot[1] == 0 || (int)tot[0] >= m) return PT_E_INVALID;  // cannot happen (see above)
+      made_ranges.push_back({idbase - (int)tot[1] + 1, idbase});
+      made += (int)tot[1];
+      m = (int)tot[0];
+      std::swap(d_clus, d_clus2);
+    }
+    if (made != n - 1) return PT_E_INVALID;
+    BCHK(hipMemsetAsync(d_start, 0, 4, st));  // root 0 starts at 0
+    for (size_t t = made_ranges.size(); t-- > 0;) {
+      const int lo = made_ranges[t].first, hi = made_ranges[t].second;
+      hipLaunchKernelGGL(k_ploc_offsets, dim3((hi - lo + 1 + TPB - 1) / TPB), dim3(TPB), 0, st, lo, hi, n, d_child,
+                         d_pcnt, d_start, d_range, d_ppos);
+    }
+    hipLaunchKernelGGL(k_ploc_remap, g, dim3(TPB), 0, st, n, d_child, d_ppos, d_nbox, d_nbox2, d_idx2, d_sorted2);
+    BCHK(hipMemcpyAsync(d_nbox + (n - 1), d_nbox2 + (n - 1), (size_t)n * sizeof(Box), hipMemcpyDeviceToDevice, st));
+    d_sorted = d_sorted2;
+  } else {
+    if (n > 1)
+      hipLaunchKernelGGL(k_karras, dim3((n - 1 + TPB - 1) / TPB), dim3(TPB), 0, st, d_key2, n, d_child, d_range,
+                         d_parent);
+    hipLaunchKernelGGL(k_bottom_up, g, dim3(TPB), 0, st, d_pbox, d_idx2, n, d_child, d_parent, d_nbox, d_arr);
+  }
+  hipLaunchKernelGGL(k_prim_records, g, dim3(TPB), 0, st, d_pos, d_nrm, d_tb, n_tris, d_sph, d_sb, d_sorted, n,
                      d_prims, d_shading);
   BCHK(hipGetLastError());
 
@@ -474,7 +662,7 @@ static int build_on_device(const pt_mesh_desc* md, int max_leaf, ptscene::Scene&
   S.dprims.resize(n);
   S.dshading.resize(n);
   S.dnodes.resize(base);
-  BCHK(hipMemcpyAsync(sorted.data(), d_idx2, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  BCHK(hipMemcpyAsync(sorted.data(), d_sorted, (size_t)n * 4, hipMemcpyDeviceToHost, st));
   BCHK(hipMemcpyAsync(S.dprims.data(), d_prims, (size_t)n * sizeof(pt_prim), hipMemcpyDeviceToHost, st));
   BCHK(hipMemcpyAsync(S.dshading.data(), d_shading, (size_t)n * sizeof(pt_prim_shading), hipMemcpyDeviceToHost,
                       st));
