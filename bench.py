@@ -55,7 +55,7 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scene", default="CBempty", help="headline scene (configs[1] = CBempty)")
-    p.add_argument("--configs", default="CBspheres,CBbunny,dragon_proxy,dragon_proxy_lbvh",
+    p.add_argument("--configs", default="CBspheres,CBbunny,dragon_proxy,dragon_proxy_gpubvh",
                    help="other single-GPU configs measured in the same run ('' = none)")
     p.add_argument("--width", type=int, default=1024)
     p.add_argument("--height", type=int, default=1024)

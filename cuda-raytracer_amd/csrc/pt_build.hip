@@ -530,7 +530,7 @@ using namespace ptb;
     if ((x) != hipSuccess) return PT_E_HIP; \
   } while (0)
 
-static int build_on_device(const pt_mesh_desc* md, int max_leaf, ptscene::Scene& S, hipStream_t st) {
+static int build_on_device(const pt_mesh_desc* md, int max_leaf, int builder, ptscene::Scene& S, hipStream_t st) {
   const int n_tris = md->n_tris, n = md->n_tris + md->n_spheres;
   DevBuf B;
   float* d_pos = B.alloc<float>((size_t)n_tris * 9);
@@ -573,9 +573,8 @@ static int build_on_device(const pt_mesh_desc* md, int max_leaf, ptscene::Scene&
   void* d_tmp = B.alloc<uint8_t>(tmp_bytes);
   if (!d_tmp) return PT_E_HIP;
   BCHK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp_bytes, d_key, d_key2, d_idx, d_idx2, n, 0, 63, st));
-  // binary tree: PLOC (default) or the radix tree (PT_GPU_BVH=lbvh)
-  const char* gb = getenv("PT_GPU_BVH");
-  const bool ploc = n > 1 && !(gb && strcmp(gb, "lbvh") == 0);
+  // binary tree: PLOC or the radix tree
+  const bool ploc = n > 1 && builder == PT_GPU_BVH_PLOC;
   uint32_t* d_sorted = d_idx2;  // final primitive order
   if (ploc) {
     int *d_clus = B.alloc<int>(n), *d_clus2 = B.alloc<int>(n), *d_nn = B.alloc<int>(n);
@@ -679,9 +678,15 @@ static int build_on_device(const pt_mesh_desc* md, int max_leaf, ptscene::Scene&
 
 extern "C" int pt_scene_build_gpu(const pt_mesh_desc* mesh, int32_t device, int32_t max_leaf, pt_scene** out,
                                   double* build_ms) {
+  return pt_scene_build_gpu_ex(mesh, device, max_leaf, PT_GPU_BVH_PLOC, out, build_ms);
+}
+
+extern "C" int pt_scene_build_gpu_ex(const pt_mesh_desc* mesh, int32_t device, int32_t max_leaf, int32_t builder,
+                                     pt_scene** out, double* build_ms) {
   if (!out) return PT_E_INVALID;
   *out = nullptr;
   if (max_leaf < 1 || max_leaf > 64) return PT_E_INVALID;
+  if (builder != PT_GPU_BVH_PLOC && builder != PT_GPU_BVH_LBVH) return PT_E_INVALID;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PT_E_NODEVICE;
   if (device < 0 || device >= ndev) return PT_E_INVALID;
@@ -699,7 +704,7 @@ extern "C" int pt_scene_build_gpu(const pt_mesh_desc* mesh, int32_t device, int3
     return PT_E_HIP;
   }
   const auto t0 = std::chrono::steady_clock::now();
-  rc = build_on_device(mesh, max_leaf, sc->s, st);
+  rc = build_on_device(mesh, max_leaf, builder, sc->s, st);
   const auto t1 = std::chrono::steady_clock::now();
   hipStreamDestroy(st);
   if (rc) {

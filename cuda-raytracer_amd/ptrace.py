@@ -37,6 +37,7 @@ PT_FLAG_REF_SCHEDULE = 0x20      # reference quirk (vi): 2 bounces, NEE 2/2/1 we
 PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION = 0, 1, 2, 3
 PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT = 0, 1, 2
 PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1
+PT_GPU_BVH_PLOC, PT_GPU_BVH_LBVH = 0, 1
 PT_POST_PROCESS_THRESHOLD = 32
 
 
@@ -110,7 +111,7 @@ class pt_mesh_desc(C.Structure):
 
 # every symbol include/pt_api.h declares (tests check the library exports them)
 API_SYMBOLS = [
-    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_build_gpu", "pt_scene_camera_scotty", "pt_scene_free", "pt_scene_get_desc",
+    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_build_gpu", "pt_scene_build_gpu_ex", "pt_scene_camera_scotty", "pt_scene_free", "pt_scene_get_desc",
     "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
     "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect",
@@ -139,6 +140,8 @@ def _load():
                                               C.POINTER(pt_light), C.POINTER(pt_camera), C.POINTER(P)]),
         "pt_scene_from_mesh": (C.c_int, [C.POINTER(pt_mesh_desc), C.POINTER(P)]),
         "pt_scene_build_gpu": (C.c_int, [C.POINTER(pt_mesh_desc), I32, I32, C.POINTER(P), C.POINTER(C.c_double)]),
+        "pt_scene_build_gpu_ex": (C.c_int, [C.POINTER(pt_mesh_desc), I32, I32, I32, C.POINTER(P),
+                                            C.POINTER(C.c_double)]),
         "pt_scene_camera_scotty": (C.c_int, [P, I32, I32, C.POINTER(pt_camera)]),
         "pt_scene_free": (None, [P]),
         "pt_median_filter": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_float), I32, I32]),
@@ -213,11 +216,12 @@ class Scene:
 
     @classmethod
     def from_mesh(cls, positions, bsdfs, normals=None, tri_bsdf=None, spheres=None, sphere_bsdf=None,
-                  light=None, camera=None, gpu_device=None, max_leaf=32):
+                  light=None, camera=None, gpu_device=None, max_leaf=32, builder="ploc"):
         """General flattened input (pt_scene_from_mesh): triangles (n, 9),
         optional vertex normals (n, 9), per-triangle bsdf ids, spheres (m, 4)
         and a list of pt_bsdf.  gpu_device=k builds the BVH on GPU k
-        (pt_scene_build_gpu, wide leaves of <= max_leaf primitives)."""
+        (pt_scene_build_gpu_ex, wide leaves of <= max_leaf primitives;
+        builder "ploc" or "lbvh")."""
         keep = []
 
         def arr(a, dt, k):
@@ -250,7 +254,8 @@ class Scene:
             rc = LIB.pt_scene_from_mesh(C.byref(m), C.byref(h))
         else:
             ms = C.c_double()
-            rc = LIB.pt_scene_build_gpu(C.byref(m), gpu_device, max_leaf, C.byref(h), C.byref(ms))
+            b = {"ploc": PT_GPU_BVH_PLOC, "lbvh": PT_GPU_BVH_LBVH}[builder]
+            rc = LIB.pt_scene_build_gpu_ex(C.byref(m), gpu_device, max_leaf, b, C.byref(h), C.byref(ms))
         if rc != PT_OK:
             raise PTError(rc, "pt_scene_from_mesh failed" if gpu_device is None else "pt_scene_build_gpu failed")
         sc = cls(h)

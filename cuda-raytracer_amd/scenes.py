@@ -9,7 +9,8 @@ CBbunny.npz): the Cornell box walls and area light once, three copies of the
 side by side on the floor) and a tessellated mirror sphere (60 x 120 UV
 sphere, 14,160 triangles) under the light: 99,900 triangles in total, run
 through the same reference BVH build (pt_scene_from_mesh) or, as
-"dragon_proxy_lbvh", through the GPU build (pt_scene_build_gpu).
+"dragon_proxy_gpubvh", through the GPU build (pt_scene_build_gpu: PLOC
+clustering; "dragon_proxy_lbvh" is the same scene with the radix tree).
 """
 import math
 from pathlib import Path
@@ -94,20 +95,23 @@ def dragon_proxy_arrays():
     return (np.concatenate(out_p), np.concatenate(out_n), np.concatenate(out_b), bsdfs, light, camera)
 
 
-def dragon_proxy(gpu_device=None, max_leaf=32):
+def dragon_proxy(gpu_device=None, max_leaf=32, builder="ploc"):
     """The ~100k-triangle config-4/5 scene as a ptrace.Scene: the reference's
-    host SAH build, or (gpu_device=k) the GPU linear BVH build with wide
-    leaves of <= max_leaf primitives (32, the reference's leaf size: 5,073
-    Mrays/s vs 4,918 at 16 and 4,556 at 8 on the dragon proxy)."""
+    host SAH build, or (gpu_device=k) the GPU build ("ploc" clustering or the
+    "lbvh" radix tree) with wide leaves of <= max_leaf primitives (32, the
+    reference's leaf size; the radix tree: 5,073 Mrays/s vs 4,918 at 16 and
+    4,556 at 8 on the dragon proxy)."""
     pos, nrm, tb, bsdfs, light, camera = dragon_proxy_arrays()
     return ptrace.Scene.from_mesh(pos, bsdfs, normals=nrm, tri_bsdf=tb, light=light, camera=camera,
-                                  gpu_device=gpu_device, max_leaf=max_leaf)
+                                  gpu_device=gpu_device, max_leaf=max_leaf, builder=builder)
 
 
 def load(name):
     """A bench/test workload by name: a committed fixture or a synthetic scene."""
     if name == "dragon_proxy":
         return dragon_proxy()
-    if name == "dragon_proxy_lbvh":
+    if name == "dragon_proxy_gpubvh":
         return dragon_proxy(gpu_device=0)
+    if name == "dragon_proxy_lbvh":
+        return dragon_proxy(gpu_device=0, builder="lbvh")
     return ptrace.ArrayScene.load(FIXTURES / f"{name}.npz")

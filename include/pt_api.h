@@ -192,12 +192,17 @@ typedef struct pt_mesh_desc {
   const pt_camera* camera;  /* NULL: default                                  */
 } pt_mesh_desc;
 int pt_scene_from_mesh(const pt_mesh_desc* mesh, pt_scene** out);
-/* The same input built on GPU `device`: Morton-ordered
- * linear BVH collapsed to the 4-wide, level-major layout (wide leaves hold
+/* The same input built on GPU `device`: a binary BVH
+ * on the device collapsed to the 4-wide, level-major layout (wide leaves hold
  * <= max_leaf primitives; the reference's host SAH build, bvh.cpp:48-337, is
- * pt_scene_from_mesh).  *build_ms (optional) receives the build's wall time. */
+ * pt_scene_from_mesh).  *build_ms (optional) receives the build's wall time.
+ * pt_scene_build_gpu uses PT_GPU_BVH_PLOC. */
+#define PT_GPU_BVH_PLOC 0 /* agglomerative clustering in Morton order (PLOC) */
+#define PT_GPU_BVH_LBVH 1 /* Karras radix tree over Morton codes            */
 int pt_scene_build_gpu(const pt_mesh_desc* mesh, int32_t device, int32_t max_leaf, pt_scene** out,
                        double* build_ms);
+int pt_scene_build_gpu_ex(const pt_mesh_desc* mesh, int32_t device, int32_t max_leaf, int32_t builder,
+                          pt_scene** out, double* build_ms);
 /* The Scotty3D framing of a COLLADA scene's camera (SURVEY §8(a) parity
  * decision vii, camera=scotty): Application::load places the camera at the
  * scene bbox centroid + 3 x half the bbox diagonal along the COLLADA view

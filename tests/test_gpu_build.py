@@ -48,12 +48,12 @@ def _check_layout(sc, max_leaf):
     assert (covered == 1).all()
 
 
-@pytest.mark.parametrize("max_leaf", [4, 8, 32])
-def test_gpu_build_dragon_proxy(gpu_ctx, max_leaf):
+@pytest.mark.parametrize("max_leaf,builder", [(4, "ploc"), (8, "ploc"), (32, "ploc"), (8, "lbvh"), (32, "lbvh")])
+def test_gpu_build_dragon_proxy(gpu_ctx, max_leaf, builder):
     t = time.perf_counter()
     host = scenes.dragon_proxy()
     host_s = time.perf_counter() - t
-    sc = scenes.dragon_proxy(gpu_device=0, max_leaf=max_leaf)
+    sc = scenes.dragon_proxy(gpu_device=0, max_leaf=max_leaf, builder=builder)
     d = sc.desc()
     assert d.n_prims == host.desc().n_prims
     # same primitive records, permuted
@@ -85,15 +85,18 @@ def test_gpu_build_small_and_spheres(gpu_ctx):
     for k in range(3):
         b.albedo[k] = 0.5
     rng = np.random.default_rng(9)
-    for n_tris, n_sph in [(1, 0), (0, 1), (2, 3), (37, 5), (5000, 0)]:
+    cases = [(1, 0, False), (0, 1, False), (2, 3, False), (37, 5, False), (5000, 0, False), (300, 0, True)]
+    for (n_tris, n_sph, dup), builder in [(c, bld) for c in cases for bld in ("ploc", "lbvh")]:
         tris = None
         if n_tris:  # small triangles scattered in the box (big ones only for the tiny cases)
             size = 2.0 if n_tris < 100 else 0.15
             v0 = rng.random((n_tris, 1, 3), dtype=np.float32) * 4 - 2
             tris = (v0 + (rng.random((n_tris, 3, 3), dtype=np.float32) - 0.5) * size).reshape(n_tris, 9)
+            if dup:  # groups of identical triangles: equal boxes, equal merge costs
+                tris = np.repeat(tris[: n_tris // 10], 10, axis=0)
         sph = np.concatenate([rng.random((n_sph, 3), dtype=np.float32) * 4 - 2,
                               rng.random((n_sph, 1), dtype=np.float32) * 0.3 + 0.05], axis=1) if n_sph else None
-        sc = ptrace.Scene.from_mesh(tris, [b], spheres=sph, gpu_device=0, max_leaf=4)
+        sc = ptrace.Scene.from_mesh(tris, [b], spheres=sph, gpu_device=0, max_leaf=4, builder=builder)
         d = sc.desc()
         assert d.n_prims == n_tris + n_sph
         _check_layout(sc, 4)
