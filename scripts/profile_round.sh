@@ -10,7 +10,7 @@ echo "bench ok"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
   python bench.py --steps 1 --warmup 0 --no-cpu > gpurun_out/prof.log 2>&1 || { echo "rocprof rc=$?"; exit 1; }
 echo "rocprof ok"
-for sc in ${PMC_SCENES:-CBempty CBspheres CBbunny dragon_proxy}; do
+for sc in ${PMC_SCENES:-CBempty CBspheres CBbunny dragon_proxy dragon_proxy_gpubvh}; do
   TAG=$sc PMC_ARGS="--scene $sc --configs none" PASSES="FETCH_SIZE;WRITE_SIZE" bash scripts/pmc.sh || exit 1
 done
 echo "pmc ok"
