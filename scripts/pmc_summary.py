@@ -16,11 +16,12 @@ from collections import defaultdict
 
 
 def short(name):
-    """pt::k_shade_push<16, 1>(pt::ShadeArgs) -> k_shade_push"""
-    n = name.split("(")[0].replace("pt::", "")
+    """pt::k_shade_push<16, 1>(pt::ShadeArgs) -> k_shade_push (also for
+    kernels in an anonymous namespace: "(anonymous namespace)::pt::...")"""
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     if n.startswith("void "):
         n = n[5:]
-    return n.split("<")[0].strip()
+    return n.split("<")[0].strip().split("::")[-1]
 
 
 def main():
