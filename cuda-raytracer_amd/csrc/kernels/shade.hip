@@ -292,8 +292,9 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
             const float c = front ? cosi : cost;
             const float m = 1.0f - c;
             const float F = r0 + (1.0f - r0) * (((m * m) * (m * m)) * m);
-            const u4 u2 = rng<M64>(S.seed, g, sidx, vtx, 1);
-            refl = u01(u2.x) < F;
+            // u.x: a glass vertex takes no NEE sample, so the vertex's first
+            // Philox word is free (no second Philox call in a divergent branch)
+            refl = u01(u.x) < F;
           }
           if (refl) {
             const float dn = dot(d, n);

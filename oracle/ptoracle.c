@@ -478,8 +478,7 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
         float c = front ? cosi : cost;
         float m = 1.0f - c;
         float F = r0 + (1.0f - r0) * (((m * m) * (m * m)) * m);
-        u4 r2 = rng(J->seed, g, s, vtx, 1);
-        refl = u01(r2.v[0]) < F;
+        refl = u01(r.v[0]) < F; /* the vertex's first word: no NEE at glass */
       }
       if (refl) {
         float dd = dot(d, n);
