@@ -66,12 +66,13 @@ __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]);
 __device__ __forceinline__ f3 xyz(float4 a) { return mk(a.x, a.y, a.z); }
 
 // Camera ray of path p (pixel g = pix_of[p % npix], sample sample_base + p / npix).
+template <bool M64 = false>
 __device__ __forceinline__ f3 camera_dir(const ShadeArgs& S, uint32_t p, uint32_t& g) {
   const uint32_t j = udiv_q(p, S.div_npix), q = p - j * S.npix;
   g = S.pix_of[q];
   const uint32_t row = udiv_q(g, S.div_width), col = g - row * (uint32_t)S.width;
   const uint32_t s = S.sample_base + j;
-  const u4 u = rng(S.seed, g, s, 0, 0);
+  const u4 u = rng<M64>(S.seed, g, s, 0, 0);
   // cu:338-354: ss = (x + u, y + v); k = ((ss.y/W)-.5, -((ss.x/H)-.5), 1) / |k|
   float ssx = (float)row + u01(u.x);
   float ssy = (float)col + u01(u.y);
@@ -758,7 +759,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       if (!active && r < avail) {
         p = next + r;
         active = true;
-        const f3 dir = camera_dir(S, p, st.g);
+        const f3 dir = camera_dir<PT_PATH_MAD64>(S, p, st.g);
         st.T = mk(1.0f, 1.0f, 1.0f);
         st.L = mk(0.0f, 0.0f, 0.0f);
         st.flags = F_EXT | (1u << 8);
