@@ -25,11 +25,15 @@ constexpr uint32_t PT_PRIM_NONE = 0xFFFFFFFFu;
 constexpr int TPB = 256;          // threads per workgroup (4 waves)
 constexpr int RPT = 4;            // rays per thread in a traversal item
 constexpr int TILE = TPB * RPT;   // rays per traversal item
+// rays per lane of a wave item (2: same, 8: -30 % on the dragon proxy)
 #ifndef PT_RPTW
 #define PT_RPTW 4
 #endif
+// a level runs 1024-ray workgroup items when its (node, lane) queues hold
+// this many rays on average, wave items otherwise (dragon proxy levels: 512:
+// 135 ms, 1024: 130, 4096: 130, 16384: 131, wave items only: 132)
 #ifndef PT_BLOCK_MODE_RAYS
-#define PT_BLOCK_MODE_RAYS 512
+#define PT_BLOCK_MODE_RAYS 4096
 #endif
 // level-kernel workgroups: 16384 (vs 8192: dragon proxy levels -4 %; 2048
 // -15 %, 32768 within noise)
