@@ -188,7 +188,10 @@ static constexpr uint32_t DEFAULT_BATCH_PATHS = 36u << 20;
 // paths per chunk (per-path radiance buffer: 16 B each); POLL_GROUP passes
 // are queued between two reads of the finished-path count
 static constexpr uint32_t CHUNK_PATHS = 1u << 28;
-static constexpr int POLL_GROUP = 4;
+#ifndef PT_POLL_GROUP
+#define PT_POLL_GROUP 4
+#endif
+static constexpr int POLL_GROUP = PT_POLL_GROUP;
 // ray-id queues hold ID_FACTOR x qfactor ids per ray slot and parity half
 // (the entry queues qfactor entries of 32 B)
 static constexpr size_t ID_FACTOR = 6;
