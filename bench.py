@@ -27,6 +27,9 @@ instrumented frame (the headline frames run without events):
     in registers, no HBM stream): VALU-bound, algorithmic FP32 operations of
     the primitive tests (69 per ray-triangle test, 20 per ray-sphere test,
     every primitive of the leaf per ray) against the 157.3 TFLOP/s vector peak.
+Each workload also reports "ms_1spp" (one 1-spp frame, outside the timed
+steps) and, under "trace", the traversal passes of a frame and ms per pass
+(SURVEY §8(d)).
 "traffic" is HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x 2 +
 WRITE_SIZE, MI355X_MICROARCH.md) when a matching summary is committed under
 profiles/ (scripts/pmc.sh, scripts/pmc_summary.py), else null.
@@ -172,6 +175,15 @@ def run_workload(name, args, ctx, rank, world, dev, dist):
         torch.cuda.synchronize()
         instrumented_ms = (time.perf_counter() - t1) * 1e3
     st = ctx.stats()
+    # one 1-spp frame of the same workload (outside the timed
+    # steps; this rank's tiles, no gather)
+    ctx.clear()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    ctx.render(args.width, args.height, 1, max_bounces=args.bounces, seed=args.seed, batch_paths=args.batch,
+               tile_size=args.tile, rank=rank, nranks=world)
+    torch.cuda.synchronize()
+    ms_1spp = (time.perf_counter() - t2) * 1e3
     lvl_ms = sum(st.ms_level[l] for l in range(1, 16))
     V = [st.level_visits[l] for l in range(16)]
     lvl_bytes = sum(32 * V[l] for l in range(1, 16)) + sum(4 * V[l] for l in range(2, 16))
@@ -233,8 +245,11 @@ def run_workload(name, args, ctx, rank, world, dev, dist):
                 "gpu_build_ms": round(getattr(scene, "build_ms", 0.0), 2) or None},
         "roofline": roof,
         "roofline_other": others,
+        "ms_1spp": round(ms_1spp, 2),
         "trace": {"visits_per_ray": round(st.visits / max(1, st.rays), 2),
                   "instrumented_frame_ms": None if instrumented_ms is None else round(instrumented_ms, 2),
+                  "passes": int(st.passes),
+                  "ms_per_pass": None if instrumented_ms is None else round(instrumented_ms / max(1, st.passes), 3),
                   "ms_path": round(st.ms_path, 1), "ms_trace": round(st.ms_trace, 1),
                   "ms_shade": round(st.ms_shade, 1), "ms_shade_push": round(st.ms_shade_push, 1),
                   "ms_root": round(st.ms_root, 1),
@@ -298,6 +313,7 @@ def main():
                        "max_bounces": args.bounces, "batch_paths": head["batch_paths"],
                        "parallelism": f"tiles{args.tile}x{world}"},
             "ms_per_frame": head["ms_per_frame"],
+            "ms_1spp": head["ms_1spp"],
             "rays_per_frame": head["rays_per_frame"],
             "roofline": head["roofline"],
             "scene_build_ms": head["scene_build_ms"],
