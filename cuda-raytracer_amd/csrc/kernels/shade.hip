@@ -657,14 +657,18 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
   int bp = -1;
   const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * 6);
   for (int k = 0; k < pcount; ++k, P += 6) {
-    const float4 q0 = f4(P[0]), q1 = f4(P[1]);
+    // the whole 96-B record in one scalar round trip: the empty use pins the
+    // loads above the sphere/triangle branch, which the compiler would wait on
+    // before issuing the rest (CBempty +0.8 %, CBspheres +0.4 %)
+    const float4 q0 = f4(P[0]), q1 = f4(P[1]), q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
+    asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q2.x), "s"(q3.x), "s"(q4.x), "s"(q5.x));
     float tt;
     if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
       tt = sphere_test(r.o, r.d, q0, q1);
     } else {
       // (a tri_outside pre-test does not pay here: extension rays of one wave
       // rarely all miss a plane, measured -7 % on CBempty)
-      tt = tri_test(r.o, r.d, q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), bt);
+      tt = tri_test(r.o, r.d, q0, q1, q2, q3, q4, q5, bt);
     }
     if (tt >= 0.0f && (tt < bt || (tt == bt && bp < 0))) {
       bt = tt;
@@ -682,12 +686,14 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
   const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * 6);
   bool hit = false;
   for (int k = 0; k < pcount; ++k, P += 6) {
-    const float4 q0 = f4(P[0]), q1 = f4(P[1]);
+    // q0, q1 and q3 (the pre-test's operands) in one round trip; loading all
+    // six here as well measured -0.7 % (CBempty, CBspheres)
+    const float4 q0 = f4(P[0]), q1 = f4(P[1]), q3 = f4(P[3]);
+    asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q3.x));
     float tt = -1.0f;
     if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
       tt = sphere_test(r.o, r.d, q0, q1);
     } else {
-      const float4 q3 = f4(P[3]);
       const float ndd = fdot(q3.x, q3.y, q3.z, r.d.x, r.d.y, r.d.z);
       const float num = q1.w - fdot(q3.x, q3.y, q3.z, r.o.x, r.o.y, r.o.z);
       if (!tri_outside(ndd, num, r.tmax)) tt = tri_test(r.o, r.d, q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), r.tmax);
