@@ -72,6 +72,8 @@ def parse():
     p.add_argument("--config5", choices=["auto", "on", "off"], default="auto",
                    help="also run BASELINE config 5 (dragon proxy, 2048x2048, 1024 spp, tiles over all ranks); "
                         "auto = when n_gpus >= 8")
+    p.add_argument("--no-1spp", action="store_true",
+                   help="skip the ms_1spp frame (profiler runs: keeps per-launch averages to full frames)")
     p.add_argument("--stats-in-timed", action="store_true",
                    help="record per-kernel HIP events inside the timed steps (default: one extra instrumented frame)")
     return p.parse_args()
@@ -177,13 +179,15 @@ def run_workload(name, args, ctx, rank, world, dev, dist):
     st = ctx.stats()
     # one 1-spp frame of the same workload (outside the timed
     # steps; this rank's tiles, no gather)
-    ctx.clear()
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    ctx.render(args.width, args.height, 1, max_bounces=args.bounces, seed=args.seed, batch_paths=args.batch,
-               tile_size=args.tile, rank=rank, nranks=world)
-    torch.cuda.synchronize()
-    ms_1spp = (time.perf_counter() - t2) * 1e3
+    ms_1spp = None
+    if not args.no_1spp:
+        ctx.clear()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        ctx.render(args.width, args.height, 1, max_bounces=args.bounces, seed=args.seed, batch_paths=args.batch,
+                   tile_size=args.tile, rank=rank, nranks=world)
+        torch.cuda.synchronize()
+        ms_1spp = (time.perf_counter() - t2) * 1e3
     lvl_ms = sum(st.ms_level[l] for l in range(1, 16))
     V = [st.level_visits[l] for l in range(16)]
     lvl_bytes = sum(32 * V[l] for l in range(1, 16)) + sum(4 * V[l] for l in range(2, 16))
@@ -245,7 +249,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist):
                 "gpu_build_ms": round(getattr(scene, "build_ms", 0.0), 2) or None},
         "roofline": roof,
         "roofline_other": others,
-        "ms_1spp": round(ms_1spp, 2),
+        "ms_1spp": None if ms_1spp is None else round(ms_1spp, 2),
         "trace": {"visits_per_ray": round(st.visits / max(1, st.rays), 2),
                   "instrumented_frame_ms": None if instrumented_ms is None else round(instrumented_ms, 2),
                   "passes": int(st.passes),

@@ -28,5 +28,5 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 900 python bench.py ${BENCH_ARGS:-}
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
-  step rocprof 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu ${PROF_ARGS:-}
+  step rocprof 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu --no-1spp ${PROF_ARGS:-}
 fi
