@@ -104,32 +104,53 @@ struct RayV {
 // from the shading point pt with normal n; (ux, uy) pick the point on an area
 // light.  weight < 0: unweighted (the default schedule); otherwise the
 // reference schedule's per-sample weight (cu:2515-2533).
+// KR: re-read the light from the kernel argument segment at each use (only in
+// a kernel whose first argument is the ShadeArgs): its 16 SGPRs are then not
+// held, and spilled, across the whole path loop.
+template <bool KR>
+__device__ __forceinline__ pt_light light_of(const ShadeArgs& S) {
+  if (KR) {
+    const CPTR(char) kp = (const CPTR(char))__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));  // not loop-invariant for the compiler
+    constexpr int NW = sizeof(pt_light) / 4;
+    const CPTR(uint32_t) q = (const CPTR(uint32_t))(kp + offsetof(ShadeArgs, light));
+    uint32_t w[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) w[i] = q[i];
+    pt_light L;
+    __builtin_memcpy(&L, w, sizeof(L));
+    return L;
+  }
+  return S.light;
+}
+template <bool KR = false>
 __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const f3 alb, const f3 n, const f3 pt,
                                            float ux, float uy, float weight, f3& C, RayV& r) {
-  if (S.light.type == PT_LIGHT_AREA) {
+  const pt_light L = light_of<KR>(S);
+  if (L.type == PT_LIGHT_AREA) {
     const float sx = ux - 0.5f, sy = uy - 0.5f;
-    const f3 pos = ld3(S.light.position), dx = ld3(S.light.dim_x), dy = ld3(S.light.dim_y);
+    const f3 pos = ld3(L.position), dx = ld3(L.dim_x), dy = ld3(L.dim_y);
     const f3 lpt = mk(pos.x + sx * dx.x + sy * dy.x, pos.y + sx * dx.y + sy * dy.y, pos.z + sx * dx.z + sy * dy.z);
     const f3 dv = lpt - pt;
     const float sq = dot(dv, dv);
     const float dist = sqrtf(sq);
     const float inv = 1.0f / dist;
     const f3 w = mk(dv.x * inv, dv.y * inv, dv.z * inv);
-    const float cosl = dot(w, ld3(S.light.direction));
+    const float cosl = dot(w, ld3(L.direction));
     const float cosn = dot(n, w);
     if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
       // cosn / pdf with pdf = sq / (area * -cosl) (solid-angle pdf of the
       // light sample), as one division
-      float scale = ((cosn * (S.light.area * -cosl)) / sq) * INV_PI;
+      float scale = ((cosn * (L.area * -cosl)) / sq) * INV_PI;
       if (weight >= 0.0f) scale = scale * weight;
-      C = mulv(mulv(T, alb), ld3(S.light.radiance)) * scale;
+      C = mulv(mulv(T, alb), ld3(L.radiance)) * scale;
       r.o = pt;
       r.d = w;
       r.tmax = dist - EPS;
       return true;
     }
-  } else if (S.light.type == PT_LIGHT_POINT) {
-    const f3 dv = ld3(S.light.position) - pt;
+  } else if (L.type == PT_LIGHT_POINT) {
+    const f3 dv = ld3(L.position) - pt;
     const float sq = dot(dv, dv);
     const float dist = sqrtf(sq);
     const float inv = 1.0f / dist;
@@ -138,7 +159,7 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
     if (dist > 1e-2f && cosn > 0.0f) {
       float scale = cosn * INV_PI;
       if (weight >= 0.0f) scale = scale * weight;
-      C = mulv(mulv(T, alb), ld3(S.light.radiance)) * scale;
+      C = mulv(mulv(T, alb), ld3(L.radiance)) * scale;
       r.o = pt;
       r.d = w;
       r.tmax = dist - EPS;
@@ -153,7 +174,7 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
 // extension hit (prim != PT_PRIM_NONE at distance t along ext), and produces
 // the next extension ray and/or shadow rays with their pending contributions.
 // NSH = 2 only under PT_FLAG_REF_SCHEDULE (NEE samples 2, 2, 1 per vertex).
-template <int NSH, bool M64 = false>
+template <int NSH, bool M64 = false, bool KR = false>
 __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, PathState& st, const f3 o,
                                              const f3 d, uint32_t prim, float t, const bool (&clear)[NSH],
                                              f3 (&C)[NSH], bool& new_ext, RayV& ext, bool (&new_sh)[NSH],
@@ -244,7 +265,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
                 uy = u01(v.y);
               }
               const float weight = NSH == 2 ? (nee == 2 ? 0.5f : 1.0f) : -1.0f;
-              new_sh[s] = nee_sample(S, T, alb, n, pt, ux, uy, weight, C[s], shr[s]);
+              new_sh[s] = nee_sample<KR>(S, T, alb, n, pt, ux, uy, weight, C[s], shr[s]);
             }
           }
           // BSDF sample
@@ -727,6 +748,12 @@ constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 // 0.6 % of it but spill ~20 VGPRs around the shading code, which turns into
 // ~35 GB of scratch write-back per 1024^2 x 256 spp frame (PMC WRITE_SIZE);
 // 8 waves spill ~60 and lose 10 %.
+// the light re-read from the kernel arguments at each NEE sample (light_of):
+// SGPR spills 34 -> 13, v_readlane reloads 42 -> 13 (CBempty +0.8 %,
+// CBspheres +1.1 %)
+#ifndef PT_PATH_LIGHT_RELOAD
+#define PT_PATH_LIGHT_RELOAD true
+#endif
 #ifndef PT_PATH_WAVES
 #define PT_PATH_WAVES 6
 #endif
@@ -800,7 +827,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       bool new_ext, new_sh[NSH];
       RayV e2, s2[NSH];
       // (the sample index is recomputed, not carried: one register less)
-      shade_vertex<NSH, PT_PATH_MAD64>(S, S.sample_base + udiv_q(p, S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
+      shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD>(S, S.sample_base + udiv_q(p, S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
                         new_sh, s2);
       if (new_ext) ext = e2;
 #pragma unroll
