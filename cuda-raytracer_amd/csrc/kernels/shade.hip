@@ -11,8 +11,15 @@
 // Deviations (all mirrored by oracle/ptoracle.c): per-path radiance
 // accumulator (a miss keeps the light gathered so far); orthonormal frame with
 // a guide that cannot be parallel to n; counter-based Philox streams instead of
-// curand XORWOW; normalised light cosine (cu:422 uses the unnormalised
-// direction); glass, spheres and point lights; parametric bounce count.
+// curand XORWOW; glass, spheres and point lights; parametric bounce count; and
+// in the default arithmetic: normalised camera / BSDF directions, the
+// normalised light cosine (cu:422 uses the unnormalised direction), a
+// one-sided emitter (cosl < -0.01: lights emit along their direction; cu:440
+// tests |cosTheta|), NEE only toward the front of the shading normal (cu:429
+// takes |n.w|), 1/pi = 0.3183099 (cu:272: 0.3183), the flat-triangle normal
+// shortcut.  PT_FLAG_REF_ARITH (template parameter REFA) replaces each of
+// these arithmetic choices by the reference's literal expression (see
+// shade_vertex, nee_sample, camera_dir).
 #include "trace.h"
 
 namespace pt {
@@ -23,6 +30,7 @@ constexpr uint32_t F_SPEC = 4u;    // last scattering was specular
 constexpr uint32_t F_SHADOW2 = 8u; // second shadow ray pending in slot 2N + p (reference schedule)
 __device__ __forceinline__ uint32_t sh_bit(int s) { return s ? F_SHADOW2 : F_SHADOW; }
 constexpr float INV_PI = 0.318309886183790671f;
+constexpr float REF_DIFFUSE_MULT = 0.3183f;  // BSDF_DIFFUSE_MULTIPLIER, cu:272
 constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
 constexpr int SHADE_REC = 5;  // float4 per hit-shading record (ShadeArgs::shade)
 
@@ -66,7 +74,10 @@ __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]);
 __device__ __forceinline__ f3 xyz(float4 a) { return mk(a.x, a.y, a.z); }
 
 // Camera ray of path p (pixel g = pix_of[p % npix], sample sample_base + p / npix).
-template <bool M64 = false>
+// REFA: cu:347-354 literally -- k / length(k) as k * (1 / length(k))
+// (cuda_util.h operator/), dir = k.x left + k.y up + k.z lookAt as an FMA chain,
+// not normalised.
+template <bool M64 = false, bool REFA = false>
 __device__ __forceinline__ f3 camera_dir(const ShadeArgs& S, uint32_t p, uint32_t& g) {
   const uint32_t j = udiv_q(p, S.div_npix), q = p - j * S.npix;
   g = S.pix_of[q];
@@ -79,11 +90,16 @@ __device__ __forceinline__ f3 camera_dir(const ShadeArgs& S, uint32_t p, uint32_
   float kx = ssy / (float)S.width - 0.5f;
   float ky = -(ssx / (float)S.height - 0.5f);
   float kz = 1.0f;
+  const f3 L = ld3(S.cam.left), U = ld3(S.cam.up), K = ld3(S.cam.look_at);
+  if constexpr (REFA) {
+    const float inv = 1.0f / length(mk(kx, ky, kz));
+    const f3 k = mk(kx, ky, kz) * inv;
+    return mk(dot(k, mk(L.x, U.x, K.x)), dot(k, mk(L.y, U.y, K.y)), dot(k, mk(L.z, U.z, K.z)));
+  }
   float len = sqrtf(kx * kx + ky * ky + kz * kz);
   kx = kx / len;
   ky = ky / len;
   kz = kz / len;
-  const f3 L = ld3(S.cam.left), U = ld3(S.cam.up), K = ld3(S.cam.look_at);
   f3 dir = mk(kx * L.x + ky * U.x + kz * K.x, kx * L.y + ky * U.y + kz * K.y, kx * L.z + ky * U.z + kz * K.z);
   return normalize(dir);
 }
@@ -123,10 +139,58 @@ __device__ __forceinline__ pt_light light_of(const ShadeArgs& S) {
   }
   return S.light;
 }
-template <bool KR = false>
+// Shadow-ray tmax of the reference (cu:446, 1279): the light counts when the
+// closest hit t satisfies t > maxT - 1e-3 in double precision (1e-3 is a
+// double literal), i.e. the ray is occluded by any hit t <= D = maxT - 1e-3,
+// and for an fp32 t that is t <= D rounded down to fp32.
+__device__ __forceinline__ float ref_shadow_tmax(float dist) { return __double2float_rd((double)dist - 1e-3); }
+
+template <bool KR = false, bool REFA = false>
 __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const f3 alb, const f3 n, const f3 pt,
                                            float ux, float uy, float weight, f3& C, RayV& r) {
   const pt_light L = light_of<KR>(S);
+  if (REFA && L.type == PT_LIGHT_AREA) {
+    // kernelDirectLightRays, cu:416-446, expression for expression
+    const float sx = ux - 0.5f, sy = uy - 0.5f;
+    const f3 pos = ld3(L.position), dx = ld3(L.dim_x), dy = ld3(L.dim_y);
+    const f3 lpt = mk(__builtin_fmaf(sy, dy.x, __builtin_fmaf(sx, dx.x, pos.x)),
+                      __builtin_fmaf(sy, dy.y, __builtin_fmaf(sx, dx.y, pos.y)),
+                      __builtin_fmaf(sy, dy.z, __builtin_fmaf(sx, dx.z, pos.z)));
+    const f3 dv = lpt - pt;
+    const float cosTheta = dot(dv, ld3(L.direction));  // unnormalised d (cu:422)
+    const float sq = dot(dv, dv);
+    const float dist = sqrtf(sq);
+    const f3 w = dv * (1.0f / dist);
+    const float pdf = sq / (L.area * fabsf(cosTheta));
+    const float fpdf = fabsf(dot(n, w)) / pdf;
+    // dist > 1e-2 and |cosTheta| > 1e-2 are double comparisons: for fp32
+    // values the same as against 1e-2f (no float lies in (1e-2f, 0.01])
+    if (dist > 1e-2f && fabsf(cosTheta) > 1e-2f) {
+      C = mulv(mulv(T, alb) * fpdf, ld3(L.radiance)) * REF_DIFFUSE_MULT * (weight >= 0.0f ? weight : 1.0f);
+      r.o = pt;
+      r.d = w;
+      r.tmax = ref_shadow_tmax(dist);
+      return true;
+    }
+    return false;
+  }
+  if (REFA && L.type == PT_LIGHT_POINT) {
+    // (the reference has no point light, cu:1741 reinterpret_casts every light
+    // to an AreaLight): the same expression with fpdf = |n.w|
+    const f3 dv = ld3(L.position) - pt;
+    const float sq = dot(dv, dv);
+    const float dist = sqrtf(sq);
+    const f3 w = dv * (1.0f / dist);
+    const float fpdf = fabsf(dot(n, w));
+    if (dist > 1e-2f) {
+      C = mulv(mulv(T, alb) * fpdf, ld3(L.radiance)) * REF_DIFFUSE_MULT * (weight >= 0.0f ? weight : 1.0f);
+      r.o = pt;
+      r.d = w;
+      r.tmax = ref_shadow_tmax(dist);
+      return true;
+    }
+    return false;
+  }
   if (L.type == PT_LIGHT_AREA) {
     const float sx = ux - 0.5f, sy = uy - 0.5f;
     const f3 pos = ld3(L.position), dx = ld3(L.dim_x), dy = ld3(L.dim_y);
@@ -174,7 +238,17 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
 // extension hit (prim != PT_PRIM_NONE at distance t along ext), and produces
 // the next extension ray and/or shadow rays with their pending contributions.
 // NSH = 2 only under PT_FLAG_REF_SCHEDULE (NEE samples 2, 2, 1 per vertex).
-template <int NSH, bool M64 = false, bool KR = false>
+// REFA (PT_FLAG_REF_ARITH): the hit record, NEE and BSDF sample are the
+// reference's expressions (cu:1205-1234, 416-446, 570-653): P = o + d t and the
+// barycentric normal blend as FMA chains with no flat-triangle shortcut, pt +=
+// -d 1e-3, an emission BSDF read as a diffuse one whose albedo is its
+// radiance (cu:1705-1711 reinterpret_casts it), every hit adding
+// radiance * importance unless PT_FLAG_NO_EMISSION (REAL_TIME, cu:1242-1246),
+// the unnormalised diffuse direction n z + x dpdu + y dpdv, the mirror
+// direction through the local-frame wi (cu:643-650), origins pt + n 1e-3.
+// The scene must be triangles with diffuse / mirror / emission BSDFs
+// (pt_render refuses spheres and glass under REFA: the reference has neither).
+template <int NSH, bool M64 = false, bool KR = false, bool REFA = false>
 __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, PathState& st, const f3 o,
                                              const f3 d, uint32_t prim, float t, const bool (&clear)[NSH],
                                              f3 (&C)[NSH], bool& new_ext, RayV& ext, bool (&new_sh)[NSH],
@@ -204,7 +278,8 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
   // 2. shade the hit of the extension ray
   if (flags & F_EXT) {
     if (prim != PT_PRIM_NONE) {
-      const f3 P = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+      const f3 P = REFA ? mk(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z))
+                        : mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
       const float4* Q = S.shade + (size_t)prim * SHADE_REC;
       // the whole record in one round trip (a sphere needs only q0)
       const float4 q0 = Q[0], q1 = Q[1], q2 = Q[2], q3 = Q[3], q4 = Q[4];
@@ -215,7 +290,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
         ns = normalize(mk(P.x - q0.x, P.y - q0.y, P.z - q0.z));
       } else {
         const f3 n0 = mk(q1.w, q2.w, q3.x), n1 = mk(q3.y, q3.z, q3.w), n2 = mk(q4.x, q4.y, q4.z);
-        if (q4.w != 0.0f) {
+        if (!REFA && q4.w != 0.0f) {
           // flat triangle (n0 == n1 == n2): the barycentric blend is a
           // positive multiple of n0, so its normalisation is normalize(n0)
           ns = normalize(n0);
@@ -226,23 +301,40 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           float bC = length(cross(A - P, B - P)) / total;
           float bA = length(cross(B - P, Cv - P)) / total;
           float bB = length(cross(Cv - P, A - P)) / total;
-          ns = normalize(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y,
-                            bA * n0.z + bB * n1.z + bC * n2.z));
+          const f3 bw = mk(bA, bB, bC);
+          ns = REFA ? normalize(mk(dot(bw, mk(n0.x, n1.x, n2.x)), dot(bw, mk(n0.y, n1.y, n2.y)),
+                                   dot(bw, mk(n0.z, n1.z, n2.z))))
+                    : normalize(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y,
+                                   bA * n0.z + bB * n1.z + bC * n2.z));
         }
       }
       const bool front = dot(ns, d) < 0.0f;
       const f3 n = front ? ns : mk(-ns.x, -ns.y, -ns.z);  // faces the incoming ray (cu:1222)
-      const f3 pt = P - d * EPS;                          // cu:1224
-      const pt_bsdf B = S.bsdfs[meta & 0x0FFFFFFFu];
-      if (B.type == PT_BSDF_EMISSION) {
+      // cu:1224 (its.pt += -r->d * 1e-3)
+      const f3 pt = REFA ? mk(__builtin_fmaf(-d.x, EPS, P.x), __builtin_fmaf(-d.y, EPS, P.y),
+                              __builtin_fmaf(-d.z, EPS, P.z))
+                         : P - d * EPS;
+      pt_bsdf B = S.bsdfs[meta & 0x0FFFFFFFu];
+      bool emitter = false;
+      if (REFA) {
+        // cu:1243 (without REAL_TIME): its.light = radiance * importance + light
+        const f3 rad = B.type == PT_BSDF_EMISSION ? ld3(B.albedo) : mk(0.f, 0.f, 0.f);
+        if (!(S.flags & PT_FLAG_NO_EMISSION)) {
+          L = mk(__builtin_fmaf(rad.x, T.x, L.x), __builtin_fmaf(rad.y, T.y, L.y), __builtin_fmaf(rad.z, T.z, L.z));
+          emitter = rad.x != 0.0f || rad.y != 0.0f || rad.z != 0.0f;  // cu:436
+        }
+        if (B.type == PT_BSDF_EMISSION) B.type = PT_BSDF_DIFFUSE;  // albedo = radiance (cu:1705-1711)
+      }
+      if (!REFA && B.type == PT_BSDF_EMISSION) {
         if (!(S.flags & PT_FLAG_NO_EMISSION) && (vtx == 1u || spec))
           L = L + mulv(T, ld3(B.albedo));
       } else {
         const u4 u = rng<M64>(S.seed, g, sidx, vtx, 0);
         f3 dpdu, dpdv;
         if (S.flags & PT_FLAG_REF_GUIDE) {
-          // reference quirk (ii): cu:572-574 (NaN when n is (0,-1,0))
-          const f3 guide = (n.y < 1e-4f) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+          // reference quirk (ii): cu:572-574 (NaN when n is (0,-1,0)); n.y <
+          // 1e-4 is a double comparison: n.y <= 1e-4f for an fp32 n.y
+          const f3 guide = (n.y <= 1e-4f) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
           dpdu = normalize(cross(guide, n));
           dpdv = normalize(cross(dpdu, n));
         } else {
@@ -254,7 +346,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           const f3 alb = ld3(B.albedo);
           // next-event estimation toward the scene light (cu:380-481); the
           // reference schedule takes 2, 2, 1 samples at vertices 1, 2, 3
-          const int nee = (NSH == 2 && vtx <= 2u) ? 2 : 1;
+          const int nee = emitter ? 0 : (NSH == 2 && vtx <= 2u) ? 2 : 1;
 #pragma unroll
           for (int s = 0; s < NSH; ++s) {
             if (s < nee) {
@@ -265,7 +357,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
                 uy = u01(v.y);
               }
               const float weight = NSH == 2 ? (nee == 2 ? 0.5f : 1.0f) : -1.0f;
-              new_sh[s] = nee_sample<KR>(S, T, alb, n, pt, ux, uy, weight, C[s], shr[s]);
+              new_sh[s] = nee_sample<KR, REFA>(S, T, alb, n, pt, ux, uy, weight, C[s], shr[s]);
             }
           }
           // BSDF sample
@@ -284,21 +376,41 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
             x = r * cs;
             y = r * sn;
           }
-          d_new = normalize(mk(n.x * z + x * dpdu.x + y * dpdv.x, n.y * z + x * dpdu.y + y * dpdv.y,
-                               n.z * z + x * dpdu.z + y * dpdv.z));
+          if constexpr (REFA) {  // cu:631-637: not normalised
+            d_new = mk(__builtin_fmaf(y, dpdv.x, __builtin_fmaf(x, dpdu.x, n.x * z)),
+                       __builtin_fmaf(y, dpdv.y, __builtin_fmaf(x, dpdu.y, n.y * z)),
+                       __builtin_fmaf(y, dpdv.z, __builtin_fmaf(x, dpdu.z, n.z * z)));
+          } else {
+            d_new = normalize(mk(n.x * z + x * dpdu.x + y * dpdv.x, n.y * z + x * dpdu.y + y * dpdv.y,
+                                 n.z * z + x * dpdu.z + y * dpdv.z));
+          }
           if (S.flags & PT_FLAG_COSINE_DIFFUSE) {
             T = mulv(T, alb);
           } else {
             const float c = fabsf(dot(d_new, n));
             T = mk(((T.x * c) * alb.x) * 2.0f, ((T.y * c) * alb.y) * 2.0f, ((T.z * c) * alb.z) * 2.0f);
           }
-          o_new = pt + n * EPS;  // cu:593
+          o_new = REFA ? mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y),
+                            __builtin_fmaf(n.z, EPS, pt.z))
+                       : pt + n * EPS;  // cu:593
           spec = 0;
         } else if (B.type == PT_BSDF_MIRROR) {
-          const float dn = dot(d, n);
-          d_new = normalize(d - n * (2.0f * dn));
+          if constexpr (REFA) {
+            // cu:1234 wi = normalize(dot(dpdu, -d), dot(dpdv, -d), dot(n, -d));
+            // cu:643-650 wo = (-wi.x, -wi.y, wi.z) back to world space
+            const f3 md = mk(-d.x, -d.y, -d.z);
+            const f3 wi = normalize(mk(dot(dpdu, md), dot(dpdv, md), dot(n, md)));
+            const float wx = -wi.x, wy = -wi.y, wz = wi.z;
+            d_new = mk(__builtin_fmaf(wy, dpdv.x, __builtin_fmaf(wx, dpdu.x, n.x * wz)),
+                       __builtin_fmaf(wy, dpdv.y, __builtin_fmaf(wx, dpdu.y, n.y * wz)),
+                       __builtin_fmaf(wy, dpdv.z, __builtin_fmaf(wx, dpdu.z, n.z * wz)));
+            o_new = mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y), __builtin_fmaf(n.z, EPS, pt.z));
+          } else {
+            const float dn = dot(d, n);
+            d_new = normalize(d - n * (2.0f * dn));
+            o_new = pt + n * EPS;
+          }
           T = mulv(T, ld3(B.albedo));
-          o_new = pt + n * EPS;
           spec = F_SPEC;
         } else {  // PT_BSDF_GLASS (Fresnel-weighted reflect / refract, bsdf.h:187-212)
           const float ior = B.ior;
@@ -360,7 +472,7 @@ constexpr int SLOT_FREE = 0, SLOT_LIVE = 1, SLOT_ENDED = 2;
 // shade_vertex, write the new state and ray records.  Returns the new rays in
 // registers.  A path with nothing left to trace (or `passes` vertices done)
 // writes its radiance to res[P] and frees the slot.
-template <int NSH>
+template <int NSH, bool REFA = false>
 __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& new_ext, RayV& ext,
                                           bool (&new_sh)[NSH], RayV (&shr)[NSH]) {
   new_ext = false;
@@ -401,7 +513,7 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
   const uint32_t prim = (flags & F_EXT) ? __float_as_uint(r1.z) : PT_PRIM_NONE;
   const float t = ext_hit ? r1.w : 0.0f;
   const f3 o = ext_hit ? xyz(r0) : mk(0, 0, 0), d = ext_hit ? mk(r0.w, r1.x, r1.y) : mk(0, 0, 1);
-  shade_vertex<NSH>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
+  shade_vertex<NSH, false, false, REFA>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
   // (vertices done = vtx - 1: the last one resolves shadow rays only)
   const bool ended =
       !(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || ((st.flags >> 8) & 0xffu) - 1u >= (uint32_t)S.passes;
@@ -426,9 +538,10 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
 }
 
 // Start path P in slot p: state and camera ray (kernelPrimaryRays, cu:312-376).
+template <bool REFA = false>
 __device__ __forceinline__ f3 start_path(const ShadeArgs& S, uint32_t p, uint32_t P) {
   uint32_t g;
-  const f3 d = camera_dir(S, P, g);
+  const f3 d = camera_dir<false, REFA>(S, P, g);
   // (the ray record is written by root_pass)
   S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
   S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
@@ -484,7 +597,7 @@ __device__ __forceinline__ int claim_block(const ShadeArgs& S, uint32_t nblocks)
 // be tested against the root -- the producing kernel tests them against the
 // root's targets and pushes their ids into those queues (lane = workgroup & 7).
 // First fill: workgroup b runs block b, slot i its path i.
-template <int NSH>
+template <int NSH, bool REFA>
 __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
   const uint32_t p = blockIdx.x * TPB + threadIdx.x;
@@ -501,11 +614,11 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
     // (records are written by root_pass for the rays it receives; a path's
     // flags say which of its records are meaningful)
     if (live)
-      d[0] = start_path(S, p, base + threadIdx.x);
+      d[0] = start_path<REFA>(S, p, base + threadIdx.x);
     else
       S.ps0[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
   }
-  root_pass<1>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh);
+  root_pass<1, REFA>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh);
   count_rays(S.rcount, live ? 1u : 0u, sh + MAX_ROOT_TARGETS * 8);
 }
 
@@ -521,7 +634,7 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
 #ifndef PT_SHADE_ATTR
 #define PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(7, 8)))
 #endif
-template <int NSH>
+template <int NSH, bool REFA>
 __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
   __shared__ uint32_t s_free[4], s_live[4], s_busy[4], s_next, s_end, s_shaded, s_nb, s_nbn;
@@ -557,7 +670,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
   }
   int state = SLOT_LIVE;
-  if (p < S.N) state = shade_slot<NSH>(S, p, new_ext, ext, new_sh, shr);
+  if (p < S.N) state = shade_slot<NSH, REFA>(S, p, new_ext, ext, new_sh, shr);
   // ---- regeneration: free slots take the next paths in rank order, from the
   // current block and then from a newly claimed one
   const bool fr = p < S.N && state != SLOT_LIVE;
@@ -598,7 +711,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     for (int w = 0; w < wave; ++w) rank += s_free[w];
     const int P = rank < t1 ? (int)(next + rank) : (rank - t1 < s_nbn ? (int)(s_nb + rank - t1) : -1);
     if (P >= 0) {
-      ext = RayV{ld3(S.cam.origin), start_path(S, p, (uint32_t)P), __builtin_inff()};
+      ext = RayV{ld3(S.cam.origin), start_path<REFA>(S, p, (uint32_t)P), __builtin_inff()};
       new_ext = true;
     } else if (state == SLOT_ENDED) {
       S.ps0[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));  // the slot stays free
@@ -625,7 +738,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     anyhit[1 + s] = true;
     n += new_sh[s] ? 1u : 0u;
   }
-  root_pass<1 + NSH>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh);
+  root_pass<1 + NSH, REFA>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh);
   count_rays(S.rcount, n, sh + MAX_ROOT_TARGETS * 8);
 }
 
@@ -672,6 +785,7 @@ __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wst
 // in registers (no ray records, hit words or path state in HBM).  Closest hits
 // use the same primitive tests and tie rule as the leaf code of
 // process_item (trace.hip); results are bit-identical to the wavefront path.
+template <bool REFA>
 __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, int pcount, const RayV& r,
                                              uint32_t& prim, float& t) {
   float bt = r.tmax;
@@ -689,7 +803,7 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
     } else {
       // (a tri_outside pre-test does not pay here: extension rays of one wave
       // rarely all miss a plane, measured -7 % on CBempty)
-      tt = tri_test(r.o, r.d, q0, q1, q2, q3, q4, q5, bt);
+      tt = tri_test<REFA>(r.o, r.d, q0, q1, q2, q3, q4, q5, bt);
     }
     if (tt >= 0.0f && (tt < bt || (tt == bt && bp < 0))) {
       bt = tt;
@@ -703,6 +817,7 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
 // any primitive at t in [0, tmax]; triangles whose plane hit is certainly
 // outside [0, tmax] for every lane (tri_outside: shadow rays toward the light
 // mostly point away from the walls or end before them) cost no division
+template <bool REFA>
 __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, int pcount, const RayV& r) {
   const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * 6);
   bool hit = false;
@@ -717,7 +832,7 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
     } else {
       const float ndd = fdot(q3.x, q3.y, q3.z, r.d.x, r.d.y, r.d.z);
       const float num = q1.w - fdot(q3.x, q3.y, q3.z, r.o.x, r.o.y, r.o.z);
-      if (!tri_outside(ndd, num, r.tmax)) tt = tri_test(r.o, r.d, q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), r.tmax);
+      if (!tri_outside(ndd, num, r.tmax)) tt = tri_test<REFA>(r.o, r.d, q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), r.tmax);
     }
     hit = hit || (tt >= 0.0f && tt <= r.tmax);
     if (!__any(!hit)) break;  // every active lane is occluded
@@ -757,7 +872,9 @@ constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 #ifndef PT_PATH_WAVES
 #define PT_PATH_WAVES 6
 #endif
-template <int NSH>
+// (PT_PATH_LIGHT_RELOAD reads the light from the kernel-argument segment at
+// offsetof(ShadeArgs, light): S must stay this kernel's FIRST parameter)
+template <int NSH, bool REFA>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
     uint32_t* __restrict__ work) {
@@ -794,7 +911,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       if (!active && r < avail) {
         p = next + r;
         active = true;
-        const f3 dir = camera_dir<PT_PATH_MAD64>(S, p, st.g);
+        const f3 dir = camera_dir<PT_PATH_MAD64, REFA>(S, p, st.g);
         st.T = mk(1.0f, 1.0f, 1.0f);
         st.L = mk(0.0f, 0.0f, 0.0f);
         st.flags = F_EXT | (1u << 8);
@@ -812,7 +929,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       float t = 0.0f;
       if (st.flags & F_EXT) {
         // (extension rays have tmax = inf: not carried across iterations)
-        leaf_closest(S.prims, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t);
+        leaf_closest<REFA>(S.prims, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t);
         nrays++;
       }
       bool clear[NSH];
@@ -820,14 +937,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       for (int s = 0; s < NSH; ++s) {
         clear[s] = false;
         if (st.flags & sh_bit(s)) {
-          clear[s] = !leaf_occluded(S.prims, pstart, pcount, shr[s]);
+          clear[s] = !leaf_occluded<REFA>(S.prims, pstart, pcount, shr[s]);
           nrays++;
         }
       }
       bool new_ext, new_sh[NSH];
       RayV e2, s2[NSH];
       // (the sample index is recomputed, not carried: one register less)
-      shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD>(S, S.sample_base + udiv_q(p, S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
+      shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD, REFA>(S, S.sample_base + udiv_q(p, S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
                         new_sh, s2);
       if (new_ext) ext = e2;
 #pragma unroll

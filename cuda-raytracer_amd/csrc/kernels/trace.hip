@@ -48,15 +48,34 @@ namespace pt {
 __device__ __forceinline__ float fdot(float ax, float ay, float az, float bx, float by, float bz) {
   return __builtin_fmaf(az, bz, __builtin_fmaf(ay, by, ax * bx));
 }
+// PT_FLAG_REF_ARITH (REFA): the literal edge test of cu:251-267,
+// dot(N, cross(e_k, P - v_k)) < 0, on the reference-arithmetic primitive
+// records (pt_ctx::d_prims_ref): the edge-normal slots hold the edges
+// e0 = v1 - v0, e1 = v2 - v1, e2 = v0 - v2 and q3 / q1.w hold
+// N = cross(v1 - v0, v2 - v0) and dot(N, v0) in this file's FMA-chain
+// arithmetic (cu:223-237).  The parallel test |N.d| < 1e-6 is a double
+// comparison in the reference (1e-6 is a double literal): for an fp32 x,
+// x < 1e-6 holds exactly when x <= 1e-6f.
+__device__ __forceinline__ float edge_ref(const float4 N, float ex, float ey, float ez, const f3 P, const float4 v) {
+  const f3 C = cross(mk(ex, ey, ez), mk(P.x - v.x, P.y - v.y, P.z - v.z));
+  return fdot(N.x, N.y, N.z, C.x, C.y, C.z);
+}
+template <bool REFA = false>
 __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q0, const float4 q1,
                                           const float4 q2, const float4 q3, const float4 q4,
                                           const float4 q5, const float tbest) {
   float ndd = fdot(q3.x, q3.y, q3.z, d.x, d.y, d.z);
-  if (fabsf(ndd) < 1e-6f) return -1.0f;
+  if (REFA ? fabsf(ndd) <= 1e-6f : fabsf(ndd) < 1e-6f) return -1.0f;
   float t = (q1.w - fdot(q3.x, q3.y, q3.z, o.x, o.y, o.z)) / ndd;
   // t > tbest cannot win (ties need t == tbest): skip the edge tests
   if (t < 0.0f || t > tbest) return -1.0f;
   f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
+  if constexpr (REFA) {
+    if (edge_ref(q3, q2.w, q3.w, q4.w, P, q0) < 0.0f) return -1.0f;
+    if (edge_ref(q3, q4.x, q4.y, q4.z, P, q1) < 0.0f) return -1.0f;
+    if (edge_ref(q3, q5.x, q5.y, q5.z, P, q2) < 0.0f) return -1.0f;
+    return t == 0.0f ? 0.0f : t;
+  }
   // edge 0 (v0 -> v1)
   if (fdot(q2.w, q3.w, q4.w, P.x - q0.x, P.y - q0.y, P.z - q0.z) < 0.0f) return -1.0f;
   // edge 1 (v1 -> v2)
@@ -104,16 +123,25 @@ __device__ __forceinline__ f2v edge_side2(const f3x2& P, const f3x2& v, const f3
   return fma2(m.z, P.z - v.z, fma2(m.y, P.y - v.y, m.x * (P.x - v.x)));
 }
 
-// N: normal, pd: plane offset, v0..v2: vertices, m0..m2: edge normals (pt_prim layout)
+// dot(N, cross(e, P - v)) on two lanes (REFA: edge_ref, element for element)
+__device__ __forceinline__ f2v edge_ref2(const f3x2& N, const f3x2& P, const f3x2& v, const f3x2& e) {
+  const f3x2 w{P.x - v.x, P.y - v.y, P.z - v.z};
+  const f3x2 C{fma2(e.y, w.z, -(e.z * w.y)), fma2(e.z, w.x, -(e.x * w.z)), fma2(e.x, w.y, -(e.y * w.x))};
+  return fdot2(N, C);
+}
+
+// N: normal, pd: plane offset, v0..v2: vertices, m0..m2: edge normals (pt_prim
+// layout; under REFA the edges e0..e2, see tri_test)
+template <bool REFA = false>
 __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const f3x2& N, f2v pd, const f3x2& v0,
                                          const f3x2& v1, const f3x2& v2, const f3x2& m0, const f3x2& m1,
                                          const f3x2& m2, f2v tbest) {
   const f2v ndd = fdot2(N, d);
   const f2v t = (pd - fdot2(N, o)) / ndd;
   const f3x2 P{fma2(t, d.x, o.x), fma2(t, d.y, o.y), fma2(t, d.z, o.z)};
-  const f2v s0 = edge_side2(P, v0, m0);
-  const f2v s1 = edge_side2(P, v1, m1);
-  const f2v s2 = edge_side2(P, v2, m2);
+  const f2v s0 = REFA ? edge_ref2(N, P, v0, m0) : edge_side2(P, v0, m0);
+  const f2v s1 = REFA ? edge_ref2(N, P, v1, m1) : edge_side2(P, v1, m1);
+  const f2v s2 = REFA ? edge_ref2(N, P, v2, m2) : edge_side2(P, v2, m2);
   // t + 0 maps -0 to +0 and leaves every other value unchanged (strict fp:
   // the add is not folded away)
   const f2v tz = t + sp(0.0f);
@@ -121,8 +149,8 @@ __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const f3x
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     // non-short-circuit: every comparison is one v_cmp, combined on the SALU
-    const bool miss = (fabsf(ndd[i]) < 1e-6f) | (t[i] < 0.0f) | (t[i] > tbest[i]) | (s0[i] < 0.0f) |
-                      (s1[i] < 0.0f) | (s2[i] < 0.0f);
+    const bool flat = REFA ? fabsf(ndd[i]) <= 1e-6f : fabsf(ndd[i]) < 1e-6f;
+    const bool miss = flat | (t[i] < 0.0f) | (t[i] > tbest[i]) | (s0[i] < 0.0f) | (s1[i] < 0.0f) | (s2[i] < 0.0f);
     r[i] = miss ? -1.0f : tz[i];
   }
   return r;
@@ -310,7 +338,7 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 //     here (the callers write the empty r1 of invalid slots);
 //  3. a shadow ray (anyhit) occluded by an inline leaf is done: not queued;
 //     the others are pushed into the targets' queues with the tightened tmax.
-template <int R>
+template <int R, bool REFA = false>
 __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T, int lane, const uint32_t (&id)[R],
                                           const f3 (&o)[R], const f3 (&d)[R], const float (&tmax)[R],
                                           const bool (&valid)[R], const bool (&anyhit)[R], uint32_t* sh) {
@@ -352,9 +380,9 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
             const float ndd = fdot(q3.x, q3.y, q3.z, d[j].x, d[j].y, d[j].z);
             const float num = q1.w - fdot(q3.x, q3.y, q3.z, o[j].x, o[j].y, o[j].z);
             tt = -1.0f;
-            if (!tri_outside(ndd, num, bt)) tt = tri_test(o[j], d[j], q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), bt);
+            if (!tri_outside(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), bt);
           } else
-            tt = tri_test(o[j], d[j], q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), bt);
+            tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), bt);
           if (tt >= 0.0f && (tt < bt || (tt == bt && bp < 0))) {
             bt = tt;
             bp = pstart + kk;
@@ -373,7 +401,7 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
   push_children<R, MAX_ROOT_TARGETS>(A, TableTargets{T}, lane, id, o, d, tm, pv, R, sh, false);
 }
 
-template <bool IMPLICIT>
+template <bool IMPLICIT, bool REFA = false>
 __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, uint32_t base, int n, int lane,
                                              uint32_t* sh, bool ids = true, bool out_ids = true) {
   const int tid = threadIdx.x;
@@ -449,7 +477,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 #pragma unroll
         for (int j = 0; j < RPT; j += 2) {
           if (j >= nj) break;
-          const f2v t2 = tri_test2(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
+          const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
                                    e2, f2v{bt[j], bt[j + 1]});
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
@@ -479,6 +507,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 // ---- root pass (level 0) of pt_intersect: implicit queue = slots [r0, r1) ------------
 // Single-leaf trees: the root leaf's primitives against every ray (process_item).
 // Otherwise root_pass: inline leaves, then the root table's targets.
+template <bool REFA>
 __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, uint32_t r0, uint32_t r1,
                                                     unsigned long long* __restrict__ rcount) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
@@ -488,7 +517,7 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, ui
   const int lane = item & (NLANE - 1);
   uint32_t v = 0;
   if (((const CPTR(pt_node))A.nodes)->prim_count > 0) {
-    v = process_item<true>(A, 0, first, n, lane, sh);
+    v = process_item<true, REFA>(A, 0, first, n, lane, sh);
   } else {
     uint32_t id[RPT];
     f3 o[RPT], d[RPT];
@@ -515,7 +544,7 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, ui
         }
       }
     }
-    root_pass<RPT>(A, T, lane, id, o, d, tmax, valid, anyhit, sh);
+    root_pass<RPT, REFA>(A, T, lane, id, o, d, tmax, valid, anyhit, sh);
   }
   // valid-ray count (R of the roofline formula): one fire-and-forget atomic per
   // workgroup into this lane's counter line
@@ -534,6 +563,7 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, ui
 // Levels >= 1 are processed at wave granularity: no LDS, no workgroup barrier,
 // one returning atomic per wave per child.  Deep levels hold many nodes with a
 // few hundred rays each, where 1024-ray workgroup items would run mostly empty.
+template <bool REFA = false>
 __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane, bool ids,
                                              bool out_ids) {
   const uint32_t lid = lane_id();
@@ -585,7 +615,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 #pragma unroll
         for (int j = 0; j < RPTW; j += 2) {
           if (j >= nj) break;
-          const f2v t2 = tri_test2(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
+          const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
                                    e2, f2v{bt[j], bt[j + 1]});
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
@@ -660,6 +690,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 #ifndef PT_LEVEL_ATTR
 #define PT_LEVEL_ATTR __attribute__((amdgpu_waves_per_eu(6, 8)))
 #endif
+template <bool REFA>
 __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, LevelArgs L) {
   const int lane = blockIdx.x & (NLANE - 1);
   const uint32_t lid = lane_id();
@@ -697,7 +728,7 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
       const uint32_t base = __builtin_amdgcn_readfirstlane(s_base);
       const int n = __builtin_amdgcn_readfirstlane(s_n);
       __syncthreads();
-      process_item<false>(A, node, base, n, lane, sh, L.ids != 0, L.out_ids != 0);
+      process_item<false, REFA>(A, node, base, n, lane, sh, L.ids != 0, L.out_ids != 0);
       __syncthreads();
     }
     return;
@@ -721,7 +752,7 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
     const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
     const uint32_t base = A.qoff[(size_t)node * NLANE + lane] + i * WTILE;
     const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
-    process_wave(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane,
+    process_wave<REFA>(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane,
                  L.ids != 0, L.out_ids != 0);
   }
 }

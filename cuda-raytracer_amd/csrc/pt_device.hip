@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -29,8 +30,8 @@
 #include "kernels/post.hip"
 
 // k_shade_push lives in pt_shade.hip (its own compile flags)
-hipError_t pt_launch_shade_push(int nsh, unsigned grid, hipStream_t stream, hipEvent_t e0, hipEvent_t e1,
-                                const void* S);
+hipError_t pt_launch_shade_push(int nsh, bool refa, unsigned grid, hipStream_t stream, hipEvent_t e0,
+                                hipEvent_t e1, const void* S);
 
 using namespace pt;
 
@@ -61,6 +62,9 @@ struct pt_ctx {
   pt_camera camera{};
   pt_node* d_nodes = nullptr;
   float4* d_prims = nullptr;
+  float4* d_prims_ref = nullptr;  // PT_FLAG_REF_ARITH records (ref_prim_records)
+  bool has_sphere = false, has_glass = false;
+  bool refa = false;              // the current render / intersect runs PT_FLAG_REF_ARITH
   float4* d_shade = nullptr;  // hit-shading records (SHADE_REC float4 per primitive)
   pt_bsdf* d_bsdfs = nullptr;
 
@@ -94,7 +98,7 @@ struct pt_ctx {
   uint32_t* d_live = nullptr;  // live slots after a pass group (k_live_sum)
   uint32_t* h_poll = nullptr;  // pinned: {live, err} x 2 poll slots
   hipEvent_t ev_poll[2] = {};
-  int path_grid[2] = {0, 0};   // resident workgroups of k_path_leaf<1>, <2>
+  int path_grid[4] = {0, 0, 0, 0};  // resident workgroups of k_path_leaf<1|2, refa>
 
   // framebuffer
   int fb_w = 0, fb_h = 0, fb_tile = 0, fb_rank = 0, fb_nranks = 0;
@@ -166,7 +170,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 }
 
 static void free_all(pt_ctx* c) {
-  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_shade, c->d_bsdfs,   c->d_ray,
+  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live, c->d_pool,
                   c->d_pix_of, c->d_accum};
@@ -342,7 +346,7 @@ static int set_root_child_offsets(pt_ctx* c) {
 static TraceArgs trace_args(pt_ctx* c) {
   TraceArgs A;
   A.nodes = c->d_nodes;
-  A.prims = c->d_prims;
+  A.prims = c->refa ? c->d_prims_ref : c->d_prims;
   A.ray = c->d_ray;
   A.cnt = c->d_cnt;
   A.qoff = c->d_qoff;
@@ -378,7 +382,10 @@ static int trace_levels(pt_ctx* c) {
     const uint32_t out_base = (uint32_t)(((l + 1) & 1) ? (L.out_ids ? c->qcap : c->qecap) : 0);
     c->launch(pt_ctx::K_SCAN, l, k_scan_level, dim3(1), dim3(1024), A, L, (uint32_t)lanecap, out_base,
               c->d_stats, l, c->d_err);
-    c->launch(pt_ctx::K_LEVEL, l, k_trace_level, dim3(LEVEL_GRID), dim3(TPB), A, L);
+    if (c->refa)
+      c->launch(pt_ctx::K_LEVEL, l, k_trace_level<true>, dim3(LEVEL_GRID), dim3(TPB), A, L);
+    else
+      c->launch(pt_ctx::K_LEVEL, l, k_trace_level<false>, dim3(LEVEL_GRID), dim3(TPB), A, L);
   }
   HIPCHK(c, hipGetLastError());
   c->stats.passes++;
@@ -392,7 +399,10 @@ static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
   const uint32_t items = (r1 - r0 + TILE - 1) / TILE;
   // the (node, lane) counters are zero here: each level's scan re-zeroes them
   // after taking its snapshot (pt_load_scene zeroes them once)
-  c->launch(pt_ctx::K_ROOT, 0, k_trace_root, dim3(items), dim3(TPB), A, c->rt, r0, r1, c->d_rcount);
+  if (c->refa)
+    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<true>, dim3(items), dim3(TPB), A, c->rt, r0, r1, c->d_rcount);
+  else
+    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<false>, dim3(items), dim3(TPB), A, c->rt, r0, r1, c->d_rcount);
   if (c->root_leaf) {
     HIPCHK(c, hipGetLastError());
     c->stats.passes++;
@@ -467,6 +477,47 @@ static int read_device_stats(pt_ctx* c) {
   return PT_OK;
 }
 
+// PT_FLAG_REF_ARITH primitive records (trace.hip tri_test<true>): the
+// operands of intersectRayTriangle computed as the reference does per call
+// (cu:223-237) in the kernels' arithmetic -- N = cross(v1 - v0, v2 - v0) and
+// dot(N, v0) as the FMA chains of ptmath.h -- and the edges e0 = v1 - v0,
+// e1 = v2 - v1, e2 = v0 - v2 in the slots of the edge normals.  Spheres are
+// copied (pt_render refuses them under PT_FLAG_REF_ARITH).
+static std::vector<pt_prim> ref_prim_records(const pt_scene_desc* s) {
+  std::vector<pt_prim> out(s->prims, s->prims + s->n_prims);
+  for (int i = 0; i < s->n_prims; ++i) {
+    float* q = out[i].q;
+    uint32_t meta;
+    memcpy(&meta, &q[3], 4);
+    if ((meta >> 28) != PT_PRIM_TRIANGLE) continue;
+    const float v0[3] = {q[0], q[1], q[2]}, v1[3] = {q[4], q[5], q[6]}, v2[3] = {q[8], q[9], q[10]};
+    float e0[3], v02[3], e1[3], e2[3];
+    for (int k = 0; k < 3; ++k) {
+      e0[k] = v1[k] - v0[k];
+      v02[k] = v2[k] - v0[k];
+      e1[k] = v2[k] - v1[k];
+      e2[k] = v0[k] - v2[k];
+    }
+    const float N[3] = {std::fma(e0[1], v02[2], -(e0[2] * v02[1])), std::fma(e0[2], v02[0], -(e0[0] * v02[2])),
+                        std::fma(e0[0], v02[1], -(e0[1] * v02[0]))};
+    q[7] = std::fma(N[2], v0[2], std::fma(N[1], v0[1], N[0] * v0[0]));
+    q[11] = e0[0];
+    q[12] = N[0];
+    q[13] = N[1];
+    q[14] = N[2];
+    q[15] = e0[1];
+    q[16] = e1[0];
+    q[17] = e1[1];
+    q[18] = e1[2];
+    q[19] = e0[2];
+    q[20] = e2[0];
+    q[21] = e2[1];
+    q[22] = e2[2];
+    q[23] = 0.0f;
+  }
+  return out;
+}
+
 static void build_owned_pixels(pt_ctx* c, int W, int H, int T, int rank, int nranks) {
   c->pix_of.clear();
   const int ntx = (W + T - 1) / T, nty = (H + T - 1) / T;
@@ -521,12 +572,13 @@ int pt_create(pt_ctx** out, int device) {
   hipMemset(c->d_err, 0, 4);
   // k_path_leaf runs persistent waves: one grid of exactly the resident workgroups
   {
-    int ncu = 0, nb1 = 0, nb2 = 0;
+    int ncu = 0, nb[4] = {0, 0, 0, 0};
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb1, k_path_leaf<1>, TPB, 0);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, k_path_leaf<2>, TPB, 0);
-    c->path_grid[0] = std::max(1, ncu * std::max(1, nb1));
-    c->path_grid[1] = std::max(1, ncu * std::max(1, nb2));
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[0], k_path_leaf<1, false>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[1], k_path_leaf<2, false>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[2], k_path_leaf<1, true>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[3], k_path_leaf<2, true>, TPB, 0);
+    for (int i = 0; i < 4; ++i) c->path_grid[i] = std::max(1, ncu * std::max(1, nb[i]));
   }
   *out = c;
   return PT_OK;
@@ -570,14 +622,19 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
       if (nd.child[k] >= s->n_nodes || (nd.child[k] >= 0 && nd.child[k] <= i))
         return fail(c, PT_E_INVALID, "node child out of range / not breadth-first");
   }
+  c->has_sphere = c->has_glass = false;
   for (int i = 0; i < s->n_prims; ++i) {
     uint32_t meta;
     memcpy(&meta, &s->prims[i].q[3], 4);
     if ((int)(meta & 0x0FFFFFFFu) >= s->n_bsdfs) return fail(c, PT_E_INVALID, "primitive bsdf out of range");
+    if ((meta >> 28) == PT_PRIM_SPHERE) c->has_sphere = true;
   }
+  for (int i = 0; i < s->n_bsdfs; ++i)
+    if (s->bsdfs[i].type == PT_BSDF_GLASS) c->has_glass = true;
   build_root_table(c);
   if ((rc = dalloc(c, &c->d_nodes, s->n_nodes))) return rc;
   if ((rc = dalloc(c, &c->d_prims, (size_t)s->n_prims * 6))) return rc;
+  if ((rc = dalloc(c, &c->d_prims_ref, (size_t)s->n_prims * 6))) return rc;
   if ((rc = dalloc(c, &c->d_shade, (size_t)s->n_prims * SHADE_REC))) return rc;
   if ((rc = dalloc(c, &c->d_bsdfs, std::max(1, s->n_bsdfs)))) return rc;
   if ((rc = dalloc(c, &c->d_cnt, (size_t)s->n_nodes * NLANE * CSTRIDE))) return rc;
@@ -587,6 +644,10 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   if ((rc = dalloc(c, &c->d_nitems, 2 * std::max(1, s->n_levels) + NLANE))) return rc;
   HIPCHK(c, hipMemcpy(c->d_nodes, s->nodes, sizeof(pt_node) * s->n_nodes, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_prims, s->prims, sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));
+  {
+    const std::vector<pt_prim> ref = ref_prim_records(s);
+    HIPCHK(c, hipMemcpy(c->d_prims_ref, ref.data(), sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));
+  }
   {
     // {A, meta}{B, n0.x}{C, n0.y}{n0.z, n1}{n2, flat} (shade.hip ShadeArgs::shade)
     std::vector<float4> rec((size_t)s->n_prims * SHADE_REC);
@@ -689,6 +750,9 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   // the reference schedule (cu:2499-2533) casts up to two shadow rays per vertex
   const bool ref_sched = (P->flags & PT_FLAG_REF_SCHEDULE) != 0;
   const uint32_t nsh = ref_sched ? 2u : 1u;
+  c->refa = (P->flags & PT_FLAG_REF_ARITH) != 0;
+  if (c->refa && (c->has_sphere || c->has_glass))
+    return fail(c, PT_E_UNSUPPORTED, "PT_FLAG_REF_ARITH: the reference renders triangles with diffuse/mirror BSDFs only");
   const int max_bounces = ref_sched ? 2 : P->max_bounces;
   const int passes = max_bounces + 2;  // vertices per path at most
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
@@ -708,7 +772,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       c->res_cap = M;
     }
     ShadeArgs S;
-    S.prims = c->d_prims;
+    S.prims = c->refa ? c->d_prims_ref : c->d_prims;
     S.shade = c->d_shade;
     S.bsdfs = c->d_bsdfs;
     S.pix_of = c->d_pix_of;
@@ -737,12 +801,11 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       S.N = M;
       const uint32_t want = (M + 4 * PATH_CHUNK - 1) / (4 * PATH_CHUNK);
       HIPCHK(c, hipMemsetAsync(c->d_work, 0, 4, c->stream));
-      if (nsh == 2)
-        c->launch(pt_ctx::K_PATH, 0, k_path_leaf<2>, dim3(std::min<uint32_t>(want, c->path_grid[1])), dim3(TPB), S,
-                  root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work);
-      else
-        c->launch(pt_ctx::K_PATH, 0, k_path_leaf<1>, dim3(std::min<uint32_t>(want, c->path_grid[0])), dim3(TPB), S,
-                  root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work);
+      const int kv = (nsh == 2 ? 1 : 0) + (c->refa ? 2 : 0);
+      auto kpath = kv == 0 ? k_path_leaf<1, false> : kv == 1 ? k_path_leaf<2, false>
+                 : kv == 2 ? k_path_leaf<1, true> : k_path_leaf<2, true>;
+      c->launch(pt_ctx::K_PATH, 0, kpath, dim3(std::min<uint32_t>(want, c->path_grid[kv])), dim3(TPB), S,
+                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work);
       c->stats.passes += passes;
       if (first) c->stats.batch_paths = (int32_t)M;
     } else {
@@ -782,8 +845,9 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         HIPCHK(c, hipMemcpyAsync(c->d_pool, init.data(), init.size() * 4, hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));  // (init is a host temporary)
       }
-      if (nsh == 1) c->launch(pt_ctx::K_CAM, 0, k_camera_push<1>, grid, dim3(TPB), S);
-      if (nsh == 2) c->launch(pt_ctx::K_CAM, 0, k_camera_push<2>, grid, dim3(TPB), S);
+      auto kcam = c->refa ? (nsh == 2 ? k_camera_push<2, true> : k_camera_push<1, true>)
+                          : (nsh == 2 ? k_camera_push<2, false> : k_camera_push<1, false>);
+      c->launch(pt_ctx::K_CAM, 0, kcam, grid, dim3(TPB), S);
       // passes in groups of POLL_GROUP; the host reads the finished-path count
       // of group g (pinned memory, event) while group g + 1 is already queued
       auto enqueue_group = [&](int g) -> int {
@@ -792,9 +856,9 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
           if (r) return r;
           if (c->timing) {
             const auto e = c->pair(pt_ctx::K_SHADE, 0);
-            HIPCHK(c, pt_launch_shade_push(nsh, grid.x, c->stream, e.first, e.second, &S));
+            HIPCHK(c, pt_launch_shade_push(nsh, c->refa, grid.x, c->stream, e.first, e.second, &S));
           } else {
-            HIPCHK(c, pt_launch_shade_push(nsh, grid.x, c->stream, nullptr, nullptr, &S));
+            HIPCHK(c, pt_launch_shade_push(nsh, c->refa, grid.x, c->stream, nullptr, nullptr, &S));
           }
         }
         HIPCHK(c, hipMemsetAsync(c->d_live, 0, 4, c->stream));
@@ -926,9 +990,14 @@ int pt_owned_pixels(pt_ctx* c, int32_t* n_pixels, int32_t* pixel_index, size_t m
   return PT_OK;
 }
 
-int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) {
+int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) { return pt_intersect_ex(c, rays, n, hits, 0); }
+
+int pt_intersect_ex(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits, uint32_t flags) {
   if (!c || (!rays && n > 0) || (!hits && n > 0) || n < 0) return PT_E_INVALID;
   if (!c->have_scene) return fail(c, PT_E_NOSCENE, "no scene loaded");
+  c->refa = (flags & PT_FLAG_REF_ARITH) != 0;
+  if (c->refa && c->has_sphere)
+    return fail(c, PT_E_UNSUPPORTED, "PT_FLAG_REF_ARITH: the reference intersects triangles only");
   if (n == 0) return PT_OK;
   hipSetDevice(c->device);
   int rc;

@@ -34,6 +34,7 @@ PT_FLAG_STATS = 0x4
 PT_FLAG_REF_DROP_ON_MISS = 0x8   # reference quirk (i)
 PT_FLAG_REF_GUIDE = 0x10         # reference quirk (ii)
 PT_FLAG_REF_SCHEDULE = 0x20      # reference quirk (vi): 2 bounces, NEE 2/2/1 weighted 0.5/0.5/1
+PT_FLAG_REF_ARITH = 0x40         # the reference kernels' literal arithmetic (pt_api.h)
 PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION = 0, 1, 2, 3
 PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT = 0, 1, 2
 PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1
@@ -114,7 +115,7 @@ API_SYMBOLS = [
     "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_build_gpu", "pt_scene_build_gpu_ex", "pt_scene_camera_scotty", "pt_scene_free", "pt_scene_get_desc",
     "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
-    "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect",
+    "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex",
     "pt_get_stats", "pt_reset_stats", "pt_median_filter", "pt_get_display_image", "pt_tonemap",
     "pt_write_png", "pt_write_pfm",
 ]
@@ -164,6 +165,7 @@ def _load():
         "pt_owned_pixels": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32), SZ, C.POINTER(P)]),
         "pt_samples": (C.c_int, [P, C.POINTER(I32)]),
         "pt_intersect": (C.c_int, [P, C.POINTER(C.c_float), I32, C.POINTER(C.c_uint64)]),
+        "pt_intersect_ex": (C.c_int, [P, C.POINTER(C.c_float), I32, C.POINTER(C.c_uint64), U32]),
         "pt_get_stats": (C.c_int, [P, C.POINTER(pt_stats)]),
         "pt_reset_stats": (C.c_int, [P]),
     }
@@ -435,11 +437,15 @@ class Context:
         self._chk(LIB.pt_owned_pixels(self.h, C.byref(n), _ptr(idx, C.c_int32), idx.size, C.byref(dptr)))
         return idx[: n.value], dptr.value
 
-    def intersect(self, rays):
-        """rays: (n, 8) float32 [o.xyz, tmax, d.xyz, 0] -> uint64 hit keys."""
+    def intersect(self, rays, flags=0):
+        """rays: (n, 8) float32 [o.xyz, tmax, d.xyz, 0] -> uint64 hit keys.
+        flags: PT_FLAG_REF_ARITH selects the reference's literal triangle test."""
         rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
         hits = np.zeros(len(rays), dtype=np.uint64)
-        self._chk(LIB.pt_intersect(self.h, _ptr(rays, C.c_float), len(rays), _ptr(hits, C.c_uint64)))
+        if flags:
+            self._chk(LIB.pt_intersect_ex(self.h, _ptr(rays, C.c_float), len(rays), _ptr(hits, C.c_uint64), flags))
+        else:
+            self._chk(LIB.pt_intersect(self.h, _ptr(rays, C.c_float), len(rays), _ptr(hits, C.c_uint64)))
         return hits
 
     def stats(self) -> pt_stats:

@@ -250,6 +250,24 @@ int pt_set_camera(pt_ctx* ctx, const pt_camera* camera);
                                          2 bounces, NEE samples 2, 2, 1 at
                                          vertices 1, 2, 3 weighted 0.5, 0.5, 1;
                                          max_bounces is ignored              */
+#define PT_FLAG_REF_ARITH 0x40u       /* the reference kernels' literal fp32
+                                         arithmetic instead of the build's:
+                                         the edge test dot(N, cross(e_k, P-v_k))
+                                         (cu:251-267), the unnormalised camera
+                                         direction (cu:354), NEE with the
+                                         unnormalised two-sided cosine, |n.w| and
+                                         BSDF_DIFFUSE_MULTIPLIER 0.3183 (cu:416-446,
+                                         272), shadow rays unoccluded when
+                                         t > maxT - 1e-3 in double (cu:1279), the
+                                         barycentric normal without the
+                                         flat-triangle shortcut (cu:1213-1224),
+                                         unnormalised diffuse / local-frame
+                                         mirror directions (cu:631-650), an
+                                         emission BSDF read as diffuse with
+                                         albedo = radiance (cu:1705-1711).
+                                         Triangles with diffuse / mirror /
+                                         emission BSDFs only (PT_E_UNSUPPORTED
+                                         for spheres and glass)              */
 
 typedef struct pt_render_params {
   int32_t width, height;
@@ -310,6 +328,9 @@ int pt_write_pfm(const char* path, const float* rgba, int32_t width, int32_t hei
  * PT_HIT_NONE when nothing is hit with t <= tmax. */
 #define PT_HIT_NONE 0xFFFFFFFFFFFFFFFFull
 int pt_intersect(pt_ctx* ctx, const float* rays, int32_t n, uint64_t* hits);
+/* The same with render flags: PT_FLAG_REF_ARITH selects the reference's
+ * literal triangle test (cu:217-270); other flags are ignored. */
+int pt_intersect_ex(pt_ctx* ctx, const float* rays, int32_t n, uint64_t* hits, uint32_t flags);
 
 typedef struct pt_stats {
   uint64_t rays;      /* R: valid rays entering the root, summed over passes */

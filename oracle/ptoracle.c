@@ -21,6 +21,16 @@
  * reference's streams are not reproducible without the CUDA toolkit
  * (parity unpinned for RNG streams).
  *
+ * PT_FLAG_REF_ARITH selects the reference kernels' literal arithmetic
+ * (pto_tri_ref, camera_dir_ref, nee_ref and the REF branches of
+ * path_radiance): every expression of cu:217-270, 347-354, 416-446, 570-653
+ * and 1205-1234 in source order, with the build's single contraction
+ * convention (a*b + c is fma(a, b, c), so dot = fma(a.z, b.z, fma(a.y, b.y,
+ * a.x*b.x)) and cross = (fma(a.y, b.z, -(a.z*b.y)), ...) -- what nvcc's
+ * default --fmad=true makes of cuda_util.h; the exact contraction nvcc chose
+ * is unknowable here), double-literal comparisons evaluated exactly, and
+ * rsqrtf (an approximate hardware instruction on NVIDIA) as 1/sqrtf.
+ *
  * Every float expression keeps the operation order of the HIP kernels and is
  * compiled with -ffp-contract=off, so per-sample radiance is bit-identical.
  */
@@ -147,6 +157,24 @@ static float pto_tri(v3 o, v3 d, const float* q) {
   if (fdot(q[20], q[21], q[22], P.x - q[8], P.y - q[9], P.z - q[10]) < 0.0f) return -1.0f;
   return t == 0.0f ? 0.0f : t;
 }
+/* intersectRayTriangle, cu:217-270, literally (PT_FLAG_REF_ARITH): N and
+ * dot(N, v0) per call, edge k rejected when dot(N, cross(e_k, P - v_k)) < 0,
+ * the parallel test |N.d| < 1e-6 against the double literal. */
+static float pto_tri_ref(v3 o, v3 d, const float* q) {
+  v3 v0 = mk(q[0], q[1], q[2]), v1 = mk(q[4], q[5], q[6]), v2 = mk(q[8], q[9], q[10]);
+  v3 v0v1 = sub(v1, v0), v0v2 = sub(v2, v0);
+  v3 N = cross(v0v1, v0v2);
+  float ndd = dot(N, d);
+  if ((double)fabsf(ndd) < 1e-6) return -1.0f;
+  float dd = dot(N, v0);
+  float t = (dd - dot(N, o)) / ndd;
+  if (t < 0.0f) return -1.0f;
+  v3 P = mk(fmaf(t, d.x, o.x), fmaf(t, d.y, o.y), fmaf(t, d.z, o.z));
+  if (dot(N, cross(sub(v1, v0), sub(P, v0))) < 0.0f) return -1.0f;
+  if (dot(N, cross(sub(v2, v1), sub(P, v1))) < 0.0f) return -1.0f;
+  if (dot(N, cross(sub(v0, v2), sub(P, v2))) < 0.0f) return -1.0f;
+  return t == 0.0f ? 0.0f : t;
+}
 static float pto_sphere(v3 o, v3 d, const float* q) {
   v3 oc = mk(o.x - q[0], o.y - q[1], o.z - q[2]);
   float b = fdot(oc.x, oc.y, oc.z, d.x, d.y, d.z);
@@ -159,10 +187,11 @@ static float pto_sphere(v3 o, v3 d, const float* q) {
   if (t < 0.0f) return -1.0f;
   return t == 0.0f ? 0.0f : t;
 }
-static inline float prim_test(const pt_prim* p, v3 o, v3 d) {
+static inline float prim_test(const pt_prim* p, v3 o, v3 d, int ref) {
   uint32_t meta;
   memcpy(&meta, &p->q[3], 4);
-  return (meta >> 28) == PT_PRIM_SPHERE ? pto_sphere(o, d, p->q) : pto_tri(o, d, p->q);
+  if ((meta >> 28) == PT_PRIM_SPHERE) return pto_sphere(o, d, p->q);
+  return ref ? pto_tri_ref(o, d, p->q) : pto_tri(o, d, p->q);
 }
 static inline uint64_t key(float t, uint32_t prim) {
   uint32_t b;
@@ -171,12 +200,12 @@ static inline uint64_t key(float t, uint32_t prim) {
 }
 
 /* Closest hit by brute force: min over all primitives of (t, index), t <= tmax. */
-uint64_t pto_closest_brute(const pt_scene_desc* S, const float* ray) {
+static uint64_t closest_brute(const pt_scene_desc* S, const float* ray, int ref) {
   v3 o = mk(ray[0], ray[1], ray[2]), d = mk(ray[4], ray[5], ray[6]);
   float tmax = ray[3];
   uint64_t best = PT_HIT_NONE;
   for (int i = 0; i < S->n_prims; ++i) {
-    float t = prim_test(&S->prims[i], o, d);
+    float t = prim_test(&S->prims[i], o, d, ref);
     if (t >= 0.0f && t <= tmax) {
       uint64_t k = key(t, (uint32_t)i);
       if (k < best) best = k;
@@ -211,7 +240,7 @@ static int box_hit_d(const pt_node* nd, int c, v3 o, v3 d, double tmax) {
   }
   return 1;
 }
-uint64_t pto_closest_bvh(const pt_scene_desc* S, const float* ray) {
+static uint64_t closest_bvh(const pt_scene_desc* S, const float* ray, int ref) {
   v3 o = mk(ray[0], ray[1], ray[2]), d = mk(ray[4], ray[5], ray[6]);
   float tmax = ray[3];
   uint64_t best = PT_HIT_NONE;
@@ -223,7 +252,7 @@ uint64_t pto_closest_bvh(const pt_scene_desc* S, const float* ray) {
     if (nd->prim_count > 0) {
       for (int k = 0; k < nd->prim_count; ++k) {
         int i = nd->prim_start + k;
-        float t = prim_test(&S->prims[i], o, d);
+        float t = prim_test(&S->prims[i], o, d, ref);
         if (t >= 0.0f && t <= tmax) {
           uint64_t kk = key(t, (uint32_t)i);
           if (kk < best) best = kk;
@@ -244,8 +273,16 @@ uint64_t pto_closest_bvh(const pt_scene_desc* S, const float* ray) {
   return best;
 }
 
+uint64_t pto_closest_brute(const pt_scene_desc* S, const float* ray) { return closest_brute(S, ray, 0); }
+uint64_t pto_closest_bvh(const pt_scene_desc* S, const float* ray) { return closest_bvh(S, ray, 0); }
+
+void pto_intersect_ex(const pt_scene_desc* S, const float* rays, int n, uint64_t* hits, int use_bvh, uint32_t flags) {
+  const int ref = (flags & PT_FLAG_REF_ARITH) != 0;
+  for (int i = 0; i < n; ++i)
+    hits[i] = use_bvh ? closest_bvh(S, rays + 8 * i, ref) : closest_brute(S, rays + 8 * i, ref);
+}
 void pto_intersect(const pt_scene_desc* S, const float* rays, int n, uint64_t* hits, int use_bvh) {
-  for (int i = 0; i < n; ++i) hits[i] = use_bvh ? pto_closest_bvh(S, rays + 8 * i) : pto_closest_brute(S, rays + 8 * i);
+  pto_intersect_ex(S, rays, n, hits, use_bvh, 0);
 }
 
 /* Level-synchronous breadth-first traversal statistics: R rays, V (ray, node)
@@ -286,7 +323,8 @@ typedef struct {
 
 static uint64_t trace(const job_t* J, v3 o, v3 d, float tmax) {
   float r[8] = {o.x, o.y, o.z, tmax, d.x, d.y, d.z, 0.0f};
-  return J->use_bvh ? pto_closest_bvh(J->S, r) : pto_closest_brute(J->S, r);
+  const int ref = (J->flags & PT_FLAG_REF_ARITH) != 0;
+  return J->use_bvh ? closest_bvh(J->S, r, ref) : closest_brute(J->S, r, ref);
 }
 
 /* Radiance of sample s of pixel g: the per-path state machine of k_shade. */
@@ -335,6 +373,55 @@ static int nee_sample(const pt_scene_desc* S, v3 T, v3 alb, v3 n, v3 pt, float u
   return 0;
 }
 
+/* PT_FLAG_REF_ARITH NEE: kernelDirectLightRays, cu:416-446, REAL_TIME.  The
+ * shadow ray's tmax: the light counts when its closest hit t > maxT - 1e-3 in
+ * double (cu:1279), so it is occluded by any t <= D = dist - 1e-3, i.e. by any
+ * fp32 t <= D rounded down. */
+static float rd_f32(double D) {
+  float f = (float)D;
+  if ((double)f > D) f = nextafterf(f, -INFINITY);
+  return f;
+}
+static int nee_ref(const pt_scene_desc* S, v3 T, v3 alb, v3 n, v3 pt, float ux, float uy, float weight, v3* C,
+                   v3* sw, float* stmax) {
+  const float MULT = (float)0.3183; /* BSDF_DIFFUSE_MULTIPLIER, cu:272 */
+  const float wgt = weight >= 0.0f ? weight : 1.0f;
+  if (S->light.type == PT_LIGHT_AREA) {
+    float sx = ux - 0.5f, sy = uy - 0.5f;
+    v3 pos = ld3(S->light.position), dx = ld3(S->light.dim_x), dy = ld3(S->light.dim_y);
+    /* e.position + sampleX * e.dim_x + sampleY * e.dim_y */
+    v3 lpt = mk(fmaf(sy, dy.x, fmaf(sx, dx.x, pos.x)), fmaf(sy, dy.y, fmaf(sx, dx.y, pos.y)),
+                fmaf(sy, dy.z, fmaf(sx, dx.z, pos.z)));
+    v3 d = sub(lpt, pt);
+    float cosTheta = dot(d, ld3(S->light.direction));
+    float sqDist = dot(d, d);
+    float dist = sqrtf(sqDist);
+    v3 w = scl(d, 1.0f / dist); /* d / dist (cuda_util.h: a * (1 / s)) */
+    float pdf = sqDist / (S->light.area * fabsf(cosTheta));
+    float fpdf = fabsf(dot(n, w)) / pdf;
+    if ((double)dist > 1e-2 && (double)fabsf(cosTheta) > 1e-2) {
+      *C = scl(scl(mulv(scl(mulv(T, alb), fpdf), ld3(S->light.radiance)), MULT), wgt);
+      *sw = w;
+      *stmax = rd_f32((double)dist - 1e-3);
+      return 1;
+    }
+    return 0;
+  }
+  if (S->light.type == PT_LIGHT_POINT) { /* no reference counterpart: fpdf = |n.w| */
+    v3 d = sub(ld3(S->light.position), pt);
+    float dist = sqrtf(dot(d, d));
+    v3 w = scl(d, 1.0f / dist);
+    float fpdf = fabsf(dot(n, w));
+    if ((double)dist > 1e-2) {
+      *C = scl(scl(mulv(scl(mulv(T, alb), fpdf), ld3(S->light.radiance)), MULT), wgt);
+      *sw = w;
+      *stmax = rd_f32((double)dist - 1e-3);
+      return 1;
+    }
+  }
+  return 0;
+}
+
 static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays) {
   const pt_scene_desc* S = J->S;
   const float EPS = 1e-3f;
@@ -353,7 +440,15 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
   ky = ky / len;
   kz = kz / len;
   v3 Lf = ld3(S->camera.left), Up = ld3(S->camera.up), K = ld3(S->camera.look_at);
-  v3 d = nrm(mk(kx * Lf.x + ky * Up.x + kz * K.x, kx * Lf.y + ky * Up.y + kz * K.y, kx * Lf.z + ky * Up.z + kz * K.z));
+  const int refa = (J->flags & PT_FLAG_REF_ARITH) != 0;
+  v3 d;
+  if (refa) { /* cu:347-354: k = k / length(k); dir = k.x left + k.y up + k.z lookAt */
+    v3 k = mk(ssy / (float)J->W - 0.5f, -(ssx / (float)J->H - 0.5f), 1.0f);
+    k = scl(k, 1.0f / len3(k));
+    d = mk(dot(k, mk(Lf.x, Up.x, K.x)), dot(k, mk(Lf.y, Up.y, K.y)), dot(k, mk(Lf.z, Up.z, K.z)));
+  } else {
+    d = nrm(mk(kx * Lf.x + ky * Up.x + kz * K.x, kx * Lf.y + ky * Up.y + kz * K.y, kx * Lf.z + ky * Up.z + kz * K.z));
+  }
   v3 o = ld3(S->camera.origin);
   v3 T = mk(1.0f, 1.0f, 1.0f), L = mk(0.0f, 0.0f, 0.0f);
   int spec = 0;
@@ -369,7 +464,9 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
     uint32_t tb = (uint32_t)(h >> 32), prim = (uint32_t)h;
     float t;
     memcpy(&t, &tb, 4);
-    v3 P = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+    /* cu:1205 its.pt = r->o + r->d * t */
+    v3 P = refa ? mk(fmaf(d.x, t, o.x), fmaf(d.y, t, o.y), fmaf(d.z, t, o.z))
+                : mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
     const float* q = S->prims[prim].q;
     uint32_t meta;
     memcpy(&meta, &q[3], 4);
@@ -379,7 +476,7 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
     } else {
       const pt_prim_shading* sh = &S->shading[prim];
       v3 n0 = ld3(sh->n0), n1 = ld3(sh->n1), n2 = ld3(sh->n2);
-      if (n0.x == n1.x && n0.y == n1.y && n0.z == n1.z && n1.x == n2.x && n1.y == n2.y && n1.z == n2.z) {
+      if (!refa && n0.x == n1.x && n0.y == n1.y && n0.z == n1.z && n1.x == n2.x && n1.y == n2.y && n1.z == n2.z) {
         /* flat triangle: the barycentric blend is a positive multiple of n0 */
         ns = nrm(n0);
       } else { /* barycentric shading normal, cu:1213-1221 */
@@ -388,22 +485,40 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
         float bC = len3(cross(sub(A, P), sub(B, P))) / total;
         float bA = len3(cross(sub(B, P), sub(Cv, P))) / total;
         float bB = len3(cross(sub(Cv, P), sub(A, P))) / total;
-        ns = nrm(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y,
-                    bA * n0.z + bB * n1.z + bC * n2.z));
+        if (refa) { /* cu:1221 normalize(bA * n0 + bB * n1 + bC * n2) */
+          v3 bw = mk(bA, bB, bC);
+          ns = nrm(mk(dot(bw, mk(n0.x, n1.x, n2.x)), dot(bw, mk(n0.y, n1.y, n2.y)), dot(bw, mk(n0.z, n1.z, n2.z))));
+        } else {
+          ns = nrm(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y,
+                      bA * n0.z + bB * n1.z + bC * n2.z));
+        }
       }
     }
     int front = dot(ns, d) < 0.0f;
     v3 n = front ? ns : mk(-ns.x, -ns.y, -ns.z);
-    v3 pt = sub(P, scl(d, EPS));
-    const pt_bsdf* Bs = &S->bsdfs[meta & 0x0FFFFFFFu];
-    if (Bs->type == PT_BSDF_EMISSION) {
+    /* cu:1224 its.pt += -r->d * 1e-3 */
+    v3 pt = refa ? mk(fmaf(-d.x, EPS, P.x), fmaf(-d.y, EPS, P.y), fmaf(-d.z, EPS, P.z)) : sub(P, scl(d, EPS));
+    pt_bsdf Bv = S->bsdfs[meta & 0x0FFFFFFFu];
+    const pt_bsdf* Bs = &Bv;
+    int emitter = 0;
+    if (refa) {
+      /* cu:1243 (without REAL_TIME) its.light = radiance * importance + light;
+       * an emission BSDF is a diffuse one with albedo = radiance (cu:1705-1711) */
+      v3 rad = Bv.type == PT_BSDF_EMISSION ? ld3(Bv.albedo) : mk(0.0f, 0.0f, 0.0f);
+      if (!(J->flags & PT_FLAG_NO_EMISSION)) {
+        L = mk(fmaf(rad.x, T.x, L.x), fmaf(rad.y, T.y, L.y), fmaf(rad.z, T.z, L.z));
+        emitter = rad.x != 0.0f || rad.y != 0.0f || rad.z != 0.0f; /* cu:436 */
+      }
+      if (Bv.type == PT_BSDF_EMISSION) Bv.type = PT_BSDF_DIFFUSE;
+    }
+    if (!refa && Bs->type == PT_BSDF_EMISSION) {
       if (!(J->flags & PT_FLAG_NO_EMISSION) && (vtx == 1 || spec)) L = add(L, mulv(T, ld3(Bs->albedo)));
       break;
     }
     u4 r = rng(J->seed, g, s, vtx, 0);
     v3 dpdu, dpdv;
     if (J->flags & PT_FLAG_REF_GUIDE) { /* reference quirk (ii), cu:572-574 */
-      v3 guide = (n.y < 1e-4f) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+      v3 guide = ((double)n.y < 1e-4) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
       dpdu = nrm(cross(guide, n));
       dpdv = nrm(cross(dpdu, n));
     } else {
@@ -415,7 +530,7 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
     if (Bs->type == PT_BSDF_DIFFUSE) {
       v3 alb = ld3(Bs->albedo);
       /* NEE: one sample, or 2, 2, 1 at vertices 1, 2, 3 (reference schedule) */
-      const int nee = (ref_sched && vtx <= 2u) ? 2 : 1;
+      const int nee = emitter ? 0 : (ref_sched && vtx <= 2u) ? 2 : 1;
       int have_sh[2] = {0, 0};
       v3 C[2] = {{0, 0, 0}, {0, 0, 0}}, sw[2] = {{0, 0, 1}, {0, 0, 1}};
       float stmax[2] = {-1.0f, -1.0f};
@@ -427,7 +542,8 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
           uy = u01(r2.v[1]);
         }
         float weight = ref_sched ? (nee == 2 ? 0.5f : 1.0f) : -1.0f;
-        have_sh[k] = nee_sample(S, T, alb, n, pt, ux, uy, weight, &C[k], &sw[k], &stmax[k]);
+        have_sh[k] = refa ? nee_ref(S, T, alb, n, pt, ux, uy, weight, &C[k], &sw[k], &stmax[k])
+                          : nee_sample(S, T, alb, n, pt, ux, uy, weight, &C[k], &sw[k], &stmax[k]);
       }
       float x, y, z, sn, cs;
       sincos2pi(u01(r.v[3]), &sn, &cs);
@@ -443,14 +559,18 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
         x = rr * cs;
         y = rr * sn;
       }
-      dn = nrm(mk(n.x * z + x * dpdu.x + y * dpdv.x, n.y * z + x * dpdu.y + y * dpdv.y, n.z * z + x * dpdu.z + y * dpdv.z));
+      if (refa) /* cu:631-637, not normalised */
+        dn = mk(fmaf(y, dpdv.x, fmaf(x, dpdu.x, n.x * z)), fmaf(y, dpdv.y, fmaf(x, dpdu.y, n.y * z)),
+                fmaf(y, dpdv.z, fmaf(x, dpdu.z, n.z * z)));
+      else
+        dn = nrm(mk(n.x * z + x * dpdu.x + y * dpdv.x, n.y * z + x * dpdu.y + y * dpdv.y, n.z * z + x * dpdu.z + y * dpdv.z));
       if (J->flags & PT_FLAG_COSINE_DIFFUSE) {
         T = mulv(T, alb);
       } else {
         float c = fabsf(dot(dn, n));
         T = mk(((T.x * c) * alb.x) * 2.0f, ((T.y * c) * alb.y) * 2.0f, ((T.z * c) * alb.z) * 2.0f);
       }
-      on = add(pt, scl(n, EPS));
+      on = refa ? mk(fmaf(n.x, EPS, pt.x), fmaf(n.y, EPS, pt.y), fmaf(n.z, EPS, pt.z)) : add(pt, scl(n, EPS)); /* cu:593 */
       spec = 0;
       for (int k = 0; k < nee; ++k) {
         if (!have_sh[k]) continue;
@@ -459,10 +579,20 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
         if (hs == PT_HIT_NONE) L = add(L, C[k]);
       }
     } else if (Bs->type == PT_BSDF_MIRROR) {
-      float dd = dot(d, n);
-      dn = nrm(sub(d, scl(n, 2.0f * dd)));
+      if (refa) {
+        /* cu:1234 wi in the local frame; cu:643-650 wo = (-wi.x, -wi.y, wi.z) */
+        v3 md = mk(-d.x, -d.y, -d.z);
+        v3 wi = nrm(mk(dot(dpdu, md), dot(dpdv, md), dot(n, md)));
+        float wx = -wi.x, wy = -wi.y, wz = wi.z;
+        dn = mk(fmaf(wy, dpdv.x, fmaf(wx, dpdu.x, n.x * wz)), fmaf(wy, dpdv.y, fmaf(wx, dpdu.y, n.y * wz)),
+                fmaf(wy, dpdv.z, fmaf(wx, dpdu.z, n.z * wz)));
+        on = mk(fmaf(n.x, EPS, pt.x), fmaf(n.y, EPS, pt.y), fmaf(n.z, EPS, pt.z));
+      } else {
+        float dd = dot(d, n);
+        dn = nrm(sub(d, scl(n, 2.0f * dd)));
+        on = add(pt, scl(n, EPS));
+      }
       T = mulv(T, ld3(Bs->albedo));
-      on = add(pt, scl(n, EPS));
       spec = 1;
     } else { /* glass */
       float ior = Bs->ior;

@@ -31,6 +31,8 @@ def _load():
     lib.pto_closest_bvh.argtypes = [P, C.POINTER(C.c_float)]
     lib.pto_intersect.restype = None
     lib.pto_intersect.argtypes = [P, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_uint64), C.c_int]
+    lib.pto_intersect_ex.restype = None
+    lib.pto_intersect_ex.argtypes = [P, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_uint64), C.c_int, C.c_uint32]
     lib.pto_bfs_visits.restype = None
     lib.pto_bfs_visits.argtypes = [P, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_uint64), C.c_int]
     lib.pto_render.restype = C.c_uint64
@@ -55,11 +57,12 @@ def _f(a):
     return a.ctypes.data_as(C.POINTER(C.c_float))
 
 
-def intersect(desc, rays, use_bvh=True):
+def intersect(desc, rays, use_bvh=True, flags=0):
+    """Closest-hit keys; flags & PT_FLAG_REF_ARITH: the literal cu:217-270 test."""
     rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
     hits = np.zeros(len(rays), dtype=np.uint64)
-    LIB.pto_intersect(C.addressof(desc), _f(rays), len(rays),
-                      hits.ctypes.data_as(C.POINTER(C.c_uint64)), 1 if use_bvh else 0)
+    LIB.pto_intersect_ex(C.addressof(desc), _f(rays), len(rays),
+                         hits.ctypes.data_as(C.POINTER(C.c_uint64)), 1 if use_bvh else 0, flags)
     return hits
 
 

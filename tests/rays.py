@@ -37,3 +37,29 @@ def interior_rays(desc, n, seed=1, tmax=np.inf):
     r[:, 3] = tmax
     r[:, 4:7] = d
     return r
+
+
+def edge_rays(desc, n, seed=2, vertex_frac=0.25):
+    """Rays from near the camera aimed at points on triangle edges (and, for a
+    `vertex_frac` share, exactly at vertices): the grazing cases where edge-test
+    rounding and box conservativeness matter."""
+    import ctypes as C
+    rng = np.random.default_rng(seed)
+    q = np.ctypeslib.as_array(C.cast(desc.prims, C.POINTER(C.c_float)), shape=(desc.n_prims, 24))
+    tri = np.nonzero((q[:, 3].view(np.uint32) >> 28) == 0)[0]
+    idx = rng.choice(tri, n)
+    v = np.stack([q[idx, 0:3], q[idx, 4:7], q[idx, 8:11]], axis=1)
+    k = rng.integers(0, 3, n)
+    w = rng.random(n, dtype=np.float32)
+    w[: int(n * vertex_frac)] = 0.0
+    a = v[np.arange(n), k]
+    b = v[np.arange(n), (k + 1) % 3]
+    target = (a + (b - a) * w[:, None]).astype(np.float32)
+    o = np.array(desc.camera.origin, np.float32)[None, :] + (rng.random((n, 3), dtype=np.float32) - 0.5) * 0.2
+    d = target - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    r = np.zeros((n, 8), np.float32)
+    r[:, :3] = o
+    r[:, 3] = np.inf
+    r[:, 4:7] = d
+    return r

@@ -14,7 +14,7 @@ import pytest
 import ptrace
 import pyoracle
 from conftest import load_fixture
-from rays import camera_rays, interior_rays
+from rays import camera_rays, edge_rays, interior_rays
 
 pytestmark = pytest.mark.gpu
 
@@ -140,6 +140,10 @@ def _images_equal(gimg, oimg):
 
 
 REF = ptrace.PT_FLAG_REF_SCHEDULE | ptrace.PT_FLAG_REF_DROP_ON_MISS
+# every reference-arithmetic switch (SURVEY §8(a) parity decisions; pt_api.h
+# PT_FLAG_REF_ARITH): the kernels' expressions of cu:217-270, 347-354,
+# 416-446, 570-653, 1205-1234 with the reference schedule and REAL_TIME
+REF_FULL = REF | ptrace.PT_FLAG_REF_ARITH | ptrace.PT_FLAG_NO_EMISSION
 
 
 @pytest.mark.parametrize("name,flags", [("CBbunny", 0), ("CBspheres", 0), ("CBgems", 0), ("CBempty", 0),
@@ -147,7 +151,12 @@ REF = ptrace.PT_FLAG_REF_SCHEDULE | ptrace.PT_FLAG_REF_DROP_ON_MISS
                                         # reference-quirk modes (SURVEY §8(a) parity decisions)
                                         ("CBbunny", REF), ("CBempty", REF | ptrace.PT_FLAG_NO_EMISSION),
                                         ("CBspheres", REF), ("CBcoil", ptrace.PT_FLAG_REF_GUIDE),
-                                        ("CBempty", ptrace.PT_FLAG_REF_GUIDE)])
+                                        ("CBempty", ptrace.PT_FLAG_REF_GUIDE),
+                                        # reference arithmetic (PT_FLAG_REF_ARITH), alone and with
+                                        # every other reference switch
+                                        ("CBbunny", ptrace.PT_FLAG_REF_ARITH), ("CBcoil", ptrace.PT_FLAG_REF_ARITH),
+                                        ("CBempty", ptrace.PT_FLAG_REF_ARITH), ("CBbunny", REF_FULL),
+                                        ("CBcoil", REF_FULL | ptrace.PT_FLAG_REF_GUIDE), ("CBempty", REF_FULL)])
 def test_render_bit_exact(gpu_ctx, name, flags):
     sc = load_fixture(name)
     d = sc.desc()
@@ -162,6 +171,35 @@ def test_render_bit_exact(gpu_ctx, name, flags):
     assert l2 <= 1e-3 and ok >= 0.999, (mx, l2, ok)
     assert mx == 0.0, f"not bit-exact: max |diff| {mx}, rel L2 {l2}"
     assert o[..., :3].mean() > 0.01
+
+
+@pytest.mark.parametrize("name", ["CBempty", "CBgems", "CBcoil", "CBbunny"])
+def test_closest_hit_ref_arith_bit_exact(gpu_ctx, name):
+    """PT_FLAG_REF_ARITH: the literal cu:217-270 triangle test (edge tests
+    dot(N, cross(e_k, P - v_k)), N and N.v0 per the reference) through the
+    breadth-first traversal equals the oracle's per-call restatement, on the
+    fixture rays and on rays aimed at triangle edges (where the literal and
+    edge-normal forms disagree: see DESIGN.md §2)."""
+    sc = load_fixture(name)
+    d = sc.desc()
+    gpu_ctx.load_scene(sc)
+    rays = np.concatenate([camera_rays(d, 20000, seed=7), interior_rays(d, 20000, seed=8), edge_rays(d, 10000, seed=3)])
+    g = gpu_ctx.intersect(rays, flags=ptrace.PT_FLAG_REF_ARITH)
+    o = pyoracle.intersect(d, rays, use_bvh=True, flags=ptrace.PT_FLAG_REF_ARITH)
+    assert (o != ptrace.PT_HIT_NONE).sum() > 1000
+    bad = np.nonzero(g != o)[0]
+    assert len(bad) == 0, f"{len(bad)} mismatching hits, first {bad[:5]}: gpu {g[bad[:5]]} oracle {o[bad[:5]]}"
+    # the default (edge-normal) test differs from it on edge-aimed rays only
+    dflt = gpu_ctx.intersect(rays)
+    assert np.array_equal(dflt, pyoracle.intersect(d, rays, use_bvh=True))
+
+
+def test_ref_arith_refuses_spheres_and_glass(gpu_ctx):
+    for name in ["CBspheres", "CBgems"]:
+        gpu_ctx.load_scene(load_fixture(name))
+        with pytest.raises(ptrace.PTError) as e:
+            gpu_ctx.render(16, 16, 1, flags=ptrace.PT_FLAG_REF_ARITH)
+        assert e.value.code == ptrace.PT_E_UNSUPPORTED
 
 
 def test_dragon_proxy_parity(gpu_ctx):

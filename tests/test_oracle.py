@@ -86,3 +86,26 @@ def test_oracle_quirk_modes():
     assert np.array_equal(a, b) and ra == rb
     assert ra <= W * H * (3 + 5)  # 3 extension rays + 2 + 2 + 1 shadow rays per path at most
     assert not np.array_equal(a, base)
+
+
+def test_ref_arith_oracle_consistent():
+    """PT_FLAG_REF_ARITH in the oracle: the literal triangle test's BVH walk
+    equals its brute force, it finds the same primitives as the edge-normal
+    form on generic rays, and a full reference-mode render is finite."""
+    import ptrace
+    from conftest import load_fixture
+    from rays import camera_rays, edge_rays, interior_rays
+    RA = ptrace.PT_FLAG_REF_ARITH
+    for name in ["CBempty", "CBbunny"]:
+        d = load_fixture(name).desc()
+        rays = np.concatenate([camera_rays(d, 3000, seed=5), interior_rays(d, 3000, seed=6)])
+        a = pyoracle.intersect(d, rays, use_bvh=True, flags=RA)
+        assert np.array_equal(a, pyoracle.intersect(d, rays, use_bvh=False, flags=RA))
+        b = pyoracle.intersect(d, rays, use_bvh=True)
+        assert np.array_equal(ptrace.hit_prim(a), ptrace.hit_prim(b))
+        e = edge_rays(d, 2000, seed=4)
+        assert np.array_equal(pyoracle.intersect(d, e, use_bvh=True, flags=RA),
+                              pyoracle.intersect(d, e, use_bvh=False, flags=RA))
+        flags = RA | ptrace.PT_FLAG_REF_SCHEDULE | ptrace.PT_FLAG_REF_DROP_ON_MISS | ptrace.PT_FLAG_NO_EMISSION
+        img, rays_cast = pyoracle.image(d, 24, 24, 2, flags=flags)
+        assert np.isfinite(img).all() and img[..., :3].mean() > 0.01 and rays_cast > 24 * 24 * 2
