@@ -383,7 +383,9 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
             if (!tri_outside(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), bt);
           } else
             tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), bt);
-          if (tt >= 0.0f && (tt < bt || (tt == bt && bp < 0))) {
+          // ties go to the lowest primitive across the inline leaves too
+          // (their primitive ranges are not in increasing order)
+          if (tt >= 0.0f && (tt < bt || (tt == bt && (bp < 0 || pstart + kk < bp)))) {
             bt = tt;
             bp = pstart + kk;
           }

@@ -62,9 +62,11 @@ __device__ __forceinline__ float rup(double v) {
 }
 
 // 1. per-primitive box (exact fp32 min/max of the vertices; spheres rounded
-//    outward from double like bvh_ref.cpp) and centroid
+//    outward from double like bvh_ref.cpp) and centroid; the stored box is
+//    widened by the guard band G (scene_internal.h box_guard: the traversal's
+//    fp32 slab test is then conservative), the centroid is the unwidened one
 __global__ void k_prim_bounds(const float* __restrict__ pos, int n_tris, const float* __restrict__ sph, int n,
-                              Box* __restrict__ box, float* __restrict__ cen) {
+                              double G, Box* __restrict__ box, float* __restrict__ cen) {
   const int i = blockIdx.x * TPB + threadIdx.x;
   if (i >= n) return;
   Box b;
@@ -83,9 +85,14 @@ __global__ void k_prim_bounds(const float* __restrict__ pos, int n_tris, const f
       b.hi[k] = rup((double)s[k] + (double)s[3]);
     }
   }
-  box[i] = b;
 #pragma unroll
   for (int k = 0; k < 3; ++k) cen[(size_t)i * 3 + k] = 0.5f * (b.lo[k] + b.hi[k]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    b.lo[k] = rdown((double)b.lo[k] - G);
+    b.hi[k] = rup((double)b.hi[k] + G);
+  }
+  box[i] = b;
 }
 
 // 2. centroid bounds: lo[3], hi[3] as ordered u32 (init lo = ~0, hi = 0)
@@ -564,7 +571,8 @@ static int build_on_device(const pt_mesh_desc* md, int max_leaf, int builder, pt
   BCHK(hipMemcpyAsync(d_bounds, binit, sizeof(binit), hipMemcpyHostToDevice, st));
   BCHK(hipMemsetAsync(d_arr, 0, (size_t)n * 4, st));
   const dim3 g((n + TPB - 1) / TPB);
-  hipLaunchKernelGGL(k_prim_bounds, g, dim3(TPB), 0, st, d_pos, n_tris, d_sph, n, d_pbox, d_cen);
+  hipLaunchKernelGGL(k_prim_bounds, g, dim3(TPB), 0, st, d_pos, n_tris, d_sph, n, ptscene::box_guard(S), d_pbox,
+                     d_cen);
   hipLaunchKernelGGL(k_reduce_bounds, dim3(std::min(1024, (n + TPB - 1) / TPB)), dim3(TPB), 0, st, d_cen, n,
                      d_bounds);
   hipLaunchKernelGGL(k_morton, g, dim3(TPB), 0, st, d_cen, n, d_bounds, d_key, d_idx);

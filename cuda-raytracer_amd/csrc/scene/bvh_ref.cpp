@@ -18,6 +18,7 @@
 //    rounds to nearest, make_float3 at cu:1822-1823) so that the fp32 slab test
 //    is conservative for every primitive in the subtree.
 #include <algorithm>
+#include <cstdlib>
 #include <cfloat>
 #include <cstring>
 #include <memory>
@@ -269,6 +270,31 @@ float round_up(double v) {
 
 }  // namespace
 
+double box_guard(const Scene& S) {
+  double m = 0.0;
+  auto upd = [&](double v) { m = std::max(m, std::fabs(v)); };
+  for (const Mesh& me : S.meshes)
+    for (const V3& p : me.positions) {
+      upd(p.x);
+      upd(p.y);
+      upd(p.z);
+    }
+  for (const Prim& p : S.prims)
+    if (p.kind == PT_PRIM_SPHERE) {
+      upd(std::fabs(p.centre.x) + p.radius);
+      upd(std::fabs(p.centre.y) + p.radius);
+      upd(std::fabs(p.centre.z) + p.radius);
+    }
+  for (int k = 0; k < 3; ++k) {
+    upd(S.camera.origin[k]);
+    upd(S.light.position[k]);
+  }
+  // PT_BOX_GUARD=0 turns the band off (diagnostics: scripts/dev/guard_off.py)
+  const char* e = getenv("PT_BOX_GUARD");
+  if (e && atoi(e) == 0) return 0.0;
+  return std::ldexp(m, -17);
+}
+
 // BSDF table: one entry per scene object (cu:1694-1723)
 void flatten_bsdfs(Scene& S) {
   S.dbsdfs.clear();
@@ -382,6 +408,7 @@ void build_bvh_and_flatten(Scene& S, size_t max_leaf) {
     return;
   }
   WNode* wroot = B.compact(root);
+  const double G = box_guard(S);  // scene_internal.h: conservative fp32 slab tests
   std::vector<CNode> tree;
   std::vector<std::vector<int>> levels;
   compress(wroot, tree, levels, 0);
@@ -405,12 +432,12 @@ void build_bvh_and_flatten(Scene& S, size_t max_leaf) {
       for (int i = 0; i < 4; ++i) {
         if (c.range == 0 && c.outlets[i] >= 0) {
           d.child[i] = dfs_to_bfs[c.outlets[i]];
-          d.bmin_x[i] = round_down(c.min[i].x);
-          d.bmin_y[i] = round_down(c.min[i].y);
-          d.bmin_z[i] = round_down(c.min[i].z);
-          d.bmax_x[i] = round_up(c.max[i].x);
-          d.bmax_y[i] = round_up(c.max[i].y);
-          d.bmax_z[i] = round_up(c.max[i].z);
+          d.bmin_x[i] = round_down(c.min[i].x - G);
+          d.bmin_y[i] = round_down(c.min[i].y - G);
+          d.bmin_z[i] = round_down(c.min[i].z - G);
+          d.bmax_x[i] = round_up(c.max[i].x + G);
+          d.bmax_y[i] = round_up(c.max[i].y + G);
+          d.bmax_z[i] = round_up(c.max[i].z + G);
         } else {
           d.child[i] = -1;
           // empty slot: an inverted box no ray can enter

@@ -128,6 +128,17 @@ struct Scene {
   std::vector<pt_bsdf> dbsdfs;
 };
 
+// bvh_ref.cpp: the guard band G added to every stored BVH box (host and GPU
+// builds) so the traversal's fp32 slab test (trace.hip box_hit: approximate
+// v_rcp_f32 reciprocal, rounded o * (1/d), FMA slabs) never rejects a box the
+// exact test enters, for ray origins with |coordinates| <= M, the largest
+// magnitude among the scene's vertices, sphere extents, camera and light.
+// The computed slab plane of a face b is off by at most (2^-24 + 3 * 2^-24
+// (1 + 2^-22)) max(|b|, |o|) < 2^-21.5 M; G = 2^-17 M is 22x
+// that.  (The reference's 1e-3 triangle padding, bvh.cpp, is kept for the
+// SAH costs; the guard band widens only the stored fp32 boxes.)
+double box_guard(const Scene& s);
+
 // bvh_ref.cpp: restated BVHAccel / compactTree / compress + BFS flattening.
 void build_bvh_and_flatten(Scene& s, size_t max_leaf_size = 32);
 

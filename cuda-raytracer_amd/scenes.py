@@ -11,6 +11,9 @@ sphere, 14,160 triangles) under the light: 99,900 triangles in total, run
 through the same reference BVH build (pt_scene_from_mesh) or, as
 "dragon_proxy_gpubvh", through the GPU build (pt_scene_build_gpu: PLOC
 clustering; "dragon_proxy_lbvh" is the same scene with the radix tree).
+
+bunny_lit(): bunny.dae (config 4's wide-level scene) with CBbunny's light.
+rebuilt(name, ...): any fixture rebuilt from its meshes (host or GPU build).
 """
 import math
 from pathlib import Path
@@ -55,6 +58,51 @@ def _uv_sphere(centre, radius, nlat, nlon):
                 tris.append(np.concatenate([p[v] for v in t]))
                 nrms.append(np.concatenate([n[v] for v in t]))
     return np.asarray(tris, np.float32), np.asarray(nrms, np.float32)
+
+
+def fixture_arrays(name):
+    """A committed fixture back in mesh input order: dict of positions (n, 9),
+    normals (n, 9), tri_bsdf, spheres (m, 4), sphere_bsdf, bsdfs, light,
+    camera (the inputs of pt_scene_from_mesh / pt_scene_build_gpu)."""
+    with np.load(FIXTURES / f"{name}.npz", allow_pickle=False) as z:
+        q = z["prims"]
+        sh = z["shading"]
+        order = np.argsort(z["sorted_to_input"], kind="stable")
+        bs = np.frombuffer(z["bsdfs"].tobytes(), dtype=np.uint8)
+        light = ptrace.pt_light.from_buffer_copy(z["light"].tobytes())
+        camera = ptrace.pt_camera.from_buffer_copy(z["camera"].tobytes())
+    q, sh = q[order], sh[order]
+    meta = q[:, 3].view(np.uint32)
+    tri = (meta >> 28) == ptrace.PT_PRIM_TRIANGLE
+    sz = ptrace.C.sizeof(ptrace.pt_bsdf)
+    bsdfs = [ptrace.pt_bsdf.from_buffer_copy(bs[i * sz:(i + 1) * sz].tobytes()) for i in range(len(bs) // sz)]
+    t, sp = q[tri], q[~tri]
+    return {"positions": np.concatenate([t[:, 0:3], t[:, 4:7], t[:, 8:11]], axis=1),
+            "normals": np.concatenate([sh[tri][:, 0:3], sh[tri][:, 4:7], sh[tri][:, 8:11]], axis=1),
+            "tri_bsdf": (meta[tri] & 0x0FFFFFFF).astype(np.int32),
+            "spheres": np.concatenate([sp[:, 0:3], sp[:, 4:5]], axis=1) if len(sp) else None,
+            "sphere_bsdf": (meta[~tri] & 0x0FFFFFFF).astype(np.int32) if len(sp) else None,
+            "bsdfs": bsdfs, "light": light, "camera": camera}
+
+
+def rebuilt(name, gpu_device=None, max_leaf=32, builder="ploc"):
+    """Fixture `name` rebuilt from its meshes: the host SAH build
+    (pt_scene_from_mesh) or the GPU build (gpu_device=k)."""
+    a = fixture_arrays(name)
+    return ptrace.Scene.from_mesh(a["positions"], a["bsdfs"], normals=a["normals"], tri_bsdf=a["tri_bsdf"],
+                                  spheres=a["spheres"], sphere_bsdf=a["sphere_bsdf"], light=a["light"],
+                                  camera=a["camera"], gpu_device=gpu_device, max_leaf=max_leaf, builder=builder)
+
+
+def bunny_lit():
+    """bunny.dae (33,696 triangles; BVH level 6 holds the 1,167 nodes that
+    overflow the reference's per-level buffers) lit by CBbunny.dae's area light:
+    bunny.dae has no light of its own (the reference would add a default
+    ambient light and read it as an area light, cu:1630-1633, 1741)."""
+    sc = ptrace.ArrayScene.load(FIXTURES / "bunny.npz")
+    with np.load(FIXTURES / "CBbunny.npz", allow_pickle=False) as z:
+        sc.a["light"] = z["light"].copy()
+    return sc
 
 
 def dragon_proxy_arrays():
@@ -114,4 +162,6 @@ def load(name):
         return dragon_proxy(gpu_device=0)
     if name == "dragon_proxy_lbvh":
         return dragon_proxy(gpu_device=0, builder="lbvh")
+    if name == "bunny":
+        return bunny_lit()
     return ptrace.ArrayScene.load(FIXTURES / f"{name}.npz")

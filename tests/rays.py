@@ -39,14 +39,29 @@ def interior_rays(desc, n, seed=1, tmax=np.inf):
     return r
 
 
-def edge_rays(desc, n, seed=2, vertex_frac=0.25):
-    """Rays from near the camera aimed at points on triangle edges (and, for a
-    `vertex_frac` share, exactly at vertices): the grazing cases where edge-test
-    rounding and box conservativeness matter."""
+def _prims(desc):
     import ctypes as C
+    return np.ctypeslib.as_array(C.cast(desc.prims, C.POINTER(C.c_float)), shape=(desc.n_prims, 24))
+
+
+def axis_aligned_tris(desc):
+    """Indices of triangles whose normal lies along a coordinate axis (the
+    Cornell walls): their boxes are flat in one axis."""
+    q = _prims(desc)
+    tri = (q[:, 3].view(np.uint32) >> 28) == 0
+    N = q[:, 12:15]
+    flat = (np.count_nonzero(np.abs(N) > 1e-6 * np.abs(N).max(axis=1, keepdims=True), axis=1) == 1)
+    return np.nonzero(tri & flat)[0]
+
+
+def edge_rays(desc, n, seed=2, vertex_frac=0.25, prims=None):
+    """Rays from near the camera aimed at points on triangle edges (and, for a
+    `vertex_frac` share, exactly at vertices) of `prims` (default: every
+    triangle): the grazing cases where edge-test rounding and box
+    conservativeness matter."""
     rng = np.random.default_rng(seed)
-    q = np.ctypeslib.as_array(C.cast(desc.prims, C.POINTER(C.c_float)), shape=(desc.n_prims, 24))
-    tri = np.nonzero((q[:, 3].view(np.uint32) >> 28) == 0)[0]
+    q = _prims(desc)
+    tri = np.nonzero((q[:, 3].view(np.uint32) >> 28) == 0)[0] if prims is None else np.asarray(prims)
     idx = rng.choice(tri, n)
     v = np.stack([q[idx, 0:3], q[idx, 4:7], q[idx, 8:11]], axis=1)
     k = rng.integers(0, 3, n)
@@ -63,3 +78,29 @@ def edge_rays(desc, n, seed=2, vertex_frac=0.25):
     r[:, 3] = np.inf
     r[:, 4:7] = d
     return r
+
+
+def sphere_tangent_rays(desc, n, seed=5, rel=(-1e-6, 0.0, 1e-6)):
+    """Rays from near the camera grazing the spheres' silhouettes: aimed at
+    c + r (1 + s) u with u perpendicular to the view of the centre and s from
+    `rel` (just inside, on, just outside the tangent)."""
+    rng = np.random.default_rng(seed)
+    q = _prims(desc)
+    sph = np.nonzero((q[:, 3].view(np.uint32) >> 28) == 1)[0]
+    idx = rng.choice(sph, n)
+    c = q[idx, 0:3].astype(np.float64)
+    r = q[idx, 4].astype(np.float64)
+    o = np.array(desc.camera.origin, np.float64)[None, :] + (rng.random((n, 3)) - 0.5) * 0.2
+    w = c - o
+    w /= np.linalg.norm(w, axis=1, keepdims=True)
+    a = rng.normal(size=(n, 3))
+    u = a - (a * w).sum(1, keepdims=True) * w
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    s = np.asarray(rel)[rng.integers(0, len(rel), n)]
+    d = c + u * (r * (1.0 + s))[:, None] - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    out = np.zeros((n, 8), np.float32)
+    out[:, :3] = o
+    out[:, 3] = np.inf
+    out[:, 4:7] = d
+    return out

@@ -222,6 +222,35 @@ def test_dragon_proxy_parity(gpu_ctx):
     assert mx == 0.0, f"not bit-exact: max |diff| {mx}, rel L2 {l2}"
 
 
+def test_bunny_dae_parity(gpu_ctx):
+    """bunny.dae (BASELINE config 4, 33,696 triangles): its BVH level 6 holds
+    1,167 nodes -- the level that overflows the reference's per-level
+    buffers.  Closest hits (default and reference arithmetic) and
+    a small render (lit by CBbunny's area light, scenes.bunny_lit) bit-exact."""
+    import scenes
+    sc = scenes.bunny_lit()
+    d = sc.desc()
+    assert sc.level_counts() == [1, 4, 16, 64, 239, 780, 1167, 45]
+    gpu_ctx.load_scene(sc)
+    rays = np.concatenate([camera_rays(d, 20000, seed=47), interior_rays(d, 20000, seed=48), edge_rays(d, 5000)])
+    o = pyoracle.intersect(d, rays, use_bvh=True)
+    assert (o != ptrace.PT_HIT_NONE).sum() > 5000
+    assert np.array_equal(gpu_ctx.intersect(rays), o)
+    assert np.array_equal(gpu_ctx.intersect(rays, flags=ptrace.PT_FLAG_REF_ARITH),
+                          pyoracle.intersect(d, rays, use_bvh=True, flags=ptrace.PT_FLAG_REF_ARITH))
+    gpu_ctx.reset_stats()
+    for flags in (0, REF_FULL):
+        gpu_ctx.clear()
+        gpu_ctx.render(40, 40, 2, max_bounces=8, seed=15618, flags=flags | ptrace.PT_FLAG_STATS)
+        gi = gpu_ctx.get_image()
+        oi, _ = pyoracle.image(d, 40, 40, 2, max_bounces=8, seed=15618, flags=flags)
+        mx, l2, ok = _images_equal(gi, oi)
+        # (the reference mode drops every path that escapes the open scene)
+        assert mx == 0.0 and oi[..., :3].mean() > (0.005 if flags == 0 else 5e-4), (flags, mx, l2)
+    st = gpu_ctx.stats()
+    assert st.level_visits[6] > 0  # the 1,167-node level was traversed
+
+
 def test_batching_and_progressive_invariance(gpu_ctx):
     sc = load_fixture("CBbunny")
     gpu_ctx.load_scene(sc)

@@ -109,3 +109,17 @@ def test_ref_arith_oracle_consistent():
         flags = RA | ptrace.PT_FLAG_REF_SCHEDULE | ptrace.PT_FLAG_REF_DROP_ON_MISS | ptrace.PT_FLAG_NO_EMISSION
         img, rays_cast = pyoracle.image(d, 24, 24, 2, flags=flags)
         assert np.isfinite(img).all() and img[..., :3].mean() > 0.01 and rays_cast > 24 * 24 * 2
+
+
+@pytest.mark.parametrize("name", ["CBempty", "CBspheres", "CBbunny"])
+def test_oracle_bvh_walk_equals_brute_force_on_grazing_rays(name):
+    """The oracle's double-precision BVH walk over the guard-banded host boxes
+    finds exactly the brute-force closest hit on grazing rays (walls' edges and
+    vertices, sphere silhouettes)."""
+    from rays import axis_aligned_tris, edge_rays, sphere_tangent_rays
+    d = load_fixture(name).desc()
+    rays = [edge_rays(d, 2000, seed=1, vertex_frac=0.4, prims=axis_aligned_tris(d)), edge_rays(d, 2000, seed=2)]
+    if name == "CBspheres":
+        rays.append(sphere_tangent_rays(d, 2000, seed=3))
+    rays = np.concatenate(rays)
+    assert np.array_equal(pyoracle.intersect(d, rays, use_bvh=True), pyoracle.intersect(d, rays, use_bvh=False))
