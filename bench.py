@@ -11,8 +11,15 @@ under "configs".
 
 A step is one full frame: every rank renders its interleaved 32x32 tiles of the
 1024x1024 image at 256 spp (strong scaling: the frame is fixed, ranks split it),
-then the framebuffer is gathered to rank 0 over RCCL.  Rays are every ray cast
-(camera + extension + shadow), counted on the device.
+then the framebuffer is gathered to rank 0 over RCCL and copied to the host
+(ms/frame ends with the accumulated image on the host; one
+rank: pt_get_image into a pinned buffer).  Rays are every ray cast (camera +
+extension + shadow), counted on the device.
+
+BASELINE config 5 (the dragon proxy at 2048x2048, 1024 spp) runs tiled over
+all ranks when n_gpus >= 8; on fewer GPUs the line carries it as single-GPU
+measurements (the whole frame on one GPU, and one rank's 1/8 tile share),
+labelled as such -- not a scaling figure.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -24,17 +31,22 @@ instrumented frame (the headline frames run without events):
     (ray, node) visit (4 B queue id + 28 B of ray) + 4 B per id pushed to the
     next level (BASELINE.md §3);
   * k_path_leaf (scenes whose BVH root is a leaf: each path runs to completion
-    in registers, no HBM stream): VALU-bound, algorithmic FP32 operations of
-    the primitive tests (69 per ray-triangle test, 20 per ray-sphere test,
-    every primitive of the leaf per ray) against the 157.3 TFLOP/s vector peak.
+    in registers, no HBM stream): VALU-bound, algorithmic FP32 FLOPs of the
+    primitive tests (every primitive of the leaf per ray; an FMA counts 2, an
+    add / mul / div / sqrt 1, compares and selects 0: 42 per ray-triangle
+    test, 19 per ray-sphere test) against the 157.3 TFLOP/s vector peak (which
+    also counts an FMA as 2); PMC VALU activity beside it when profiled.
 Each workload also reports "ms_1spp" (one 1-spp frame, outside the timed
 steps) and, under "trace", the traversal passes of a frame and ms per pass
 (SURVEY §8(d)).
 "traffic" is HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x 2 +
 WRITE_SIZE, MI355X_MICROARCH.md) when a matching summary is committed under
 profiles/ (scripts/pmc.sh, scripts/pmc_summary.py), else null.
-cpu_baseline: the CPU oracle (oracle/ptoracle.c, the Scotty3D-structured tile
-renderer) on a bounded sample of the headline frame on this host.
+cpu_baseline: the CPU oracle run through the Scotty3D PathTracer surface
+(oracle/scotty_cpu.cpp over scotty::PathTracerT: 32x32-tile work queue,
+std::thread::hardware_concurrency() workers, raytrace_tile -> raytrace_pixel;
+pathtracer.cpp:183-213, 499-558) on a bounded sample of the headline frame's
+tiles, on this host.
 """
 import argparse
 import json
@@ -48,8 +60,11 @@ sys.path.insert(0, str(ROOT / "cuda-raytracer_amd"))
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 VALU_PEAK_TFLOPS = 157.3    # MI355X FP32 vector peak, same guide
-FLOP_TRI, FLOP_SPHERE = 69, 20
-PMC_DIR = ROOT / "profiles" / "r01"
+# FP32 FLOPs per primitive test (FMA = 2; trace.hip tri_test: N.d 5, N.o and
+# the plane offset 6, the division 1, P = o + t d 6, three edge tests 8 each;
+# sphere_test: o - c 3, b 5, c 6, disc 2, sqrt 1, the two roots 2)
+FLOP_TRI, FLOP_SPHERE = 42, 19
+PMC_DIR = ROOT / "profiles" / "r02"
 
 
 def parse():
@@ -58,7 +73,7 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scene", default="CBempty", help="headline scene (configs[1] = CBempty)")
-    p.add_argument("--configs", default="CBspheres,CBbunny,dragon_proxy,dragon_proxy_gpubvh",
+    p.add_argument("--configs", default="CBspheres,CBbunny,bunny,dragon_proxy,dragon_proxy_gpubvh",
                    help="other single-GPU configs measured in the same run ('' = none)")
     p.add_argument("--width", type=int, default=1024)
     p.add_argument("--height", type=int, default=1024)
@@ -70,8 +85,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--seed", type=int, default=15618)
     p.add_argument("--config5", choices=["auto", "on", "off"], default="auto",
-                   help="also run BASELINE config 5 (dragon proxy, 2048x2048, 1024 spp, tiles over all ranks); "
-                        "auto = when n_gpus >= 8")
+                   help="BASELINE config 5 (dragon proxy, 2048x2048, 1024 spp): tiled over all ranks when "
+                        "n_gpus >= 8 (auto/on), else one GPU's whole frame and 1/8 tile share (on; auto at 1 GPU)")
     p.add_argument("--no-1spp", action="store_true",
                    help="skip the ms_1spp frame (profiler runs: keeps per-launch averages to full frames)")
     p.add_argument("--stats-in-timed", action="store_true",
@@ -79,30 +94,45 @@ def parse():
     return p.parse_args()
 
 
+def _cpu_share():
+    """CPUs this process may use: affinity mask and cgroup quota (the GPU box
+    shows the whole machine in nproc / hardware_concurrency)."""
+    out = {}
+    try:
+        out["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        out["cgroup_quota_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
 def cpu_baseline(desc, args):
-    """Oracle renderer on this host: a bounded sample of the same frame (same
-    spp and bounces, a 1/nr subset of its interleaved tiles), sized to about
-    --cpu-seconds of CPU work."""
+    """The oracle through the Scotty3D PathTracer surface on this host
+    (hardware_concurrency workers): a bounded sample of the same frame (same
+    spp and bounces, every k-th 32x32 tile), sized to about --cpu-seconds."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle
-    threads = min(16, os.cpu_count() or 1)
-    cal_nr, cal_spp = 64, 4
-    t0 = time.perf_counter()
-    _, rays = pyoracle.render(desc, args.width, args.height, cal_spp, max_bounces=args.bounces, seed=args.seed,
-                              tile=args.tile, rank=0, nranks=cal_nr, threads=threads)
-    dt = time.perf_counter() - t0
-    full_s = dt * cal_nr * args.spp / cal_spp  # estimated CPU seconds for the whole frame
-    nr = 1
-    while full_s / nr > args.cpu_seconds and nr < 4096:
-        nr *= 2
-    t0 = time.perf_counter()
-    _, rays = pyoracle.render(desc, args.width, args.height, args.spp, max_bounces=args.bounces, seed=args.seed,
-                              tile=args.tile, rank=0, nranks=nr, threads=threads)
-    dt = time.perf_counter() - t0
-    npx = len(__import__("ptdist").owned_pixels(args.width, args.height, args.tile, 0, nr))
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{args.scene} {args.width}x{args.height}: tiles t%{nr}==0 ({npx} px), {args.spp} spp, "
-                      f"{args.bounces} bounces; {rays} rays in {dt:.1f} s on {threads} threads"}
+    ntiles = -(-args.width // 32) * -(-args.height // 32)
+    cal = max(1, ntiles // 16)  # calibration: 1/16 of the tiles (at least one) at 4 spp
+    _, rays, dt, thr = pyoracle.scotty_render(desc, args.width, args.height, 4, args.bounces, seed=args.seed,
+                                              tile_stride=cal)
+    full_s = dt * cal * args.spp / 4  # estimated seconds for the whole frame
+    stride = 1
+    while full_s / stride > args.cpu_seconds and stride < ntiles:
+        stride *= 2
+    _, rays, dt, thr = pyoracle.scotty_render(desc, args.width, args.height, args.spp, args.bounces,
+                                              seed=args.seed, tile_stride=stride)
+    nt = len(range(0, ntiles, stride))
+    out = {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": thr, "kind": "port",
+           "sample": f"{args.scene} {args.width}x{args.height}: {nt} of {ntiles} 32x32 tiles (every {stride}th), "
+                     f"{args.spp} spp, {args.bounces} bounces, through the Scotty3D PathTracer surface "
+                     f"(std::thread::hardware_concurrency() = {thr} workers); {rays} rays in {dt:.1f} s"}
+    out.update(_cpu_share())
+    return out
 
 
 def pmc_traffic(scene, kernel):
@@ -133,8 +163,9 @@ def root_leaf_flops(desc):
     return ntri * FLOP_TRI + nsph * FLOP_SPHERE, n.prim_count
 
 
-def run_workload(name, args, ctx, rank, world, dev, dist):
-    """One workload (scene + args' frame shape) timed over args.steps frames."""
+def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
+    """One workload (scene + args' frame shape) timed over args.steps frames.
+    share=(r, n): render only tile share r of n on this one GPU (no gather)."""
     import torch
     import ptrace
     import ptdist
@@ -145,13 +176,23 @@ def run_workload(name, args, ctx, rank, world, dev, dist):
     ctx.load_scene(scene)
     desc = scene.desc()
 
+    # the frame lands in pinned host memory (one rank: pt_get_image; more: the
+    # RCCL gather to rank 0, then rank 0's copy to the host)
+    host = torch.empty((args.height, args.width, 4), dtype=torch.float32, pin_memory=True)
+    t_rank, t_world = share if share else (rank, world)
+
     def frame(stats):
         ctx.clear()
         ctx.render(args.width, args.height, args.spp, max_bounces=args.bounces, seed=args.seed,
-                   batch_paths=args.batch, tile_size=args.tile, rank=rank, nranks=world,
+                   batch_paths=args.batch, tile_size=args.tile, rank=t_rank, nranks=t_world,
                    flags=ptrace.PT_FLAG_STATS if stats else 0)
         if world > 1:
-            ptdist.gather_frame(ptdist.local_sums_tensor(ctx, dev), args.width, args.height, args.tile, args.spp)
+            img = ptdist.gather_frame(ptdist.local_sums_tensor(ctx, dev), args.width, args.height, args.tile,
+                                      args.spp)
+            if img is not None:
+                host.copy_(img)
+        else:
+            ctx.get_image(out=host)
 
     for _ in range(args.warmup):
         frame(False)
@@ -185,7 +226,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist):
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         ctx.render(args.width, args.height, 1, max_bounces=args.bounces, seed=args.seed, batch_paths=args.batch,
-                   tile_size=args.tile, rank=rank, nranks=world)
+                   tile_size=args.tile, rank=t_rank, nranks=t_world)
         torch.cuda.synchronize()
         ms_1spp = (time.perf_counter() - t2) * 1e3
     lvl_ms = sum(st.ms_level[l] for l in range(1, 16))
@@ -287,16 +328,28 @@ def main():
         o, _ = run_workload(name, args, ctx, rank, world, dev, dist)
         o["config"] = f"{args.width}x{args.height} {args.spp}spp {args.bounces} bounces"
         others.append(o)
-    if args.config5 == "on" or (args.config5 == "auto" and world >= 8):
+    import copy
+    a5 = copy.copy(args)
+    a5.width = a5.height = 2048
+    a5.spp = 1024
+    if world >= 8 and args.config5 in ("auto", "on"):
         # BASELINE config 5: the dragon proxy at 2048x2048, 1024 spp, the
         # framebuffer tiled over all ranks and gathered over RCCL
-        import copy
-        a5 = copy.copy(args)
-        a5.width = a5.height = 2048
-        a5.spp = 1024
         a5.steps, a5.warmup = 1, 1
         o, _ = run_workload("dragon_proxy", a5, ctx, rank, world, dev, dist)
         o["config"] = "config 5: 2048x2048 1024spp 8 bounces, tiles over all ranks + RCCL gather"
+        others.append(o)
+    elif world == 1 and (args.config5 == "on" or (args.config5 == "auto" and args.configs)):
+        # config 5's workload on ONE GPU (not a scaling figure): one rank's
+        # share of the 8-GPU tiling (every 8th 32x32 tile), then the whole frame
+        a5.steps, a5.warmup = 1, 1
+        o, _ = run_workload("dragon_proxy", a5, ctx, 0, 1, dev, None, share=(0, 8))
+        o["config"] = ("config 5 workload, single GPU: rank 0's 1/8 tile share of 2048x2048 1024spp 8 bounces "
+                       "(the per-GPU work of the 8-GPU run, no gather)")
+        others.append(o)
+        a5.warmup = 0
+        o, _ = run_workload("dragon_proxy", a5, ctx, 0, 1, dev, None)
+        o["config"] = "config 5 workload, single GPU: the whole 2048x2048 1024spp 8-bounce frame on one MI355X"
         others.append(o)
     if rank == 0:
         out = {

@@ -58,4 +58,15 @@ __global__ __launch_bounds__(TPB) void k_median3(const float4* __restrict__ in, 
   out[i] = make_float4(ref_median_channel(R), ref_median_channel(G), ref_median_channel(B), 1.0f);
 }
 
+// The frame pt_get_image hands to the host (the reference's imageData after
+// kernelAccumulate, cu:739-742): owned pixel q's sum / spp at its row-major
+// position pix_of[q], alpha 1; pixels of other ranks stay as memset (0).
+__global__ __launch_bounds__(TPB) void k_frame(const float4* __restrict__ accum, const uint32_t* __restrict__ pix_of,
+                                               uint32_t npix, float ns, float4* __restrict__ frame) {
+  const uint32_t q = blockIdx.x * TPB + threadIdx.x;
+  if (q >= npix) return;
+  const float4 a = accum[q];
+  frame[pix_of[q]] = make_float4(a.x / ns, a.y / ns, a.z / ns, 1.0f);
+}
+
 }  // namespace pt

@@ -105,6 +105,8 @@ struct pt_ctx {
   std::vector<uint32_t> pix_of;  // owned pixel slot -> global pixel
   uint32_t* d_pix_of = nullptr;
   float4* d_accum = nullptr;
+  float4* d_frame = nullptr;  // row-major frame staged for pt_get_image (k_frame)
+  size_t frame_cap = 0;
   int32_t samples = 0;
 
   pt_stats stats{};
@@ -173,7 +175,7 @@ static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live, c->d_pool,
-                  c->d_pix_of, c->d_accum};
+                  c->d_pix_of, c->d_accum, c->d_frame};
   for (void* p : ptrs)
     if (p) hipFree(p);
 }
@@ -927,22 +929,41 @@ int pt_samples(pt_ctx* c, int32_t* spp) {
   return PT_OK;
 }
 
+// The frame is assembled on the device (k_frame: sums / spp at their row-major
+// positions) and copied to the host in one transfer (full PCIe rate when the
+// caller's buffer is pinned).
 int pt_get_image(pt_ctx* c, float* rgba, size_t n_floats) {
   if (!c || !rgba) return PT_E_INVALID;
-  if ((size_t)c->fb_w * c->fb_h * 4 > n_floats) return fail(c, PT_E_INVALID, "image buffer too small");
+  const size_t npx = (size_t)c->fb_w * c->fb_h;
+  if (npx * 4 > n_floats) return fail(c, PT_E_INVALID, "image buffer too small");
+  if (npx == 0) return PT_OK;
   hipSetDevice(c->device);
-  std::vector<float4> acc(c->pix_of.size());
-  if (!acc.empty())
-    HIPCHK(c, hipMemcpy(acc.data(), c->d_accum, acc.size() * sizeof(float4), hipMemcpyDeviceToHost));
-  memset(rgba, 0, (size_t)c->fb_w * c->fb_h * 4 * sizeof(float));
-  const float ns = (float)(c->samples > 0 ? c->samples : 1);
-  for (size_t q = 0; q < acc.size(); ++q) {
-    float* px = rgba + (size_t)c->pix_of[q] * 4;
-    px[0] = acc[q].x / ns;
-    px[1] = acc[q].y / ns;
-    px[2] = acc[q].z / ns;
-    px[3] = 1.0f;
+  int rc;
+  if (npx > c->frame_cap) {
+    if ((rc = dalloc(c, &c->d_frame, npx))) return rc;
+    c->frame_cap = npx;
   }
+  const uint32_t npix = (uint32_t)c->pix_of.size();
+  if (npix < npx) HIPCHK(c, hipMemsetAsync(c->d_frame, 0, npx * sizeof(float4), c->stream));
+  const float ns = (float)(c->samples > 0 ? c->samples : 1);
+  if (npix)
+    hipLaunchKernelGGL(k_frame, dim3((npix + TPB - 1) / TPB), dim3(TPB), 0, c->stream, (const float4*)c->d_accum,
+                       (const uint32_t*)c->d_pix_of, npix, ns, c->d_frame);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(rgba, c->d_frame, npx * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PT_OK;
+}
+
+int pt_copy_owned_sums(pt_ctx* c, void* dst, size_t n_bytes, int32_t dst_on_device) {
+  if (!c || (!dst && n_bytes)) return PT_E_INVALID;
+  const size_t need = c->pix_of.size() * sizeof(float4);
+  if (n_bytes < need) return fail(c, PT_E_INVALID, "pt_copy_owned_sums: buffer too small");
+  if (need == 0) return PT_OK;
+  hipSetDevice(c->device);
+  HIPCHK(c, hipMemcpyAsync(dst, c->d_accum, need, dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return PT_OK;
 }
 

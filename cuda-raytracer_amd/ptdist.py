@@ -8,8 +8,6 @@ The reference has no multi-GPU path (cu:1874-1897 only enumerates devices).
 """
 from __future__ import annotations
 
-import ctypes as C
-
 import numpy as np
 
 
@@ -25,28 +23,18 @@ def owned_pixels(width, height, tile, rank, nranks):
     return np.concatenate(out).astype(np.int64) if out else np.zeros(0, np.int64)
 
 
-_hip = None
-
-
-def _hip_memcpy_d2d(dst, src, nbytes):
-    global _hip
-    if _hip is None:
-        _hip = C.CDLL("libamdhip64.so")
-        _hip.hipMemcpy.restype = C.c_int
-        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    rc = _hip.hipMemcpy(C.c_void_p(dst), C.c_void_p(src), C.c_size_t(nbytes), 3)  # DeviceToDevice
-    if rc != 0:
-        raise RuntimeError(f"hipMemcpy failed ({rc})")
-
-
 def local_sums_tensor(ctx, device):
-    """This rank's per-pixel radiance sums (float4 per owned pixel) as a torch tensor on `device`."""
+    """This rank's per-pixel radiance sums (float4 per owned pixel, slot order
+    of pt_owned_pixels) as a torch tensor on `device` (a GPU: device-to-device
+    copy by pt_copy_owned_sums on the context's stream; "cpu": to host)."""
     import torch
-    idx, dptr = ctx.owned_pixels()
+    idx, _ = ctx.owned_pixels()
     buf = torch.empty((len(idx), 4), dtype=torch.float32, device=device)
     if len(idx):
-        torch.cuda.synchronize(device)
-        _hip_memcpy_d2d(buf.data_ptr(), dptr, len(idx) * 16)
+        on_dev = buf.device.type != "cpu"
+        if on_dev:
+            torch.cuda.synchronize(buf.device)  # (the allocation is ordered on torch's stream)
+        ctx.copy_owned_sums(buf.data_ptr(), len(idx) * 16, on_device=on_dev)
     return buf
 
 
@@ -66,7 +54,8 @@ def gather_frame(local_sums, width, height, tile, spp, group=None):
     send = torch.zeros((maxn, 4), dtype=torch.float32, device=local_sums.device)
     send[: counts[rank]] = local_sums
     recv = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
-    dist.gather(send, recv, dst=0, group=group)
+    # dst is a global rank: the group's rank 0
+    dist.gather(send, recv, dst=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
     if rank != 0:
         return None
     frame = torch.zeros((height * width, 4), dtype=torch.float32, device=local_sums.device)

@@ -115,7 +115,7 @@ API_SYMBOLS = [
     "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_build_gpu", "pt_scene_build_gpu_ex", "pt_scene_camera_scotty", "pt_scene_free", "pt_scene_get_desc",
     "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
-    "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex",
+    "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex", "pt_copy_owned_sums",
     "pt_get_stats", "pt_reset_stats", "pt_median_filter", "pt_get_display_image", "pt_tonemap",
     "pt_write_png", "pt_write_pfm",
 ]
@@ -164,6 +164,7 @@ def _load():
         "pt_get_image": (C.c_int, [P, C.POINTER(C.c_float), SZ]),
         "pt_owned_pixels": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32), SZ, C.POINTER(P)]),
         "pt_samples": (C.c_int, [P, C.POINTER(I32)]),
+        "pt_copy_owned_sums": (C.c_int, [P, P, SZ, I32]),
         "pt_intersect": (C.c_int, [P, C.POINTER(C.c_float), I32, C.POINTER(C.c_uint64)]),
         "pt_intersect_ex": (C.c_int, [P, C.POINTER(C.c_float), I32, C.POINTER(C.c_uint64), U32]),
         "pt_get_stats": (C.c_int, [P, C.POINTER(pt_stats)]),
@@ -410,10 +411,25 @@ class Context:
         self._chk(LIB.pt_samples(self.h, C.byref(n)))
         return n.value
 
-    def get_image(self):
-        img = np.zeros((self.height, self.width, 4), dtype=np.float32)
-        self._chk(LIB.pt_get_image(self.h, _ptr(img, C.c_float), img.size))
-        return img
+    def get_image(self, out=None):
+        """The accumulated frame (H, W, 4) float32 on the host.  `out`: an
+        optional preallocated host buffer (numpy array or torch CPU tensor,
+        ideally pinned: the copy then runs at full PCIe rate)."""
+        if out is None:
+            img = np.zeros((self.height, self.width, 4), dtype=np.float32)
+            self._chk(LIB.pt_get_image(self.h, _ptr(img, C.c_float), img.size))
+            return img
+        if isinstance(out, np.ndarray):
+            assert out.dtype == np.float32 and out.flags.c_contiguous
+            self._chk(LIB.pt_get_image(self.h, _ptr(out, C.c_float), out.size))
+        else:  # torch tensor
+            assert out.dtype.is_floating_point and out.is_contiguous() and out.device.type == "cpu"
+            self._chk(LIB.pt_get_image(self.h, C.cast(out.data_ptr(), C.POINTER(C.c_float)), out.numel()))
+        return out
+
+    def copy_owned_sums(self, dst_ptr, nbytes, on_device=True):
+        """pt_copy_owned_sums: the owned pixels' float4 sums into dst_ptr."""
+        self._chk(LIB.pt_copy_owned_sums(self.h, C.c_void_p(dst_ptr), nbytes, 1 if on_device else 0))
 
     def get_display_image(self):
         """What CudaRenderer::getImage shows: median-filtered below 32 spp."""

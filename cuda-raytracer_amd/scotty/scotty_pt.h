@@ -7,19 +7,25 @@
 //   StaticScene::BVHAccel(prims, 32), intersect(ray[, isect])
 //                            src/bvh.h:111-149            -> scotty::BVHAccel
 //   CMU462::PathTracer set_scene / set_camera / set_frame_size /
-//     start_raytracing / is_done / raytrace_pixel / save_image
-//                            src/pathtracer.h:51-179      -> scotty::PathTracer
+//     start_raytracing / is_done / raytrace_tile / raytrace_pixel / save_image,
+//     its WorkQueue of 32x32 tiles and worker threads
+//                            src/pathtracer.h:51-179, pathtracer.cpp:183-213,
+//                            499-558, src/work_queue.h  -> scotty::PathTracerT /
+//                                                           scotty::PathTracer
 // Everything is plain C++17 on top of include/pt_api.h; no HIP types here.
 // Errors throw scotty::Error carrying the pt_* code and message (the
 // reference printf()s and exit()s instead).
 #pragma once
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pt_api.h"
@@ -246,50 +252,190 @@ class CudaRenderer {
   int samples_ = 0;
 };
 
-// CMU462::PathTracer surface: the whole frame is traced on the GPU by
-// start_raytracing(); raytrace_pixel(x, y) returns the pixel's estimate.
-class PathTracer {
+// ---- CMU462::PathTracer surface (pathtracer.h:51-257, pathtracer.cpp:183-213,
+// 499-558) ---------------------------------------------------------------------
+// The structure of the Scotty3D renderer is kept: start_raytracing() fills a
+// work queue with imageTileSize x imageTileSize tiles (row of tiles by row,
+// pathtracer.cpp:195-205) and starts numWorkerThreads std::threads running
+// worker_thread(), which pull tiles FIFO (work_queue.h) and call raytrace_tile
+// -> raytrace_pixel(x, y) for every pixel, writing the sample buffer.  The
+// per-pixel estimate comes from an Estimator:
+//   * GpuEstimator (the product path): the whole frame is traced on the GPU
+//     through the C ABI when raytracing starts (one pt_render: the reference's
+//     CudaRenderer path); raytrace_pixel reads the pixel of that frame;
+//   * any type with begin(w, h, spp, max_depth, flags) and
+//     pixel(x, y, float rgba[4]) (e.g. the CPU oracle's estimator that times
+//     the CPU baseline and makes the config-1 golden, oracle/scotty_cpu.cpp).
+// Pixel (x, y) is column x of row y, rows counted bottom-up (the frame
+// layout of pt_api.h; save_image flips rows like pathtracer.cpp:584-586).
+
+struct WorkItem {  // src/work_queue.h / pathtracer.h WorkItem
+  size_t tile_x = 0, tile_y = 0, tile_w = 0, tile_h = 0;
+};
+class WorkQueue {
  public:
-  PathTracer(size_t ns_aa = 1, size_t max_ray_depth = 4, size_t /*ns_area_light*/ = 1, size_t /*ns_diff*/ = 1,
-             size_t /*ns_glsy*/ = 1, size_t /*ns_refr*/ = 1, size_t /*num_threads*/ = 1)
-      : ns_aa_(ns_aa), max_depth_(max_ray_depth) {}
+  void put_work(const WorkItem& w) {
+    std::lock_guard<std::mutex> g(m_);
+    q_.push_back(w);
+  }
+  bool try_get_work(WorkItem* out) {
+    std::lock_guard<std::mutex> g(m_);
+    if (next_ >= q_.size()) return false;
+    *out = q_[next_++];
+    return true;
+  }
+  void clear() {
+    std::lock_guard<std::mutex> g(m_);
+    q_.clear();
+    next_ = 0;
+  }
+
+ private:
+  std::mutex m_;
+  std::vector<WorkItem> q_;
+  size_t next_ = 0;
+};
+
+// GPU estimator: a scotty::CudaRenderer on one device.
+class GpuEstimator {
+ public:
+  explicit GpuEstimator(int device = 0) : r_(device) {}
   void set_scene(const std::string& dae_path) {
     r_.loadScene(dae_path);
     r_.setup();
   }
-  void set_camera(const Camera&) {}  // the scene's camera is used (cu:1590-1607)
-  void set_frame_size(size_t w, size_t h) { r_.allocOutputImage((int)w, (int)h); }
-  void start_raytracing() {
+  void begin(size_t w, size_t h, size_t spp, size_t max_depth, uint32_t flags) {
+    r_.allocOutputImage((int)w, (int)h);
     r_.clearImage();
-    r_.render((int)ns_aa_, (int)max_depth_);
-    img_ = r_.getImage();
+    r_.render((int)spp, (int)max_depth, flags);
+    img_ = r_.getAccumulatedImage();
   }
-  bool is_done() const { return img_ != nullptr; }
-  Vector3D raytrace_pixel(size_t x, size_t y) const {
-    if (!img_) throw Error(PT_E_INVALID, "raytrace_pixel before start_raytracing");
+  void pixel(size_t x, size_t y, float rgba[4]) const {
     const float* p = &img_->data[((size_t)y * img_->width + x) * 4];
-    return Vector3D(p[0], p[1], p[2]);
-  }
-  // pathtracer.cpp:577-591 writes a tonemapped PNG; ".pfm" keeps the floats
-  void save_image(const std::string& filename) const {
-    if (!img_) throw Error(PT_E_INVALID, "save_image before start_raytracing");
-    const bool pfm = filename.size() >= 4 && filename.compare(filename.size() - 4, 4, ".pfm") == 0;
-    int rc;
-    if (pfm) {
-      rc = pt_write_pfm(filename.c_str(), img_->data.data(), img_->width, img_->height);
-    } else {
-      std::vector<uint8_t> rgba8((size_t)img_->width * img_->height * 4);
-      rc = pt_tonemap(img_->data.data(), img_->width, img_->height, 2.2f, 1.0f, rgba8.data());
-      if (!rc) rc = pt_write_png(filename.c_str(), rgba8.data(), img_->width, img_->height);
-    }
-    if (rc) throw Error(rc, "save_image: cannot write " + filename);
+    for (int k = 0; k < 4; ++k) rgba[k] = p[k];
   }
   CudaRenderer& renderer() { return r_; }
 
  private:
-  size_t ns_aa_, max_depth_;
   CudaRenderer r_;
   const Image* img_ = nullptr;
+};
+
+template <class Estimator>
+class PathTracerT {
+ public:
+  enum State { INIT, READY, RENDERING, DONE };
+  // (ns_aa, max_ray_depth, ns_area_light, ns_diff, ns_glsy, ns_refr,
+  // num_threads) as pathtracer.h:57-60; num_threads 0 = hardware_concurrency
+  PathTracerT(Estimator& est, size_t ns_aa = 1, size_t max_ray_depth = 4, size_t /*ns_area_light*/ = 1,
+              size_t /*ns_diff*/ = 1, size_t /*ns_glsy*/ = 1, size_t /*ns_refr*/ = 1, size_t num_threads = 0)
+      : est_(est), ns_aa_(ns_aa), max_depth_(max_ray_depth) {
+    num_threads_ = num_threads ? num_threads : std::max(1u, std::thread::hardware_concurrency());
+  }
+  ~PathTracerT() { join(); }
+  PathTracerT(const PathTracerT&) = delete;
+  PathTracerT& operator=(const PathTracerT&) = delete;
+
+  void set_frame_size(size_t w, size_t h) {
+    w_ = w;
+    h_ = h;
+    buf_.assign(w * h * 4, 0.0f);
+    state_ = READY;
+  }
+  void set_flags(uint32_t flags) { flags_ = flags; }  // pt_render_params.flags (PT_FLAG_*)
+  size_t num_worker_threads() const { return num_threads_; }
+
+  void start_raytracing() {  // pathtracer.cpp:183-213
+    if (state_ != READY) throw Error(PT_E_INVALID, "start_raytracing: set_frame_size first");
+    join();
+    state_ = RENDERING;
+    work_.clear();
+    std::fill(buf_.begin(), buf_.end(), 0.0f);
+    est_.begin(w_, h_, ns_aa_, max_depth_, flags_);
+    for (size_t y = 0; y < h_; y += tile_)
+      for (size_t x = 0; x < w_; x += tile_) work_.put_work(WorkItem{x, y, tile_, tile_});
+    done_ = 0;
+    for (size_t i = 0; i < num_threads_; ++i) threads_.emplace_back(&PathTracerT::worker_thread, this);
+  }
+  // blocks until every worker is done (the reference polls is_done from its
+  // GUI loop; here the caller waits)
+  bool is_done() {
+    join();
+    return state_ == DONE;
+  }
+  void raytrace_tile(size_t tx, size_t ty, size_t tw, size_t th) {  // pathtracer.cpp:510-535
+    const size_t xe = std::min(tx + tw, w_), ye = std::min(ty + th, h_);
+    for (size_t y = ty; y < ye; ++y)
+      for (size_t x = tx; x < xe; ++x) raytrace_pixel(x, y, &buf_[(y * w_ + x) * 4]);
+  }
+  void raytrace_pixel(size_t x, size_t y, float rgba[4]) { est_.pixel(x, y, rgba); }  // pathtracer.cpp:499-508
+  Vector3D raytrace_pixel(size_t x, size_t y) {
+    float p[4];
+    raytrace_pixel(x, y, p);
+    return Vector3D(p[0], p[1], p[2]);
+  }
+  // the frame of the last start_raytracing(): RGBA floats, rows bottom-up
+  const std::vector<float>& frame() {
+    if (!is_done()) throw Error(PT_E_INVALID, "frame before start_raytracing");
+    return buf_;
+  }
+  Vector3D pixel(size_t x, size_t y) {
+    const float* p = &frame()[(y * w_ + x) * 4];
+    return Vector3D(p[0], p[1], p[2]);
+  }
+  // pathtracer.cpp:577-591 writes a tonemapped PNG; ".pfm" keeps the floats
+  void save_image(const std::string& filename) {
+    const std::vector<float>& f = frame();
+    const bool pfm = filename.size() >= 4 && filename.compare(filename.size() - 4, 4, ".pfm") == 0;
+    int rc;
+    if (pfm) {
+      rc = pt_write_pfm(filename.c_str(), f.data(), (int32_t)w_, (int32_t)h_);
+    } else {
+      std::vector<uint8_t> rgba8(w_ * h_ * 4);
+      rc = pt_tonemap(f.data(), (int32_t)w_, (int32_t)h_, 2.2f, 1.0f, rgba8.data());
+      if (!rc) rc = pt_write_png(filename.c_str(), rgba8.data(), (int32_t)w_, (int32_t)h_);
+    }
+    if (rc) throw Error(rc, "save_image: cannot write " + filename);
+  }
+  Estimator& estimator() { return est_; }
+
+ private:
+  void worker_thread() {  // pathtracer.cpp:537-558
+    WorkItem w;
+    while (work_.try_get_work(&w)) raytrace_tile(w.tile_x, w.tile_y, w.tile_w, w.tile_h);
+    std::lock_guard<std::mutex> g(m_);
+    if (++done_ == num_threads_) state_ = DONE;
+  }
+  void join() {
+    for (auto& t : threads_)
+      if (t.joinable()) t.join();
+    threads_.clear();
+  }
+
+  Estimator& est_;
+  size_t ns_aa_, max_depth_, num_threads_;
+  size_t tile_ = 32;  // imageTileSize, pathtracer.cpp:55
+  size_t w_ = 0, h_ = 0;
+  uint32_t flags_ = 0;
+  std::vector<float> buf_;
+  WorkQueue work_;
+  std::vector<std::thread> threads_;
+  std::mutex m_;
+  size_t done_ = 0;
+  State state_ = INIT;
+};
+
+// The GPU-backed Scotty3D PathTracer (the drop-in): owns its GpuEstimator.
+class PathTracer : private GpuEstimator, public PathTracerT<GpuEstimator> {
+ public:
+  PathTracer(size_t ns_aa = 1, size_t max_ray_depth = 4, size_t ns_area_light = 1, size_t ns_diff = 1,
+             size_t ns_glsy = 1, size_t ns_refr = 1, size_t num_threads = 1, int device = 0)
+      : GpuEstimator(device),
+        PathTracerT<GpuEstimator>(*static_cast<GpuEstimator*>(this), ns_aa, max_ray_depth, ns_area_light, ns_diff,
+                                  ns_glsy, ns_refr, num_threads) {}
+  void set_scene(const std::string& dae_path) { GpuEstimator::set_scene(dae_path); }
+  void set_camera(const Camera&) {}  // the scene's camera is used (cu:1590-1607)
+  CudaRenderer& renderer() { return GpuEstimator::renderer(); }
 };
 
 }  // namespace scotty

@@ -33,6 +33,7 @@ int main(int argc, char** argv) {
     pt.set_scene(argv[1]);
     auto t0 = std::chrono::steady_clock::now();
     pt.start_raytracing();
+    pt.is_done();
     double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     pt_stats st{};
     pt_get_stats(pt.renderer().device().get(), &st);

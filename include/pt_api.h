@@ -296,6 +296,11 @@ int pt_get_image(pt_ctx* ctx, float* rgba, size_t n_floats);
  * pointer to their float4 radiance sums (not divided by spp). */
 int pt_owned_pixels(pt_ctx* ctx, int32_t* n_pixels, int32_t* pixel_index, size_t max_idx,
                     void** device_sums);
+/* Copy the owned pixels' float4 radiance sums (slot order of pt_owned_pixels,
+ * not divided by spp) into dst: device memory of this context's GPU
+ * (dst_on_device != 0, e.g. a torch tensor handed to the RCCL gather) or host
+ * memory.  n_bytes >= 16 * owned pixels.  Synchronous. */
+int pt_copy_owned_sums(pt_ctx* ctx, void* dst, size_t n_bytes, int32_t dst_on_device);
 /* Samples per pixel accumulated so far. */
 int pt_samples(pt_ctx* ctx, int32_t* spp);
 

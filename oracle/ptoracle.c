@@ -719,6 +719,37 @@ void pto_sample(const pt_scene_desc* S, int W, int H, int max_bounces, uint32_t 
   out3[2] = l.z;
 }
 
+/* One pixel's estimate as the context reports it (pt_get_image): the fp32 sum
+ * of its spp samples in sample order, divided by spp; *rays += rays cast.
+ * The per-pixel estimator of the Scotty3D-surface CPU renderer
+ * (oracle/scotty_cpu.cpp, PathTracer::raytrace_pixel, pathtracer.cpp:499-508). */
+void pto_pixel(const pt_scene_desc* S, int W, int H, int spp, int max_bounces, uint32_t seed, uint32_t flags,
+               int sample_offset, uint32_t g, float* out4, uint64_t* rays) {
+  job_t J;
+  memset(&J, 0, sizeof(J));
+  J.S = S;
+  J.W = W;
+  J.H = H;
+  J.max_bounces = max_bounces;
+  J.seed = seed;
+  J.flags = flags;
+  J.use_bvh = 1;
+  uint64_t nr = 0;
+  float ax = 0.0f, ay = 0.0f, az = 0.0f;
+  for (int s = 0; s < spp; ++s) {
+    v3 l = path_radiance(&J, g, (uint32_t)(sample_offset + s), &nr);
+    ax = ax + l.x;
+    ay = ay + l.y;
+    az = az + l.z;
+  }
+  const float ns = (float)(spp > 0 ? spp : 1);
+  out4[0] = ax / ns;
+  out4[1] = ay / ns;
+  out4[2] = az / ns;
+  out4[3] = 1.0f;
+  if (rays) *rays += nr;
+}
+
 /* ---- display filter: kernelMedianFilter, cu:773-842 --------------------------
  * Per channel: remove the maximum of the 3x3 neighbourhood three times (max
  * search from 0.0 with >=, the last index wins, the removed value becomes 0)

@@ -53,6 +53,30 @@ def _load():
 LIB = _load()
 
 
+def _load_scotty():
+    lib = C.CDLL(str(HERE / "build" / "libptscotty.so"))
+    lib.pto_scotty_render.restype = C.c_uint64
+    lib.pto_scotty_render.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
+                                      C.c_int, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_double),
+                                      C.POINTER(C.c_int)]
+    return lib
+
+
+SCOTTY = _load_scotty()
+
+
+def scotty_render(desc, width, height, spp, max_bounces=8, seed=15618, flags=0, threads=0, tile_stride=1):
+    """The oracle through the Scotty3D PathTracer surface (oracle/scotty_cpu.cpp:
+    32x32-tile work queue, `threads` workers, 0 = hardware_concurrency).
+    Returns (image (H, W, 4) = sum / spp like pt_get_image, rays, seconds,
+    threads used).  tile_stride > 1 renders only tiles t % tile_stride == 0."""
+    img = np.zeros((height, width, 4), dtype=np.float32)
+    sec, thr = C.c_double(), C.c_int()
+    rays = SCOTTY.pto_scotty_render(C.addressof(desc), width, height, spp, max_bounces, seed, flags, threads,
+                                    tile_stride, _f(img), C.byref(sec), C.byref(thr))
+    return img, int(rays), sec.value, thr.value
+
+
 def _f(a):
     return a.ctypes.data_as(C.POINTER(C.c_float))
 
