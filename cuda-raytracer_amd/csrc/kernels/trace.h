@@ -133,6 +133,12 @@ struct LevelArgs {
   uint32_t* mode_w;
   int ids;      // 1: the level's queues hold ray ids, 0: ray entries
   int out_ids;  // format of the queues it pushes into (the next level's ids)
+  // two-level traversal (pt_device.hip trace_levels): on a "real" level an
+  // interior node's rays go straight to its leaf children and to the children
+  // of its interior children (two BVH levels per visit); interior nodes of the
+  // levels in between are never queued and allocate nothing
+  int real;       // interior nodes of this level receive rays and allocate their targets
+  int two_level;  // their targets are leaf children + grandchildren (else the 4 children)
 };
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {

@@ -565,9 +565,106 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, ui
 // Levels >= 1 are processed at wave granularity: no LDS, no workgroup barrier,
 // one returning atomic per wave per child.  Deep levels hold many nodes with a
 // few hundred rays each, where 1024-ray workgroup items would run mostly empty.
+// Two-level push (real levels of the two-level traversal): the wave's rays
+// that enter child c of the node go straight to c's queue when c is a leaf,
+// else to the queues of c's children that they enter (c itself is never
+// queued: one ray gather, one queue round trip and one scan instead of two per
+// pair of BVH levels).  Target t = 4c + g (g = 0 for a leaf child); lane t
+// holds its node, count and slot base, so the up to 16 slot reservations take
+// one atomic round trip.  A grandchild's box is tested only for rays that
+// entered its parent's box.  Ray ids only (the queues hold ids).
+__device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, const CPTR(pt_node) nd, int lane,
+                                               const uint32_t (&id)[RPTW], const f3 (&inv)[RPTW],
+                                               const f3 (&oi)[RPTW], const float (&tmax)[RPTW],
+                                               const bool (&valid)[RPTW], int nj) {
+  const uint32_t lid = lane_id();
+  // the targets (node data only): lane t = 4c + g holds the node of target
+  // t -- leaf child c (g = 0) or child g of interior child c -- or -1
+  int tnode = -1;
+  bool tleaf = false;
+  if (lid < 16) {
+    const int ch = A.nodes[node].child[lid >> 2];
+    if (ch >= 0) {
+      tleaf = A.nodes[ch].prim_count > 0;
+      tnode = tleaf ? ((lid & 3) == 0 ? ch : -1) : A.nodes[ch].child[lid & 3];
+    }
+  }
+  const uint32_t tmask = (uint32_t)__ballot(tnode >= 0);           // (uniform)
+  const uint32_t lmask = (uint32_t)__ballot(tnode >= 0 && tleaf);  // targets that are leaf children
+  uint32_t bits[RPTW];
+#pragma unroll
+  for (int j = 0; j < RPTW; ++j) bits[j] = 0;
+  // (not unrolled: one child node's records in SGPRs at a time)
+#pragma unroll 1
+  for (int c = 0; c < 4; ++c) {
+    const uint32_t cm = (tmask >> (4 * c)) & 0xFu;
+    if (!cm) continue;
+    uint32_t hc = 0;  // rays j that enter child c (bit j)
+#pragma unroll
+    for (int j = 0; j < RPTW; ++j) {
+      if (j >= nj) break;
+      const bool h = valid[j] && box_hit(nd->bmin_x[c], nd->bmax_x[c], nd->bmin_y[c], nd->bmax_y[c], nd->bmin_z[c],
+                                         nd->bmax_z[c], oi[j], inv[j], tmax[j]);
+      hc |= h ? (1u << j) : 0u;
+    }
+    if (!__any(hc != 0)) continue;
+    if ((lmask >> (4 * c)) & 1u) {
+#pragma unroll
+      for (int j = 0; j < RPTW; ++j) bits[j] |= ((hc >> j) & 1u) << (4 * c);
+      continue;
+    }
+    const CPTR(pt_node) cn = (const CPTR(pt_node))(A.nodes + nd->child[c]);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (!((cm >> g) & 1u)) continue;
+#pragma unroll
+      for (int j = 0; j < RPTW; ++j) {
+        if (j >= nj) break;
+        const bool h = ((hc >> j) & 1u) && box_hit(cn->bmin_x[g], cn->bmax_x[g], cn->bmin_y[g], cn->bmax_y[g],
+                                                   cn->bmin_z[g], cn->bmax_z[g], oi[j], inv[j], tmax[j]);
+        bits[j] |= h ? (1u << (4 * c + g)) : 0u;
+      }
+    }
+  }
+  // lane t: rays pushed to target t
+  uint32_t tot = 0;
+  for (uint32_t m = tmask; m; m &= m - 1) {
+    const uint32_t t = (uint32_t)__builtin_ctz(m);
+    uint32_t cntt = 0;
+#pragma unroll
+    for (int j = 0; j < RPTW; ++j) cntt += (uint32_t)__popcll(__ballot((bits[j] >> t) & 1u));
+    tot = lid == t ? cntt : tot;
+  }
+#ifdef PT_DBG_SEQ_TARGETS
+  for (uint32_t m = tmask; m; m &= m - 1) {
+    const uint32_t t = (uint32_t)__builtin_ctz(m);
+    const int tn = __builtin_amdgcn_readlane(tnode, t);
+    const uint32_t tt = __builtin_amdgcn_readlane(tot, t);
+    if (tt == 0) continue;
+    uint32_t bb = 0;
+    if (lid == 0) bb = atomicAdd(A.cnt + cnt_idx(tn, lane), tt) + A.qoff[(size_t)tn * NLANE + lane];
+    uint32_t off = __builtin_amdgcn_readfirstlane(bb);
+#else
+  // every target's slot reservation and queue offset in one round trip
+  uint32_t b = 0;
+  if (tnode >= 0 && tot) b = atomicAdd(A.cnt + cnt_idx(tnode, lane), tot) + A.qoff[(size_t)tnode * NLANE + lane];
+  for (uint32_t m = tmask; m; m &= m - 1) {
+    const uint32_t t = (uint32_t)__builtin_ctz(m);
+    uint32_t off = __builtin_amdgcn_readlane(b, t);
+#endif
+#pragma unroll
+    for (int j = 0; j < RPTW; ++j) {
+      const bool h = (bits[j] >> t) & 1u;
+      const unsigned long long mm = __ballot(h);
+      if (h) A.q[off + mbcnt64(mm)] = id[j];
+      off += (uint32_t)__popcll(mm);
+    }
+  }
+}
+
 template <bool REFA = false>
 __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane, bool ids,
-                                             bool out_ids) {
+                                             bool out_ids, bool two_level) {
   const uint32_t lid = lane_id();
   const CPTR(pt_node) nd = (const CPTR(pt_node))(A.nodes + node);
   uint32_t id[RPTW];
@@ -636,6 +733,17 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     }
     return;
   }
+  if (two_level) {
+    f3 inv[RPTW], oi[RPTW];
+#pragma unroll
+    for (int j = 0; j < RPTW; ++j) {
+      inv[j] = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
+                  __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
+      oi[j] = mk(o[j].x * inv[j].x, o[j].y * inv[j].y, o[j].z * inv[j].z);
+    }
+    push_two_level(A, node, nd, lane, id, inv, oi, tmax, valid, nj);
+    return;
+  }
   uint32_t bits[RPTW];
 #pragma unroll
   for (int j = 0; j < RPTW; ++j) {
@@ -687,10 +795,11 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 // ---- per-level pass: every wave walks the items of its block's lane ----------------
 // Lane s's items are processed by blocks b with b % 8 == s (same XCD under the
 // observed round-robin placement: a speed hint only).
-// 6 waves per SIMD (<= 80 VGPRs, no spills): +2-3 % over the unconstrained
-// 106 VGPRs (4 waves); 7 waves spill and lose 4 %
+// 5 waves per SIMD (<= 96 VGPRs): the two-level push needs 91 without spills
+// (at 6 waves, 80 VGPRs, it spilled 19; round 1's one-level push: 6 waves
+// +2-3 % over 4, 7 waves spilled and lost 4 %)
 #ifndef PT_LEVEL_ATTR
-#define PT_LEVEL_ATTR __attribute__((amdgpu_waves_per_eu(6, 8)))
+#define PT_LEVEL_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
 #endif
 template <bool REFA>
 __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, LevelArgs L) {
@@ -755,7 +864,7 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
     const uint32_t base = A.qoff[(size_t)node * NLANE + lane] + i * WTILE;
     const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
     process_wave<REFA>(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane,
-                 L.ids != 0, L.out_ids != 0);
+                       L.ids != 0, L.out_ids != 0, L.two_level != 0);
   }
 }
 
@@ -772,6 +881,26 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
 // their counter loads are issued together, and a level that fits one chunk
 // (all but the widest) keeps its counts in registers between the passes.
 constexpr int SCAN_NPT = 2;
+// Target t = 4c + g of an interior node (the same numbering as
+// push_two_level): one level -- child c (g = 0); two-level -- the leaf child
+// c (g = 0) or child g of the interior child c.  -1 if none.
+__device__ __forceinline__ int scan_target(const TraceArgs& A, int node, int t, bool two_level) {
+  const int ch = A.nodes[node].child[t >> 2];
+  if (ch < 0) return -1;
+  const bool direct = !two_level || A.nodes[ch].prim_count > 0;
+  const int gc = A.nodes[ch].child[t & 3];
+  return direct ? ((t & 3) == 0 ? ch : -1) : gc;
+}
+// Number of targets through child c (0, 1, or up to 4 grandchildren).
+__device__ __forceinline__ uint32_t scan_targets_of(const TraceArgs& A, int node, int c, bool two_level) {
+  const int ch = A.nodes[node].child[c];
+  if (ch < 0) return 0u;
+  const bool direct = !two_level || A.nodes[ch].prim_count > 0;
+  const int* gcp = A.nodes[ch].child;
+  const uint32_t ng = (gcp[0] >= 0 ? 1u : 0u) + (gcp[1] >= 0 ? 1u : 0u) + (gcp[2] >= 0 ? 1u : 0u) +
+                      (gcp[3] >= 0 ? 1u : 0u);
+  return direct ? 1u : ng;
+}
 __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, uint32_t lanecap,
                                                      uint32_t out_parity_base, unsigned long long* stats,
                                                      int level, uint32_t* err) {
@@ -839,7 +968,9 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
   }
   // workgroup items when the (node, lane) queues are long (few nodes, high
   // atomic contention), wave items otherwise
-  const bool block_mode = V >= (unsigned long long)BLOCK_MODE_RAYS_PER_PAIR * (PAIRS ? PAIRS : 1ull);
+  // (the two-level push exists for wave items only)
+  const bool block_mode =
+      !L.two_level && V >= (unsigned long long)BLOCK_MODE_RAYS_PER_PAIR * (PAIRS ? PAIRS : 1ull);
   const uint32_t itile = block_mode ? TILE : WTILE;
   const uint32_t ishift = (uint32_t)__builtin_ctz(itile);
 
@@ -847,21 +978,25 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
   // child capacity per lane), thread-sequential over its nodes, then a block
   // exclusive scan of the thread totals
   for (int chunk = 0; chunk < L.nl; chunk += CH) {
-    int child[SCAN_NPT][4];
+    // queue targets of each node: its children, or (two-level) its leaf
+    // children and the children of its interior children; none for the
+    // interior nodes of a level that is not real (their children's queues are
+    // allocated by the real level above them)
+    // (the targets are counted here and listed again where their queues are
+    // written: 16 of them per node do not fit this kernel's registers.  The
+    // count is written without early exits: an increment in a `continue`
+    // branch of this loop was dropped by the compiler -- hipcc, ROCm 7.2 --
+    // for the first child, the first two-level build lost rays)
     uint32_t nch[SCAN_NPT];
 #pragma unroll
     for (int i = 0; i < SCAN_NPT; ++i) {
       const int k = chunk + tid * SCAN_NPT + i;
-      nch[i] = 0;
+      uint32_t n = 0;
+      if (L.real && k < L.nl && A.nodes[L.first + k].prim_count == 0) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) child[i][c] = -1;
-      if (k < L.nl && A.nodes[L.first + k].prim_count == 0) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          child[i][c] = A.nodes[L.first + k].child[c];
-          nch[i] += child[i][c] >= 0 ? 1u : 0u;
-        }
+        for (int c = 0; c < 4; ++c) n += scan_targets_of(A, L.first + k, c, L.two_level != 0);
       }
+      nch[i] = n;
       if (!one) {
 #pragma unroll
         for (int s = 0; s < NLANE; ++s) cnt[i][s] = k < L.nl ? L.icnt_w[s * row + k] : 0u;
@@ -913,14 +1048,17 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
             for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + k] = ex[s];
           } else {
             uint32_t jj = 0;
+            auto alloc = [&](int target) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              if (child[i][c] >= 0) {
-#pragma unroll
-                for (int s = 0; s < NLANE; ++s)
-                  A.qoff[(size_t)child[i][c] * NLANE + s] =
-                      out_parity_base + (uint32_t)s * lanecap + ex[s] + jj * cnt[i][s];
-                jj++;
+              for (int s = 0; s < NLANE; ++s)
+                A.qoff[(size_t)target * NLANE + s] = out_parity_base + (uint32_t)s * lanecap + ex[s] + jj * cnt[i][s];
+              jj++;
+            };
+            if (nch[i]) {
+              const int node = L.first + k;
+              for (int t = 0; t < 16; ++t) {
+                const int tn = scan_target(A, node, t, L.two_level != 0);
+                if (tn >= 0) alloc(tn);
               }
             }
           }

@@ -56,6 +56,8 @@ struct pt_ctx {
   int max_level_nodes = 0;
   bool root_leaf = true;
   bool skip_l1 = false;  // root pass pushes straight into the level-2 queues
+  bool two_level = true; // two-level traversal (trace_levels; PT_TWO_LEVEL=0: one level per pass)
+  std::vector<char> level_has_leaf;
   RootTable rt{};        // root pass: inline leaves and queue targets (build_root_table)
   std::vector<pt_node> nodes_host;
   pt_light light{};
@@ -75,12 +77,12 @@ struct pt_ctx {
   size_t cap_qfactor = 0;
   float4* d_ray = nullptr;  // 2N ray records (trace.h), RSTRIDE float4 each
   float4 *d_ps0 = nullptr, *d_ps1 = nullptr, *d_ps2 = nullptr, *d_ps3 = nullptr;
-  uint32_t* d_q = nullptr;   // ray-id queues (two parity halves): the root's targets and the levels above entry_level
-  size_t qcap = 0;           // ids per parity half
+  uint32_t* d_q = nullptr;   // ray-id queues (QREGIONS regions): the root's targets and the levels above entry_level
+  size_t qcap = 0;           // ids per region
   int entry_level = 0;       // first level whose queues hold ray entries (build_root_table)
   uint32_t shadow_base = 0xFFFFFFFFu;  // ray slots >= it are shadow rays (pt_render sets N; pt_intersect none)
   float4* d_qe = nullptr;    // ray-entry queues of the levels below the root's targets
-  size_t qecap = 0;          // entries per parity half
+  size_t qecap = 0;          // entries per region
   uint32_t* d_cnt = nullptr;
   uint32_t* d_qoff = nullptr;
   uint32_t* d_iprefix = nullptr;
@@ -198,9 +200,13 @@ static constexpr uint32_t CHUNK_PATHS = 1u << 28;
 #define PT_POLL_GROUP 4
 #endif
 static constexpr int POLL_GROUP = PT_POLL_GROUP;
-// ray-id queues hold ID_FACTOR x qfactor ids per ray slot and parity half
-// (the entry queues qfactor entries of 32 B)
-static constexpr size_t ID_FACTOR = 6;
+// ray-id queues hold ID_FACTOR x qfactor ids per ray slot and region (the
+// entry queues qfactor entries of 32 B).  Queues live in QREGIONS rotating
+// regions: the scan of level l allocates its targets' queues (levels l + 1 and,
+// two-level, l + 2) in region l % 3, the root pass in region 0; region l % 3 is
+// next written by the scan of level l + 3, after the last reader (level l + 2).
+static constexpr size_t ID_FACTOR = 4;
+static constexpr size_t QREGIONS = 3;
 // Ray entries below the root targets' level measured -3 % on CBbunny and
 // +1.5-4 % on the dragon proxy trees (the leaf-heavy levels are bound by the
 // leaf loop and the closest-hit atomics, not by the ray gathers): off by default.
@@ -211,7 +217,7 @@ static constexpr int ENTRY_LEVEL_DEFAULT = PT_ENTRY_LEVEL_DEFAULT;
 static uint32_t max_batch_paths(const pt_ctx* c, uint32_t slots_per_path) {
   // u32 entry offsets: both halves of the entry queues, and the root's id
   // queues (<= 16 targets x every ray, see root_per_lane)
-  const uint64_t a = (1ull << 32) / (2 * ID_FACTOR * c->qfactor * slots_per_path);
+  const uint64_t a = (1ull << 32) / (QREGIONS * ID_FACTOR * c->qfactor * slots_per_path);
   const uint64_t b = (1ull << 32) / (20ull * slots_per_path);
   return (uint32_t)std::min<uint64_t>(std::min(a, b), 0xFFFFFFFFull) & ~4095u;
 }
@@ -250,10 +256,10 @@ static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
   const bool entries = !c->root_leaf && c->entry_level < c->n_levels;
   c->qecap = entries ? c->qfactor * slots : NLANE * 64;
   c->qecap = (c->qecap + NLANE * 64 - 1) / (NLANE * 64) * (NLANE * 64);
-  if (2 * c->qcap >= (1ull << 32) || 2 * c->qecap >= (1ull << 32))
+  if (QREGIONS * c->qcap >= (1ull << 32) || QREGIONS * c->qecap >= (1ull << 32))
     return fail(c, PT_E_UNSUPPORTED, "batch too large for u32 queue offsets");
-  if ((rc = dalloc(c, &c->d_q, 2 * c->qcap))) return rc;
-  if ((rc = dalloc(c, &c->d_qe, 2 * c->qecap * QESTRIDE))) return rc;
+  if ((rc = dalloc(c, &c->d_q, QREGIONS * c->qcap))) return rc;
+  if ((rc = dalloc(c, &c->d_qe, QREGIONS * c->qecap * QESTRIDE))) return rc;
   c->cap_paths = N;
   c->cap_spp = spp;
   c->cap_qfactor = c->qfactor;
@@ -317,10 +323,14 @@ static void build_root_table(pt_ctx* c) {
       if (nd[ch].child[g] >= 0 && !try_inline(ch, g)) add_target(ch, g);
   }
   c->skip_l1 = skip;
-  // ray entries from PT_ENTRY_LEVEL levels below the root's targets on (0: ids only)
+  // two-level traversal (default; PT_TWO_LEVEL=0 restores one level per pass)
+  const char* tl = getenv("PT_TWO_LEVEL");
+  c->two_level = !(tl && atoi(tl) == 0);
+  // ray entries from PT_ENTRY_LEVEL levels below the root's targets on (0: ids
+  // only; the two-level push writes ids)
   const char* el = getenv("PT_ENTRY_LEVEL");
   const int eoff = el ? atoi(el) : ENTRY_LEVEL_DEFAULT;
-  c->entry_level = eoff > 0 ? (skip ? 2 : 1) + eoff : 1 << 20;
+  c->entry_level = (eoff > 0 && !c->two_level) ? (skip ? 2 : 1) + eoff : 1 << 20;
 }
 
 // Queue offsets of the root's targets: each gets root_per_lane ids in every
@@ -333,7 +343,7 @@ static int set_root_child_offsets(pt_ctx* c) {
   // targets: nodes of level 1 or, when level 1 is skipped, of level 2
   std::vector<int> targets(c->rt.tnode, c->rt.tnode + c->rt.nt);
   if (targets.size() * per_lane > lanecap) return fail(c, PT_E_OVERFLOW, "root queue capacity");
-  const size_t half = c->skip_l1 ? 0 : c->qcap;  // the parity half of their level
+  const size_t half = 0;  // region 0 (the root pass's allocation)
   // ordered on the context's (non-blocking) stream behind any work in flight
   std::vector<uint32_t> off(targets.size() * NLANE);
   for (size_t jj = 0; jj < targets.size(); ++jj)
@@ -363,9 +373,19 @@ static TraceArgs trace_args(pt_ctx* c) {
 // or fused into k_camera_push / k_shade_push).
 static int trace_levels(pt_ctx* c) {
   TraceArgs A = trace_args(c);
+  // Two-level traversal: the root targets' level l0 and every second level
+  // below it are "real" -- their interior nodes push rays straight to their
+  // leaf children and to their grandchildren; interior nodes of the levels in
+  // between are never queued, so those levels run only for their leaves (and
+  // not at all when they have none).  One ray gather, one queue round trip and
+  // one scan per two BVH levels.
   const int l0 = c->skip_l1 ? 2 : 1;  // the root targets' level: its queues hold ids
   for (int l = l0; l < c->n_levels; ++l) {
+    const bool real = !c->two_level || ((l - l0) & 1) == 0;
+    if (!real && !c->level_has_leaf[l]) continue;
     LevelArgs L;
+    L.real = real;
+    L.two_level = c->two_level && real;
     L.first = c->level_start[l];
     L.nl = c->level_start[l + 1] - c->level_start[l];
     L.maxln = c->max_level_nodes;
@@ -381,7 +401,7 @@ static int trace_levels(pt_ctx* c) {
     L.ids = l < c->entry_level;
     L.out_ids = l + 1 < c->entry_level;
     const size_t lanecap = (L.out_ids ? c->qcap : c->qecap) / NLANE;
-    const uint32_t out_base = (uint32_t)(((l + 1) & 1) ? (L.out_ids ? c->qcap : c->qecap) : 0);
+    const uint32_t out_base = (uint32_t)((size_t)(l % QREGIONS) * (L.out_ids ? c->qcap : c->qecap));
     c->launch(pt_ctx::K_SCAN, l, k_scan_level, dim3(1), dim3(1024), A, L, (uint32_t)lanecap, out_base,
               c->d_stats, l, c->d_err);
     if (c->refa)
@@ -616,6 +636,10 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     c->max_level_nodes = std::max(c->max_level_nodes, c->level_start[l + 1] - c->level_start[l]);
   c->nodes_host.assign(s->nodes, s->nodes + s->n_nodes);
   c->root_leaf = c->nodes_host[0].prim_count > 0;
+  c->level_has_leaf.assign(s->n_levels, 0);
+  for (int l = 0; l < s->n_levels; ++l)
+    for (int i = std::max(0, s->level_start[l]); i < std::min(s->n_nodes, s->level_start[l + 1]); ++i)
+      if (s->nodes[i].prim_count > 0) c->level_has_leaf[l] = 1;
   for (int i = 0; i < s->n_nodes; ++i) {
     const pt_node& nd = s->nodes[i];
     if (nd.prim_start < 0 || nd.prim_count < 0 || nd.prim_start + nd.prim_count > s->n_prims)

@@ -8,7 +8,8 @@ FETCH_SIZE and WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE counts 128-B
 memory-side requests at 64 B (MI355X_MICROARCH.md, HBM section), so the
 corrected read bytes are 2 x FETCH_SIZE; the table shows them as READ_GB and
 WRITE_GB.  With --levels L, k_trace_level dispatches are split by level
-(launch order cycles through levels 1..L-1 in every traversal pass).
+(launch order cycles through levels F..L-1 in every traversal pass; F =
+--first-level, default 1, 2 for trees whose root pass skips level 1).
 """
 import csv
 import sys
@@ -27,12 +28,13 @@ def short(name):
 def main():
     args = sys.argv[1:]
     opts = {}
-    for o in ("--levels", "--json", "--config"):
+    for o in ("--levels", "--first-level", "--json", "--config"):
         if o in args:
             i = args.index(o)
             opts[o] = args[i + 1]
             del args[i:i + 2]
     levels = int(opts.get("--levels", 0))
+    first = int(opts.get("--first-level", 1))  # 2 when the root pass skips level 1
     agg = defaultdict(lambda: defaultdict(float))  # key -> counter -> value
     ndisp = defaultdict(set)
     per_file = defaultdict(dict)  # key -> path -> dispatch ids
@@ -48,7 +50,7 @@ def main():
             d = int(r["Dispatch_Id"])
             k = short(r["Kernel_Name"])
             if levels and k == "k_trace_level" and d not in lvl_of:
-                lvl_of[d] = li % (levels - 1) + 1
+                lvl_of[d] = li % (levels - first) + first
                 li += 1
         for r in rows:
             d = int(r["Dispatch_Id"])
