@@ -135,17 +135,41 @@ def cpu_baseline(desc, args):
     return out
 
 
-def pmc_traffic(scene, kernel):
-    """HBM bytes per launch of `kernel` from a committed PMC summary, if any."""
+def pmc_kernel(scene, kernel):
+    """The committed PMC summary of `kernel` in `scene`'s profile, if any."""
     f = PMC_DIR / f"pmc_{scene}.json"
     if not f.exists():
         return None, None
     try:
         d = json.loads(f.read_text())
-        k = d["kernels"][kernel]
-        return k["hbm_bytes_per_launch"], f"{f.relative_to(ROOT)} ({d.get('config', '')})"
+        return d["kernels"][kernel], f"{f.relative_to(ROOT)} ({d.get('config', '')})"
     except (KeyError, ValueError):
         return None, None
+
+
+def pmc_traffic(scene, kernel):
+    """HBM bytes per launch of `kernel` from a committed PMC summary, if any."""
+    k, src = pmc_kernel(scene, kernel)
+    if not k or "hbm_bytes_per_launch" not in k:
+        return None, None
+    return k["hbm_bytes_per_launch"], src
+
+
+# gfx950: 256 CUs x 4 SIMDs, 8 XCDs; a wave64 fp32 VALU instruction occupies
+# its SIMD for 2 cycles (32 lanes per cycle: 157.3 TF = 1024 SIMDs x 2.4 GHz x
+# 32 FMA x 2); GRBM_GUI_ACTIVE is summed over the 8 XCDs.
+N_SIMD, N_XCD, VALU_CYCLES_PER_INST = 1024, 8, 2
+
+
+def pmc_valu_busy(scene, kernel):
+    """Fraction of SIMD cycles issuing VALU work during `kernel`'s launches
+    (SQ_INSTS_VALU x 2 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)); transcendental
+    and 64-bit ops take longer, so this is a lower bound."""
+    k, _ = pmc_kernel(scene, kernel)
+    try:
+        return round(k["SQ_INSTS_VALU"] * VALU_CYCLES_PER_INST / (N_SIMD * k["GRBM_GUI_ACTIVE"] / N_XCD), 3)
+    except (TypeError, KeyError, ZeroDivisionError):
+        return None
 
 
 def root_leaf_flops(desc):
@@ -251,7 +275,10 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
                 "frac": round(ach / VALU_PEAK_TFLOPS, 4), "traffic": traffic, "kernel": kernel,
                 "launches": int(launches), "avg_launch_us": round(st.ms_path * 1e3 / max(1, launches), 2),
                 "flop_per_launch": int(path_flops / max(1, launches)),
-                "note": "single-leaf BVH: paths run to completion in registers; FP32 VALU, not HBM, bounds it"}
+                "valu_busy": pmc_valu_busy(name, kernel),
+                "note": "single-leaf BVH: paths run to completion in registers; FP32 VALU, not HBM, bounds it; "
+                        "achieved counts only the leaf's intersection flops (FMA = 2), valu_busy (PMC) is the "
+                        "share of SIMD cycles issuing any VALU instruction (shading, NEE, RNG included)"}
     else:
         kernel, launches = "k_trace_level", lvl_launches
         ach = (lvl_bytes / (lvl_ms * 1e-3) / 1e9) if lvl_ms > 0 else 0.0
@@ -259,7 +286,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
                 "launches": int(launches), "avg_launch_us": round(lvl_ms * 1e3 / max(1, launches), 2),
-                "bytes_per_launch": int(lvl_bytes / max(1, launches))}
+                "bytes_per_launch": int(lvl_bytes / max(1, launches)), "valu_busy": pmc_valu_busy(name, kernel)}
     if src:
         roof["traffic_source"] = src
     others = []
@@ -273,7 +300,8 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
                  "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": straffic, "kernel": "k_shade_push",
                  "launches": int(st.shade_launches),
                  "avg_launch_us": round(st.ms_shade_push * 1e3 / max(1, st.shade_launches), 2),
-                 "bytes_per_launch": int(sbytes / max(1, st.shade_launches)), "shaded_vertices": int(st.shaded)}
+                 "bytes_per_launch": int(sbytes / max(1, st.shade_launches)), "shaded_vertices": int(st.shaded),
+                 "valu_busy": pmc_valu_busy(name, "k_shade_push")}
         if ssrc:
             sroof["traffic_source"] = ssrc
         if st.ms_shade_push > lvl_ms:  # the dominant kernel first
@@ -301,6 +329,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
                   "ms_scan": round(st.ms_scan, 1), "ms_levels": round(lvl_ms, 1),
                   "levels": [{"level": l, "ms": round(st.ms_level[l], 2), "visits": int(st.level_visits[l]),
                               "leaf_visits": int(st.level_leaf_visits[l]), "items": int(st.level_items[l]),
+                              "scan_ms": round(st.ms_scan_level[l], 2),
                               "Gvisits_per_s": round(st.level_visits[l] / max(st.ms_level[l], 1e-9) / 1e6, 2)}
                              for l in range(1, st.n_levels) if st.level_launches[l] > 0]},
     }

@@ -880,26 +880,37 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
 // Each thread owns SCAN_NPT consecutive nodes of a chunk of 1024 * SCAN_NPT:
 // their counter loads are issued together, and a level that fits one chunk
 // (all but the widest) keeps its counts in registers between the passes.
-constexpr int SCAN_NPT = 2;
-// Target t = 4c + g of an interior node (the same numbering as
-// push_two_level): one level -- child c (g = 0); two-level -- the leaf child
-// c (g = 0) or child g of the interior child c.  -1 if none.
-__device__ __forceinline__ int scan_target(const TraceArgs& A, int node, int t, bool two_level) {
-  const int ch = A.nodes[node].child[t >> 2];
-  if (ch < 0) return -1;
-  const bool direct = !two_level || A.nodes[ch].prim_count > 0;
-  const int gc = A.nodes[ch].child[t & 3];
-  return direct ? ((t & 3) == 0 ? ch : -1) : gc;
+#ifndef PT_SCAN_NPT
+#define PT_SCAN_NPT 2
+#endif
+constexpr int SCAN_NPT = PT_SCAN_NPT;
+// A node's child ids and prim_count in two 16-B loads (pt_node: child[4] at
+// byte 96, {prim_start, prim_count, level, ref_id} at 112).
+__device__ __forceinline__ void load_links(const TraceArgs& A, int node, int4& ch, int& pc) {
+  const int4* q = reinterpret_cast<const int4*>(&A.nodes[node].child[0]);
+  ch = q[0];
+  pc = q[1].y;
 }
-// Number of targets through child c (0, 1, or up to 4 grandchildren).
-__device__ __forceinline__ uint32_t scan_targets_of(const TraceArgs& A, int node, int c, bool two_level) {
-  const int ch = A.nodes[node].child[c];
-  if (ch < 0) return 0u;
-  const bool direct = !two_level || A.nodes[ch].prim_count > 0;
-  const int* gcp = A.nodes[ch].child;
-  const uint32_t ng = (gcp[0] >= 0 ? 1u : 0u) + (gcp[1] >= 0 ? 1u : 0u) + (gcp[2] >= 0 ? 1u : 0u) +
-                      (gcp[3] >= 0 ? 1u : 0u);
-  return direct ? 1u : ng;
+__device__ __forceinline__ int i4(const int4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+// Queue targets of an interior node: t = 4c + g (the numbering of
+// push_two_level) -- one level: child c (g = 0); two-level: the leaf child c
+// (g = 0) or child g of the interior child c.  The node's links c4, its
+// children's g4 / gpc (prim_count); -1 if none.
+__device__ __forceinline__ int scan_target(const int4& c4, const int4 (&g4)[4], const int (&gpc)[4], int t,
+                                           bool two_level) {
+  const int ch = i4(c4, t >> 2);
+  const bool direct = !two_level || gpc[t >> 2] > 0;
+  return ch < 0 ? -1 : direct ? ((t & 3) == 0 ? ch : -1) : i4(g4[t >> 2], t & 3);
+}
+__device__ __forceinline__ void load_targets(const TraceArgs& A, int node, int4& c4, int4 (&g4)[4], int (&gpc)[4]) {
+  int pc;
+  load_links(A, node, c4, pc);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    g4[c] = make_int4(-1, -1, -1, -1);
+    gpc[c] = 1;
+    if (i4(c4, c) >= 0) load_links(A, i4(c4, c), g4[c], gpc[c]);
+  }
 }
 __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, uint32_t lanecap,
                                                      uint32_t out_parity_base, unsigned long long* stats,
@@ -993,8 +1004,11 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
       const int k = chunk + tid * SCAN_NPT + i;
       uint32_t n = 0;
       if (L.real && k < L.nl && A.nodes[L.first + k].prim_count == 0) {
+        int4 c4, g4[4];
+        int gpc[4];
+        load_targets(A, L.first + k, c4, g4, gpc);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) n += scan_targets_of(A, L.first + k, c, L.two_level != 0);
+        for (int t = 0; t < 16; ++t) n += scan_target(c4, g4, gpc, t, L.two_level != 0) >= 0 ? 1u : 0u;
       }
       nch[i] = n;
       if (!one) {
@@ -1055,9 +1069,15 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
               jj++;
             };
             if (nch[i]) {
-              const int node = L.first + k;
+              // the node's links and its children's, all loaded before the
+              // first qoff store (a load issued after a store waits for it:
+              // one memory round trip per target otherwise)
+              int4 c4, g4[4];
+              int gpc[4];
+              load_targets(A, L.first + k, c4, g4, gpc);
+#pragma unroll
               for (int t = 0; t < 16; ++t) {
-                const int tn = scan_target(A, node, t, L.two_level != 0);
+                const int tn = scan_target(c4, g4, gpc, t, L.two_level != 0);
                 if (tn >= 0) alloc(tn);
               }
             }
@@ -1089,6 +1109,207 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
       if (level < 16) {
         atomicAdd(stats + STAT_LV0 + level, V);
         atomicAdd(stats + STAT_LEAF0 + level, LEAFV);
+        atomicAdd(stats + STAT_ITEMS0 + level, items);
+      }
+      atomicMax(stats + STAT_PEAKQ, need * NLANE);
+    }
+  }
+}
+
+
+// ---- multi-workgroup level scan (wide levels) --------------------------------------
+// The results of k_scan_level in two launches of G = ceil(nl / SCAN_WG)
+// workgroups, one node per thread, for levels too wide for one workgroup to
+// scan quickly (a single workgroup walks them in chunks, one memory round trip
+// after another):
+//  k_scan_count: snapshot + re-zero the node's counters, count its queue
+//    targets (kept in aux for the second launch) and reduce the workgroup's
+//    partials: items per lane at TILE and at WTILE rays per item (the item
+//    shape is not known before the level's totals are), child capacity per
+//    lane, V, PAIRS, LEAFV;
+//  k_scan_alloc: every workgroup sums the partials of the workgroups before
+//    it (its exclusive offset) and of all (the level's totals: item shape,
+//    overflow), scans its own nodes and writes their item prefixes and their
+//    targets' queue offsets; the last workgroup writes the sentinels, the
+//    mode, the overflow flag and the stats.
+// aux: SCAN_MAXG rows of AGG_STRIDE u32 partials, then one target count per node.
+constexpr int SCAN_WG = 256;
+constexpr int AGG_N = 27, AGG_STRIDE = 32, SCAN_MAXG = 256;
+enum { AGG_IT = 0, AGG_IW = 8, AGG_CAP = 16, AGG_V = 24, AGG_PAIRS = 25, AGG_LEAFV = 26 };
+
+__global__ __launch_bounds__(SCAN_WG) void k_scan_count(TraceArgs A, LevelArgs L, uint32_t* __restrict__ aux) {
+  __shared__ uint32_t red[SCAN_WG / 64][AGG_N];
+  const int tid = threadIdx.x, wave = tid >> 6, ln = tid & 63;
+  const int k = blockIdx.x * SCAN_WG + tid;
+  const size_t row = (size_t)L.maxln + 1;
+  uint32_t c[NLANE], nch = 0;
+  bool leaf = false;
+#pragma unroll
+  for (int s = 0; s < NLANE; ++s) c[s] = 0u;
+  if (k < L.nl) {
+    const int node = L.first + k;
+    int4 c4;
+    int pc;
+    load_links(A, node, c4, pc);
+#pragma unroll
+    for (int s = 0; s < NLANE; ++s) c[s] = A.cnt[cnt_idx(node, s)];
+    leaf = pc > 0;
+    if (L.real && !leaf) {
+      int4 g4[4];
+      int gpc[4];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        g4[cc] = make_int4(-1, -1, -1, -1);
+        gpc[cc] = 1;
+        if (i4(c4, cc) >= 0) load_links(A, i4(c4, cc), g4[cc], gpc[cc]);
+      }
+#pragma unroll
+      for (int t = 0; t < 16; ++t) nch += scan_target(c4, g4, gpc, t, L.two_level != 0) >= 0 ? 1u : 0u;
+    }
+#pragma unroll
+    for (int s = 0; s < NLANE; ++s) {
+      L.icnt_w[s * row + k] = c[s];
+      A.cnt[cnt_idx(node, s)] = 0u;
+    }
+    aux[SCAN_MAXG * AGG_STRIDE + k] = nch;
+  }
+  constexpr uint32_t sT = __builtin_ctz(TILE), sW = __builtin_ctz(WTILE);
+  uint32_t v = 0, pairs = 0;
+#pragma unroll
+  for (int s = 0; s < NLANE; ++s) {
+    const uint32_t a = wave_sum((c[s] + TILE - 1) >> sT), b = wave_sum((c[s] + WTILE - 1) >> sW),
+                   d = wave_sum(c[s] * nch);
+    if (ln == 0) {
+      red[wave][AGG_IT + s] = a;
+      red[wave][AGG_IW + s] = b;
+      red[wave][AGG_CAP + s] = d;
+    }
+    v += c[s];
+    pairs += c[s] ? 1u : 0u;
+  }
+  const uint32_t wv = wave_sum(v), wp = wave_sum(pairs), wl = wave_sum(leaf ? v : 0u);
+  if (ln == 0) {
+    red[wave][AGG_V] = wv;
+    red[wave][AGG_PAIRS] = wp;
+    red[wave][AGG_LEAFV] = wl;
+  }
+  __syncthreads();
+  if (tid < AGG_N) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < SCAN_WG / 64; ++w) t += red[w][tid];
+    aux[(size_t)blockIdx.x * AGG_STRIDE + tid] = t;
+  }
+}
+
+__global__ __launch_bounds__(SCAN_WG) void k_scan_alloc(TraceArgs A, LevelArgs L, const uint32_t* __restrict__ aux,
+                                                       uint32_t lanecap, uint32_t out_parity_base,
+                                                       unsigned long long* stats, int level, uint32_t* err) {
+  __shared__ uint32_t s_pre[AGG_N], s_tot[AGG_N];
+  __shared__ uint32_t wsum[SCAN_WG / 64][2 * NLANE];
+  const int tid = threadIdx.x, wave = tid >> 6, ln = tid & 63;
+  const int G = gridDim.x, b = blockIdx.x;
+  const size_t row = (size_t)L.maxln + 1;
+  // partials of the workgroups before this one, and of all: wave 0, one
+  // workgroup row per lane (all of a row's loads in flight together)
+  if (wave == 0) {
+    uint32_t pre[AGG_N], tot[AGG_N];
+#pragma unroll
+    for (int i = 0; i < AGG_N; ++i) pre[i] = tot[i] = 0u;
+    for (int r0 = 0; r0 < G; r0 += 64) {
+      const int r = r0 + ln;
+      uint32_t x[AGG_N];
+#pragma unroll
+      for (int i = 0; i < AGG_N; ++i) x[i] = r < G ? aux[(size_t)r * AGG_STRIDE + i] : 0u;
+#pragma unroll
+      for (int i = 0; i < AGG_N; ++i) {
+        tot[i] += x[i];
+        pre[i] += r < b ? x[i] : 0u;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < AGG_N; ++i) {
+      const uint32_t a = wave_sum(pre[i]), t = wave_sum(tot[i]);
+      if (ln == 0) {
+        s_pre[i] = a;
+        s_tot[i] = t;
+      }
+    }
+  }
+  __syncthreads();
+  const bool block_mode =
+      !L.two_level && (unsigned long long)s_tot[AGG_V] >=
+                          (unsigned long long)BLOCK_MODE_RAYS_PER_PAIR * (s_tot[AGG_PAIRS] ? s_tot[AGG_PAIRS] : 1u);
+  const uint32_t itile = block_mode ? TILE : WTILE;
+  const uint32_t ishift = (uint32_t)__builtin_ctz(itile);
+  const int ia = block_mode ? AGG_IT : AGG_IW;
+
+  const int k = b * SCAN_WG + tid;
+  uint32_t c[NLANE], nch = 0;
+#pragma unroll
+  for (int s = 0; s < NLANE; ++s) c[s] = 0u;
+  if (k < L.nl) {
+#pragma unroll
+    for (int s = 0; s < NLANE; ++s) c[s] = L.icnt[s * row + k];
+    nch = aux[SCAN_MAXG * AGG_STRIDE + k];
+  }
+  // workgroup exclusive scan of 16 values (items, capacity per lane)
+  uint32_t ex[2 * NLANE];
+#pragma unroll
+  for (int j = 0; j < 2 * NLANE; ++j) {
+    const uint32_t tv = j < NLANE ? (c[j] + itile - 1) >> ishift : c[j - NLANE] * nch;
+    uint32_t x = tv;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off, 64);
+      if (ln >= off) x += y;
+    }
+    ex[j] = x - tv;
+    if (ln == 63) wsum[wave][j] = x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2 * NLANE; ++j) {
+    uint32_t w = j < NLANE ? s_pre[ia + j] : s_pre[AGG_CAP + j - NLANE];
+    for (int q = 0; q < wave; ++q) w += wsum[q][j];
+    ex[j] += w;
+  }
+  if (k < L.nl) {
+#pragma unroll
+    for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + k] = ex[s];
+    if (nch) {
+      int4 c4, g4[4];
+      int gpc[4];
+      load_targets(A, L.first + k, c4, g4, gpc);
+      uint32_t jj = 0;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int tn = scan_target(c4, g4, gpc, t, L.two_level != 0);
+        if (tn >= 0) {
+#pragma unroll
+          for (int s = 0; s < NLANE; ++s)
+            A.qoff[(size_t)tn * NLANE + s] = out_parity_base + (uint32_t)s * lanecap + ex[NLANE + s] + jj * c[s];
+          jj++;
+        }
+      }
+    }
+  }
+  if (b == G - 1 && tid == 0) {
+    bool ovf = false;
+    unsigned long long items = 0, need = 0;
+    for (int s = 0; s < NLANE; ++s) {
+      if (s_tot[AGG_CAP + s] > lanecap) ovf = true;
+      items += s_tot[ia + s];
+      need = max(need, (unsigned long long)s_tot[AGG_CAP + s]);
+    }
+    for (int s = 0; s < NLANE; ++s) L.iprefix_w[s * row + L.nl] = ovf ? 0u : s_tot[ia + s];
+    *L.mode_w = block_mode ? MODE_BLOCK : MODE_WAVE;
+    if (ovf) atomicOr(err, 1u);
+    if (stats) {
+      atomicAdd(stats + STAT_V, (unsigned long long)s_tot[AGG_V]);
+      if (level < 16) {
+        atomicAdd(stats + STAT_LV0 + level, (unsigned long long)s_tot[AGG_V]);
+        atomicAdd(stats + STAT_LEAF0 + level, (unsigned long long)s_tot[AGG_LEAFV]);
         atomicAdd(stats + STAT_ITEMS0 + level, items);
       }
       atomicMax(stats + STAT_PEAKQ, need * NLANE);

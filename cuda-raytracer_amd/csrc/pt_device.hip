@@ -88,6 +88,8 @@ struct pt_ctx {
   uint32_t* d_iprefix = nullptr;
   uint32_t* d_nitems = nullptr;  // one per level
   uint32_t* d_icnt = nullptr;
+  uint32_t* d_scan_aux = nullptr;  // multi-workgroup scan: partials + per-node target counts
+  int scan_multi_min = 0;          // levels with more nodes use k_scan_count + k_scan_alloc
   unsigned long long* d_rcount = nullptr;  // valid root rays: RCOUNT_SLOTS counters, one 128-B line each
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
@@ -176,7 +178,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
-                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live, c->d_pool,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live, c->d_pool,
                   c->d_pix_of, c->d_accum, c->d_frame};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -214,6 +216,10 @@ static constexpr size_t QREGIONS = 3;
 #define PT_ENTRY_LEVEL_DEFAULT 0
 #endif
 static constexpr int ENTRY_LEVEL_DEFAULT = PT_ENTRY_LEVEL_DEFAULT;
+#ifndef PT_SCAN_MULTI_MIN_DEFAULT
+#define PT_SCAN_MULTI_MIN_DEFAULT 512
+#endif
+static constexpr int SCAN_MULTI_MIN_DEFAULT = PT_SCAN_MULTI_MIN_DEFAULT;
 static uint32_t max_batch_paths(const pt_ctx* c, uint32_t slots_per_path) {
   // u32 entry offsets: both halves of the entry queues, and the root's id
   // queues (<= 16 targets x every ray, see root_per_lane)
@@ -331,6 +337,9 @@ static void build_root_table(pt_ctx* c) {
   const char* el = getenv("PT_ENTRY_LEVEL");
   const int eoff = el ? atoi(el) : ENTRY_LEVEL_DEFAULT;
   c->entry_level = (eoff > 0 && !c->two_level) ? (skip ? 2 : 1) + eoff : 1 << 20;
+  // levels wider than this scan with many workgroups (PT_SCAN_MULTI_MIN nodes)
+  const char* sm = getenv("PT_SCAN_MULTI_MIN");
+  c->scan_multi_min = sm ? atoi(sm) : SCAN_MULTI_MIN_DEFAULT;
 }
 
 // Queue offsets of the root's targets: each gets root_per_lane ids in every
@@ -402,8 +411,15 @@ static int trace_levels(pt_ctx* c) {
     L.out_ids = l + 1 < c->entry_level;
     const size_t lanecap = (L.out_ids ? c->qcap : c->qecap) / NLANE;
     const uint32_t out_base = (uint32_t)((size_t)(l % QREGIONS) * (L.out_ids ? c->qcap : c->qecap));
-    c->launch(pt_ctx::K_SCAN, l, k_scan_level, dim3(1), dim3(1024), A, L, (uint32_t)lanecap, out_base,
-              c->d_stats, l, c->d_err);
+    const int G = (L.nl + SCAN_WG - 1) / SCAN_WG;
+    if (L.nl > c->scan_multi_min && G <= SCAN_MAXG) {
+      c->launch(pt_ctx::K_SCAN, l, k_scan_count, dim3(G), dim3(SCAN_WG), A, L, c->d_scan_aux);
+      c->launch(pt_ctx::K_SCAN, l, k_scan_alloc, dim3(G), dim3(SCAN_WG), A, L, (const uint32_t*)c->d_scan_aux,
+                (uint32_t)lanecap, out_base, c->d_stats, l, c->d_err);
+    } else {
+      c->launch(pt_ctx::K_SCAN, l, k_scan_level, dim3(1), dim3(1024), A, L, (uint32_t)lanecap, out_base,
+                c->d_stats, l, c->d_err);
+    }
     if (c->refa)
       c->launch(pt_ctx::K_LEVEL, l, k_trace_level<true>, dim3(LEVEL_GRID), dim3(TPB), A, L);
     else
@@ -446,6 +462,7 @@ static void collect_marks(pt_ctx* c) {
         break;
       case pt_ctx::K_SCAN:
         c->stats.ms_scan += ms;
+        if (m.level < 16) c->stats.ms_scan_level[m.level] += ms;
         c->stats.ms_trace += ms;
         break;
       case pt_ctx::K_LEVEL:
@@ -667,6 +684,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   if ((rc = dalloc(c, &c->d_qoff, (size_t)s->n_nodes * NLANE))) return rc;
   if ((rc = dalloc(c, &c->d_iprefix, (size_t)NLANE * (c->max_level_nodes + 1)))) return rc;
   if ((rc = dalloc(c, &c->d_icnt, (size_t)NLANE * (c->max_level_nodes + 1)))) return rc;
+  if ((rc = dalloc(c, &c->d_scan_aux, (size_t)SCAN_MAXG * AGG_STRIDE + c->max_level_nodes + 1))) return rc;
   if ((rc = dalloc(c, &c->d_nitems, 2 * std::max(1, s->n_levels) + NLANE))) return rc;
   HIPCHK(c, hipMemcpy(c->d_nodes, s->nodes, sizeof(pt_node) * s->n_nodes, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_prims, s->prims, sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));

@@ -100,7 +100,8 @@ class pt_stats(C.Structure):
                 ("peak_queue_entries", C.c_uint64), ("n_levels", C.c_int32), ("batch_paths", C.c_int32),
                 ("ms_path", C.c_double), ("path_launches", C.c_uint64),
                 ("shaded", C.c_uint64), ("ms_shade_push", C.c_double), ("shade_launches", C.c_uint64),
-                ("queue_factor", C.c_int32), ("pad_", C.c_int32)]
+                ("queue_factor", C.c_int32), ("pad_", C.c_int32),
+                ("ms_scan_level", C.c_double * 16)]
 
 
 class pt_mesh_desc(C.Structure):

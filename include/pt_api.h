@@ -365,6 +365,7 @@ typedef struct pt_stats {
   uint64_t shade_launches;
   int32_t queue_factor;   /* current queue factor (grows when a level overflows) */
   int32_t pad_;
+  double ms_scan_level[16]; /* k_scan_level per BVH level (part of ms_scan)  */
 } pt_stats;
 int pt_get_stats(pt_ctx* ctx, pt_stats* out);
 int pt_reset_stats(pt_ctx* ctx);

@@ -12,7 +12,7 @@ import json, sys
 l = [x for x in open(sys.argv[2]) if x.startswith("{")][-1]
 d = json.loads(l)
 t = d["trace"]
-lv = " ".join(f"L{x['level']}:{x['ms']:.1f}" for x in t["levels"])
+lv = " ".join(f"L{x['level']}:{x['ms']:.1f}/s{x.get('scan_ms', 0):.1f}" for x in t["levels"])
 print(f"[{sys.argv[1] or 'base'}] {d['value']:.0f} Mrays/s {d['ms_per_frame']:.1f} ms  levels {t['ms_levels']:.1f} shade {t['ms_shade_push']:.1f} scan {t['ms_scan']:.1f} | {lv}", flush=True)
 PY
   n=$((n+1))
