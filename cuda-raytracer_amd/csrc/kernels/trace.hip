@@ -573,6 +573,7 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, ui
 // holds its node, count and slot base, so the up to 16 slot reservations take
 // one atomic round trip.  A grandchild's box is tested only for rays that
 // entered its parent's box.  Ray ids only (the queues hold ids).
+__device__ __forceinline__ float f4c(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
 __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, const CPTR(pt_node) nd, int lane,
                                                const uint32_t (&id)[RPTW], const f3 (&inv)[RPTW],
                                                const f3 (&oi)[RPTW], const float (&tmax)[RPTW],
@@ -599,12 +600,16 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
   for (int c = 0; c < 4; ++c) {
     const uint32_t cm = (tmask >> (4 * c)) & 0xFu;
     if (!cm) continue;
+    // the child's box in SGPRs once (the compiler re-issued the six scalar
+    // loads inside every ray's branch, one round trip each)
+    const float cb0 = nd->bmin_x[c], cb1 = nd->bmax_x[c], cb2 = nd->bmin_y[c], cb3 = nd->bmax_y[c],
+                cb4 = nd->bmin_z[c], cb5 = nd->bmax_z[c];
+    asm volatile("" ::"s"(cb0), "s"(cb1), "s"(cb2), "s"(cb3), "s"(cb4), "s"(cb5));
     uint32_t hc = 0;  // rays j that enter child c (bit j)
 #pragma unroll
     for (int j = 0; j < RPTW; ++j) {
       if (j >= nj) break;
-      const bool h = valid[j] && box_hit(nd->bmin_x[c], nd->bmax_x[c], nd->bmin_y[c], nd->bmax_y[c], nd->bmin_z[c],
-                                         nd->bmax_z[c], oi[j], inv[j], tmax[j]);
+      const bool h = valid[j] && box_hit(cb0, cb1, cb2, cb3, cb4, cb5, oi[j], inv[j], tmax[j]);
       hc |= h ? (1u << j) : 0u;
     }
     if (!__any(hc != 0)) continue;
@@ -613,15 +618,20 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
       for (int j = 0; j < RPTW; ++j) bits[j] |= ((hc >> j) & 1u) << (4 * c);
       continue;
     }
-    const CPTR(pt_node) cn = (const CPTR(pt_node))(A.nodes + nd->child[c]);
+    // the four grandchild boxes (SoA rows of the child node) in one round trip
+    const CPTR(f4v) cn = (const CPTR(f4v))(A.nodes + nd->child[c]);
+    const float4 gx0 = f4(cn[0]), gx1 = f4(cn[1]), gy0 = f4(cn[2]), gy1 = f4(cn[3]), gz0 = f4(cn[4]),
+                 gz1 = f4(cn[5]);
+    asm volatile("" ::"s"(gx0.x), "s"(gx1.x), "s"(gy0.x), "s"(gy1.x), "s"(gz0.x), "s"(gz1.x));
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       if (!((cm >> g) & 1u)) continue;
+      const float b0 = f4c(gx0, g), b1 = f4c(gx1, g), b2 = f4c(gy0, g), b3 = f4c(gy1, g), b4 = f4c(gz0, g),
+                  b5 = f4c(gz1, g);
 #pragma unroll
       for (int j = 0; j < RPTW; ++j) {
         if (j >= nj) break;
-        const bool h = ((hc >> j) & 1u) && box_hit(cn->bmin_x[g], cn->bmax_x[g], cn->bmin_y[g], cn->bmax_y[g],
-                                                   cn->bmin_z[g], cn->bmax_z[g], oi[j], inv[j], tmax[j]);
+        const bool h = ((hc >> j) & 1u) && box_hit(b0, b1, b2, b3, b4, b5, oi[j], inv[j], tmax[j]);
         bits[j] |= h ? (1u << (4 * c + g)) : 0u;
       }
     }

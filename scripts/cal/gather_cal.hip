@@ -34,6 +34,35 @@ __global__ void k_gather32(const float4* __restrict__ rec, const uint32_t* __res
   }
   if (s == 1234.5f) out[0] = s;
 }
+// the same gather with the loads' cache-policy bits set (gfx950 global_load
+// sc0 / sc1 / nt): does a non-default policy fetch less than a 128-B line?
+template <int POL>
+__device__ __forceinline__ float4 ldpol(const float4* p) {
+  float4 r;
+  if constexpr (POL == 1)
+    asm volatile("global_load_dwordx4 %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+  else if constexpr (POL == 2)
+    asm volatile("global_load_dwordx4 %0, %1, off sc0\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+  else if constexpr (POL == 3)
+    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+  else if constexpr (POL == 4)
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+  else if constexpr (POL == 5)
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+  else
+    asm volatile("global_load_dwordx4 %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+template <int POL>
+__global__ void k_gather32p(const float4* __restrict__ rec, const uint32_t* __restrict__ ids, size_t n, float* out) {
+  float s = 0.f;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t id = ids[i];
+    float4 a = ldpol<POL>(rec + 2 * (size_t)id), b = ldpol<POL>(rec + 2 * (size_t)id + 1);
+    s += a.x + a.w + b.x + b.w;
+  }
+  if (s == 1234.5f) out[0] = s;
+}
 __global__ void k_gather64(const float4* __restrict__ rec, const uint32_t* __restrict__ ids, size_t n, float* out) {
   float s = 0.f;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -87,6 +116,23 @@ int main() {
   hipLaunchKernelGGL(k_fill_ids, g, b, 0, 0, ids, n, nrec32, 7u, 0);
   run("gather32", [&] { hipLaunchKernelGGL(k_gather32, g, b, 0, 0, buf, ids, n, out); }, (double)n * 36);
   run("amin64", [&] { hipLaunchKernelGGL(k_amin64, g, b, 0, 0, buf, ids, n); }, (double)n * 12);
+  run("g32asm", [&] { hipLaunchKernelGGL(k_gather32p<0>, g, b, 0, 0, buf, ids, n, out); }, (double)n * 36);
+  run("g32nt", [&] { hipLaunchKernelGGL(k_gather32p<1>, g, b, 0, 0, buf, ids, n, out); }, (double)n * 36);
+  run("g32sc0", [&] { hipLaunchKernelGGL(k_gather32p<2>, g, b, 0, 0, buf, ids, n, out); }, (double)n * 36);
+  run("g32sc1", [&] { hipLaunchKernelGGL(k_gather32p<3>, g, b, 0, 0, buf, ids, n, out); }, (double)n * 36);
+  run("g32sc01", [&] { hipLaunchKernelGGL(k_gather32p<4>, g, b, 0, 0, buf, ids, n, out); }, (double)n * 36);
+  run("g32sc01nt", [&] { hipLaunchKernelGGL(k_gather32p<5>, g, b, 0, 0, buf, ids, n, out); }, (double)n * 36);
+  {
+    // uncached allocation (MTYPE UC)
+    float4* ubuf = nullptr;
+    if (hipExtMallocWithFlags((void**)&ubuf, bytes, hipDeviceMallocUncached) == hipSuccess) {
+      CHK(hipMemset(ubuf, 0, bytes));
+      run("g32uc", [&] { hipLaunchKernelGGL(k_gather32, g, b, 0, 0, ubuf, ids, n, out); }, (double)n * 36);
+      CHK(hipFree(ubuf));
+    } else {
+      printf("uncached allocation failed\n");
+    }
+  }
   hipLaunchKernelGGL(k_fill_ids, g, b, 0, 0, ids, n, nrec64, 9u, 0);
   run("gather64", [&] { hipLaunchKernelGGL(k_gather64, g, b, 0, 0, buf, ids, n, out); }, (double)n * 68);
   CHK(hipDeviceSynchronize());
