@@ -638,6 +638,7 @@ template <int NSH, bool REFA>
 __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
   __shared__ uint32_t s_free[4], s_live[4], s_busy[4], s_next, s_end, s_shaded, s_nb, s_nbn;
+  __shared__ float s_dir[3][TPB];
   __shared__ int s_skip;
   const int tid = threadIdx.x, wave = tid >> 6;
   const uint32_t nblocks = (S.M + POOL_BLOCK - 1) / POOL_BLOCK;
@@ -706,12 +707,28 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     }
   }
   __syncthreads();
+  // camera rays of the paths that start here, computed by the first ns threads
+  // of the workgroup (whole waves, not one lane in four of every wave: the
+  // camera code then runs in ceil(ns / 64) waves instead of all four), handed
+  // to the free slots through LDS in rank order
+  const uint32_t ns = min(nf, t1 + s_nbn);
+  if ((uint32_t)tid < ns) {
+    const uint32_t P = (uint32_t)tid < t1 ? next + (uint32_t)tid : s_nb + (uint32_t)tid - t1;
+    uint32_t g;
+    const f3 dir = camera_dir<false, REFA>(S, P, g);
+    s_dir[0][tid] = dir.x;
+    s_dir[1][tid] = dir.y;
+    s_dir[2][tid] = dir.z;
+  }
+  __syncthreads();
   if (fr) {
     uint32_t rank = mbcnt64(mf);
     for (int w = 0; w < wave; ++w) rank += s_free[w];
-    const int P = rank < t1 ? (int)(next + rank) : (rank - t1 < s_nbn ? (int)(s_nb + rank - t1) : -1);
-    if (P >= 0) {
-      ext = RayV{ld3(S.cam.origin), start_path<REFA>(S, p, (uint32_t)P), __builtin_inff()};
+    if (rank < ns) {
+      const uint32_t P = rank < t1 ? next + rank : s_nb + rank - t1;
+      S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
+      S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
+      ext = RayV{ld3(S.cam.origin), mk(s_dir[0][rank], s_dir[1][rank], s_dir[2][rank]), __builtin_inff()};
       new_ext = true;
     } else if (state == SLOT_ENDED) {
       S.ps0[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));  // the slot stays free
