@@ -403,7 +403,15 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
   push_children<R, MAX_ROOT_TARGETS>(A, TableTargets{T}, lane, id, o, d, tm, pv, R, sh, false);
 }
 
-template <bool IMPLICIT, bool REFA = false>
+// the shared level kernel loads a leaf record in one round trip too (it now
+// fits its register budget: levels -0.3 to -0.5 ms per frame; round 1's
+// one-level kernel lost interior speed to it)
+#ifndef PT_SHARED_LEAF_LOAD1
+#define PT_SHARED_LEAF_LOAD1 1
+#endif
+// LEAF: the node is known to be a leaf (the leaf-only level kernel): the
+// interior code is not compiled in (fewer registers, more waves)
+template <bool IMPLICIT, bool REFA = false, bool LEAF = false>
 __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, uint32_t base, int n, int lane,
                                              uint32_t* sh, bool ids = true, bool out_ids = true) {
   const int tid = threadIdx.x;
@@ -447,7 +455,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 
   const int nj = (n + TPB - 1) / TPB;  // ray groups with at least one valid thread (uniform)
   const int pcount = nd->prim_count;
-  if (pcount > 0) {
+  if (LEAF || pcount > 0) {
     // ---------------- leaf: all primitives against every ray -----------------
     const int pstart = nd->prim_start;
     float bt[RPT];
@@ -460,6 +468,10 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
     const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);
     for (int k = 0; k < pcount; ++k, P += 6) {
       const float4 q0 = f4(P[0]), q1 = f4(P[1]);
+      if constexpr (LEAF) {  // one scalar round trip per record (see process_wave)
+        const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
+        asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q2.x), "s"(q3.x), "s"(q4.x), "s"(q5.x));
+      }
       const uint32_t meta = __float_as_uint(q0.w);
       if ((meta >> 28) == PT_PRIM_SPHERE) {
 #pragma unroll
@@ -502,7 +514,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
   }
 
   // ---------------- interior: NC child boxes, compaction, push ----------------
-  push_children<RPT, 4>(A, ChildTargets{nd}, lane, id, o, d, tmax, valid, nj, sh, !out_ids);
+  if constexpr (!LEAF) push_children<RPT, 4>(A, ChildTargets{nd}, lane, id, o, d, tmax, valid, nj, sh, !out_ids);
   return nvalid;
 }
 
@@ -672,7 +684,7 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
   }
 }
 
-template <bool REFA = false>
+template <bool REFA = false, bool LEAF = false>
 __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane, bool ids,
                                              bool out_ids, bool two_level) {
   const uint32_t lid = lane_id();
@@ -693,7 +705,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
   }
   const int nj = (n + 63) >> 6;  // ray groups with at least one valid lane (uniform)
   const int pcount = nd->prim_count;
-  if (pcount > 0) {
+  if (LEAF || pcount > 0) {
     const int pstart = nd->prim_start;
     float bt[RPTW];
     int bp[RPTW];
@@ -705,6 +717,12 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);
     for (int k = 0; k < pcount; ++k, P += 6) {
       const float4 q0 = f4(P[0]), q1 = f4(P[1]);
+      if constexpr (LEAF || PT_SHARED_LEAF_LOAD1) {
+        // the whole 96-B record in one scalar round trip (the compiler waits
+        // on q0, q1 for the sphere/triangle branch before issuing the rest)
+        const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
+        asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q2.x), "s"(q3.x), "s"(q4.x), "s"(q5.x));
+      }
       const uint32_t meta = __float_as_uint(q0.w);
       if ((meta >> 28) == PT_PRIM_SPHERE) {
 #pragma unroll
@@ -743,6 +761,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     }
     return;
   }
+  if constexpr (LEAF) return;
   if (two_level) {
     f3 inv[RPTW], oi[RPTW];
 #pragma unroll
@@ -811,8 +830,25 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 #ifndef PT_LEVEL_ATTR
 #define PT_LEVEL_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
 #endif
+// LEAF: a level whose queued nodes are all leaves (the levels between two
+// real levels hold only the leaf rays of the real level above them): the
+// leaf-only code needs fewer registers and runs PT_LEAF_WAVES waves per SIMD
+#ifndef PT_LEAF_WAVES
+#define PT_LEAF_WAVES 6
+#endif
+template <bool REFA, bool LEAF>
+__device__ __forceinline__ void trace_level_body(const TraceArgs& A, const LevelArgs& L);
 template <bool REFA>
 __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, LevelArgs L) {
+  trace_level_body<REFA, false>(A, L);
+}
+template <bool REFA>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_LEAF_WAVES, 8))) void k_trace_leaves(
+    TraceArgs A, LevelArgs L) {
+  trace_level_body<REFA, true>(A, L);
+}
+template <bool REFA, bool LEAF>
+__device__ __forceinline__ void trace_level_body(const TraceArgs& A, const LevelArgs& L) {
   const int lane = blockIdx.x & (NLANE - 1);
   const uint32_t lid = lane_id();
   const uint32_t wave = threadIdx.x >> 6;
@@ -849,7 +885,7 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
       const uint32_t base = __builtin_amdgcn_readfirstlane(s_base);
       const int n = __builtin_amdgcn_readfirstlane(s_n);
       __syncthreads();
-      process_item<false, REFA>(A, node, base, n, lane, sh, L.ids != 0, L.out_ids != 0);
+      process_item<false, REFA, LEAF>(A, node, base, n, lane, sh, L.ids != 0, L.out_ids != 0);
       __syncthreads();
     }
     return;
@@ -873,7 +909,7 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
     const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
     const uint32_t base = A.qoff[(size_t)node * NLANE + lane] + i * WTILE;
     const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
-    process_wave<REFA>(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane,
+    process_wave<REFA, LEAF>(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane,
                        L.ids != 0, L.out_ids != 0, L.two_level != 0);
   }
 }

@@ -57,6 +57,7 @@ struct pt_ctx {
   bool root_leaf = true;
   bool skip_l1 = false;  // root pass pushes straight into the level-2 queues
   bool two_level = true; // two-level traversal (trace_levels; PT_TWO_LEVEL=0: one level per pass)
+  bool leaf_kernel = true;  // k_trace_leaves for the leaf-only levels (PT_LEAF_KERNEL=0: k_trace_level)
   std::vector<char> level_has_leaf;
   RootTable rt{};        // root pass: inline leaves and queue targets (build_root_table)
   std::vector<pt_node> nodes_host;
@@ -332,6 +333,8 @@ static void build_root_table(pt_ctx* c) {
   // two-level traversal (default; PT_TWO_LEVEL=0 restores one level per pass)
   const char* tl = getenv("PT_TWO_LEVEL");
   c->two_level = !(tl && atoi(tl) == 0);
+  const char* lk = getenv("PT_LEAF_KERNEL");
+  c->leaf_kernel = !(lk && atoi(lk) == 0);
   // ray entries from PT_ENTRY_LEVEL levels below the root's targets on (0: ids
   // only; the two-level push writes ids)
   const char* el = getenv("PT_ENTRY_LEVEL");
@@ -420,10 +423,14 @@ static int trace_levels(pt_ctx* c) {
       c->launch(pt_ctx::K_SCAN, l, k_scan_level, dim3(1), dim3(1024), A, L, (uint32_t)lanecap, out_base,
                 c->d_stats, l, c->d_err);
     }
-    if (c->refa)
-      c->launch(pt_ctx::K_LEVEL, l, k_trace_level<true>, dim3(LEVEL_GRID), dim3(TPB), A, L);
-    else
-      c->launch(pt_ctx::K_LEVEL, l, k_trace_level<false>, dim3(LEVEL_GRID), dim3(TPB), A, L);
+    // a level between two real ones holds only leaf rays: the leaf-only kernel
+    // (fewer registers, more waves per SIMD); PT_LEAF_KERNEL=0 disables it
+    // (a real level's leaf items stay in the shared kernel: running them in a
+    // second, leaf-only launch that skips the other items measured -3 to -5 %)
+    const bool leaves = !real && c->leaf_kernel;
+    auto kl = c->refa ? (leaves ? k_trace_leaves<true> : k_trace_level<true>)
+                      : (leaves ? k_trace_leaves<false> : k_trace_level<false>);
+    c->launch(pt_ctx::K_LEVEL, l, kl, dim3(LEVEL_GRID), dim3(TPB), A, L);
   }
   HIPCHK(c, hipGetLastError());
   c->stats.passes++;

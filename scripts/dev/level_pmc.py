@@ -1,11 +1,16 @@
 """Per-level PMC of k_trace_level (and k_shade_push) from one scene's pmc passes:
-  python scripts/dev/level_pmc.py <scene> <first_level> <last_level>"""
+  python scripts/dev/level_pmc.py <scene> <first_level> <last_level>
+  python scripts/dev/level_pmc.py <scene> 2,4,6,7,8     (the launched levels of a pass, in order)"""
 import collections
 import csv
 import glob
 import sys
 
-sc, first, last = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+sc = sys.argv[1]
+if "," in sys.argv[2]:
+    LEVELS = [int(x) for x in sys.argv[2].split(",")]
+else:
+    LEVELS = list(range(int(sys.argv[2]), int(sys.argv[3]) + 1))
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 cnt = collections.defaultdict(set)
 for f in sorted(glob.glob(f"gpurun_out/pmc_{sc}_[0-9]/**/*counter_collection.csv", recursive=True)):
@@ -14,7 +19,7 @@ for f in sorted(glob.glob(f"gpurun_out/pmc_{sc}_[0-9]/**/*counter_collection.csv
     for r in rows:
         d = int(r["Dispatch_Id"])
         if "k_trace_level" in r["Kernel_Name"] and d not in lvl:
-            lvl[d] = first + i % (last - first + 1)
+            lvl[d] = LEVELS[i % len(LEVELS)]
             i += 1
     for r in rows:
         d = int(r["Dispatch_Id"])
