@@ -148,11 +148,20 @@ def pmc_kernel(scene, kernel):
 
 
 def pmc_traffic(scene, kernel):
-    """HBM bytes per launch of `kernel` from a committed PMC summary, if any."""
-    k, src = pmc_kernel(scene, kernel)
-    if not k or "hbm_bytes_per_launch" not in k:
-        return None, None
-    return k["hbm_bytes_per_launch"], src
+    """HBM bytes per launch of `kernel` from a committed PMC summary, if any.
+    kernel may be a tuple: the launch-weighted mean over those kernels (the
+    level roofline covers k_trace_level and k_trace_leaves)."""
+    names = kernel if isinstance(kernel, tuple) else (kernel,)
+    tot = n = 0
+    src = None
+    for kn in names:
+        k, s = pmc_kernel(scene, kn)
+        if not k or "hbm_bytes_per_launch" not in k:
+            continue
+        tot += k["hbm_bytes_per_launch"] * k.get("dispatches", 1)
+        n += k.get("dispatches", 1)
+        src = s
+    return (int(tot / n), src) if n else (None, None)
 
 
 # gfx950: 256 CUs x 4 SIMDs, 8 XCDs; a wave64 fp32 VALU instruction occupies
@@ -164,12 +173,16 @@ N_SIMD, N_XCD, VALU_CYCLES_PER_INST = 1024, 8, 2
 def pmc_valu_busy(scene, kernel):
     """Fraction of SIMD cycles issuing VALU work during `kernel`'s launches
     (SQ_INSTS_VALU x 2 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)); transcendental
-    and 64-bit ops take longer, so this is a lower bound."""
-    k, _ = pmc_kernel(scene, kernel)
-    try:
-        return round(k["SQ_INSTS_VALU"] * VALU_CYCLES_PER_INST / (N_SIMD * k["GRBM_GUI_ACTIVE"] / N_XCD), 3)
-    except (TypeError, KeyError, ZeroDivisionError):
-        return None
+    and 64-bit ops take longer, so this is a lower bound.  kernel: a name or
+    a tuple of names (summed)."""
+    names = kernel if isinstance(kernel, tuple) else (kernel,)
+    vi = ga = 0.0
+    for kn in names:
+        k, _ = pmc_kernel(scene, kn)
+        if k and "SQ_INSTS_VALU" in k and "GRBM_GUI_ACTIVE" in k:
+            vi += k["SQ_INSTS_VALU"]
+            ga += k["GRBM_GUI_ACTIVE"]
+    return round(vi * VALU_CYCLES_PER_INST / (N_SIMD * ga / N_XCD), 3) if ga else None
 
 
 def root_leaf_flops(desc):
@@ -255,7 +268,14 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
         ms_1spp = (time.perf_counter() - t2) * 1e3
     lvl_ms = sum(st.ms_level[l] for l in range(1, 16))
     V = [st.level_visits[l] for l in range(16)]
-    lvl_bytes = sum(32 * V[l] for l in range(1, 16)) + sum(4 * V[l] for l in range(2, 16))
+    # 40 B per ray entering the root (record written at generation
+    # + final hit word), 32 B per visit, 4 B per push.  The root pass runs inside
+    # the producers (k_camera_push / k_shade_push): their share is 40 R + 4 B per
+    # id pushed into the first queued level l0; the level kernels' share is
+    # 32 B per visit + 4 B per id they push (into the levels below l0)
+    l0 = next((l for l in range(1, 16) if V[l] > 0), 1)
+    lvl_bytes = sum(32 * V[l] for l in range(1, 16)) + sum(4 * V[l] for l in range(l0 + 1, 16))
+    root_bytes = 40 * st.rays + 4 * V[l0]
     lvl_launches = sum(st.level_launches[l] for l in range(1, 16))
     flop_ray, _ = root_leaf_flops(desc)
     path_flops = flop_ray * st.rays
@@ -282,18 +302,30 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
     else:
         kernel, launches = "k_trace_level", lvl_launches
         ach = (lvl_bytes / (lvl_ms * 1e-3) / 1e9) if lvl_ms > 0 else 0.0
-        traffic, src = pmc_traffic(name, kernel)
+        lk = ("k_trace_level", "k_trace_leaves")
+        traffic, src = pmc_traffic(name, lk)
+        avg_s = lvl_ms * 1e-3 / max(1, launches)
+        # the same visits priced at the hardware's fetch granularity: a random
+        # 32-B record gather is one 128-B DRAM line (scripts/cal/gather_cal.hip)
+        line_bytes = sum(132 * V[l] for l in range(1, 16)) + sum(4 * V[l] for l in range(2, 16))
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
-                "launches": int(launches), "avg_launch_us": round(lvl_ms * 1e3 / max(1, launches), 2),
-                "bytes_per_launch": int(lvl_bytes / max(1, launches)), "valu_busy": pmc_valu_busy(name, kernel)}
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_trace_level+k_trace_leaves",
+                "launches": int(launches), "avg_launch_us": round(avg_s * 1e6, 2),
+                "bytes_per_launch": int(lvl_bytes / max(1, launches)), "valu_busy": pmc_valu_busy(name, lk),
+                "traffic_gbs": round(traffic / avg_s / 1e9, 1) if traffic and avg_s > 0 else None,
+                "line_bytes_per_launch": int(line_bytes / max(1, launches)),
+                "line_frac": round(line_bytes / max(lvl_ms * 1e-3, 1e-12) / 1e9 / HBM_PEAK_GBS, 4),
+                "note": "achieved/frac: SURVEY 8(d)'s 32 B per visit + 4 B per push; line_frac: the same visits at "
+                        "the 128-B line a random record gather fetches; traffic_gbs: PMC HBM bytes per launch / "
+                        "average launch time"}
     if src:
         roof["traffic_source"] = src
     others = []
     if st.shade_launches > 0:
         # shading with the fused root pass: 96 B per shaded path
-        # vertex (hit 8 + path state 44 read + 44 write)
-        sbytes = 96 * st.shaded
+        # vertex (hit 8 + path state 44 read + 44 write) + the root pass's share
+        # of the traversal bytes (root_bytes above)
+        sbytes = 96 * st.shaded + root_bytes
         ach = sbytes / (st.ms_shade_push * 1e-3) / 1e9 if st.ms_shade_push > 0 else 0.0
         straffic, ssrc = pmc_traffic(name, "k_shade_push")
         sroof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -302,6 +334,11 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
                  "avg_launch_us": round(st.ms_shade_push * 1e3 / max(1, st.shade_launches), 2),
                  "bytes_per_launch": int(sbytes / max(1, st.shade_launches)), "shaded_vertices": int(st.shaded),
                  "valu_busy": pmc_valu_busy(name, "k_shade_push")}
+        sroof["note"] = ("96 B per shaded vertex + the fused root pass's traversal share (40 B per ray "
+                         "entering the root + 4 B per id it pushes); the first fill's camera rays (k_camera_push, "
+                         "<= 2 % of the rays) are counted here too")
+        savg = st.ms_shade_push * 1e-3 / max(1, st.shade_launches)
+        sroof["traffic_gbs"] = round(straffic / savg / 1e9, 1) if straffic and savg > 0 else None
         if ssrc:
             sroof["traffic_source"] = ssrc
         if st.ms_shade_push > lvl_ms:  # the dominant kernel first

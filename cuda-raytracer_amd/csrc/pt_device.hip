@@ -225,7 +225,9 @@ static uint32_t max_batch_paths(const pt_ctx* c, uint32_t slots_per_path) {
   // u32 entry offsets: both halves of the entry queues, and the root's id
   // queues (<= 16 targets x every ray, see root_per_lane)
   const uint64_t a = (1ull << 32) / (QREGIONS * ID_FACTOR * c->qfactor * slots_per_path);
-  const uint64_t b = (1ull << 32) / (20ull * slots_per_path);
+  // every region is as large as the root targets' allocation (root_per_lane:
+  // ~nt x every ray slot of the lane, plus the per-workgroup rounding)
+  const uint64_t b = (1ull << 32) / (QREGIONS * (uint64_t)(std::max(1, c->rt.nt) + 1) * slots_per_path);
   return (uint32_t)std::min<uint64_t>(std::min(a, b), 0xFFFFFFFFull) & ~4095u;
 }
 
@@ -241,8 +243,12 @@ static size_t root_per_lane(size_t N, size_t spp) {
 
 static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
   if (N <= c->cap_paths && spp <= c->cap_spp && c->qfactor == c->cap_qfactor) return PT_OK;
-  if (c->qfactor != c->cap_qfactor) N = std::min(N, max_batch_paths(c, spp));
-  N = std::max(N, c->cap_paths);
+  // (after a queue overflow doubled qfactor the batch may have to shrink: the
+  // old capacity would overflow the u32 queue offsets)
+  if (c->qfactor != c->cap_qfactor)
+    N = std::min(N, max_batch_paths(c, std::max(spp, c->cap_spp)));
+  else
+    N = std::max(N, c->cap_paths);
   spp = std::max(spp, c->cap_spp);
   const size_t slots = (size_t)spp * N;
   int rc;

@@ -104,6 +104,36 @@ def test_queue_overflow_rerun(monkeypatch):
         ctx.close()
 
 
+def test_overflow_rerun_shrinks_large_batch(gpu_ctx):
+    """A large path pool whose level queues overflow: the chunk re-runs with
+    twice the queue factor, which the pool no longer fits under u32 queue
+    offsets, so the batch shrinks (it used to fail with PT_E_UNSUPPORTED).
+    The soup of overlapping triangles overflows the default queue factor
+    twice; the image equals the default context's bit for bit."""
+    rng = np.random.default_rng(11)
+    c = rng.random((3000, 1, 3), dtype=np.float32)
+    tris = (c + 0.6 * (rng.random((3000, 3, 3), dtype=np.float32) - 0.5)).reshape(-1, 9)
+    sc = ptrace.Scene.from_triangles(tris)
+    W = H = 1024
+    spp, batch = 144, 150_000_000  # 151 M paths; the pool asks for 150 M slots
+    gpu_ctx.load_scene(sc)
+    gpu_ctx.clear()
+    gpu_ctx.render(W, H, spp, max_bounces=2, seed=15618)
+    ref = gpu_ctx.get_image()
+    ctx = ptrace.Context(0)
+    try:
+        ctx.load_scene(sc)
+        ctx.reset_stats()
+        ctx.render(W, H, spp, max_bounces=2, seed=15618, batch_paths=batch)
+        assert np.array_equal(ctx.get_image(), ref)
+        st = ctx.stats()
+        # the re-runs did run (queue factor 4 -> 16: a pool of 42 M slots no
+        # longer fits u32 offsets at 8), with a smaller pool
+        assert st.queue_factor >= 8 and st.batch_paths < 40_000_000, (st.queue_factor, st.batch_paths)
+    finally:
+        ctx.close()
+
+
 def test_tie_break_lowest_prim(gpu_ctx):
     # two identical triangles: every hit must report the lower sorted index
     tri = np.array([[-1, -1, 0, 1, -1, 0, 0, 1, 0]] * 2, np.float32)
