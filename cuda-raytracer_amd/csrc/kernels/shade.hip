@@ -248,14 +248,33 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
 // direction through the local-frame wi (cu:643-650), origins pt + n 1e-3.
 // The scene must be triangles with diffuse / mirror / emission BSDFs
 // (pt_render refuses spheres and glass under REFA: the reference has neither).
-template <int NSH, bool M64 = false, bool KR = false, bool REFA = false>
+// LDSSH: the new shadow rays and their pending contributions go to this
+// thread's column of sh_lds ([NSH][10][TPB]: o, d, tmax, C) as soon as the NEE
+// sample has made them, instead of staying in registers through the BSDF
+// sample (k_path_leaf: fewer VGPRs live at its peak)
+template <int NSH, bool M64 = false, bool KR = false, bool REFA = false, bool LDSSH = false>
 __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, PathState& st, const f3 o,
                                              const f3 d, uint32_t prim, float t, const bool (&clear)[NSH],
                                              f3 (&C)[NSH], bool& new_ext, RayV& ext, bool (&new_sh)[NSH],
-                                             RayV (&shr)[NSH]) {
+                                             RayV (&shr)[NSH], float* sh_lds = nullptr) {
   const uint32_t flags = st.flags;
-  f3 T = st.T;
-  f3 L = st.L;
+  // (LDSSH: the radiance and the throughput live in rows 10 NSH .. 10 NSH + 5
+  // of sh_lds, re-read where they are used; a memory clobber after each store
+  // keeps the compiler from carrying them in registers anyway)
+  float* const Lq = LDSSH ? sh_lds + (size_t)10 * NSH * TPB + threadIdx.x : nullptr;
+  float* const Tq = LDSSH ? Lq + 3 * TPB : nullptr;
+  f3 T = LDSSH ? mk(0.f, 0.f, 0.f) : st.T;
+  auto Tv = [&]() { return LDSSH ? mk(Tq[0], Tq[TPB], Tq[2 * TPB]) : T; };
+  auto Tset = [&](f3 v) {
+    T = v;
+    if constexpr (LDSSH) {
+      Tq[0] = v.x;
+      Tq[TPB] = v.y;
+      Tq[2 * TPB] = v.z;
+      asm volatile("" ::: "memory");
+    }
+  };
+  f3 L = LDSSH ? mk(Lq[0], Lq[TPB], Lq[2 * TPB]) : st.L;
   const uint32_t g = st.g;
   // 1. resolve the shadow rays of the previous vertex
 #pragma unroll
@@ -264,6 +283,12 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
   // reference quirk (i): a path whose extension ray misses contributes
   // nothing (kernelUpdateSSImage writes 0 for an invalid intersection, cu:679-698)
   if ((S.flags & PT_FLAG_REF_DROP_ON_MISS) && (flags & F_EXT) && prim == PT_PRIM_NONE) L = mk(0.f, 0.f, 0.f);
+  if constexpr (LDSSH) {
+    Lq[0] = L.x;
+    Lq[TPB] = L.y;
+    Lq[2 * TPB] = L.z;
+    asm volatile("" ::: "memory");
+  }
   new_ext = false;
   f3 o_new = mk(0, 0, 0), d_new = mk(0, 0, 1);
 #pragma unroll
@@ -320,14 +345,30 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
         // cu:1243 (without REAL_TIME): its.light = radiance * importance + light
         const f3 rad = B.type == PT_BSDF_EMISSION ? ld3(B.albedo) : mk(0.f, 0.f, 0.f);
         if (!(S.flags & PT_FLAG_NO_EMISSION)) {
-          L = mk(__builtin_fmaf(rad.x, T.x, L.x), __builtin_fmaf(rad.y, T.y, L.y), __builtin_fmaf(rad.z, T.z, L.z));
+          if constexpr (LDSSH) L = mk(Lq[0], Lq[TPB], Lq[2 * TPB]);
+          const f3 T0 = Tv();
+          L = mk(__builtin_fmaf(rad.x, T0.x, L.x), __builtin_fmaf(rad.y, T0.y, L.y), __builtin_fmaf(rad.z, T0.z, L.z));
+          if constexpr (LDSSH) {
+            Lq[0] = L.x;
+            Lq[TPB] = L.y;
+            Lq[2 * TPB] = L.z;
+            asm volatile("" ::: "memory");
+          }
           emitter = rad.x != 0.0f || rad.y != 0.0f || rad.z != 0.0f;  // cu:436
         }
         if (B.type == PT_BSDF_EMISSION) B.type = PT_BSDF_DIFFUSE;  // albedo = radiance (cu:1705-1711)
       }
       if (!REFA && B.type == PT_BSDF_EMISSION) {
-        if (!(S.flags & PT_FLAG_NO_EMISSION) && (vtx == 1u || spec))
-          L = L + mulv(T, ld3(B.albedo));
+        if (!(S.flags & PT_FLAG_NO_EMISSION) && (vtx == 1u || spec)) {
+          if constexpr (LDSSH) L = mk(Lq[0], Lq[TPB], Lq[2 * TPB]);
+          L = L + mulv(Tv(), ld3(B.albedo));
+          if constexpr (LDSSH) {
+            Lq[0] = L.x;
+            Lq[TPB] = L.y;
+            Lq[2 * TPB] = L.z;
+            asm volatile("" ::: "memory");
+          }
+        }
       } else {
         const u4 u = rng<M64>(S.seed, g, sidx, vtx, 0);
         f3 dpdu, dpdv;
@@ -357,7 +398,20 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
                 uy = u01(v.y);
               }
               const float weight = NSH == 2 ? (nee == 2 ? 0.5f : 1.0f) : -1.0f;
-              new_sh[s] = nee_sample<KR, REFA>(S, T, alb, n, pt, ux, uy, weight, C[s], shr[s]);
+              new_sh[s] = nee_sample<KR, REFA>(S, Tv(), alb, n, pt, ux, uy, weight, C[s], shr[s]);
+              if constexpr (LDSSH) {
+                float* q = sh_lds + (size_t)s * 10 * TPB + threadIdx.x;
+                q[0 * TPB] = shr[s].o.x;
+                q[1 * TPB] = shr[s].o.y;
+                q[2 * TPB] = shr[s].o.z;
+                q[3 * TPB] = shr[s].d.x;
+                q[4 * TPB] = shr[s].d.y;
+                q[5 * TPB] = shr[s].d.z;
+                q[6 * TPB] = shr[s].tmax;
+                q[7 * TPB] = C[s].x;
+                q[8 * TPB] = C[s].y;
+                q[9 * TPB] = C[s].z;
+              }
             }
           }
           // BSDF sample
@@ -385,10 +439,11 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
                                  n.z * z + x * dpdu.z + y * dpdv.z));
           }
           if (S.flags & PT_FLAG_COSINE_DIFFUSE) {
-            T = mulv(T, alb);
+            Tset(mulv(Tv(), alb));
           } else {
             const float c = fabsf(dot(d_new, n));
-            T = mk(((T.x * c) * alb.x) * 2.0f, ((T.y * c) * alb.y) * 2.0f, ((T.z * c) * alb.z) * 2.0f);
+            const f3 T0 = Tv();
+            Tset(mk(((T0.x * c) * alb.x) * 2.0f, ((T0.y * c) * alb.y) * 2.0f, ((T0.z * c) * alb.z) * 2.0f));
           }
           o_new = REFA ? mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y),
                             __builtin_fmaf(n.z, EPS, pt.z))
@@ -410,7 +465,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
             d_new = normalize(d - n * (2.0f * dn));
             o_new = pt + n * EPS;
           }
-          T = mulv(T, ld3(B.albedo));
+          Tset(mulv(Tv(), ld3(B.albedo)));
           spec = F_SPEC;
         } else {  // PT_BSDF_GLASS (Fresnel-weighted reflect / refract, bsdf.h:187-212)
           const float ior = B.ior;
@@ -433,11 +488,11 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           if (refl) {
             const float dn = dot(d, n);
             d_new = normalize(d - n * (2.0f * dn));
-            T = mulv(T, ld3(B.albedo));
+            Tset(mulv(Tv(), ld3(B.albedo)));
             o_new = pt + n * EPS;
           } else {
             d_new = normalize(d * eta + n * (eta * cosi - cost));
-            T = mulv(T, ld3(B.transmittance));
+            Tset(mulv(Tv(), ld3(B.transmittance)));
             o_new = P - n * EPS;
           }
           spec = F_SPEC;
@@ -447,8 +502,10 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
     }
   }
 
-  st.T = T;
-  st.L = L;
+  if constexpr (!LDSSH) {
+    st.T = T;
+    st.L = L;
+  }
   uint32_t fl = spec | (new_ext ? F_EXT : 0u) | ((vtx + 1u) << 8);
 #pragma unroll
   for (int s = 0; s < NSH; ++s) fl |= new_sh[s] ? sh_bit(s) : 0u;
@@ -876,18 +933,26 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
 #endif
 constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 
-// 6 waves per SIMD (80 VGPRs, no spills).  7 waves (72 VGPRs) run within
-// 0.6 % of it but spill ~20 VGPRs around the shading code, which turns into
-// ~35 GB of scratch write-back per 1024^2 x 256 spp frame (PMC WRITE_SIZE);
-// 8 waves spill ~60 and lose 10 %.
+// With all path state in registers: 6 waves per SIMD (80 VGPRs, no spills);
+// 7 waves (72 VGPRs) ran within 0.6 % of it but spilled ~20 VGPRs around the
+// shading code (~35 GB of scratch write-back per 1024^2 x 256 spp frame, PMC
+// WRITE_SIZE); 8 waves spilled ~60 and lost 10 %.
 // the light re-read from the kernel arguments at each NEE sample (light_of):
 // SGPR spills 34 -> 13, v_readlane reloads 42 -> 13 (CBempty +0.8 %,
 // CBspheres +1.1 %)
 #ifndef PT_PATH_LIGHT_RELOAD
 #define PT_PATH_LIGHT_RELOAD true
 #endif
+// 8 waves per SIMD with the pending shadow rays, their contributions, the
+// radiance and the throughput in LDS (PT_PATH_LDS_SH, 16 KB per workgroup):
+// 64 VGPRs, 9 spilled; CBempty 51,700 -> 54,700 Mrays/s, CBspheres 38,500 ->
+// 40,800 (7 waves: 68 VGPRs without spills, 54,000; the same state in
+// registers at 6 waves: 80 VGPRs, see above)
 #ifndef PT_PATH_WAVES
-#define PT_PATH_WAVES 6
+#define PT_PATH_WAVES 8
+#endif
+#ifndef PT_PATH_LDS_SH
+#define PT_PATH_LDS_SH 1
 #endif
 // (PT_PATH_LIGHT_RELOAD reads the light from the kernel-argument segment at
 // offsetof(ShadeArgs, light): S must stay this kernel's FIRST parameter)
@@ -911,6 +976,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
     shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
     C[s] = mk(0, 0, 0);
   }
+  // PT_PATH_LDS_SH: the pending shadow rays live in LDS between vertices
+  __shared__ float sh_lds[PT_PATH_LDS_SH ? (NSH * 10 + 6) * TPB : 1];
+  float* const Lq = sh_lds + (size_t)10 * NSH * TPB + threadIdx.x;  // (PT_PATH_LDS_SH: the radiance)
   for (;;) {
     // ---- refill idle lanes from the pool (new paths start at their camera ray)
     unsigned long long idle = __ballot(!active);
@@ -931,6 +999,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
         const f3 dir = camera_dir<PT_PATH_MAD64, REFA>(S, p, st.g);
         st.T = mk(1.0f, 1.0f, 1.0f);
         st.L = mk(0.0f, 0.0f, 0.0f);
+        if constexpr (PT_PATH_LDS_SH) {
+          Lq[0] = 0.0f;
+          Lq[TPB] = 0.0f;
+          Lq[2 * TPB] = 0.0f;
+          Lq[3 * TPB] = 1.0f;  // (the throughput)
+          Lq[4 * TPB] = 1.0f;
+          Lq[5 * TPB] = 1.0f;
+        }
         st.flags = F_EXT | (1u << 8);
         ext = RayV{ld3(S.cam.origin), dir, __builtin_inff()};
       }
@@ -953,7 +1029,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
 #pragma unroll
       for (int s = 0; s < NSH; ++s) {
         clear[s] = false;
+        if constexpr (PT_PATH_LDS_SH) {  // (no value carried across iterations in registers)
+          shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
+          C[s] = mk(0, 0, 0);
+        }
         if (st.flags & sh_bit(s)) {
+          if constexpr (PT_PATH_LDS_SH) {
+            const float* q = sh_lds + (size_t)s * 10 * TPB + threadIdx.x;
+            shr[s] = RayV{mk(q[0], q[TPB], q[2 * TPB]), mk(q[3 * TPB], q[4 * TPB], q[5 * TPB]), q[6 * TPB]};
+            C[s] = mk(q[7 * TPB], q[8 * TPB], q[9 * TPB]);
+          }
           clear[s] = !leaf_occluded<REFA>(S.prims, pstart, pcount, shr[s]);
           nrays++;
         }
@@ -961,16 +1046,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       bool new_ext, new_sh[NSH];
       RayV e2, s2[NSH];
       // (the sample index is recomputed, not carried: one register less)
-      shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD, REFA>(S, S.sample_base + udiv_q(p, S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
-                        new_sh, s2);
+      shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD, REFA, PT_PATH_LDS_SH>(
+          S, S.sample_base + udiv_q(p, S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2, new_sh, s2,
+          sh_lds);
       if (new_ext) ext = e2;
+      if constexpr (!PT_PATH_LDS_SH) {
 #pragma unroll
-      for (int s = 0; s < NSH; ++s)
-        if (new_sh[s]) shr[s] = s2[s];
+        for (int s = 0; s < NSH; ++s)
+          if (new_sh[s]) shr[s] = s2[s];
+      }
       // vertices done = vtx - 1 (shade_vertex advanced it); the path ends
       // after `passes` of them or when it has no ray left to trace
       const uint32_t done = ((st.flags >> 8) & 0xffu) - 1u;
       if (!(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || done >= (uint32_t)passes) {
+        if constexpr (PT_PATH_LDS_SH) st.L = mk(Lq[0], Lq[TPB], Lq[2 * TPB]);
         S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(st.g));
         active = false;
       }
