@@ -836,25 +836,38 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 #ifndef PT_LEAF_WAVES
 #define PT_LEAF_WAVES 6
 #endif
-template <bool REFA, bool LEAF>
+template <bool REFA, bool LEAF, bool BLOCK = true>
 __device__ __forceinline__ void trace_level_body(const TraceArgs& A, const LevelArgs& L);
 template <bool REFA>
 __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, LevelArgs L) {
   trace_level_body<REFA, false>(A, L);
+}
+// The real levels of the two-level traversal always run wave items (their
+// push exists for wave items only): without the workgroup-item code the
+// kernel needs 22 SGPR spills instead of 51, and runs 6 waves per SIMD (80
+// VGPRs, 5 spilled): dragon proxy level 6 30.1 -> 28.4 ms, frame +0.9 %
+// (at 5 waves it measured the same as k_trace_level)
+#ifndef PT_REAL_WAVES
+#define PT_REAL_WAVES 6
+#endif
+#define PT_REAL_ATTR __attribute__((amdgpu_waves_per_eu(PT_REAL_WAVES, 8)))
+template <bool REFA>
+__global__ __launch_bounds__(TPB) PT_REAL_ATTR void k_trace_real(TraceArgs A, LevelArgs L) {
+  trace_level_body<REFA, false, false>(A, L);
 }
 template <bool REFA>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_LEAF_WAVES, 8))) void k_trace_leaves(
     TraceArgs A, LevelArgs L) {
   trace_level_body<REFA, true>(A, L);
 }
-template <bool REFA, bool LEAF>
+template <bool REFA, bool LEAF, bool BLOCK>
 __device__ __forceinline__ void trace_level_body(const TraceArgs& A, const LevelArgs& L) {
   const int lane = blockIdx.x & (NLANE - 1);
   const uint32_t lid = lane_id();
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t* __restrict__ ep = L.iprefix + (size_t)lane * (L.maxln + 1);
   const uint32_t M = ep[L.nl];  // items of this lane
-  if (*L.mode == MODE_BLOCK) {
+  if (BLOCK && *L.mode == MODE_BLOCK) {
     // few nodes with many rays: 1024-ray items, one atomic per workgroup per child
     __shared__ uint32_t sh[64];
     __shared__ int s_node;

@@ -58,6 +58,7 @@ struct pt_ctx {
   bool skip_l1 = false;  // root pass pushes straight into the level-2 queues
   bool two_level = true; // two-level traversal (trace_levels; PT_TWO_LEVEL=0: one level per pass)
   bool leaf_kernel = true;  // k_trace_leaves for the leaf-only levels (PT_LEAF_KERNEL=0: k_trace_level)
+  bool real_kernel = true;  // k_trace_real for the real levels of two-level mode (PT_REAL_KERNEL=0: k_trace_level)
   std::vector<char> level_has_leaf;
   RootTable rt{};        // root pass: inline leaves and queue targets (build_root_table)
   std::vector<pt_node> nodes_host;
@@ -341,6 +342,8 @@ static void build_root_table(pt_ctx* c) {
   c->two_level = !(tl && atoi(tl) == 0);
   const char* lk = getenv("PT_LEAF_KERNEL");
   c->leaf_kernel = !(lk && atoi(lk) == 0);
+  const char* rk = getenv("PT_REAL_KERNEL");
+  c->real_kernel = !(rk && atoi(rk) == 0);
   // ray entries from PT_ENTRY_LEVEL levels below the root's targets on (0: ids
   // only; the two-level push writes ids)
   const char* el = getenv("PT_ENTRY_LEVEL");
@@ -434,8 +437,10 @@ static int trace_levels(pt_ctx* c) {
     // (a real level's leaf items stay in the shared kernel: running them in a
     // second, leaf-only launch that skips the other items measured -3 to -5 %)
     const bool leaves = !real && c->leaf_kernel;
-    auto kl = c->refa ? (leaves ? k_trace_leaves<true> : k_trace_level<true>)
-                      : (leaves ? k_trace_leaves<false> : k_trace_level<false>);
+    // (a real level of the two-level traversal: wave items only, k_trace_real)
+    const bool wave_only = L.two_level && c->real_kernel;
+    auto kl = c->refa ? (leaves ? k_trace_leaves<true> : wave_only ? k_trace_real<true> : k_trace_level<true>)
+                      : (leaves ? k_trace_leaves<false> : wave_only ? k_trace_real<false> : k_trace_level<false>);
     c->launch(pt_ctx::K_LEVEL, l, kl, dim3(LEVEL_GRID), dim3(TPB), A, L);
   }
   HIPCHK(c, hipGetLastError());
