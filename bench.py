@@ -27,9 +27,14 @@ labelled as such -- not a scaling figure.
 Rank 0 prints one JSON line.  "roofline" describes the workload's dominant
 kernel, timed by HIP events attached to its dispatch packets in one extra,
 instrumented frame (the headline frames run without events):
-  * k_trace_level (BVH levels >= 1, HBM-bound): algorithmic bytes = 32 B per
-    (ray, node) visit (4 B queue id + 28 B of ray) + 4 B per id pushed to the
-    next level (BASELINE.md §3);
+  * the level kernels (k_trace_real / k_trace_leaves / k_trace_level: BVH
+    levels >= 1, HBM-bound): algorithmic bytes = 32 B per (ray, node) visit
+    (4 B queue id + 28 B of ray) + 4 B per id they push (BASELINE.md §3);
+    "line_frac" prices the same visits at the 128-B line a random record
+    gather fetches;
+  * k_shade_push (shading + the fused root pass): 96 B per shaded vertex +
+    the root pass's share of the traversal bytes (40 B per ray entering the
+    root + 4 B per id it pushes);
   * k_path_leaf (scenes whose BVH root is a leaf: each path runs to completion
     in registers, no HBM stream): VALU-bound, algorithmic FP32 FLOPs of the
     primitive tests (every primitive of the leaf per ray; an FMA counts 2, an
@@ -150,7 +155,7 @@ def pmc_kernel(scene, kernel):
 def pmc_traffic(scene, kernel):
     """HBM bytes per launch of `kernel` from a committed PMC summary, if any.
     kernel may be a tuple: the launch-weighted mean over those kernels (the
-    level roofline covers k_trace_level and k_trace_leaves)."""
+    level roofline covers k_trace_real, k_trace_leaves and k_trace_level)."""
     names = kernel if isinstance(kernel, tuple) else (kernel,)
     tot = n = 0
     src = None
@@ -302,14 +307,14 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
     else:
         kernel, launches = "k_trace_level", lvl_launches
         ach = (lvl_bytes / (lvl_ms * 1e-3) / 1e9) if lvl_ms > 0 else 0.0
-        lk = ("k_trace_level", "k_trace_leaves")
+        lk = ("k_trace_level", "k_trace_real", "k_trace_leaves")
         traffic, src = pmc_traffic(name, lk)
         avg_s = lvl_ms * 1e-3 / max(1, launches)
         # the same visits priced at the hardware's fetch granularity: a random
         # 32-B record gather is one 128-B DRAM line (scripts/cal/gather_cal.hip)
         line_bytes = sum(132 * V[l] for l in range(1, 16)) + sum(4 * V[l] for l in range(2, 16))
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_trace_level+k_trace_leaves",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_trace_real+k_trace_leaves+k_trace_level",
                 "launches": int(launches), "avg_launch_us": round(avg_s * 1e6, 2),
                 "bytes_per_launch": int(lvl_bytes / max(1, launches)), "valu_busy": pmc_valu_busy(name, lk),
                 "traffic_gbs": round(traffic / avg_s / 1e9, 1) if traffic and avg_s > 0 else None,

@@ -18,7 +18,7 @@ for f in sorted(glob.glob(f"gpurun_out/pmc_{sc}_[0-9]/**/*counter_collection.csv
     lvl, i = {}, 0
     for r in rows:
         d = int(r["Dispatch_Id"])
-        if "k_trace_level" in r["Kernel_Name"] and d not in lvl:
+        if any(k in r["Kernel_Name"] for k in ("k_trace_level", "k_trace_real", "k_trace_leaves")) and d not in lvl:
             lvl[d] = LEVELS[i % len(LEVELS)]
             i += 1
     for r in rows:
