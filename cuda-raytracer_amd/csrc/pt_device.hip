@@ -59,7 +59,8 @@ struct pt_ctx {
   bool two_level = true; // two-level traversal (trace_levels; PT_TWO_LEVEL=0: one level per pass)
   bool leaf_kernel = true;  // k_trace_leaves for the leaf-only levels (PT_LEAF_KERNEL=0: k_trace_level)
   bool real_kernel = true;  // k_trace_real for the real levels of two-level mode (PT_REAL_KERNEL=0: k_trace_level)
-  std::vector<char> level_has_leaf;
+  std::vector<char> level_has_leaf;          // levels with a leaf the traversal can reach
+  std::vector<std::pair<int, int>> detached;  // (parent, slot) of leaves tested inline by the root pass
   RootTable rt{};        // root pass: inline leaves and queue targets (build_root_table)
   std::vector<pt_node> nodes_host;
   pt_light light{};
@@ -242,15 +243,21 @@ static size_t root_per_lane(size_t N, size_t spp) {
   return std::max((items + NLANE - 1) / NLANE * TILE, (blocks + NLANE - 1) / NLANE * TPB * spp);
 }
 
+// The caller runs N paths of spp slots and must be able to rely on that: the
+// buffers always hold at least N x spp.  They keep the larger of the old and
+// the requested shape when that fits the u32 queue offsets at the current
+// queue factor, else exactly the request (after a queue overflow doubled the
+// factor, or a reference-schedule render left 3 slots per path).
 static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
   if (N <= c->cap_paths && spp <= c->cap_spp && c->qfactor == c->cap_qfactor) return PT_OK;
-  // (after a queue overflow doubled qfactor the batch may have to shrink: the
-  // old capacity would overflow the u32 queue offsets)
-  if (c->qfactor != c->cap_qfactor)
-    N = std::min(N, max_batch_paths(c, std::max(spp, c->cap_spp)));
-  else
-    N = std::max(N, c->cap_paths);
-  spp = std::max(spp, c->cap_spp);
+  if (N > max_batch_paths(c, spp)) return fail(c, PT_E_UNSUPPORTED, "batch too large for u32 queue offsets");
+  uint32_t aN = std::max(N, c->cap_paths), aspp = std::max(spp, c->cap_spp);
+  if (aN > max_batch_paths(c, aspp)) {
+    aN = N;
+    aspp = spp;
+  }
+  N = aN;
+  spp = aspp;
   const size_t slots = (size_t)spp * N;
   int rc;
   if ((rc = dalloc(c, &c->d_ray, slots * RSTRIDE))) return rc;
@@ -337,6 +344,37 @@ static void build_root_table(pt_ctx* c) {
       if (nd[ch].child[g] >= 0 && !try_inline(ch, g)) add_target(ch, g);
   }
   c->skip_l1 = skip;
+  // Hot small leaves one level deeper (children of the root's targets): a
+  // leaf of <= 4 primitives whose box has >= PT_INLINE_SA (default 5 %) of
+  // the root's surface area is tested inline too (CBbunny: a 2-triangle leaf
+  // entered by 21 % of all rays, 10.8 ms per frame as a queued level) and
+  // detached from its parent in the device's copy of the tree, so the
+  // traversal never queues it (c->detached)
+  c->detached.clear();
+  if (skip) {
+    auto sa = [](const pt_node& n, int k) {
+      const double dx = n.bmax_x[k] - n.bmin_x[k], dy = n.bmax_y[k] - n.bmin_y[k], dz = n.bmax_z[k] - n.bmin_z[k];
+      return 2.0 * (dx * dy + dy * dz + dz * dx);
+    };
+    double rsa = 0;
+    for (int k = 0; k < 4; ++k)
+      if (nd[0].child[k] >= 0) rsa += sa(nd[0], k);
+    const char* se = getenv("PT_INLINE_SA");
+    const double min_ratio = se ? atof(se) : 0.05;
+    std::vector<std::pair<double, std::pair<int, int>>> cand;  // (area ratio, (parent, slot))
+    for (int t = 0; t < T.nt; ++t) {
+      const int par = T.tnode[t];
+      for (int k = 0; k < 4; ++k) {
+        const int ch = nd[par].child[k];
+        if (ch < 0 || nd[ch].prim_count <= 0 || nd[ch].prim_count > 4 || rsa <= 0) continue;
+        const double r = sa(nd[par], k) / rsa;
+        if (r >= min_ratio) cand.push_back({r, {par, k}});
+      }
+    }
+    std::sort(cand.begin(), cand.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    for (const auto& cd : cand)
+      if (try_inline(cd.second.first, cd.second.second)) c->detached.push_back(cd.second);
+  }
   // two-level traversal (default; PT_TWO_LEVEL=0 restores one level per pass)
   const char* tl = getenv("PT_TWO_LEVEL");
   c->two_level = !(tl && atoi(tl) == 0);
@@ -704,7 +742,21 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   if ((rc = dalloc(c, &c->d_icnt, (size_t)NLANE * (c->max_level_nodes + 1)))) return rc;
   if ((rc = dalloc(c, &c->d_scan_aux, (size_t)SCAN_MAXG * AGG_STRIDE + c->max_level_nodes + 1))) return rc;
   if ((rc = dalloc(c, &c->d_nitems, 2 * std::max(1, s->n_levels) + NLANE))) return rc;
-  HIPCHK(c, hipMemcpy(c->d_nodes, s->nodes, sizeof(pt_node) * s->n_nodes, hipMemcpyHostToDevice));
+  {
+    // the device's tree: the inlined deep leaves detached from their parents
+    std::vector<pt_node> dn(s->nodes, s->nodes + s->n_nodes);
+    for (const auto& pk : c->detached) dn[pk.first].child[pk.second] = -1;
+    HIPCHK(c, hipMemcpy(c->d_nodes, dn.data(), sizeof(pt_node) * s->n_nodes, hipMemcpyHostToDevice));
+    // levels with a reachable leaf (a detached leaf's level may have none left)
+    c->level_has_leaf.assign(s->n_levels, 0);
+    if (c->root_leaf) c->level_has_leaf[0] = 1;
+    for (int l = 0; l + 1 < s->n_levels; ++l)
+      for (int i = std::max(0, s->level_start[l]); i < std::min(s->n_nodes, s->level_start[l + 1]); ++i)
+        for (int k = 0; k < 4; ++k) {
+          const int ch = dn[i].child[k];
+          if (ch >= 0 && dn[ch].prim_count > 0) c->level_has_leaf[l + 1] = 1;  // (children sit one level down)
+        }
+  }
   HIPCHK(c, hipMemcpy(c->d_prims, s->prims, sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));
   {
     const std::vector<pt_prim> ref = ref_prim_records(s);
