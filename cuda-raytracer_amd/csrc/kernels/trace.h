@@ -73,7 +73,21 @@ struct TraceArgs {
                                      // QESTRIDE float4 per entry, {o, d.x}{d.y, d.z, id, tmax}
   uint32_t shadow_base;              // ray slots >= shadow_base are shadow rays (any hit ends them);
                                      // 0xFFFFFFFF: every ray wants its closest hit (pt_intersect)
+  // capacities, checked only by a -DPT_DBG_BOUNDS build (a debugging aid)
+  uint32_t dbg_nslots;               // ray records
+  uint32_t dbg_nnodes;
+  uint64_t dbg_qids;                 // ids in q (all regions)
 };
+#ifdef PT_DBG_BOUNDS
+#define PT_CHECK(cond, what, a, b)                                                                  \
+  if (!(cond)) {                                                                                    \
+    printf("PT_DBG_BOUNDS %s: %llu vs %llu (block %d thread %d)\n", what, (unsigned long long)(a), \
+           (unsigned long long)(b), (int)blockIdx.x, (int)threadIdx.x);                             \
+    return;                                                                                         \
+  }
+#else
+#define PT_CHECK(cond, what, a, b)
+#endif
 constexpr int QESTRIDE = 2;
 
 // A leaf's hit {t, prim} for ray id.  Closest-hit rays: atomicMin on the

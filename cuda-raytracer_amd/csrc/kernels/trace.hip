@@ -206,6 +206,8 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
 // tmax is the ray's tmax when it was pushed (conservative: it only shrinks).
 __device__ __forceinline__ void push_ray(const TraceArgs& A, bool entry, uint32_t e, uint32_t id, const f3 o,
                                          const f3 d, float tmax) {
+  PT_CHECK(entry || e < A.dbg_qids, "push id", e, A.dbg_qids);
+  PT_CHECK(id < A.dbg_nslots, "push id value", id, A.dbg_nslots);
   if (entry) {
     A.qe[QESTRIDE * (size_t)e] = make_float4(o.x, o.y, o.z, d.x);
     A.qe[QESTRIDE * (size_t)e + 1] = make_float4(d.y, d.z, __uint_as_float(id), tmax);
@@ -393,6 +395,7 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
       }
     }
     if (valid[j]) {  // the whole 32-B record at once (one full half line per ray)
+      PT_CHECK(id[j] < A.dbg_nslots, "root_pass record", id[j], A.dbg_nslots);
       A.ray[RSTRIDE * id[j]] = make_float4(o[j].x, o[j].y, o[j].z, d[j].x);
       A.ray[RSTRIDE * id[j] + 1] =
           make_float4(d[j].y, d[j].z, __uint_as_float(bp >= 0 ? (uint32_t)bp : PT_PRIM_NONE), bt);
@@ -508,6 +511,11 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
     for (int j = 0; j < RPT; ++j) {
       // the record's {prim, t} word: later box tests of this ray read the
       // tightened t as their tmax (a shadow ray: occluded, done)
+#ifdef PT_DBG_BOUNDS
+      if (valid[j] && bp[j] >= 0 && id[j] >= A.dbg_nslots)
+        printf("PT_DBG_BOUNDS report_hit %u vs %u\n", id[j], A.dbg_nslots);
+      else
+#endif
       if (valid[j] && bp[j] >= 0) report_hit(A.ray, A.shadow_base, id[j], bt[j], (uint32_t)bp[j]);
     }
     return nvalid;
@@ -678,6 +686,12 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
     for (int j = 0; j < RPTW; ++j) {
       const bool h = (bits[j] >> t) & 1u;
       const unsigned long long mm = __ballot(h);
+#ifdef PT_DBG_BOUNDS
+      if (h && off + mbcnt64(mm) >= A.dbg_qids)
+        printf("PT_DBG_BOUNDS two-level push %u vs %llu node %d target %u\n", off + mbcnt64(mm),
+               (unsigned long long)A.dbg_qids, node, t);
+      else
+#endif
       if (h) A.q[off + mbcnt64(mm)] = id[j];
       off += (uint32_t)__popcll(mm);
     }
@@ -757,6 +771,11 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     }
 #pragma unroll
     for (int j = 0; j < RPTW; ++j) {
+#ifdef PT_DBG_BOUNDS
+      if (valid[j] && bp[j] >= 0 && id[j] >= A.dbg_nslots)
+        printf("PT_DBG_BOUNDS report_hit %u vs %u\n", id[j], A.dbg_nslots);
+      else
+#endif
       if (valid[j] && bp[j] >= 0) report_hit(A.ray, A.shadow_base, id[j], bt[j], (uint32_t)bp[j]);
     }
     return;
@@ -1122,6 +1141,7 @@ __global__ __launch_bounds__(1024) void k_scan_level(TraceArgs A, LevelArgs L, u
           } else {
             uint32_t jj = 0;
             auto alloc = [&](int target) {
+              PT_CHECK((uint32_t)target < A.dbg_nnodes, "scan qoff", target, A.dbg_nnodes);
 #pragma unroll
               for (int s = 0; s < NLANE; ++s)
                 A.qoff[(size_t)target * NLANE + s] = out_parity_base + (uint32_t)s * lanecap + ex[s] + jj * cnt[i][s];

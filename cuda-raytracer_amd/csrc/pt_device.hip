@@ -307,6 +307,7 @@ static void build_root_table(pt_ctx* c) {
   RootTable& T = c->rt;
   memset(&T, 0, sizeof(T));
   c->skip_l1 = false;
+  c->detached.clear();  // (before the early return: a single-leaf scene keeps none of the last scene's)
   if (c->root_leaf) return;
   const char* e = getenv("PT_INLINE_MAX");
   int budget = e ? atoi(e) : 32;
@@ -350,7 +351,6 @@ static void build_root_table(pt_ctx* c) {
   // entered by 21 % of all rays, 10.8 ms per frame as a queued level) and
   // detached from its parent in the device's copy of the tree, so the
   // traversal never queues it (c->detached)
-  c->detached.clear();
   if (skip) {
     auto sa = [](const pt_node& n, int k) {
       const double dx = n.bmax_x[k] - n.bmin_x[k], dy = n.bmax_y[k] - n.bmin_y[k], dz = n.bmax_z[k] - n.bmin_z[k];
@@ -424,6 +424,9 @@ static TraceArgs trace_args(pt_ctx* c) {
   A.q = c->d_q;
   A.qe = c->d_qe;
   A.shadow_base = c->shadow_base;
+  A.dbg_nslots = (uint32_t)std::min<size_t>((size_t)c->cap_paths * c->cap_spp, 0xFFFFFFFFu);
+  A.dbg_nnodes = (uint32_t)c->n_nodes;
+  A.dbg_qids = (uint64_t)QREGIONS * c->qcap;
   return A;
 }
 
@@ -655,7 +658,7 @@ int pt_create(pt_ctx** out, int device) {
   for (auto& e : c->ev_poll) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
-      hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, 4) != hipSuccess ||
+      hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, 8) != hipSuccess ||
       hipMalloc((void**)&c->d_live, 4) != hipSuccess ||
       hipMalloc((void**)&c->d_pool, POOLS * CSTRIDE * 4) != hipSuccess ||
       hipHostMalloc((void**)&c->h_poll, 16, hipHostMallocDefault) != hipSuccess) {
@@ -745,7 +748,8 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   {
     // the device's tree: the inlined deep leaves detached from their parents
     std::vector<pt_node> dn(s->nodes, s->nodes + s->n_nodes);
-    for (const auto& pk : c->detached) dn[pk.first].child[pk.second] = -1;
+    for (const auto& pk : c->detached)
+      if (pk.first >= 0 && pk.first < s->n_nodes && pk.second >= 0 && pk.second < 4) dn[pk.first].child[pk.second] = -1;
     HIPCHK(c, hipMemcpy(c->d_nodes, dn.data(), sizeof(pt_node) * s->n_nodes, hipMemcpyHostToDevice));
     // levels with a reachable leaf (a detached leaf's level may have none left)
     c->level_has_leaf.assign(s->n_levels, 0);
@@ -914,12 +918,17 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       S.ps1 = c->d_res;
       S.N = M;
       const uint32_t want = (M + 4 * PATH_CHUNK - 1) / (4 * PATH_CHUNK);
-      HIPCHK(c, hipMemsetAsync(c->d_work, 0, 4, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->d_work, 0, 8, c->stream));  // (big-chunk and tail counters)
       const int kv = (nsh == 2 ? 1 : 0) + (c->refa ? 2 : 0);
       auto kpath = kv == 0 ? k_path_leaf<1, false> : kv == 1 ? k_path_leaf<2, false>
                  : kv == 2 ? k_path_leaf<1, true> : k_path_leaf<2, true>;
-      c->launch(pt_ctx::K_PATH, 0, kpath, dim3(std::min<uint32_t>(want, c->path_grid[kv])), dim3(TPB), S,
-                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work);
+      const uint32_t blocks = std::min<uint32_t>(want, c->path_grid[kv]);
+      // the last round of grabs (one PATH_CHUNK per resident wave) comes in
+      // PATH_TAIL_CHUNK pieces (k_path_leaf)
+      const uint64_t last_round = (uint64_t)blocks * (TPB / 64) * PATH_CHUNK;
+      const uint32_t tail = M > last_round ? (uint32_t)(M - last_round) : 0u;
+      c->launch(pt_ctx::K_PATH, 0, kpath, dim3(blocks), dim3(TPB), S,
+                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work, tail);
       c->stats.passes += passes;
       if (first) c->stats.batch_paths = (int32_t)M;
     } else {
