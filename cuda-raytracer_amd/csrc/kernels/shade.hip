@@ -932,7 +932,6 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
 #define PT_PATH_CHUNK 512
 #endif
 constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
-constexpr uint32_t PATH_TAIL_CHUNK = PATH_CHUNK / 8;
 
 // With all path state in registers: 6 waves per SIMD (80 VGPRs, no spills);
 // 7 waves (72 VGPRs) ran within 0.6 % of it but spilled ~20 VGPRs around the
@@ -960,7 +959,7 @@ constexpr uint32_t PATH_TAIL_CHUNK = PATH_CHUNK / 8;
 template <int NSH, bool REFA>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
-    uint32_t* __restrict__ work, uint32_t tail) {
+    uint32_t* __restrict__ work) {
   const uint32_t lid = lane_id();
   uint32_t nrays = 0;
   // wave-uniform pool [next, end) of unstarted paths; `drained`: the global
@@ -984,25 +983,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
     // ---- refill idle lanes from the pool (new paths start at their camera ray)
     unsigned long long idle = __ballot(!active);
     if (idle && next == end && !drained) {
-      // PATH_CHUNK paths at a time from work[0] below `tail`, then
-      // PATH_TAIL_CHUNK at a time from work[1] (the paths from tail on): the
-      // last round of grabs is 8x finer, so the waves finish together (a
-      // wave that took a full chunk last ran up to one chunk's time after
-      // the others: ~12 % of a 1/8-share frame)
-      uint32_t b = 0, e = 0;
-      if (lid == 0) {
-        b = atomicAdd(work, PATH_CHUNK);
-        e = min(b + PATH_CHUNK, tail);
-        if (b >= tail) {
-          b = tail + atomicAdd(work + 1, PATH_TAIL_CHUNK);
-          e = min(b + PATH_TAIL_CHUNK, S.N);
-        }
-      }
-      b = __builtin_amdgcn_readfirstlane(b);
-      e = __builtin_amdgcn_readfirstlane(e);
-      drained = b >= S.N;
-      next = drained ? 0u : b;
-      end = drained ? 0u : e;
+      // (a last round of grabs 8x finer, from one counter or from 32
+      // per-region counters, did not shorten a 1/8-share frame: 5.06 ms ->
+      // 5.63 / 5.07 ms; the full frame lost 0.5 / 2 %)
+      uint32_t base = 0;
+      if (lid == 0) base = atomicAdd(work, PATH_CHUNK);
+      base = __builtin_amdgcn_readfirstlane(base);
+      drained = base >= S.N;
+      next = drained ? 0u : base;
+      end = drained ? 0u : min(base + PATH_CHUNK, S.N);
     }
     if (idle && next < end) {
       const uint32_t r = mbcnt64(idle);

@@ -658,7 +658,7 @@ int pt_create(pt_ctx** out, int device) {
   for (auto& e : c->ev_poll) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
-      hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, 8) != hipSuccess ||
+      hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, 4) != hipSuccess ||
       hipMalloc((void**)&c->d_live, 4) != hipSuccess ||
       hipMalloc((void**)&c->d_pool, POOLS * CSTRIDE * 4) != hipSuccess ||
       hipHostMalloc((void**)&c->h_poll, 16, hipHostMallocDefault) != hipSuccess) {
@@ -918,17 +918,13 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       S.ps1 = c->d_res;
       S.N = M;
       const uint32_t want = (M + 4 * PATH_CHUNK - 1) / (4 * PATH_CHUNK);
-      HIPCHK(c, hipMemsetAsync(c->d_work, 0, 8, c->stream));  // (big-chunk and tail counters)
+      HIPCHK(c, hipMemsetAsync(c->d_work, 0, 4, c->stream));
       const int kv = (nsh == 2 ? 1 : 0) + (c->refa ? 2 : 0);
       auto kpath = kv == 0 ? k_path_leaf<1, false> : kv == 1 ? k_path_leaf<2, false>
                  : kv == 2 ? k_path_leaf<1, true> : k_path_leaf<2, true>;
       const uint32_t blocks = std::min<uint32_t>(want, c->path_grid[kv]);
-      // the last round of grabs (one PATH_CHUNK per resident wave) comes in
-      // PATH_TAIL_CHUNK pieces (k_path_leaf)
-      const uint64_t last_round = (uint64_t)blocks * (TPB / 64) * PATH_CHUNK;
-      const uint32_t tail = M > last_round ? (uint32_t)(M - last_round) : 0u;
       c->launch(pt_ctx::K_PATH, 0, kpath, dim3(blocks), dim3(TPB), S,
-                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work, tail);
+                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work);
       c->stats.passes += passes;
       if (first) c->stats.batch_paths = (int32_t)M;
     } else {
