@@ -956,12 +956,43 @@ constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 #endif
 // (PT_PATH_LIGHT_RELOAD reads the light from the kernel-argument segment at
 // offsetof(ShadeArgs, light): S must stay this kernel's FIRST parameter)
+// Guided path grabs: the k-th grab from the counter takes the range
+// [S[j] + (k - G[j]) c[j], ...) of the phase j with G[j] <= k < G[j+1]; the
+// chunk size halves as the unstarted paths run out (512 down to 64), so no
+// wave takes a large chunk late.  Waves on one SIMD run at very different
+// speeds (1/8 share of a CBempty frame: 2 to 24 chunks per wave, PMC timing
+// build), and a slow wave's last 512-path chunk ran up to 0.9 ms after the
+// counter was exhausted.  Guide 4 (pt_device.hip path_schedule): 1/8 share
+// CBempty 5.18 -> 5.03 ms, CBspheres 6.32 -> 5.92 ms; full frames within
+// noise (grabs 65k -> 164k per share; each is one same-address device atomic,
+// 2-100 us under contention, timing build).
+constexpr int PATH_PHASES = 4;
+struct PathSched {
+  uint32_t S[PATH_PHASES + 1];  // first path of each phase (S[PATH_PHASES] = N)
+  uint32_t G[PATH_PHASES + 1];  // first grab index of each phase (G[PATH_PHASES] = total grabs)
+  uint32_t c[PATH_PHASES];      // chunk size of each phase
+};
+
+// PT_PATH_TIMING (diagnostic build only): per-wave wall-clock marks (entry,
+// first empty grab, exit, chunks taken) for pt_dbg_path_timing
+#ifndef PT_PATH_TIMING
+#define PT_PATH_TIMING 0
+#endif
+#if PT_PATH_TIMING
+constexpr uint32_t PT_TIMING_WAVES = 16384;
+static __device__ unsigned long long g_path_timing[PT_TIMING_WAVES * 8];
+#endif
 template <int NSH, bool REFA>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
-    uint32_t* __restrict__ work) {
+    uint32_t* __restrict__ work, PathSched sched) {
   const uint32_t lid = lane_id();
   uint32_t nrays = 0;
+#if PT_PATH_TIMING
+  const unsigned long long tm0 = wall_clock64();
+  unsigned long long tm_drain = 0, tm_grab = 0, tm_grab_max = 0;
+  uint32_t nchunks = 0;
+#endif
   // wave-uniform pool [next, end) of unstarted paths; `drained`: the global
   // counter has passed N
   uint32_t next = 0, end = 0;
@@ -983,15 +1014,29 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
     // ---- refill idle lanes from the pool (new paths start at their camera ray)
     unsigned long long idle = __ballot(!active);
     if (idle && next == end && !drained) {
-      // (a last round of grabs 8x finer, from one counter or from 32
-      // per-region counters, did not shorten a 1/8-share frame: 5.06 ms ->
-      // 5.63 / 5.07 ms; the full frame lost 0.5 / 2 %)
-      uint32_t base = 0;
-      if (lid == 0) base = atomicAdd(work, PATH_CHUNK);
-      base = __builtin_amdgcn_readfirstlane(base);
-      drained = base >= S.N;
-      next = drained ? 0u : base;
-      end = drained ? 0u : min(base + PATH_CHUNK, S.N);
+#if PT_PATH_TIMING
+      const unsigned long long tg = wall_clock64();
+#endif
+      uint32_t k = 0;
+      if (lid == 0) k = atomicAdd(work, 1u);
+      k = __builtin_amdgcn_readfirstlane(k);
+      drained = k >= sched.G[PATH_PHASES];
+      if (!drained) {
+        int j = 0;
+#pragma unroll
+        for (int q = 1; q < PATH_PHASES; ++q) j = k >= sched.G[q] ? q : j;
+        next = sched.S[j] + (k - sched.G[j]) * sched.c[j];
+        end = min(next + sched.c[j], sched.S[j + 1]);
+      } else {
+        next = end = 0;
+      }
+#if PT_PATH_TIMING
+      const unsigned long long dt = wall_clock64() - tg;
+      tm_grab += dt;
+      tm_grab_max = dt > tm_grab_max ? dt : tm_grab_max;
+      if (drained) tm_drain = wall_clock64();
+      else ++nchunks;
+#endif
     }
     if (idle && next < end) {
       const uint32_t r = mbcnt64(idle);
@@ -1073,6 +1118,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
   if (lid == 0 && w)
     atomicAdd(rcount + (size_t)((blockIdx.x * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16,
               (unsigned long long)w);
+#if PT_PATH_TIMING
+  const uint32_t gw = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  if (lid == 0 && gw < PT_TIMING_WAVES) {
+    unsigned long long* o = g_path_timing + (size_t)gw * 8;
+    o[0] = tm0;
+    o[1] = tm_drain;
+    o[2] = wall_clock64();
+    o[3] = nchunks;
+    o[4] = tm_grab;
+    o[5] = tm_grab_max;
+  }
+#endif
 }
 
 // Sum each owned pixel's samples of this batch into the accumulation buffer,

@@ -106,6 +106,7 @@ struct pt_ctx {
   uint32_t* h_poll = nullptr;  // pinned: {live, err} x 2 poll slots
   hipEvent_t ev_poll[2] = {};
   int path_grid[4] = {0, 0, 0, 0};  // resident workgroups of k_path_leaf<1|2, refa>
+  int path_guide = 4;               // k_path_leaf grab schedule (path_schedule; PT_PATH_GUIDE)
 
   // framebuffer
   int fb_w = 0, fb_h = 0, fb_tile = 0, fb_rank = 0, fb_nranks = 0;
@@ -223,6 +224,29 @@ static constexpr int ENTRY_LEVEL_DEFAULT = PT_ENTRY_LEVEL_DEFAULT;
 #define PT_SCAN_MULTI_MIN_DEFAULT 512
 #endif
 static constexpr int SCAN_MULTI_MIN_DEFAULT = PT_SCAN_MULTI_MIN_DEFAULT;
+// k_path_leaf's guided grab schedule: phase j hands out chunks of
+// PATH_CHUNK >> j paths and begins once fewer than waves * (PATH_CHUNK >>
+// (j - 1)) * guide paths are left unstarted (guide = 0: one phase)
+static PathSched path_schedule(uint32_t N, uint64_t waves, int guide) {
+  PathSched p{};
+  uint64_t prev = 0;
+  for (int j = 0; j < PATH_PHASES; ++j) {
+    uint64_t st = 0;
+    if (j > 0) {
+      const uint64_t rem = guide > 0 ? waves * (uint64_t)(PATH_CHUNK >> (j - 1)) * (uint64_t)guide : 0;
+      st = rem >= N ? 0 : N - rem;
+    }
+    st = std::max(st, prev);
+    p.S[j] = (uint32_t)st;
+    p.c[j] = PATH_CHUNK >> j;
+    prev = st;
+  }
+  p.S[PATH_PHASES] = N;
+  p.G[0] = 0;
+  for (int j = 0; j < PATH_PHASES; ++j) p.G[j + 1] = p.G[j] + (p.S[j + 1] - p.S[j] + p.c[j] - 1) / p.c[j];
+  return p;
+}
+
 static uint32_t max_batch_paths(const pt_ctx* c, uint32_t slots_per_path) {
   // u32 entry offsets: both halves of the entry queues, and the root's id
   // queues (<= 16 targets x every ray, see root_per_lane)
@@ -629,6 +653,15 @@ static void build_owned_pixels(pt_ctx* c, int W, int H, int T, int rank, int nra
 
 extern "C" {
 
+#if PT_PATH_TIMING
+// diagnostic build only: the per-wave marks of the last k_path_leaf launch
+int pt_dbg_path_timing(unsigned long long* out, int nwaves) {
+  if (!out || nwaves <= 0 || nwaves > (int)PT_TIMING_WAVES) return PT_E_INVALID;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_path_timing), (size_t)nwaves * 64) == hipSuccess ? PT_OK
+                                                                                                 : PT_E_HIP;
+}
+#endif
+
 int pt_device_count(int* n) {
   if (!n) return PT_E_INVALID;
   hipError_t e = hipGetDeviceCount(n);
@@ -650,6 +683,7 @@ int pt_create(pt_ctx** out, int device) {
   // initial queue factor (doubles whenever a level overflows; PT_QFACTOR=1
   // exercises that path in the tests)
   if (const char* q = getenv("PT_QFACTOR")) c->qfactor = std::max(1, atoi(q));
+  if (const char* q = getenv("PT_PATH_GUIDE")) c->path_guide = std::max(0, atoi(q));
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return PT_E_HIP;
@@ -923,8 +957,9 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       auto kpath = kv == 0 ? k_path_leaf<1, false> : kv == 1 ? k_path_leaf<2, false>
                  : kv == 2 ? k_path_leaf<1, true> : k_path_leaf<2, true>;
       const uint32_t blocks = std::min<uint32_t>(want, c->path_grid[kv]);
+      const PathSched sched = path_schedule(M, (uint64_t)blocks * (TPB / 64), c->path_guide);
       c->launch(pt_ctx::K_PATH, 0, kpath, dim3(blocks), dim3(TPB), S,
-                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work);
+                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work, sched);
       c->stats.passes += passes;
       if (first) c->stats.batch_paths = (int32_t)M;
     } else {
