@@ -962,16 +962,43 @@ constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 // wave takes a large chunk late.  Waves on one SIMD run at very different
 // speeds (1/8 share of a CBempty frame: 2 to 24 chunks per wave, PMC timing
 // build), and a slow wave's last 512-path chunk ran up to 0.9 ms after the
-// counter was exhausted.  Guide 4 (pt_device.hip path_schedule): 1/8 share
-// CBempty 5.18 -> 5.03 ms, CBspheres 6.32 -> 5.92 ms; full frames within
-// noise (grabs 65k -> 164k per share; each is one same-address device atomic,
-// 2-100 us under contention, timing build).
+// counter was exhausted.  The paths are split into path regions, one per
+// counter (128 B apart; a workgroup starts on region blockIdx % nreg and
+// moves on when it is empty): one counter for all waves queued the grabs,
+// each a same-address device atomic (2-100 us under contention, timing
+// build).  1/8 share of a CBempty frame: 5.18 ms (one counter, 512-path
+// chunks) -> 5.03 (guide 4) -> 4.89 (guide 4, 8 regions); ideal 4.59;
+// CBspheres 6.32 -> 5.88 ms; full frames within noise.
 constexpr int PATH_PHASES = 4;
-struct PathSched {
-  uint32_t S[PATH_PHASES + 1];  // first path of each phase (S[PATH_PHASES] = N)
-  uint32_t G[PATH_PHASES + 1];  // first grab index of each phase (G[PATH_PHASES] = total grabs)
-  uint32_t c[PATH_PHASES];      // chunk size of each phase
-};
+constexpr uint32_t PATH_REGIONS_MAX = 32;
+constexpr uint32_t PATH_CTR_STRIDE = 32;  // u32s between region counters (128 B)
+
+// The k-th grab of path region [lo, hi): phase j hands out chunks of
+// PATH_CHUNK >> j and begins tail_unit * (PATH_CHUNK >> (j - 1)) paths before
+// hi (tail_unit = the region's waves x the guide factor; 0: one phase).
+// Returns false once the region's paths are all handed out.
+__device__ __forceinline__ bool path_grab(uint32_t lo, uint32_t hi, uint32_t tail_unit, uint32_t k, uint32_t& b,
+                                          uint32_t& e) {
+  uint32_t s0 = lo, g = 0;
+#pragma unroll
+  for (int j = 0; j < PATH_PHASES; ++j) {
+    const uint32_t c = PATH_CHUNK >> j;
+    uint32_t s1 = hi;
+    if (j + 1 < PATH_PHASES) {
+      const uint64_t rem = (uint64_t)tail_unit * (PATH_CHUNK >> j);
+      s1 = rem >= (uint64_t)(hi - s0) ? s0 : hi - (uint32_t)rem;
+    }
+    const uint32_t n = (s1 - s0 + c - 1) / c;
+    if (k - g < n) {
+      b = s0 + (k - g) * c;
+      e = min(b + c, s1);
+      return true;
+    }
+    g += n;
+    s0 = s1;
+  }
+  return false;
+}
 
 // PT_PATH_TIMING (diagnostic build only): per-wave wall-clock marks (entry,
 // first empty grab, exit, chunks taken) for pt_dbg_path_timing
@@ -985,9 +1012,12 @@ static __device__ unsigned long long g_path_timing[PT_TIMING_WAVES * 8];
 template <int NSH, bool REFA>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
-    uint32_t* __restrict__ work, PathSched sched) {
+    uint32_t* __restrict__ work, uint32_t nreg, uint32_t tail_unit) {
   const uint32_t lid = lane_id();
   uint32_t nrays = 0;
+  // wave-uniform: the path region this wave grabs from (its workgroup's, then
+  // the next ones as they run out) and how many regions it has found empty
+  uint32_t reg = blockIdx.x % nreg, tried = 0;
 #if PT_PATH_TIMING
   const unsigned long long tm0 = wall_clock64();
   unsigned long long tm_drain = 0, tm_grab = 0, tm_grab_max = 0;
@@ -1017,19 +1047,24 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
 #if PT_PATH_TIMING
       const unsigned long long tg = wall_clock64();
 #endif
-      uint32_t k = 0;
-      if (lid == 0) k = atomicAdd(work, 1u);
-      k = __builtin_amdgcn_readfirstlane(k);
-      drained = k >= sched.G[PATH_PHASES];
-      if (!drained) {
-        int j = 0;
-#pragma unroll
-        for (int q = 1; q < PATH_PHASES; ++q) j = k >= sched.G[q] ? q : j;
-        next = sched.S[j] + (k - sched.G[j]) * sched.c[j];
-        end = min(next + sched.c[j], sched.S[j + 1]);
-      } else {
-        next = end = 0;
+      uint32_t b = 0, e = 0;
+      if (lid == 0) {
+        while (tried < nreg) {
+          const uint32_t k = atomicAdd(work + reg * PATH_CTR_STRIDE, 1u);
+          const uint32_t lo = (uint32_t)((uint64_t)S.N * reg / nreg);
+          const uint32_t hi = (uint32_t)((uint64_t)S.N * (reg + 1) / nreg);
+          if (path_grab(lo, hi, tail_unit, k, b, e)) break;
+          reg = reg + 1 == nreg ? 0u : reg + 1;
+          ++tried;
+        }
       }
+      b = __builtin_amdgcn_readfirstlane(b);
+      e = __builtin_amdgcn_readfirstlane(e);
+      reg = __builtin_amdgcn_readfirstlane(reg);
+      tried = __builtin_amdgcn_readfirstlane(tried);
+      drained = tried >= nreg;
+      next = drained ? 0u : b;
+      end = drained ? 0u : e;
 #if PT_PATH_TIMING
       const unsigned long long dt = wall_clock64() - tg;
       tm_grab += dt;

@@ -96,7 +96,7 @@ struct pt_ctx {
   unsigned long long* d_rcount = nullptr;  // valid root rays: RCOUNT_SLOTS counters, one 128-B line each
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
-  uint32_t* d_work = nullptr;  // k_path_leaf path counter
+  uint32_t* d_work = nullptr;  // k_path_leaf path-region counters (128 B apart)
   float4* d_res = nullptr;     // per-path radiance of a chunk
   size_t res_cap = 0;
   uint4* d_wstate = nullptr;   // per shade workgroup {block next, block end, live slots, shaded vertices}
@@ -106,7 +106,8 @@ struct pt_ctx {
   uint32_t* h_poll = nullptr;  // pinned: {live, err} x 2 poll slots
   hipEvent_t ev_poll[2] = {};
   int path_grid[4] = {0, 0, 0, 0};  // resident workgroups of k_path_leaf<1|2, refa>
-  int path_guide = 4;               // k_path_leaf grab schedule (path_schedule; PT_PATH_GUIDE)
+  int path_guide = 4;               // k_path_leaf grab schedule (path_grab; PT_PATH_GUIDE)
+  int path_regions = 8;             // k_path_leaf path regions / counters (PT_PATH_REGIONS)
 
   // framebuffer
   int fb_w = 0, fb_h = 0, fb_tile = 0, fb_rank = 0, fb_nranks = 0;
@@ -224,29 +225,6 @@ static constexpr int ENTRY_LEVEL_DEFAULT = PT_ENTRY_LEVEL_DEFAULT;
 #define PT_SCAN_MULTI_MIN_DEFAULT 512
 #endif
 static constexpr int SCAN_MULTI_MIN_DEFAULT = PT_SCAN_MULTI_MIN_DEFAULT;
-// k_path_leaf's guided grab schedule: phase j hands out chunks of
-// PATH_CHUNK >> j paths and begins once fewer than waves * (PATH_CHUNK >>
-// (j - 1)) * guide paths are left unstarted (guide = 0: one phase)
-static PathSched path_schedule(uint32_t N, uint64_t waves, int guide) {
-  PathSched p{};
-  uint64_t prev = 0;
-  for (int j = 0; j < PATH_PHASES; ++j) {
-    uint64_t st = 0;
-    if (j > 0) {
-      const uint64_t rem = guide > 0 ? waves * (uint64_t)(PATH_CHUNK >> (j - 1)) * (uint64_t)guide : 0;
-      st = rem >= N ? 0 : N - rem;
-    }
-    st = std::max(st, prev);
-    p.S[j] = (uint32_t)st;
-    p.c[j] = PATH_CHUNK >> j;
-    prev = st;
-  }
-  p.S[PATH_PHASES] = N;
-  p.G[0] = 0;
-  for (int j = 0; j < PATH_PHASES; ++j) p.G[j + 1] = p.G[j] + (p.S[j + 1] - p.S[j] + p.c[j] - 1) / p.c[j];
-  return p;
-}
-
 static uint32_t max_batch_paths(const pt_ctx* c, uint32_t slots_per_path) {
   // u32 entry offsets: both halves of the entry queues, and the root's id
   // queues (<= 16 targets x every ray, see root_per_lane)
@@ -684,6 +662,7 @@ int pt_create(pt_ctx** out, int device) {
   // exercises that path in the tests)
   if (const char* q = getenv("PT_QFACTOR")) c->qfactor = std::max(1, atoi(q));
   if (const char* q = getenv("PT_PATH_GUIDE")) c->path_guide = std::max(0, atoi(q));
+  if (const char* q = getenv("PT_PATH_REGIONS")) c->path_regions = std::max(1, atoi(q));
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return PT_E_HIP;
@@ -692,7 +671,7 @@ int pt_create(pt_ctx** out, int device) {
   for (auto& e : c->ev_poll) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
-      hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, 4) != hipSuccess ||
+      hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, PATH_REGIONS_MAX * PATH_CTR_STRIDE * 4) != hipSuccess ||
       hipMalloc((void**)&c->d_live, 4) != hipSuccess ||
       hipMalloc((void**)&c->d_pool, POOLS * CSTRIDE * 4) != hipSuccess ||
       hipHostMalloc((void**)&c->h_poll, 16, hipHostMallocDefault) != hipSuccess) {
@@ -952,14 +931,18 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       S.ps1 = c->d_res;
       S.N = M;
       const uint32_t want = (M + 4 * PATH_CHUNK - 1) / (4 * PATH_CHUNK);
-      HIPCHK(c, hipMemsetAsync(c->d_work, 0, 4, c->stream));
       const int kv = (nsh == 2 ? 1 : 0) + (c->refa ? 2 : 0);
       auto kpath = kv == 0 ? k_path_leaf<1, false> : kv == 1 ? k_path_leaf<2, false>
                  : kv == 2 ? k_path_leaf<1, true> : k_path_leaf<2, true>;
       const uint32_t blocks = std::min<uint32_t>(want, c->path_grid[kv]);
-      const PathSched sched = path_schedule(M, (uint64_t)blocks * (TPB / 64), c->path_guide);
+      // guided grabs from nreg path regions (k_path_leaf path_grab): each
+      // region's tail phases begin path_guide chunks per wave before its end
+      const uint32_t nreg = (uint32_t)std::max(1, std::min<int>(c->path_regions, (int)std::min<uint32_t>(blocks, PATH_REGIONS_MAX)));
+      const uint32_t tail_unit = (uint32_t)std::min<uint64_t>(
+          ((uint64_t)blocks * (TPB / 64) + nreg - 1) / nreg * (uint64_t)c->path_guide, 1u << 22);
+      HIPCHK(c, hipMemsetAsync(c->d_work, 0, (size_t)nreg * PATH_CTR_STRIDE * 4, c->stream));
       c->launch(pt_ctx::K_PATH, 0, kpath, dim3(blocks), dim3(TPB), S,
-                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work, sched);
+                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work, nreg, tail_unit);
       c->stats.passes += passes;
       if (first) c->stats.batch_paths = (int32_t)M;
     } else {
