@@ -222,6 +222,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
     # RCCL gather to rank 0, then rank 0's copy to the host)
     host = torch.empty((args.height, args.width, 4), dtype=torch.float32, pin_memory=True)
     t_rank, t_world = share if share else (rank, world)
+    sums = [None]  # this rank's owned-pixel sums, reused frame to frame
 
     def frame(stats):
         ctx.clear()
@@ -229,8 +230,8 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
                    batch_paths=args.batch, tile_size=args.tile, rank=t_rank, nranks=t_world,
                    flags=ptrace.PT_FLAG_STATS if stats else 0)
         if world > 1:
-            img = ptdist.gather_frame(ptdist.local_sums_tensor(ctx, dev), args.width, args.height, args.tile,
-                                      args.spp)
+            sums[0] = ptdist.local_sums_tensor(ctx, dev, out=sums[0])
+            img = ptdist.gather_frame(sums[0], args.width, args.height, args.tile, args.spp)
             if img is not None:
                 host.copy_(img)
         else:

@@ -68,6 +68,7 @@ struct ShadeArgs {
   uint32_t* pool;     // POOLS dispensers, CSTRIDE apart (block counters)
   int passes;         // vertices per path at most (max_bounces + 2)
   unsigned long long* rcount;    // rays entering the traversal (RCOUNT_SLOTS counters)
+  uint32_t kshift;    // record-order key of a path: its hit primitive >> kshift (PT_SORT_WAVE)
 };
 
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -525,12 +526,45 @@ __device__ __forceinline__ void path_pixel(const ShadeArgs& S, uint32_t P, uint3
 // Slot states returned by shade_slot
 constexpr int SLOT_FREE = 0, SLOT_LIVE = 1, SLOT_ENDED = 2;
 
+// Record order (PT_SORT_WAVE): a wave writes its paths' new state and ray
+// records back into its own 64 slots in the order of a key -- the primitive
+// the path's extension ray hit, in SORT_KEYS equal ranges of the BVH order,
+// i.e. roughly the subtree the new rays start in; camera rays, misses and
+// free slots last.  Rays of one wave that start in the same subtree (and so
+// mostly enter the same queues) then have adjacent 32-B records, so a level
+// kernel's gather of consecutive queue entries shares 128-B lines instead of
+// fetching one line per ray.  The slots of a path change from pass to pass
+// within its wave; results do not depend on it (a permutation of the wave's
+// slots, read before any is written).
+#ifndef PT_SORT_WAVE
+#define PT_SORT_WAVE 1
+#endif
+#ifndef PT_SORT_KEY_BITS
+#define PT_SORT_KEY_BITS 4
+#endif
+constexpr uint32_t SORT_KEY_BITS = PT_SORT_KEY_BITS, SORT_KEYS = 1u << SORT_KEY_BITS;
+// Rank of this lane among the wave's active lanes ordered by (key, lane);
+// key in [0, SORT_KEYS].
+__device__ __forceinline__ uint32_t wave_key_rank(uint32_t key) {
+  uint32_t rank = 0, base = 0;
+#pragma unroll
+  for (uint32_t c = 0; c <= SORT_KEYS; ++c) {
+    const unsigned long long m = __ballot(key == c);
+    rank = key == c ? base + mbcnt64(m) : rank;
+    base += (uint32_t)__popcll(m);
+  }
+  return rank;
+}
+
 // Shade the path in slot p: read its state, hit words and rays, run
 // shade_vertex, write the new state and ray records.  Returns the new rays in
 // registers.  A path with nothing left to trace (or `passes` vertices done)
 // writes its radiance to res[P] and frees the slot.
+// q: the slot the path's state and new rays are written to (p, or with
+// PT_SORT_WAVE its place in the wave's key order; every active lane of the
+// wave must call this, free slots included).
 template <int NSH, bool REFA = false>
-__device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& new_ext, RayV& ext,
+__device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, uint32_t& q, bool& new_ext, RayV& ext,
                                           bool (&new_sh)[NSH], RayV (&shr)[NSH]) {
   new_ext = false;
 #pragma unroll
@@ -554,6 +588,12 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
 #pragma unroll
   for (int s = 0; s < NSH; ++s) asm volatile("" ::"v"(hs[s].z), "v"(cs[s].x));
   const uint32_t flags = __float_as_uint(s0.w);
+  q = p;
+  if constexpr (PT_SORT_WAVE != 0) {
+    const uint32_t hp = __float_as_uint(r1.z);
+    const bool key_hit = (flags & F_EXT) && hp != PT_PRIM_NONE;
+    q = (p & ~63u) + wave_key_rank(key_hit ? min(hp >> S.kshift, SORT_KEYS - 1u) : SORT_KEYS);
+  }
   if ((flags & (F_EXT | F_SHADOW | F_SHADOW2)) == 0) return SLOT_FREE;
   const uint32_t P = __float_as_uint(s1.w);
   PathState st{xyz(s0), flags, xyz(s1), 0u};
@@ -581,8 +621,8 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
     S.res[P] = make_float4(st.L.x, st.L.y, st.L.z, 0.0f);
     // (the caller frees the slot -- ps0 flags 0 -- unless it starts a new path)
   } else {
-    S.ps0[p] = make_float4(st.T.x, st.T.y, st.T.z, __uint_as_float(st.flags));
-    S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(P));
+    S.ps0[q] = make_float4(st.T.x, st.T.y, st.T.z, __uint_as_float(st.flags));
+    S.ps1[q] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(P));
   }
   // new rays: their records are written by root_pass (with the key of the
   // inline leaves).  A slot without a new ray keeps its stale record: only
@@ -590,7 +630,7 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool& 
   // else reads a record that was not queued (no 16-B "empty" partial writes)
 #pragma unroll
   for (int s = 0; s < NSH; ++s)
-    if (new_sh[s]) (s ? S.ps3 : S.ps2)[p] = make_float4(C[s].x, C[s].y, C[s].z, 0.0f);
+    if (new_sh[s]) (s ? S.ps3 : S.ps2)[q] = make_float4(C[s].x, C[s].y, C[s].z, 0.0f);
   return ended ? SLOT_ENDED : SLOT_LIVE;
 }
 
@@ -728,7 +768,8 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
   }
   int state = SLOT_LIVE;
-  if (p < S.N) state = shade_slot<NSH, REFA>(S, p, new_ext, ext, new_sh, shr);
+  uint32_t q = p;  // where this lane's path state and new rays go
+  if (p < S.N) state = shade_slot<NSH, REFA>(S, p, q, new_ext, ext, new_sh, shr);
   // ---- regeneration: free slots take the next paths in rank order, from the
   // current block and then from a newly claimed one
   const bool fr = p < S.N && state != SLOT_LIVE;
@@ -783,19 +824,21 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     for (int w = 0; w < wave; ++w) rank += s_free[w];
     if (rank < ns) {
       const uint32_t P = rank < t1 ? next + rank : s_nb + rank - t1;
-      S.ps0[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
-      S.ps1[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
+      S.ps0[q] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
+      S.ps1[q] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
       ext = RayV{ld3(S.cam.origin), mk(s_dir[0][rank], s_dir[1][rank], s_dir[2][rank]), __builtin_inff()};
       new_ext = true;
-    } else if (state == SLOT_ENDED) {
-      S.ps0[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));  // the slot stays free
+    } else if (state == SLOT_ENDED || (PT_SORT_WAVE && q != p)) {
+      // the slot stays free (with PT_SORT_WAVE slot q may have held another
+      // lane's path until now)
+      S.ps0[q] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
     }
   }
   uint32_t id[1 + NSH];
   f3 o[1 + NSH], d[1 + NSH];
   float tm[1 + NSH];
   bool valid[1 + NSH], anyhit[1 + NSH];
-  id[0] = p;
+  id[0] = q;
   o[0] = ext.o;
   d[0] = ext.d;
   tm[0] = __builtin_inff();
@@ -804,7 +847,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   uint32_t n = new_ext ? 1u : 0u;
 #pragma unroll
   for (int s = 0; s < NSH; ++s) {
-    id[1 + s] = (1 + s) * S.N + p;
+    id[1 + s] = (1 + s) * S.N + q;
     o[1 + s] = shr[s].o;
     d[1 + s] = shr[s].d;
     tm[1 + s] = shr[s].tmax;

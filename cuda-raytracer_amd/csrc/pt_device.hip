@@ -922,6 +922,11 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.res = c->d_res;
     S.M = M;
     S.passes = passes;
+    {  // record-order keys: SORT_KEYS equal primitive ranges (BVH order, so ~subtrees)
+      uint32_t b = 0;
+      while ((1u << b) < (uint32_t)c->n_prims) ++b;
+      S.kshift = b > SORT_KEY_BITS ? b - SORT_KEY_BITS : 0u;
+    }
     if (c->root_leaf) {
       // single-leaf tree: every path runs to completion in one kernel
       // (persistent waves with path regeneration, output res[P])

@@ -446,6 +446,12 @@ class Context:
                                        img.shape[0]))
         return out
 
+    def owned_count(self):
+        """Pixels this context renders (its tile share of the last render)."""
+        n = C.c_int32()
+        self._chk(LIB.pt_owned_pixels(self.h, C.byref(n), None, 0, None))
+        return n.value
+
     def owned_pixels(self):
         n = C.c_int32()
         self._chk(LIB.pt_owned_pixels(self.h, C.byref(n), None, 0, None))
