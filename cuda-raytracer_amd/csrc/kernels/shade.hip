@@ -555,20 +555,62 @@ __device__ __forceinline__ uint32_t wave_key_rank(uint32_t key) {
   }
   return rank;
 }
+// The same over the whole workgroup (PT_SORT_WAVE 2): rank among the
+// workgroup's lanes with act set, ordered by (key, wave, lane).  Every thread
+// of the workgroup calls it (two barriers); kc: LDS [SORT_KEYS + 1][4].
+__device__ __forceinline__ uint32_t block_key_rank(uint32_t key, bool act, uint32_t (*kc)[4]) {
+  const uint32_t wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  uint32_t wr = 0;
+#pragma unroll
+  for (uint32_t c = 0; c <= SORT_KEYS; ++c) {
+    const unsigned long long m = __ballot(act && key == c);
+    wr = key == c ? mbcnt64(m) : wr;
+    if (ln == 0) kc[c][wave] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  if (wave == 0) {  // lane c: key c's base = exclusive scan of the per-key totals
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (ln <= SORT_KEYS) {
+      w[0] = kc[ln][0];
+      w[1] = kc[ln][1];
+      w[2] = kc[ln][2];
+      w[3] = kc[ln][3];
+    }
+    const uint32_t tot = w[0] + w[1] + w[2] + w[3];
+    uint32_t inc = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t v = __shfl_up(inc, off, 64);
+      if ((int)ln >= off) inc += v;
+    }
+    const uint32_t b = inc - tot;
+    if (ln <= SORT_KEYS) {
+      kc[ln][0] = b;
+      kc[ln][1] = b + w[0];
+      kc[ln][2] = b + w[0] + w[1];
+      kc[ln][3] = b + w[0] + w[1] + w[2];
+    }
+  }
+  __syncthreads();
+  return act ? kc[key][wave] + wr : 0u;
+}
 
 // Shade the path in slot p: read its state, hit words and rays, run
 // shade_vertex, write the new state and ray records.  Returns the new rays in
 // registers.  A path with nothing left to trace (or `passes` vertices done)
 // writes its radiance to res[P] and frees the slot.
 // q: the slot the path's state and new rays are written to (p, or with
-// PT_SORT_WAVE its place in the wave's key order; every active lane of the
-// wave must call this, free slots included).
+// PT_SORT_WAVE its place in the key order of the wave (1) or workgroup (2)).
+// Every thread of the workgroup calls this; act = the thread has a slot
+// (p < N).  kc: LDS for block_key_rank.
 template <int NSH, bool REFA = false>
-__device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, uint32_t& q, bool& new_ext, RayV& ext,
-                                          bool (&new_sh)[NSH], RayV (&shr)[NSH]) {
+__device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool act, uint32_t& q, bool& new_ext,
+                                          RayV& ext, bool (&new_sh)[NSH], RayV (&shr)[NSH], uint32_t (*kc)[4]) {
   new_ext = false;
 #pragma unroll
   for (int s = 0; s < NSH; ++s) new_sh[s] = false;
+  q = p;
+  if (!act) p = 0;  // (loads from slot 0, ignored)
   // every word the slot may need is loaded at once (one memory round trip
   // instead of three dependent ones: flags, then records, then the ray and the
   // pending contributions); words the flags do not cover are stale and only
@@ -587,12 +629,19 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, uint32
   asm volatile("" ::"v"(s0.w), "v"(s1.w), "v"(r0.x), "v"(r1.x));
 #pragma unroll
   for (int s = 0; s < NSH; ++s) asm volatile("" ::"v"(hs[s].z), "v"(cs[s].x));
-  const uint32_t flags = __float_as_uint(s0.w);
-  q = p;
+  const uint32_t flags = act ? __float_as_uint(s0.w) : 0u;
   if constexpr (PT_SORT_WAVE != 0) {
+    // (every load above has completed -- the asm uses -- before any thread
+    // passes the rank's barriers and writes slots other threads read)
     const uint32_t hp = __float_as_uint(r1.z);
     const bool key_hit = (flags & F_EXT) && hp != PT_PRIM_NONE;
-    q = (p & ~63u) + wave_key_rank(key_hit ? min(hp >> S.kshift, SORT_KEYS - 1u) : SORT_KEYS);
+    const uint32_t key = key_hit ? min(hp >> S.kshift, SORT_KEYS - 1u) : SORT_KEYS;
+    if constexpr (PT_SORT_WAVE == 2) {
+      const uint32_t r = block_key_rank(key, act, kc);
+      if (act) q = blockIdx.x * TPB + r;
+    } else if (act) {
+      q = (p & ~63u) + wave_key_rank(key);
+    }
   }
   if ((flags & (F_EXT | F_SHADOW | F_SHADOW2)) == 0) return SLOT_FREE;
   const uint32_t P = __float_as_uint(s1.w);
@@ -767,9 +816,9 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     new_sh[s] = false;
     shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
   }
-  int state = SLOT_LIVE;
+  __shared__ uint32_t s_kc[SORT_KEYS + 1][4];
   uint32_t q = p;  // where this lane's path state and new rays go
-  if (p < S.N) state = shade_slot<NSH, REFA>(S, p, q, new_ext, ext, new_sh, shr);
+  int state = shade_slot<NSH, REFA>(S, p, p < S.N, q, new_ext, ext, new_sh, shr, s_kc);
   // ---- regeneration: free slots take the next paths in rank order, from the
   // current block and then from a newly claimed one
   const bool fr = p < S.N && state != SLOT_LIVE;
