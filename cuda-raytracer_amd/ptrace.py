@@ -523,3 +523,53 @@ def write_pfm(path, img):
     rc = LIB.pt_write_pfm(str(path).encode(), _ptr(img, C.c_float), img.shape[1], img.shape[0])
     if rc != PT_OK:
         raise PTError(rc, f"pt_write_pfm {path}")
+
+
+# ---- the Scotty3D surface on the GPU (scotty/scotty_capi.cpp) ----------------
+SCOTTY_LIB_PATH = LIB_PATH.parent / "libscotty_gpu.so"
+_SCOTTY = None
+
+
+def _scotty():
+    global _SCOTTY
+    if _SCOTTY is None:
+        if not SCOTTY_LIB_PATH.exists():
+            raise ImportError(f"libscotty_gpu.so not built ({SCOTTY_LIB_PATH}); run __graft_entry__.build()")
+        lib = C.CDLL(str(SCOTTY_LIB_PATH))
+        P, I32, U32, SZ, F = C.c_void_p, C.c_int32, C.c_uint32, C.c_size_t, C.POINTER(C.c_float)
+        lib.scotty_render.restype = C.c_int
+        lib.scotty_render.argtypes = [C.POINTER(pt_scene_desc), I32, I32, I32, I32, U32, I32, I32, F, C.c_char_p, SZ]
+        lib.scotty_viewer.restype = C.c_int
+        lib.scotty_viewer.argtypes = [C.POINTER(pt_scene_desc), I32, I32, I32, I32, U32, C.c_char_p, I32, F,
+                                      C.POINTER(I32), C.c_char_p, SZ]
+        _SCOTTY = lib
+    return _SCOTTY
+
+
+def scotty_render(scene, width, height, spp, max_depth, flags=0, threads=0, device=0):
+    """CMU462::PathTracer on the GPU: start_raytracing's 32x32 tile queue and
+    `threads` workers (0 = hardware_concurrency) over one pt_render; the
+    (H, W, 4) frame."""
+    out = np.zeros((height, width, 4), dtype=np.float32)
+    err = C.create_string_buffer(512)
+    d = scene.desc()
+    rc = _scotty().scotty_render(C.byref(d), width, height, spp, max_depth, flags, threads, device,
+                                 _ptr(out, C.c_float), err, len(err))
+    if rc:
+        raise PTError(rc, err.value.decode(errors="replace"))
+    return out
+
+
+def scotty_viewer(scene, width, height, samples_per_frame, keys, max_bounces=2, flags=0, device=0):
+    """The display.cpp viewer loop, headless: one renderPicture per character
+    of `keys` after handleKeyPress(c) ('.' = no key).  Returns (the last
+    displayed frame, samples accumulated in it)."""
+    out = np.zeros((height, width, 4), dtype=np.float32)
+    err = C.create_string_buffer(512)
+    n = C.c_int32()
+    d = scene.desc()
+    rc = _scotty().scotty_viewer(C.byref(d), width, height, samples_per_frame, max_bounces, flags,
+                                 keys.encode(), device, _ptr(out, C.c_float), C.byref(n), err, len(err))
+    if rc:
+        raise PTError(rc, err.value.decode(errors="replace"))
+    return out, n.value

@@ -12,6 +12,9 @@
 //                            src/pathtracer.h:51-179, pathtracer.cpp:183-213,
 //                            499-558, src/work_queue.h  -> scotty::PathTracerT /
 //                                                           scotty::PathTracer
+//   the progressive viewer loop  src/display.cpp:99-190 (key handler, renderPicture)
+//     + CudaRenderer::renderAccumulate / setViewpoint, cu:1845-1870, 2419-2457
+//                                                        -> scotty::Viewer
 // Everything is plain C++17 on top of include/pt_api.h; no HIP types here.
 // Errors throw scotty::Error carrying the pt_* code and message (the
 // reference printf()s and exit()s instead).
@@ -67,7 +70,12 @@ class Scene {
     if (rc) throw Error(rc, std::string("loadScene: ") + err);
     pt_scene_get_desc(s_, &d_);
   }
-  ~Scene() { pt_scene_free(s_); }
+  // a flattened scene the caller owns (must outlive this object): e.g. a
+  // pt_scene_from_mesh result or a host array scene
+  explicit Scene(const pt_scene_desc& d) : d_(d) {}
+  ~Scene() {
+    if (s_) pt_scene_free(s_);
+  }
   Scene(const Scene&) = delete;
   Scene& operator=(const Scene&) = delete;
   const pt_scene_desc& desc() const { return d_; }
@@ -199,6 +207,10 @@ class CudaRenderer {
     scene_ = std::make_unique<Scene>(path);
     camera_ = Camera(scene_->desc().camera);
   }
+  void loadScene(const pt_scene_desc& desc) {  // an already flattened scene
+    scene_ = std::make_unique<Scene>(desc);
+    camera_ = Camera(desc.camera);
+  }
   void setup() { dev_.check(pt_load_scene(dev_.get(), &scene_->desc()), "pt_load_scene"); }  // cu:1872
   // one progressive frame of spp samples (renderAccumulate, cu:2419-2457)
   void render(int spp = 2, int max_bounces = 2, uint32_t flags = 0) {
@@ -225,7 +237,9 @@ class CudaRenderer {
     dev_.check(pt_get_image(dev_.get(), image_.data.data(), image_.data.size()), "pt_get_image");
     return &image_;
   }
-  void setViewpoint(const Vector3D& origin, const Vector3D& lookAt) {  // cu:1845
+  // cu:1845-1870: new origin and look-at (float, as v2f3), left/up kept,
+  // accumulation cleared
+  void setViewpoint(const Vector3D& origin, const Vector3D& lookAt) {
     pt_camera c = camera_.params();
     c.origin[0] = (float)origin.x;
     c.origin[1] = (float)origin.y;
@@ -302,6 +316,10 @@ class GpuEstimator {
   explicit GpuEstimator(int device = 0) : r_(device) {}
   void set_scene(const std::string& dae_path) {
     r_.loadScene(dae_path);
+    r_.setup();
+  }
+  void set_scene(const pt_scene_desc& desc) {
+    r_.loadScene(desc);
     r_.setup();
   }
   void begin(size_t w, size_t h, size_t spp, size_t max_depth, uint32_t flags) {
@@ -434,8 +452,82 @@ class PathTracer : private GpuEstimator, public PathTracerT<GpuEstimator> {
         PathTracerT<GpuEstimator>(*static_cast<GpuEstimator*>(this), ns_aa, max_ray_depth, ns_area_light, ns_diff,
                                   ns_glsy, ns_refr, num_threads) {}
   void set_scene(const std::string& dae_path) { GpuEstimator::set_scene(dae_path); }
+  void set_scene(const pt_scene_desc& desc) { GpuEstimator::set_scene(desc); }
   void set_camera(const Camera&) {}  // the scene's camera is used (cu:1590-1607)
   CudaRenderer& renderer() { return GpuEstimator::renderer(); }
+};
+
+// ---- the progressive viewer (display.cpp:99-190 without the GLUT window) -----
+// Each displayed frame is renderPicture(): unless paused, one more
+// renderAccumulate of samples_per_frame samples on top of the accumulation
+// (sample indices continue: sample_offset), then the display image (median
+// filtered below 32 accumulated samples, cu:1539-1569).  handleKeyPress moves
+// the camera like the reference's w/a/s/d keys (origin += (0, 0, -+0.01) /
+// (-+0.01, 0, 0) in double, then setViewpoint: the accumulation restarts), p
+// toggles pause, + resumes.  A GUI would call these from its event loop; the
+// headless loop drives them from a key script (ptrender --viewer).
+class Viewer {
+ public:
+  Viewer(CudaRenderer& r, int samples_per_frame = 2, int max_bounces = 2, uint32_t flags = 0)
+      : r_(r), spf_(samples_per_frame), bounces_(max_bounces), flags_(flags) {
+    const pt_camera& c = r_.camera().params();
+    origin_ = Vector3D(c.origin[0], c.origin[1], c.origin[2]);
+    look_at_ = Vector3D(c.look_at[0], c.look_at[1], c.look_at[2]);
+  }
+  // display.cpp:99-139 handleKeyPress (q/Q is the caller's to handle)
+  void handleKeyPress(char key) {
+    switch (key) {
+      case '=':
+      case '+':
+        update_ = true;
+        break;
+      case 'p':
+      case 'P':
+        paused_ = !paused_;
+        if (!paused_) update_ = true;
+        break;
+      case 'w':
+      case 'W':
+        move(0, 0, -0.01);
+        break;
+      case 's':
+      case 'S':
+        move(0, 0, 0.01);
+        break;
+      case 'a':
+      case 'A':
+        move(-0.01, 0, 0);
+        break;
+      case 'd':
+      case 'D':
+        move(0.01, 0, 0);
+        break;
+      default:
+        break;
+    }
+  }
+  // display.cpp:145-190 renderPicture: returns the frame to display
+  const Image* renderPicture() {
+    if (!paused_) r_.render(spf_, bounces_, flags_);
+    if (paused_) update_ = false;
+    ++frames_;
+    return r_.getImage();
+  }
+  bool paused() const { return paused_; }
+  int frames() const { return frames_; }
+  const Vector3D& origin() const { return origin_; }
+
+ private:
+  void move(double dx, double dy, double dz) {
+    origin_ = Vector3D(origin_.x + dx, origin_.y + dy, origin_.z + dz);
+    r_.setViewpoint(origin_, look_at_);
+  }
+  CudaRenderer& r_;
+  int spf_, bounces_;
+  uint32_t flags_;
+  Vector3D origin_, look_at_;
+  bool paused_ = false, update_ = true;
+  int frames_ = 0;
 };
 
 }  // namespace scotty

@@ -50,3 +50,18 @@ def test_from_triangles_builds_bvh():
         assert 0 <= nd.prim_start and nd.prim_start + nd.prim_count <= 500
         for c in nd.child:
             assert c == -1 or c > i
+
+
+def test_scotty_surface_library_exports():
+    """The Scotty3D surface's C entry points (scotty/scotty_capi.cpp) load;
+    without a GPU they report the device error through the return code."""
+    lib = ptrace._scotty()
+    assert hasattr(lib, "scotty_render") and hasattr(lib, "scotty_viewer")
+    if have_gpu():
+        return
+    scene = ptrace.ArrayScene.load(ROOT / "tests" / "golden" / "scenes" / "CBempty.npz")
+    with pytest.raises(ptrace.PTError) as e:
+        ptrace.scotty_render(scene, 8, 8, 1, 2, threads=2)
+    assert e.value.code in (ptrace.PT_E_NODEVICE, ptrace.PT_E_HIP)
+    with pytest.raises(ptrace.PTError):
+        ptrace.scotty_viewer(scene, 8, 8, 1, "..")
