@@ -340,6 +340,9 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 //     here (the callers write the empty r1 of invalid slots);
 //  3. a shadow ray (anyhit) occluded by an inline leaf is done: not queued;
 //     the others are pushed into the targets' queues with the tightened tmax.
+#ifndef PT_ROOT_EXT_PRETEST
+#define PT_ROOT_EXT_PRETEST 0
+#endif
 template <int R, bool REFA = false>
 __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T, int lane, const uint32_t (&id)[R],
                                           const f3 (&o)[R], const f3 (&d)[R], const float (&tmax)[R],
@@ -378,6 +381,12 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
           else if (anyhit[j]) {
             // shadow rays: division-free pre-test (they mostly point away from
             // the walls or end before them, see tri_outside)
+            const float4 q3 = f4(P[3]);
+            const float ndd = fdot(q3.x, q3.y, q3.z, d[j].x, d[j].y, d[j].z);
+            const float num = q1.w - fdot(q3.x, q3.y, q3.z, o[j].x, o[j].y, o[j].z);
+            tt = -1.0f;
+            if (!tri_outside(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), bt);
+          } else if (PT_ROOT_EXT_PRETEST) {
             const float4 q3 = f4(P[3]);
             const float ndd = fdot(q3.x, q3.y, q3.z, d[j].x, d[j].y, d[j].z);
             const float num = q1.w - fdot(q3.x, q3.y, q3.z, o[j].x, o[j].y, o[j].z);
