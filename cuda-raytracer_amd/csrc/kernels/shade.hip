@@ -537,7 +537,7 @@ constexpr int SLOT_FREE = 0, SLOT_LIVE = 1, SLOT_ENDED = 2;
 // within its wave; results do not depend on it (a permutation of the wave's
 // slots, read before any is written).
 #ifndef PT_SORT_WAVE
-#define PT_SORT_WAVE 1
+#define PT_SORT_WAVE 3
 #endif
 #ifndef PT_SORT_KEY_BITS
 #define PT_SORT_KEY_BITS 4
@@ -554,6 +554,44 @@ __device__ __forceinline__ uint32_t wave_key_rank(uint32_t key) {
     base += (uint32_t)__popcll(m);
   }
   return rank;
+}
+// PT_SORT_WAVE 3: the key is taken after shading -- the hit primitive's range
+// and the octant of the new extension ray's direction (PT_SORT_DIR) -- and
+// ranked through a per-wave LDS histogram (one LDS atomic per lane, a 64-lane
+// scan over the bins) instead of one ballot per key.  The order of lanes with
+// equal keys is the order the LDS serves the atomics in; results do not
+// depend on slots.
+#ifndef PT_SORT_DIR
+#define PT_SORT_DIR 0
+#endif
+constexpr uint32_t HIST_BINS = 256;  // >= SORT_KEYS * 8 + 1
+__device__ __forceinline__ uint32_t wave_hist_rank(uint32_t key, bool act, uint32_t* bins) {
+  const uint32_t ln = lane_id();
+#pragma unroll
+  for (uint32_t i = 0; i < HIST_BINS / 64; ++i) bins[ln * (HIST_BINS / 64) + i] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const uint32_t r = act ? atomicAdd(bins + key, 1u) : 0u;
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  uint32_t c[HIST_BINS / 64], tot = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < HIST_BINS / 64; ++i) {
+    c[i] = bins[ln * (HIST_BINS / 64) + i];
+    tot += c[i];
+  }
+  uint32_t inc = tot;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t v = __shfl_up(inc, off, 64);
+    if ((int)ln >= off) inc += v;
+  }
+  uint32_t b = inc - tot;
+#pragma unroll
+  for (uint32_t i = 0; i < HIST_BINS / 64; ++i) {
+    bins[ln * (HIST_BINS / 64) + i] = b;
+    b += c[i];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  return act ? bins[key] + r : 0u;
 }
 // The same over the whole workgroup (PT_SORT_WAVE 2): rank among the
 // workgroup's lanes with act set, ordered by (key, wave, lane).  Every thread
@@ -605,7 +643,8 @@ __device__ __forceinline__ uint32_t block_key_rank(uint32_t key, bool act, uint3
 // (p < N).  kc: LDS for block_key_rank.
 template <int NSH, bool REFA = false>
 __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool act, uint32_t& q, bool& new_ext,
-                                          RayV& ext, bool (&new_sh)[NSH], RayV (&shr)[NSH], uint32_t (*kc)[4]) {
+                                          RayV& ext, bool (&new_sh)[NSH], RayV (&shr)[NSH], uint32_t (*kc)[4],
+                                          uint32_t* bins) {
   new_ext = false;
 #pragma unroll
   for (int s = 0; s < NSH; ++s) new_sh[s] = false;
@@ -630,7 +669,7 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
 #pragma unroll
   for (int s = 0; s < NSH; ++s) asm volatile("" ::"v"(hs[s].z), "v"(cs[s].x));
   const uint32_t flags = act ? __float_as_uint(s0.w) : 0u;
-  if constexpr (PT_SORT_WAVE != 0) {
+  if constexpr (PT_SORT_WAVE == 1 || PT_SORT_WAVE == 2) {
     // (every load above has completed -- the asm uses -- before any thread
     // passes the rank's barriers and writes slots other threads read)
     const uint32_t hp = __float_as_uint(r1.z);
@@ -643,26 +682,40 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
       q = (p & ~63u) + wave_key_rank(key);
     }
   }
-  if ((flags & (F_EXT | F_SHADOW | F_SHADOW2)) == 0) return SLOT_FREE;
+  const bool live = (flags & (F_EXT | F_SHADOW | F_SHADOW2)) != 0;
+  if (PT_SORT_WAVE != 3 && !live) return SLOT_FREE;
   const uint32_t P = __float_as_uint(s1.w);
   PathState st{xyz(s0), flags, xyz(s1), 0u};
-  uint32_t sidx;
-  path_pixel(S, P, st.g, sidx);
-  bool clear[NSH];
-  f3 C[NSH];
-#pragma unroll
-  for (int s = 0; s < NSH; ++s) {
-    clear[s] = (flags & sh_bit(s)) && __float_as_uint(hs[s].z) == PT_PRIM_NONE;
-    C[s] = clear[s] ? xyz(cs[s]) : mk(0, 0, 0);
-  }
   const bool ext_hit = (flags & F_EXT) && __float_as_uint(r1.z) != PT_PRIM_NONE;
   const uint32_t prim = (flags & F_EXT) ? __float_as_uint(r1.z) : PT_PRIM_NONE;
-  const float t = ext_hit ? r1.w : 0.0f;
-  const f3 o = ext_hit ? xyz(r0) : mk(0, 0, 0), d = ext_hit ? mk(r0.w, r1.x, r1.y) : mk(0, 0, 1);
-  shade_vertex<NSH, false, false, REFA>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
-  // (vertices done = vtx - 1: the last one resolves shadow rays only)
-  const bool ended =
-      !(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || ((st.flags >> 8) & 0xffu) - 1u >= (uint32_t)S.passes;
+  bool ended = true;
+  f3 C[NSH];
+  if (live) {
+    uint32_t sidx;
+    path_pixel(S, P, st.g, sidx);
+    bool clear[NSH];
+#pragma unroll
+    for (int s = 0; s < NSH; ++s) {
+      clear[s] = (flags & sh_bit(s)) && __float_as_uint(hs[s].z) == PT_PRIM_NONE;
+      C[s] = clear[s] ? xyz(cs[s]) : mk(0, 0, 0);
+    }
+    const float t = ext_hit ? r1.w : 0.0f;
+    const f3 o = ext_hit ? xyz(r0) : mk(0, 0, 0), d = ext_hit ? mk(r0.w, r1.x, r1.y) : mk(0, 0, 1);
+    shade_vertex<NSH, false, false, REFA>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
+    // (vertices done = vtx - 1: the last one resolves shadow rays only)
+    ended = !(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || ((st.flags >> 8) & 0xffu) - 1u >= (uint32_t)S.passes;
+  }
+  if constexpr (PT_SORT_WAVE == 3) {  // (every lane of the wave: uniform control flow here)
+    uint32_t key = HIST_BINS - 1;
+    if (live && !ended && new_ext && ext_hit) {
+      key = min(prim >> S.kshift, SORT_KEYS - 1u);
+      if (PT_SORT_DIR)
+        key = (key << 3) | (ext.d.x < 0.0f ? 1u : 0u) | (ext.d.y < 0.0f ? 2u : 0u) | (ext.d.z < 0.0f ? 4u : 0u);
+    }
+    const uint32_t r = wave_hist_rank(key, act, bins);
+    if (act) q = (q & ~63u) + r;
+    if (!live) return SLOT_FREE;
+  }
   if (ended) {
     new_ext = false;
 #pragma unroll
@@ -817,8 +870,10 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
   }
   __shared__ uint32_t s_kc[SORT_KEYS + 1][4];
+  __shared__ uint32_t s_bins[PT_SORT_WAVE == 3 ? 4 * HIST_BINS : 1];
   uint32_t q = p;  // where this lane's path state and new rays go
-  int state = shade_slot<NSH, REFA>(S, p, p < S.N, q, new_ext, ext, new_sh, shr, s_kc);
+  int state = shade_slot<NSH, REFA>(S, p, p < S.N, q, new_ext, ext, new_sh, shr, s_kc,
+                                    s_bins + (PT_SORT_WAVE == 3 ? wave * HIST_BINS : 0));
   // ---- regeneration: free slots take the next paths in rank order, from the
   // current block and then from a newly claimed one
   const bool fr = p < S.N && state != SLOT_LIVE;
@@ -1101,7 +1156,13 @@ __device__ __forceinline__ bool path_grab(uint32_t lo, uint32_t hi, uint32_t tai
 constexpr uint32_t PT_TIMING_WAVES = 16384;
 static __device__ unsigned long long g_path_timing[PT_TIMING_WAVES * 8];
 #endif
-template <int NSH, bool REFA>
+// GUIDED: the guided grabs above; otherwise every grab is PATH_CHUNK paths
+// from one counter (work[0]).  The guided schedule's bookkeeping costs SGPRs
+// (52 spilled instead of 30) and a whole 1024^2 x 256 spp CBempty frame 2.6 %
+// (35.9 -> 36.8 ms), while it shortens the tail of small chunks (a 1/8 share:
+// 5.05 -> 4.89 ms): the host takes it only when the chunk is small against the
+// resident lanes (PT_PATH_GUIDED_BELOW paths per lane, default 128).
+template <int NSH, bool REFA, bool GUIDED>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
     uint32_t* __restrict__ work, uint32_t nreg, uint32_t tail_unit) {
@@ -1140,6 +1201,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       const unsigned long long tg = wall_clock64();
 #endif
       uint32_t b = 0, e = 0;
+      if constexpr (!GUIDED) {
+        if (lid == 0) b = atomicAdd(work, PATH_CHUNK);
+        b = __builtin_amdgcn_readfirstlane(b);
+        drained = b >= S.N;
+        next = drained ? 0u : b;
+        end = drained ? 0u : min(b + PATH_CHUNK, S.N);
+      } else {
       if (lid == 0) {
         while (tried < nreg) {
           const uint32_t k = atomicAdd(work + reg * PATH_CTR_STRIDE, 1u);
@@ -1157,6 +1225,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       drained = tried >= nreg;
       next = drained ? 0u : b;
       end = drained ? 0u : e;
+      }
 #if PT_PATH_TIMING
       const unsigned long long dt = wall_clock64() - tg;
       tm_grab += dt;

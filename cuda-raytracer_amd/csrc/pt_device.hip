@@ -108,6 +108,7 @@ struct pt_ctx {
   int path_grid[4] = {0, 0, 0, 0};  // resident workgroups of k_path_leaf<1|2, refa>
   int path_guide = 4;               // k_path_leaf grab schedule (path_grab; PT_PATH_GUIDE)
   int path_regions = 8;             // k_path_leaf path regions / counters (PT_PATH_REGIONS)
+  int path_guided_below = 128;      // guided grabs below this many paths per resident lane (PT_PATH_GUIDED_BELOW)
 
   // framebuffer
   int fb_w = 0, fb_h = 0, fb_tile = 0, fb_rank = 0, fb_nranks = 0;
@@ -663,6 +664,7 @@ int pt_create(pt_ctx** out, int device) {
   if (const char* q = getenv("PT_QFACTOR")) c->qfactor = std::max(1, atoi(q));
   if (const char* q = getenv("PT_PATH_GUIDE")) c->path_guide = std::max(0, atoi(q));
   if (const char* q = getenv("PT_PATH_REGIONS")) c->path_regions = std::max(1, atoi(q));
+  if (const char* q = getenv("PT_PATH_GUIDED_BELOW")) c->path_guided_below = std::max(0, atoi(q));
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return PT_E_HIP;
@@ -685,10 +687,10 @@ int pt_create(pt_ctx** out, int device) {
   {
     int ncu = 0, nb[4] = {0, 0, 0, 0};
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[0], k_path_leaf<1, false>, TPB, 0);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[1], k_path_leaf<2, false>, TPB, 0);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[2], k_path_leaf<1, true>, TPB, 0);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[3], k_path_leaf<2, true>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[0], k_path_leaf<1, false, true>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[1], k_path_leaf<2, false, true>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[2], k_path_leaf<1, true, true>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[3], k_path_leaf<2, true, true>, TPB, 0);
     for (int i = 0; i < 4; ++i) c->path_grid[i] = std::max(1, ncu * std::max(1, nb[i]));
   }
   *out = c;
@@ -937,9 +939,13 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       S.N = M;
       const uint32_t want = (M + 4 * PATH_CHUNK - 1) / (4 * PATH_CHUNK);
       const int kv = (nsh == 2 ? 1 : 0) + (c->refa ? 2 : 0);
-      auto kpath = kv == 0 ? k_path_leaf<1, false> : kv == 1 ? k_path_leaf<2, false>
-                 : kv == 2 ? k_path_leaf<1, true> : k_path_leaf<2, true>;
       const uint32_t blocks = std::min<uint32_t>(want, c->path_grid[kv]);
+      // guided grabs only for chunks that are small against the resident lanes
+      const bool guided = (uint64_t)M < (uint64_t)c->path_guided_below * blocks * TPB;
+      auto kpath = guided ? (kv == 0 ? k_path_leaf<1, false, true> : kv == 1 ? k_path_leaf<2, false, true>
+                             : kv == 2 ? k_path_leaf<1, true, true> : k_path_leaf<2, true, true>)
+                          : (kv == 0 ? k_path_leaf<1, false, false> : kv == 1 ? k_path_leaf<2, false, false>
+                             : kv == 2 ? k_path_leaf<1, true, false> : k_path_leaf<2, true, false>);
       // guided grabs from nreg path regions (k_path_leaf path_grab): each
       // region's tail phases begin path_guide chunks per wave before its end
       const uint32_t nreg = (uint32_t)std::max(1, std::min<int>(c->path_regions, (int)std::min<uint32_t>(blocks, PATH_REGIONS_MAX)));
