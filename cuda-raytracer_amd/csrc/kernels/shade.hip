@@ -1102,7 +1102,8 @@ constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 #define PT_PATH_LDS_SH 1
 #endif
 // (PT_PATH_LIGHT_RELOAD reads the light from the kernel-argument segment at
-// offsetof(ShadeArgs, light): S must stay this kernel's FIRST parameter)
+// offsetof(ShadeArgs, light): S must stay this kernel's FIRST parameter; a
+// -DPT_DBG_BOUNDS build checks it at run time)
 // Guided path grabs: the k-th grab from the counter takes the range
 // [S[j] + (k - G[j]) c[j], ...) of the phase j with G[j] <= k < G[j+1]; the
 // chunk size halves as the unstarted paths run out (512 down to 64), so no
@@ -1167,6 +1168,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
     uint32_t* __restrict__ work, uint32_t nreg, uint32_t tail_unit) {
   const uint32_t lid = lane_id();
+#ifdef PT_DBG_BOUNDS
+  // light_of<true> reads the light at offsetof(ShadeArgs, light) of the
+  // kernel-argument segment: S must be this kernel's first parameter
+  if (PT_PATH_LIGHT_RELOAD) {
+    const pt_light a = light_of<true>(S), b = S.light;
+    uint32_t wa[sizeof a / 4], wb[sizeof b / 4];
+    __builtin_memcpy(wa, &a, sizeof a);
+    __builtin_memcpy(wb, &b, sizeof b);
+    bool same = true;
+#pragma unroll
+    for (uint32_t i = 0; i < sizeof a / 4; ++i) same = same && wa[i] == wb[i];
+    if (!same && blockIdx.x == 0 && threadIdx.x == 0) printf("PT_DBG_BOUNDS k_path_leaf: ShadeArgs is not at kernarg 0\n");
+  }
+#endif
   uint32_t nrays = 0;
   // wave-uniform: the path region this wave grabs from (its workgroup's, then
   // the next ones as they run out) and how many regions it has found empty
