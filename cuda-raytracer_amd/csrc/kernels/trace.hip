@@ -707,6 +707,9 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
   }
 }
 
+#ifndef PT_LEAF_PAIR
+#define PT_LEAF_PAIR 0
+#endif
 template <bool REFA = false, bool LEAF = false>
 __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane, bool ids,
                                              bool out_ids, bool two_level) {
@@ -738,6 +741,52 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
       bp[j] = -1;
     }
     const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);
+    // one primitive's tests against the wave's rays (its record in SGPRs)
+    auto test_prim = [&](int k, const float4& q0, const float4& q1, const float4& q2, const float4& q3,
+                         const float4& q4, const float4& q5) {
+      if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
+#pragma unroll
+        for (int j = 0; j < RPTW; ++j) {
+          if (j >= nj) break;
+          float t = sphere_test(o[j], d[j], q0, q1);
+          if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
+            bt[j] = t;
+            bp[j] = pstart + k;
+          }
+        }
+      } else {
+        const f3x2 N = sp3(q3.x, q3.y, q3.z), v0 = sp3(q0.x, q0.y, q0.z), v1 = sp3(q1.x, q1.y, q1.z),
+                   v2 = sp3(q2.x, q2.y, q2.z), e0 = sp3(q2.w, q3.w, q4.w), e1 = sp3(q4.x, q4.y, q4.z),
+                   e2 = sp3(q5.x, q5.y, q5.z);  // edge normals m0, m1, m2
+#pragma unroll
+        for (int j = 0; j < RPTW; j += 2) {
+          if (j >= nj) break;
+          const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
+                                         e2, f2v{bt[j], bt[j + 1]});
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const float t = t2[i];
+            if (valid[j + i] && t >= 0.0f && (t < bt[j + i] || (t == bt[j + i] && bp[j + i] < 0))) {
+              bt[j + i] = t;
+              bp[j + i] = pstart + k;
+            }
+          }
+        }
+      }
+    };
+    if constexpr (LEAF && PT_LEAF_PAIR) {
+      // two records per scalar round trip (leaf records come from L2, not the
+      // scalar cache: the round trip, not the tests, bounds a leaf visit)
+      for (int k = 0; k < pcount; k += 2, P += 12) {
+        const CPTR(f4v) P2 = k + 1 < pcount ? P + 6 : P;  // (uniform; an odd tail reloads the last record)
+        const float4 q0 = f4(P[0]), q1 = f4(P[1]), q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
+        const float4 u0 = f4(P2[0]), u1 = f4(P2[1]), u2 = f4(P2[2]), u3 = f4(P2[3]), u4 = f4(P2[4]), u5 = f4(P2[5]);
+        asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q2.x), "s"(q3.x), "s"(q4.x), "s"(q5.x));
+        asm volatile("" ::"s"(u0.w), "s"(u1.x), "s"(u2.x), "s"(u3.x), "s"(u4.x), "s"(u5.x));
+        test_prim(k, q0, q1, q2, q3, q4, q5);
+        if (k + 1 < pcount) test_prim(k + 1, u0, u1, u2, u3, u4, u5);
+      }
+    } else
     for (int k = 0; k < pcount; ++k, P += 6) {
       const float4 q0 = f4(P[0]), q1 = f4(P[1]);
       if constexpr (LEAF || PT_SHARED_LEAF_LOAD1) {
