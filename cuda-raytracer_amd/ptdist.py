@@ -53,8 +53,10 @@ def local_sums_tensor(ctx, device, out=None):
         buf = out[:n]
     else:
         buf = torch.empty((n, 4), dtype=torch.float32, device=device)
-        if buf.device.type != "cpu":
-            torch.cuda.synchronize(buf.device)  # (the allocation is ordered on torch's stream)
+    if buf.device.type != "cpu":
+        # the copy runs on the context's stream: torch's stream must be done
+        # with the buffer (its allocation, or the last frame's gather copy)
+        torch.cuda.synchronize(buf.device)
     if n:
         ctx.copy_owned_sums(buf.data_ptr(), n * 16, on_device=buf.device.type != "cpu")
     return buf
