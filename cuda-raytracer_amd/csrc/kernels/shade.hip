@@ -516,6 +516,30 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
   ext.tmax = __builtin_inff();
 }
 
+// A finished path's radiance in the chunk's result buffer: 12 B per path
+// (PT_RES12; the buffer is read once more by k_accum, 16 B per path -> 12 B is
+// a quarter of that stream), else a float4.
+#ifndef PT_RES12
+#define PT_RES12 1
+#endif
+struct res3 {
+  float x, y, z;
+};
+__device__ __forceinline__ void put_res(float4* res, uint32_t P, const f3 L) {
+  if (PT_RES12)
+    reinterpret_cast<res3*>(res)[P] = res3{L.x, L.y, L.z};
+  else
+    res[P] = make_float4(L.x, L.y, L.z, 0.0f);
+}
+__device__ __forceinline__ f3 get_res(const float4* res, size_t P) {
+  if (PT_RES12) {
+    const res3 r = reinterpret_cast<const res3*>(res)[P];
+    return mk(r.x, r.y, r.z);
+  }
+  const float4 r = res[P];
+  return mk(r.x, r.y, r.z);
+}
+
 // Pixel and sample of path P of the chunk.
 __device__ __forceinline__ void path_pixel(const ShadeArgs& S, uint32_t P, uint32_t& g, uint32_t& sidx) {
   const uint32_t j = udiv_q(P, S.div_npix);
@@ -720,7 +744,7 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
     new_ext = false;
 #pragma unroll
     for (int s = 0; s < NSH; ++s) new_sh[s] = false;
-    S.res[P] = make_float4(st.L.x, st.L.y, st.L.z, 0.0f);
+    put_res(S.res, P, st.L);
     // (the caller frees the slot -- ps0 flags 0 -- unless it starts a new path)
   } else {
     S.ps0[q] = make_float4(st.T.x, st.T.y, st.T.z, __uint_as_float(st.flags));
@@ -1319,7 +1343,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       const uint32_t done = ((st.flags >> 8) & 0xffu) - 1u;
       if (!(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || done >= (uint32_t)passes) {
         if constexpr (PT_PATH_LDS_SH) st.L = mk(Lq[0], Lq[TPB], Lq[2 * TPB]);
-        S.ps1[p] = make_float4(st.L.x, st.L.y, st.L.z, __uint_as_float(st.g));
+        put_res(S.ps1, p, st.L);
         active = false;
       }
     }
@@ -1352,7 +1376,7 @@ __global__ __launch_bounds__(TPB) void k_accum(const float4* __restrict__ ps1, f
   if (q >= npix) return;
   float4 a = accum[q];
   for (uint32_t j = 0; j < spp_b; ++j) {
-    const float4 l = ps1[(size_t)j * npix + q];
+    const f3 l = get_res(ps1, (size_t)j * npix + q);
     a.x = a.x + l.x;
     a.y = a.y + l.y;
     a.z = a.z + l.z;
