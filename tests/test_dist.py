@@ -57,3 +57,36 @@ def test_owned_pixels_partition():
     W, H, tile = 100, 37, 16
     seen = np.concatenate([ptdist.owned_pixels(W, H, tile, r, 5) for r in range(5)])
     assert sorted(seen.tolist()) == list(range(W * H))
+
+
+def _worker_frames(rank, world, port, out_path):
+    """Two frames through the cached gather layout: the second frame's result
+    must not keep anything of the first (reused send / receive buffers)."""
+    import sys
+    sys.path[:0] = [str(ROOT / "cuda-raytracer_amd")]
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    W, H, tile = 37, 29, 8
+    frames = []
+    for f in range(2):
+        idx = ptdist.owned_pixels(W, H, tile, rank, world)
+        vals = (idx.astype(np.float32) + 1000.0 * f)[:, None] * np.array([1, 2, 3, 4], np.float32)
+        frame = ptdist.gather_frame(torch.from_numpy(vals), W, H, tile, spp=2)
+        if rank == 0:
+            frames.append(frame.numpy().copy())
+    if rank == 0:
+        np.save(out_path, np.stack(frames))
+    dist.destroy_process_group()
+
+
+def test_gather_layout_reused_across_frames(tmp_path):
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_worker_frames, args=(3, _free_port(), out), nprocs=3, join=True)
+    frames = np.load(out)
+    pix = np.arange(37 * 29, dtype=np.float32).reshape(29, 37)
+    for f in range(2):
+        v = pix + 1000.0 * f
+        assert np.array_equal(frames[f][..., 0], v / 2)
+        assert np.array_equal(frames[f][..., 2], 3 * v / 2)
+        assert np.all(frames[f][..., 3] == 1.0)
