@@ -547,6 +547,11 @@ __device__ __forceinline__ void path_pixel(const ShadeArgs& S, uint32_t P, uint3
   sidx = S.sample_base + j;
 }
 
+// Philox products as v_mad_u64_u32 in the wavefront shade kernel too (the
+// same bits; k_path_leaf uses them, PT_PATH_MAD64)
+#ifndef PT_SHADE_MAD64
+#define PT_SHADE_MAD64 true
+#endif
 // Slot states returned by shade_slot
 constexpr int SLOT_FREE = 0, SLOT_LIVE = 1, SLOT_ENDED = 2;
 
@@ -725,7 +730,7 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
     }
     const float t = ext_hit ? r1.w : 0.0f;
     const f3 o = ext_hit ? xyz(r0) : mk(0, 0, 0), d = ext_hit ? mk(r0.w, r1.x, r1.y) : mk(0, 0, 1);
-    shade_vertex<NSH, false, false, REFA>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
+    shade_vertex<NSH, PT_SHADE_MAD64, false, REFA>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
     // (vertices done = vtx - 1: the last one resolves shadow rays only)
     ended = !(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || ((st.flags >> 8) & 0xffu) - 1u >= (uint32_t)S.passes;
   }
@@ -941,7 +946,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   if ((uint32_t)tid < ns) {
     const uint32_t P = (uint32_t)tid < t1 ? next + (uint32_t)tid : s_nb + (uint32_t)tid - t1;
     uint32_t g;
-    const f3 dir = camera_dir<false, REFA>(S, P, g);
+    const f3 dir = camera_dir<PT_SHADE_MAD64, REFA>(S, P, g);
     s_dir[0][tid] = dir.x;
     s_dir[1][tid] = dir.y;
     s_dir[2][tid] = dir.z;
