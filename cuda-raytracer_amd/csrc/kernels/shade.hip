@@ -69,6 +69,10 @@ struct ShadeArgs {
   int passes;         // vertices per path at most (max_bounces + 2)
   unsigned long long* rcount;    // rays entering the traversal (RCOUNT_SLOTS counters)
   uint32_t kshift;    // record-order key of a path: its hit primitive >> kshift (PT_SORT_WAVE)
+  // PT_SORT_KMAP: the key is kmap[hit primitive >> kmshift] instead, the root
+  // target whose subtree holds the primitive (KMAP_SIZE entries)
+  const uint32_t* __restrict__ kmap;
+  uint32_t kmshift;
 };
 
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -593,7 +597,10 @@ __device__ __forceinline__ uint32_t wave_key_rank(uint32_t key) {
 #ifndef PT_SORT_DIR
 #define PT_SORT_DIR 0
 #endif
-constexpr uint32_t HIST_BINS = 256;  // >= SORT_KEYS * 8 + 1
+constexpr uint32_t HIST_BINS = 256;  // >= SORT_KEYS * 8 + 1 (and > KMAP keys)
+#ifndef PT_SORT_KMAP
+#define PT_SORT_KMAP 0
+#endif
 __device__ __forceinline__ uint32_t wave_hist_rank(uint32_t key, bool act, uint32_t* bins) {
   const uint32_t ln = lane_id();
 #pragma unroll
@@ -737,7 +744,7 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
   if constexpr (PT_SORT_WAVE == 3) {  // (every lane of the wave: uniform control flow here)
     uint32_t key = HIST_BINS - 1;
     if (live && !ended && new_ext && ext_hit) {
-      key = min(prim >> S.kshift, SORT_KEYS - 1u);
+      key = PT_SORT_KMAP ? S.kmap[prim >> S.kmshift] : min(prim >> S.kshift, SORT_KEYS - 1u);
       if (PT_SORT_DIR)
         key = (key << 3) | (ext.d.x < 0.0f ? 1u : 0u) | (ext.d.y < 0.0f ? 2u : 0u) | (ext.d.z < 0.0f ? 4u : 0u);
     }

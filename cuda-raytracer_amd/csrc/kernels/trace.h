@@ -118,6 +118,7 @@ __host__ __device__ inline size_t cnt_idx(int node, int lane) { return ((size_t)
 // shadow ray occluded by one is never queued); every other ray is pushed into
 // the queues of the targets (nodes of one level, 1 or 2) whose boxes it hits.
 constexpr int MAX_ROOT_TARGETS = 16, MAX_INLINE_LEAVES = 4;
+constexpr uint32_t KMAP_BITS = 8, KMAP_SIZE = 1u << KMAP_BITS;  // record-order key map (shade.hip)
 struct RootTable {
   int nt;                          // queue targets
   int tnode[MAX_ROOT_TARGETS];     // target node ids

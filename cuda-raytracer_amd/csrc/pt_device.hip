@@ -97,6 +97,8 @@ struct pt_ctx {
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
   uint32_t* d_work = nullptr;  // k_path_leaf path-region counters (128 B apart)
+  uint32_t* d_kmap = nullptr;  // record-order key map (KMAP_SIZE): root target of primitive i << kmap_shift
+  uint32_t kmap_shift = 0;
   float4* d_res = nullptr;     // per-path radiance of a chunk
   size_t res_cap = 0;
   uint4* d_wstate = nullptr;   // per shade workgroup {block next, block end, live slots, shaded vertices}
@@ -184,7 +186,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
-                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live, c->d_pool,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_kmap, c->d_res, c->d_wstate, c->d_live, c->d_pool,
                   c->d_pix_of, c->d_accum, c->d_frame};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -674,6 +676,7 @@ int pt_create(pt_ctx** out, int device) {
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, PATH_REGIONS_MAX * PATH_CTR_STRIDE * 4) != hipSuccess ||
+      hipMalloc((void**)&c->d_kmap, KMAP_SIZE * 4) != hipSuccess ||
       hipMalloc((void**)&c->d_live, 4) != hipSuccess ||
       hipMalloc((void**)&c->d_pool, POOLS * CSTRIDE * 4) != hipSuccess ||
       hipHostMalloc((void**)&c->h_poll, 16, hipHostMallocDefault) != hipSuccess) {
@@ -749,6 +752,32 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   for (int i = 0; i < s->n_bsdfs; ++i)
     if (s->bsdfs[i].type == PT_BSDF_GLASS) c->has_glass = true;
   build_root_table(c);
+  {  // record-order key map: the root target whose subtree holds primitive i << kmap_shift
+    uint32_t b = 0;
+    while ((1u << b) < (uint32_t)c->n_prims) ++b;
+    c->kmap_shift = b > KMAP_BITS ? b - KMAP_BITS : 0u;
+    std::vector<uint32_t> km(KMAP_SIZE, (uint32_t)MAX_ROOT_TARGETS);
+    for (int t = 0; t < c->rt.nt; ++t) {
+      int lo = INT32_MAX, hi = -1;
+      std::vector<int> st{c->rt.tnode[t]};
+      while (!st.empty()) {
+        const pt_node& n = c->nodes_host[st.back()];
+        st.pop_back();
+        if (n.prim_count > 0) {
+          lo = std::min(lo, n.prim_start);
+          hi = std::max(hi, n.prim_start + n.prim_count);
+        } else {
+          for (int k = 0; k < 4; ++k)
+            if (n.child[k] >= 0) st.push_back(n.child[k]);
+        }
+      }
+      for (uint32_t i = 0; i < KMAP_SIZE; ++i) {
+        const int p = (int)(i << c->kmap_shift);
+        if (p >= lo && p < hi) km[i] = (uint32_t)t;
+      }
+    }
+    HIPCHK(c, hipMemcpy(c->d_kmap, km.data(), KMAP_SIZE * 4, hipMemcpyHostToDevice));
+  }
   if ((rc = dalloc(c, &c->d_nodes, s->n_nodes))) return rc;
   if ((rc = dalloc(c, &c->d_prims, (size_t)s->n_prims * 6))) return rc;
   if ((rc = dalloc(c, &c->d_prims_ref, (size_t)s->n_prims * 6))) return rc;
@@ -929,6 +958,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       while ((1u << b) < (uint32_t)c->n_prims) ++b;
       S.kshift = b > SORT_KEY_BITS ? b - SORT_KEY_BITS : 0u;
     }
+    S.kmap = c->d_kmap;
+    S.kmshift = c->kmap_shift;
     if (c->root_leaf) {
       // single-leaf tree: every path runs to completion in one kernel
       // (persistent waves with path regeneration, output res[P])
