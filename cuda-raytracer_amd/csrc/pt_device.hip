@@ -1029,8 +1029,11 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       c->launch(pt_ctx::K_CAM, 0, kcam, grid, dim3(TPB), S);
       // passes in groups of POLL_GROUP; the host reads the finished-path count
       // of group g (pinned memory, event) while group g + 1 is already queued
-      auto enqueue_group = [&](int g) -> int {
-        for (int k = 0; k < POLL_GROUP; ++k) {
+      // (np passes; the tail of a chunk polls after every pass: a pass queued
+      // after the last path ended still costs ~150 us of empty level and scan
+      // launches)
+      auto enqueue_group = [&](int g, int np) -> int {
+        for (int k = 0; k < np; ++k) {
           int r = trace_levels(c);
           if (r) return r;
           if (c->timing) {
@@ -1051,10 +1054,11 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       // every path ends within `passes` passes of its start, and while blocks
       // remain every free slot starts a path: at most (M / N + 2) rounds of
       // `passes` passes
-      const int max_groups = (int)(((uint64_t)(M / N + 2) * passes) / POLL_GROUP + 3);
+      const uint64_t max_passes = (uint64_t)(M / N + 2) * passes + 2 * POLL_GROUP;
+      uint64_t queued = 2 * POLL_GROUP;
       bool overflow = false, finished = false;
-      if ((rc = enqueue_group(0)) || (rc = enqueue_group(1))) return rc;
-      for (int g = 0; g < max_groups; ++g) {
+      if ((rc = enqueue_group(0, POLL_GROUP)) || (rc = enqueue_group(1, POLL_GROUP))) return rc;
+      for (int g = 0; queued <= max_passes + 2 * POLL_GROUP; ++g) {
         HIPCHK(c, hipEventSynchronize(c->ev_poll[g & 1]));
         const uint32_t nlive = c->h_poll[2 * (g & 1)], err = c->h_poll[2 * (g & 1) + 1];
         if (err) {
@@ -1065,7 +1069,10 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
           finished = true;
           break;
         }
-        if ((rc = enqueue_group(g + 2))) return rc;
+        // live slots + unstarted paths below 1/16 of the pool: the chunk's tail
+        const int np = (uint64_t)nlive * 16 < N ? 1 : POLL_GROUP;
+        if ((rc = enqueue_group(g + 2, np))) return rc;
+        queued += (uint64_t)np;
       }
       if (overflow) {
         // a level overflowed its queue (the pass was abandoned): re-run the
