@@ -5,6 +5,7 @@
 #include <cstring>
 #include <string>
 
+#include "scotty_capi.h"
 #include "scotty_pt.h"
 
 namespace {

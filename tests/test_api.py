@@ -56,7 +56,11 @@ def test_scotty_surface_library_exports():
     """The Scotty3D surface's C entry points (scotty/scotty_capi.cpp) load;
     without a GPU they report the device error through the return code."""
     lib = ptrace._scotty()
-    assert hasattr(lib, "scotty_render") and hasattr(lib, "scotty_viewer")
+    header = (ROOT / "include" / "scotty_capi.h").read_text()
+    declared = set(re.findall(r"\b(scotty_[a-z_]+)\s*\(", header))
+    assert declared == {"scotty_render", "scotty_viewer"}
+    for name in declared:
+        assert hasattr(lib, name), name
     if have_gpu():
         return
     scene = ptrace.ArrayScene.load(ROOT / "tests" / "golden" / "scenes" / "CBempty.npz")
