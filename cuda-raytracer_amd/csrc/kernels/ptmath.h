@@ -74,8 +74,16 @@ __device__ __forceinline__ u4 philox(u4 c, uint32_t k0, uint32_t k1) {
   }
   return c;
 }
-// uniform in [0,1): top 24 bits, exact in fp32
-__device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
+// uniform in [0,1): top 24 bits, exact in fp32.  PT_U01_LDEXP: the scaling by
+// 2^-24 as v_ldexp_f32 (the same value: an integer below 2^24 scaled by a
+// power of two), so no VGPR holds the 2^-24 constant for packed multiplies
+#ifndef PT_U01_LDEXP
+#define PT_U01_LDEXP 1
+#endif
+__device__ __forceinline__ float u01(uint32_t v) {
+  if (PT_U01_LDEXP) return __builtin_ldexpf((float)(v >> 8), -24);
+  return (float)(v >> 8) * (1.0f / 16777216.0f);
+}
 
 // Random numbers of one path vertex.  counter = (pixel, sample, 2*vertex+call, 'PT')
 template <bool M64 = false>
