@@ -24,6 +24,11 @@ labelled as such -- not a scaling figure.
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N
+ranks itself (a torch.distributed.run child process on 127.0.0.1, before
+anything touches the GPU) and exits with its status; it refuses to start when
+fewer than N GPUs are visible.  "n_gpus" is the world the gather ran over.
+
 Rank 0 prints one JSON line.  "roofline" describes the workload's dominant
 kernel, timed by HIP events attached to its dispatch packets in one extra,
 instrumented frame (the headline frames run without events):
@@ -96,7 +101,40 @@ def parse():
                    help="skip the ms_1spp frame (profiler runs: keeps per-launch averages to full frames)")
     p.add_argument("--stats-in-timed", action="store_true",
                    help="record per-kernel HIP events inside the timed steps (default: one extra instrumented frame)")
+    p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                   help="collective backend of the frame gather (nccl = RCCL over xGMI; gloo: tests only -- ranks "
+                        "may share a GPU, device LOCAL_RANK %% device_count, the gather runs on host tensors)")
+    p.add_argument("--save-frame", default=None, help="rank 0 saves the last headline frame (.npy; tests)")
+    p.add_argument("--ref-arith", default="CBbunny",
+                   help="workloads also measured with PT_FLAG_REF_ARITH, the reference kernels' literal "
+                        "arithmetic ('' = none)")
     return p.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without a torch.distributed launcher around us: start the
+    N ranks as a child torch.distributed.run (one process per GPU) and return
+    its exit status.  Nothing here touches the GPU (torch.cuda.device_count
+    does not initialise it), so the ranks own their devices."""
+    import subprocess
+    import torch
+    n = torch.cuda.device_count()
+    if n < args.gpus and args.backend == "nccl":
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {n}", file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    return subprocess.run(cmd).returncode
 
 
 def _cpu_share():
@@ -115,28 +153,43 @@ def _cpu_share():
     return out
 
 
+def usable_cpus():
+    """(CPUs this process can actually run on: the affinity mask capped by the
+    cgroup CPU quota, the share dict)."""
+    sh = _cpu_share()
+    n = sh.get("affinity") or os.cpu_count() or 1
+    q = sh.get("cgroup_quota_cpus")
+    if q:
+        n = min(n, max(1, int(q)))
+    return n, sh
+
+
 def cpu_baseline(desc, args):
-    """The oracle through the Scotty3D PathTracer surface on this host
-    (hardware_concurrency workers): a bounded sample of the same frame (same
-    spp and bounces, every k-th 32x32 tile), sized to about --cpu-seconds."""
+    """The oracle through the Scotty3D PathTracer surface on this host, one
+    worker per usable CPU (affinity mask / cgroup quota; the GPU box's
+    hardware_concurrency reports the whole machine): a bounded sample of the
+    same frame (same spp and bounces, every k-th 32x32 tile), sized to about
+    --cpu-seconds."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle
+    ncpu, share = usable_cpus()
     ntiles = -(-args.width // 32) * -(-args.height // 32)
     cal = max(1, ntiles // 16)  # calibration: 1/16 of the tiles (at least one) at 4 spp
     _, rays, dt, thr = pyoracle.scotty_render(desc, args.width, args.height, 4, args.bounces, seed=args.seed,
-                                              tile_stride=cal)
+                                              tile_stride=cal, threads=ncpu)
     full_s = dt * cal * args.spp / 4  # estimated seconds for the whole frame
     stride = 1
     while full_s / stride > args.cpu_seconds and stride < ntiles:
         stride *= 2
     _, rays, dt, thr = pyoracle.scotty_render(desc, args.width, args.height, args.spp, args.bounces,
-                                              seed=args.seed, tile_stride=stride)
+                                              seed=args.seed, tile_stride=stride, threads=ncpu)
     nt = len(range(0, ntiles, stride))
     out = {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": thr, "kind": "port",
            "sample": f"{args.scene} {args.width}x{args.height}: {nt} of {ntiles} 32x32 tiles (every {stride}th), "
                      f"{args.spp} spp, {args.bounces} bounces, through the Scotty3D PathTracer surface "
-                     f"(std::thread::hardware_concurrency() = {thr} workers); {rays} rays in {dt:.1f} s"}
-    out.update(_cpu_share())
+                     f"({thr} worker threads = the usable CPUs); {rays} rays in {dt:.1f} s",
+           "hardware_concurrency": os.cpu_count()}
+    out.update(share)
     return out
 
 
@@ -205,9 +258,10 @@ def root_leaf_flops(desc):
     return ntri * FLOP_TRI + nsph * FLOP_SPHERE, n.prim_count
 
 
-def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
+def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
     """One workload (scene + args' frame shape) timed over args.steps frames.
-    share=(r, n): render only tile share r of n on this one GPU (no gather)."""
+    share=(r, n): render only tile share r of n on this one GPU (no gather);
+    flags: extra render flags (PT_FLAG_REF_ARITH)."""
     import torch
     import ptrace
     import ptdist
@@ -228,9 +282,11 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
         ctx.clear()
         ctx.render(args.width, args.height, args.spp, max_bounces=args.bounces, seed=args.seed,
                    batch_paths=args.batch, tile_size=args.tile, rank=t_rank, nranks=t_world,
-                   flags=ptrace.PT_FLAG_STATS if stats else 0)
+                   flags=flags | (ptrace.PT_FLAG_STATS if stats else 0))
         if world > 1:
-            sums[0] = ptdist.local_sums_tensor(ctx, dev, out=sums[0])
+            # RCCL gathers device tensors; gloo (tests) host tensors
+            sdev = dev if args.backend == "nccl" else "cpu"
+            sums[0] = ptdist.local_sums_tensor(ctx, sdev, out=sums[0])
             img = ptdist.gather_frame(sums[0], args.width, args.height, args.tile, args.spp)
             if img is not None:
                 host.copy_(img)
@@ -269,7 +325,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         ctx.render(args.width, args.height, 1, max_bounces=args.bounces, seed=args.seed, batch_paths=args.batch,
-                   tile_size=args.tile, rank=t_rank, nranks=t_world)
+                   tile_size=args.tile, rank=t_rank, nranks=t_world, flags=flags)
         torch.cuda.synchronize()
         ms_1spp = (time.perf_counter() - t2) * 1e3
     lvl_ms = sum(st.ms_level[l] for l in range(1, 16))
@@ -286,12 +342,16 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
     flop_ray, _ = root_leaf_flops(desc)
     path_flops = flop_ray * st.rays
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        rdev = dev if args.backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        r = torch.tensor([rays], dtype=torch.float64, device=dev)
+        r = torch.tensor([rays], dtype=torch.float64, device=rdev)
         dist.all_reduce(r)
         rays = float(r.item())
+    if args.save_frame and rank == 0 and share is None and name == args.scene and not flags:
+        import numpy as np
+        np.save(args.save_frame, host.numpy())
     ms_step = elapsed / args.steps * 1e3
     if st.ms_path >= lvl_ms:
         kernel, launches = "k_path_leaf", st.path_launches
@@ -381,24 +441,42 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import ptrace
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the world", file=sys.stderr)
     dist = None
-    torch.cuda.set_device(local)
+    # one GPU per rank (gloo test runs may put several ranks on one GPU)
+    gpu = local if args.backend == "nccl" else local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    ctx = ptrace.Context(local)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    dev = torch.device("cuda", gpu)
+    ctx = ptrace.Context(gpu)
 
     head, head_scene = run_workload(args.scene, args, ctx, rank, world, dev, dist)
     others = []
     for name in [s for s in args.configs.split(",") if s not in ("", "none", '""') and s != args.scene]:
         o, _ = run_workload(name, args, ctx, rank, world, dev, dist)
         o["config"] = f"{args.width}x{args.height} {args.spp}spp {args.bounces} bounces"
+        others.append(o)
+    # the cost of reference parity: the same frame with PT_FLAG_REF_ARITH, the
+    # reference kernels' literal arithmetic (triangles with diffuse / mirror /
+    # emission BSDFs only)
+    for name in [s for s in args.ref_arith.split(",") if s not in ("", "none", '""')]:
+        o, _ = run_workload(name, args, ctx, rank, world, dev, dist, flags=ptrace.PT_FLAG_REF_ARITH)
+        o["config"] = f"{args.width}x{args.height} {args.spp}spp {args.bounces} bounces, PT_FLAG_REF_ARITH"
+        o["flags"] = "PT_FLAG_REF_ARITH"
         others.append(o)
     import copy
     a5 = copy.copy(args)

@@ -73,6 +73,7 @@ struct TraceArgs {
                                      // QESTRIDE float4 per entry, {o, d.x}{d.y, d.z, id, tmax}
   uint32_t shadow_base;              // ray slots >= shadow_base are shadow rays (any hit ends them);
                                      // 0xFFFFFFFF: every ray wants its closest hit (pt_intersect)
+  const float* __restrict__ tmin;    // per ray slot t_min (pt_intersect, TMIN kernels only; else unused)
   // capacities, checked only by a -DPT_DBG_BOUNDS build (a debugging aid)
   uint32_t dbg_nslots;               // ray records
   uint32_t dbg_nnodes;

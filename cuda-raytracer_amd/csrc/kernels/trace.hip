@@ -63,12 +63,13 @@ __device__ __forceinline__ float edge_ref(const float4 N, float ex, float ey, fl
 template <bool REFA = false>
 __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q0, const float4 q1,
                                           const float4 q2, const float4 q3, const float4 q4,
-                                          const float4 q5, const float tbest) {
+                                          const float4 q5, const float tbest, const float tlo = 0.0f) {
   float ndd = fdot(q3.x, q3.y, q3.z, d.x, d.y, d.z);
   if (REFA ? fabsf(ndd) <= 1e-6f : fabsf(ndd) < 1e-6f) return -1.0f;
   float t = (q1.w - fdot(q3.x, q3.y, q3.z, o.x, o.y, o.z)) / ndd;
-  // t > tbest cannot win (ties need t == tbest): skip the edge tests
-  if (t < 0.0f || t > tbest) return -1.0f;
+  // t > tbest cannot win (ties need t == tbest): skip the edge tests; hits
+  // before the ray's t_min (tlo >= 0, pt_intersect) do not count
+  if (t < tlo || t > tbest) return -1.0f;
   f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
   if constexpr (REFA) {
     if (edge_ref(q3, q2.w, q3.w, q4.w, P, q0) < 0.0f) return -1.0f;
@@ -135,7 +136,7 @@ __device__ __forceinline__ f2v edge_ref2(const f3x2& N, const f3x2& P, const f3x
 template <bool REFA = false>
 __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const f3x2& N, f2v pd, const f3x2& v0,
                                          const f3x2& v1, const f3x2& v2, const f3x2& m0, const f3x2& m1,
-                                         const f3x2& m2, f2v tbest) {
+                                         const f3x2& m2, f2v tbest, f2v tlo = f2v{0.0f, 0.0f}) {
   const f2v ndd = fdot2(N, d);
   const f2v t = (pd - fdot2(N, o)) / ndd;
   const f3x2 P{fma2(t, d.x, o.x), fma2(t, d.y, o.y), fma2(t, d.z, o.z)};
@@ -150,15 +151,17 @@ __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const f3x
   for (int i = 0; i < 2; ++i) {
     // non-short-circuit: every comparison is one v_cmp, combined on the SALU
     const bool flat = REFA ? fabsf(ndd[i]) <= 1e-6f : fabsf(ndd[i]) < 1e-6f;
-    const bool miss = flat | (t[i] < 0.0f) | (t[i] > tbest[i]) | (s0[i] < 0.0f) | (s1[i] < 0.0f) | (s2[i] < 0.0f);
+    const bool miss = flat | (t[i] < tlo[i]) | (t[i] > tbest[i]) | (s0[i] < 0.0f) | (s1[i] < 0.0f) | (s2[i] < 0.0f);
     r[i] = miss ? -1.0f : tz[i];
   }
   return r;
 }
 
 // Ray-sphere (the reference has none: spheres are reinterpret_cast to
-// triangles at cu:1760).  Nearest root with t >= 0; d must be unit length.
-__device__ __forceinline__ float sphere_test(const f3 o, const f3 d, const float4 q0, const float4 q1) {
+// triangles at cu:1760).  Nearest root with t >= tlo (the ray's t_min, >= 0);
+// d must be unit length.
+__device__ __forceinline__ float sphere_test(const f3 o, const f3 d, const float4 q0, const float4 q1,
+                                             const float tlo = 0.0f) {
   f3 oc = mk(o.x - q0.x, o.y - q0.y, o.z - q0.z);
   float b = fdot(oc.x, oc.y, oc.z, d.x, d.y, d.z);
   float cc = fdot(oc.x, oc.y, oc.z, oc.x, oc.y, oc.z) - q1.y;
@@ -167,8 +170,8 @@ __device__ __forceinline__ float sphere_test(const f3 o, const f3 d, const float
   float sq = sqrtf(disc);
   float t0 = -b - sq;
   float t1 = -b + sq;
-  float t = (t0 >= 0.0f) ? t0 : t1;
-  if (t < 0.0f) return -1.0f;
+  float t = (t0 >= tlo) ? t0 : t1;
+  if (t < tlo) return -1.0f;
   return t == 0.0f ? 0.0f : t;
 }
 
@@ -343,7 +346,7 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 #ifndef PT_ROOT_EXT_PRETEST
 #define PT_ROOT_EXT_PRETEST 0
 #endif
-template <int R, bool REFA = false>
+template <int R, bool REFA = false, bool TMIN = false>
 __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T, int lane, const uint32_t (&id)[R],
                                           const f3 (&o)[R], const f3 (&d)[R], const float (&tmax)[R],
                                           const bool (&valid)[R], const bool (&anyhit)[R], uint32_t* sh) {
@@ -353,6 +356,8 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
   for (int j = 0; j < R; ++j) {
     float bt = tmax[j];
     int bp = -1;
+    // hits before the ray's t_min do not count (pt_intersect; 0 otherwise)
+    const float tlo = (TMIN && valid[j]) ? A.tmin[id[j]] : 0.0f;
     if (T.ni > 0) {
       const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
                         __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
@@ -377,7 +382,7 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
           }
           float tt;
           if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE)
-            tt = sphere_test(o[j], d[j], q0, q1);
+            tt = sphere_test(o[j], d[j], q0, q1, tlo);
           else if (anyhit[j]) {
             // shadow rays: division-free pre-test (they mostly point away from
             // the walls or end before them, see tri_outside)
@@ -385,15 +390,15 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
             const float ndd = fdot(q3.x, q3.y, q3.z, d[j].x, d[j].y, d[j].z);
             const float num = q1.w - fdot(q3.x, q3.y, q3.z, o[j].x, o[j].y, o[j].z);
             tt = -1.0f;
-            if (!tri_outside(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), bt);
+            if (!tri_outside(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), bt, tlo);
           } else if (PT_ROOT_EXT_PRETEST) {
             const float4 q3 = f4(P[3]);
             const float ndd = fdot(q3.x, q3.y, q3.z, d[j].x, d[j].y, d[j].z);
             const float num = q1.w - fdot(q3.x, q3.y, q3.z, o[j].x, o[j].y, o[j].z);
             tt = -1.0f;
-            if (!tri_outside(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), bt);
+            if (!tri_outside(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), bt, tlo);
           } else
-            tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), bt);
+            tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), bt, tlo);
           // ties go to the lowest primitive across the inline leaves too
           // (their primitive ranges are not in increasing order)
           if (tt >= 0.0f && (tt < bt || (tt == bt && (bp < 0 || pstart + kk < bp)))) {
@@ -423,7 +428,7 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
 #endif
 // LEAF: the node is known to be a leaf (the leaf-only level kernel): the
 // interior code is not compiled in (fewer registers, more waves)
-template <bool IMPLICIT, bool REFA = false, bool LEAF = false>
+template <bool IMPLICIT, bool REFA = false, bool LEAF = false, bool TMIN = false>
 __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, uint32_t base, int n, int lane,
                                              uint32_t* sh, bool ids = true, bool out_ids = true) {
   const int tid = threadIdx.x;
@@ -462,8 +467,12 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
   }
 
   uint32_t nvalid = 0;
+  float tlo[RPT];  // the rays' t_min (pt_intersect; TMIN only)
 #pragma unroll
-  for (int j = 0; j < RPT; ++j) nvalid += valid[j] ? 1u : 0u;
+  for (int j = 0; j < RPT; ++j) {
+    nvalid += valid[j] ? 1u : 0u;
+    tlo[j] = (TMIN && valid[j]) ? A.tmin[id[j]] : 0.0f;
+  }
 
   const int nj = (n + TPB - 1) / TPB;  // ray groups with at least one valid thread (uniform)
   const int pcount = nd->prim_count;
@@ -489,7 +498,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {
           if (j >= nj) break;
-          float t = sphere_test(o[j], d[j], q0, q1);
+          float t = sphere_test(o[j], d[j], q0, q1, tlo[j]);
           if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
             bt[j] = t;
             bp[j] = pstart + k;
@@ -504,7 +513,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
         for (int j = 0; j < RPT; j += 2) {
           if (j >= nj) break;
           const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
-                                   e2, f2v{bt[j], bt[j + 1]});
+                                   e2, f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const float t = t2[i];
@@ -538,7 +547,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 // ---- root pass (level 0) of pt_intersect: implicit queue = slots [r0, r1) ------------
 // Single-leaf trees: the root leaf's primitives against every ray (process_item).
 // Otherwise root_pass: inline leaves, then the root table's targets.
-template <bool REFA>
+template <bool REFA, bool TMIN = false>
 __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, uint32_t r0, uint32_t r1,
                                                     unsigned long long* __restrict__ rcount) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
@@ -548,7 +557,7 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, ui
   const int lane = item & (NLANE - 1);
   uint32_t v = 0;
   if (((const CPTR(pt_node))A.nodes)->prim_count > 0) {
-    v = process_item<true, REFA>(A, 0, first, n, lane, sh);
+    v = process_item<true, REFA, false, TMIN>(A, 0, first, n, lane, sh);
   } else {
     uint32_t id[RPT];
     f3 o[RPT], d[RPT];
@@ -575,7 +584,7 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, ui
         }
       }
     }
-    root_pass<RPT, REFA>(A, T, lane, id, o, d, tmax, valid, anyhit, sh);
+    root_pass<RPT, REFA, TMIN>(A, T, lane, id, o, d, tmax, valid, anyhit, sh);
   }
   // valid-ray count (R of the roofline formula): one fire-and-forget atomic per
   // workgroup into this lane's counter line
@@ -710,7 +719,7 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
 #ifndef PT_LEAF_PAIR
 #define PT_LEAF_PAIR 0
 #endif
-template <bool REFA = false, bool LEAF = false>
+template <bool REFA = false, bool LEAF = false, bool TMIN = false>
 __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane, bool ids,
                                              bool out_ids, bool two_level) {
   const uint32_t lid = lane_id();
@@ -730,6 +739,9 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     if (valid[j]) load_ray(A, ids, base + (uint32_t)i, id[j], o[j], d[j], tmax[j]);
   }
   const int nj = (n + 63) >> 6;  // ray groups with at least one valid lane (uniform)
+  float tlo[RPTW];  // the rays' t_min (pt_intersect; TMIN only)
+#pragma unroll
+  for (int j = 0; j < RPTW; ++j) tlo[j] = (TMIN && valid[j]) ? A.tmin[id[j]] : 0.0f;
   const int pcount = nd->prim_count;
   if (LEAF || pcount > 0) {
     const int pstart = nd->prim_start;
@@ -748,7 +760,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 #pragma unroll
         for (int j = 0; j < RPTW; ++j) {
           if (j >= nj) break;
-          float t = sphere_test(o[j], d[j], q0, q1);
+          float t = sphere_test(o[j], d[j], q0, q1, tlo[j]);
           if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
             bt[j] = t;
             bp[j] = pstart + k;
@@ -762,7 +774,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
         for (int j = 0; j < RPTW; j += 2) {
           if (j >= nj) break;
           const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
-                                         e2, f2v{bt[j], bt[j + 1]});
+                                         e2, f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const float t = t2[i];
@@ -800,7 +812,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 #pragma unroll
         for (int j = 0; j < RPTW; ++j) {
           if (j >= nj) break;
-          float t = sphere_test(o[j], d[j], q0, q1);
+          float t = sphere_test(o[j], d[j], q0, q1, tlo[j]);
           if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
             bt[j] = t;
             bp[j] = pstart + k;
@@ -815,7 +827,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
         for (int j = 0; j < RPTW; j += 2) {
           if (j >= nj) break;
           const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
-                                   e2, f2v{bt[j], bt[j + 1]});
+                                   e2, f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const float t = t2[i];
@@ -913,11 +925,13 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 #ifndef PT_LEAF_WAVES
 #define PT_LEAF_WAVES 6
 #endif
-template <bool REFA, bool LEAF, bool BLOCK = true>
+// TMIN: the rays carry a t_min (pt_intersect with t_min > 0 somewhere in the
+// batch): hits before it do not count (TraceArgs::tmin)
+template <bool REFA, bool LEAF, bool BLOCK = true, bool TMIN = false>
 __device__ __forceinline__ void trace_level_body(const TraceArgs& A, const LevelArgs& L);
-template <bool REFA>
+template <bool REFA, bool TMIN = false>
 __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, LevelArgs L) {
-  trace_level_body<REFA, false>(A, L);
+  trace_level_body<REFA, false, true, TMIN>(A, L);
 }
 // The real levels of the two-level traversal always run wave items (their
 // push exists for wave items only): without the workgroup-item code the
@@ -928,16 +942,16 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
 #define PT_REAL_WAVES 6
 #endif
 #define PT_REAL_ATTR __attribute__((amdgpu_waves_per_eu(PT_REAL_WAVES, 8)))
-template <bool REFA>
+template <bool REFA, bool TMIN = false>
 __global__ __launch_bounds__(TPB) PT_REAL_ATTR void k_trace_real(TraceArgs A, LevelArgs L) {
-  trace_level_body<REFA, false, false>(A, L);
+  trace_level_body<REFA, false, false, TMIN>(A, L);
 }
-template <bool REFA>
+template <bool REFA, bool TMIN = false>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_LEAF_WAVES, 8))) void k_trace_leaves(
     TraceArgs A, LevelArgs L) {
-  trace_level_body<REFA, true>(A, L);
+  trace_level_body<REFA, true, true, TMIN>(A, L);
 }
-template <bool REFA, bool LEAF, bool BLOCK>
+template <bool REFA, bool LEAF, bool BLOCK, bool TMIN>
 __device__ __forceinline__ void trace_level_body(const TraceArgs& A, const LevelArgs& L) {
   const int lane = blockIdx.x & (NLANE - 1);
   const uint32_t lid = lane_id();
@@ -975,7 +989,7 @@ __device__ __forceinline__ void trace_level_body(const TraceArgs& A, const Level
       const uint32_t base = __builtin_amdgcn_readfirstlane(s_base);
       const int n = __builtin_amdgcn_readfirstlane(s_n);
       __syncthreads();
-      process_item<false, REFA, LEAF>(A, node, base, n, lane, sh, L.ids != 0, L.out_ids != 0);
+      process_item<false, REFA, LEAF, TMIN>(A, node, base, n, lane, sh, L.ids != 0, L.out_ids != 0);
       __syncthreads();
     }
     return;
@@ -999,7 +1013,7 @@ __device__ __forceinline__ void trace_level_body(const TraceArgs& A, const Level
     const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
     const uint32_t base = A.qoff[(size_t)node * NLANE + lane] + i * WTILE;
     const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
-    process_wave<REFA, LEAF>(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane,
+    process_wave<REFA, LEAF, TMIN>(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane,
                        L.ids != 0, L.out_ids != 0, L.two_level != 0);
   }
 }

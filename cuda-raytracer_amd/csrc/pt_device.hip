@@ -70,6 +70,9 @@ struct pt_ctx {
   float4* d_prims_ref = nullptr;  // PT_FLAG_REF_ARITH records (ref_prim_records)
   bool has_sphere = false, has_glass = false;
   bool refa = false;              // the current render / intersect runs PT_FLAG_REF_ARITH
+  bool tmin = false;              // the current pt_intersect has rays with t_min > 0 (d_tmin)
+  float* d_tmin = nullptr;        // their t_min per ray slot
+  size_t tmin_cap = 0;
   float4* d_shade = nullptr;  // hit-shading records (SHADE_REC float4 per primitive)
   pt_bsdf* d_bsdfs = nullptr;
 
@@ -187,7 +190,7 @@ static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_kmap, c->d_res, c->d_wstate, c->d_live, c->d_pool,
-                  c->d_pix_of, c->d_accum, c->d_frame};
+                  c->d_pix_of, c->d_accum, c->d_frame, c->d_tmin};
   for (void* p : ptrs)
     if (p) hipFree(p);
 }
@@ -429,6 +432,7 @@ static TraceArgs trace_args(pt_ctx* c) {
   A.q = c->d_q;
   A.qe = c->d_qe;
   A.shadow_base = c->shadow_base;
+  A.tmin = c->tmin ? c->d_tmin : nullptr;
   A.dbg_nslots = (uint32_t)std::min<size_t>((size_t)c->cap_paths * c->cap_spp, 0xFFFFFFFFu);
   A.dbg_nnodes = (uint32_t)c->n_nodes;
   A.dbg_qids = (uint64_t)QREGIONS * c->qcap;
@@ -485,8 +489,12 @@ static int trace_levels(pt_ctx* c) {
     const bool leaves = !real && c->leaf_kernel;
     // (a real level of the two-level traversal: wave items only, k_trace_real)
     const bool wave_only = L.two_level && c->real_kernel;
-    auto kl = c->refa ? (leaves ? k_trace_leaves<true> : wave_only ? k_trace_real<true> : k_trace_level<true>)
-                      : (leaves ? k_trace_leaves<false> : wave_only ? k_trace_real<false> : k_trace_level<false>);
+    auto kl = c->tmin ? (c->refa ? (leaves ? k_trace_leaves<true, true> : wave_only ? k_trace_real<true, true>
+                                                                                   : k_trace_level<true, true>)
+                                 : (leaves ? k_trace_leaves<false, true> : wave_only ? k_trace_real<false, true>
+                                                                                     : k_trace_level<false, true>))
+              : (c->refa ? (leaves ? k_trace_leaves<true> : wave_only ? k_trace_real<true> : k_trace_level<true>)
+                         : (leaves ? k_trace_leaves<false> : wave_only ? k_trace_real<false> : k_trace_level<false>));
     c->launch(pt_ctx::K_LEVEL, l, kl, dim3(LEVEL_GRID), dim3(TPB), A, L);
   }
   HIPCHK(c, hipGetLastError());
@@ -501,10 +509,9 @@ static int trace_pass(pt_ctx* c, uint32_t r0, uint32_t r1) {
   const uint32_t items = (r1 - r0 + TILE - 1) / TILE;
   // the (node, lane) counters are zero here: each level's scan re-zeroes them
   // after taking its snapshot (pt_load_scene zeroes them once)
-  if (c->refa)
-    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<true>, dim3(items), dim3(TPB), A, c->rt, r0, r1, c->d_rcount);
-  else
-    c->launch(pt_ctx::K_ROOT, 0, k_trace_root<false>, dim3(items), dim3(TPB), A, c->rt, r0, r1, c->d_rcount);
+  auto kr = c->tmin ? (c->refa ? k_trace_root<true, true> : k_trace_root<false, true>)
+                    : (c->refa ? k_trace_root<true> : k_trace_root<false>);
+  c->launch(pt_ctx::K_ROOT, 0, kr, dim3(items), dim3(TPB), A, c->rt, r0, r1, c->d_rcount);
   if (c->root_leaf) {
     HIPCHK(c, hipGetLastError());
     c->stats.passes++;
@@ -913,6 +920,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   const bool ref_sched = (P->flags & PT_FLAG_REF_SCHEDULE) != 0;
   const uint32_t nsh = ref_sched ? 2u : 1u;
   c->refa = (P->flags & PT_FLAG_REF_ARITH) != 0;
+  c->tmin = false;
   if (c->refa && (c->has_sphere || c->has_glass))
     return fail(c, PT_E_UNSUPPORTED, "PT_FLAG_REF_ARITH: the reference renders triangles with diffuse/mirror BSDFs only");
   const int max_bounces = ref_sched ? 2 : P->max_bounces;
@@ -1207,8 +1215,28 @@ int pt_intersect_ex(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits, uin
   hipSetDevice(c->device);
   int rc;
   c->shadow_base = 0xFFFFFFFFu;  // every ray wants its closest hit
+  // t_min (the rays' 8th float, Ray::min_t): hits with t < t_min do not count.
+  // Clamped at 0 (no hit has t < 0); a batch without any t_min > 0 runs the
+  // render kernels' traversal unchanged
+  std::vector<float> tmin;
+  for (int32_t i = 0; i < n; ++i) {
+    const float t = rays[(size_t)8 * i + 7];
+    if (t != t) return fail(c, PT_E_INVALID, "pt_intersect: t_min is NaN");
+    if (t > 0.0f) {
+      if (tmin.empty()) tmin.assign((size_t)n, 0.0f);
+      tmin[i] = t;
+    }
+  }
+  c->tmin = !tmin.empty();
+  if (c->tmin) {
+    if ((size_t)n > c->tmin_cap) {
+      if ((rc = dalloc(c, &c->d_tmin, (size_t)n))) return rc;
+      c->tmin_cap = (size_t)n;
+    }
+    HIPCHK(c, hipMemcpy(c->d_tmin, tmin.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+  }
   const uint32_t N = ((uint32_t)n + 1) / 2;
-  const bool realloc = N > c->cap_paths || 2 > c->cap_spp;
+  const bool realloc = N > c->cap_paths || 2 > c->cap_spp || c->qfactor != c->cap_qfactor;
   if ((rc = ensure_paths(c, N, 2))) return rc;
   if (realloc && (rc = set_root_child_offsets(c))) return rc;
   float4* d_in = nullptr;
@@ -1233,7 +1261,8 @@ int pt_intersect_ex(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits, uin
     }
     if (!e) break;
     // a level overflowed its queue: twice the queue factor, trace again
-    if (2 * ID_FACTOR * (2 * c->qfactor) * 2 * (size_t)N >= (1ull << 32)) {
+    // (while the doubled factor's u32 queue offsets still hold N paths)
+    if (max_batch_paths(c, 2) / 2 < N) {
       hipFree(d_in);
       return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded");
     }

@@ -168,7 +168,11 @@ int pt_scene_from_triangles(const float* positions, int32_t n_tris, const pt_bsd
 }
 
 int pt_scene_from_mesh(const pt_mesh_desc* md, pt_scene** out) {
-  if (!out) return PT_E_INVALID;
+  return pt_scene_from_mesh_ex(md, 0, out);
+}
+
+int pt_scene_from_mesh_ex(const pt_mesh_desc* md, int32_t max_leaf, pt_scene** out) {
+  if (!out || max_leaf < 0) return PT_E_INVALID;
   *out = nullptr;
   auto* sc = new pt_scene();
   int rc = ptscene::scene_from_mesh(md, sc->s);
@@ -177,7 +181,7 @@ int pt_scene_from_mesh(const pt_mesh_desc* md, pt_scene** out) {
     return rc;
   }
   try {
-    ptscene::build_bvh_and_flatten(sc->s, host_max_leaf());
+    ptscene::build_bvh_and_flatten(sc->s, max_leaf > 0 ? (size_t)max_leaf : host_max_leaf());
   } catch (const std::exception&) {
     delete sc;
     return PT_E_INVALID;

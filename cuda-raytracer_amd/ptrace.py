@@ -113,7 +113,7 @@ class pt_mesh_desc(C.Structure):
 
 # every symbol include/pt_api.h declares (tests check the library exports them)
 API_SYMBOLS = [
-    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_build_gpu", "pt_scene_build_gpu_ex", "pt_scene_camera_scotty", "pt_scene_free", "pt_scene_get_desc",
+    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_from_mesh_ex", "pt_scene_build_gpu", "pt_scene_build_gpu_ex", "pt_scene_camera_scotty", "pt_scene_free", "pt_scene_get_desc",
     "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
     "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex", "pt_copy_owned_sums",
@@ -141,6 +141,7 @@ def _load():
         "pt_scene_from_triangles": (C.c_int, [C.POINTER(C.c_float), I32, C.POINTER(pt_bsdf),
                                               C.POINTER(pt_light), C.POINTER(pt_camera), C.POINTER(P)]),
         "pt_scene_from_mesh": (C.c_int, [C.POINTER(pt_mesh_desc), C.POINTER(P)]),
+        "pt_scene_from_mesh_ex": (C.c_int, [C.POINTER(pt_mesh_desc), I32, C.POINTER(P)]),
         "pt_scene_build_gpu": (C.c_int, [C.POINTER(pt_mesh_desc), I32, I32, C.POINTER(P), C.POINTER(C.c_double)]),
         "pt_scene_build_gpu_ex": (C.c_int, [C.POINTER(pt_mesh_desc), I32, I32, I32, C.POINTER(P),
                                             C.POINTER(C.c_double)]),
@@ -461,7 +462,8 @@ class Context:
         return idx[: n.value], dptr.value
 
     def intersect(self, rays, flags=0):
-        """rays: (n, 8) float32 [o.xyz, tmax, d.xyz, 0] -> uint64 hit keys.
+        """rays: (n, 8) float32 [o.xyz, tmax, d.xyz, tmin] -> uint64 hit keys
+        (the closest hit with tmin <= t <= tmax).
         flags: PT_FLAG_REF_ARITH selects the reference's literal triangle test."""
         rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
         hits = np.zeros(len(rays), dtype=np.uint64)
@@ -542,6 +544,21 @@ def _scotty():
         lib.scotty_viewer.restype = C.c_int
         lib.scotty_viewer.argtypes = [C.POINTER(pt_scene_desc), I32, I32, I32, I32, U32, C.c_char_p, I32, F,
                                       C.POINTER(I32), C.c_char_p, SZ]
+        D = C.POINTER(C.c_double)
+        lib.scotty_generate_rays.restype = C.c_int
+        lib.scotty_generate_rays.argtypes = [C.POINTER(pt_camera), I32, D, D]
+        lib.scotty_camera_place.restype = C.c_int
+        lib.scotty_camera_place.argtypes = [D, I32, I32, D, C.c_double, C.c_double, C.c_double, C.c_double,
+                                            C.c_double, C.POINTER(pt_camera), I32, D, D, D]
+        lib.scotty_bvh_create.restype = C.c_int
+        lib.scotty_bvh_create.argtypes = [D, D, I32, C.POINTER(I32), I32, D, I32, I32, I32, C.POINTER(P),
+                                          C.c_char_p, SZ]
+        lib.scotty_bvh_intersect.restype = C.c_int
+        lib.scotty_bvh_intersect.argtypes = [P, D, I32, I32, C.POINTER(I32), D, C.POINTER(I32), D]
+        lib.scotty_bvh_occluded.restype = C.c_int
+        lib.scotty_bvh_occluded.argtypes = [P, D, I32, C.POINTER(I32)]
+        lib.scotty_bvh_destroy.restype = None
+        lib.scotty_bvh_destroy.argtypes = [P]
         _SCOTTY = lib
     return _SCOTTY
 
@@ -573,3 +590,86 @@ def scotty_viewer(scene, width, height, samples_per_frame, keys, max_bounces=2, 
     if rc:
         raise PTError(rc, err.value.decode(errors="replace"))
     return out, n.value
+
+
+def _d(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def scotty_generate_rays(cam, xy):
+    """CMU462::Camera::generate_ray (scotty::Camera over a pt_camera) for
+    normalised sensor points xy (n, 2): (n, 6) float64 = origin, unit direction."""
+    xy = np.ascontiguousarray(xy, dtype=np.float64).reshape(-1, 2)
+    out = np.zeros((len(xy), 6), dtype=np.float64)
+    rc = _scotty().scotty_generate_rays(C.byref(cam), len(xy), _d(xy), _d(out))
+    if rc:
+        raise PTError(rc, "scotty_generate_rays")
+    return out
+
+
+def scotty_camera_place(hfov, vfov, width, height, target, phi, theta, r, min_r=0.0, max_r=np.inf,
+                        xy=None, nclip=0.01, fclip=100.0):
+    """Camera::configure + place (the Scotty3D framing): returns (pt_camera,
+    rays (n, 6) for the sensor points xy, (hFov, vFov) fitted to the screen)."""
+    info = np.array([hfov, vfov, nclip, fclip], dtype=np.float64)
+    tgt = np.ascontiguousarray(target, dtype=np.float64)
+    xy = np.zeros((0, 2)) if xy is None else np.ascontiguousarray(xy, dtype=np.float64).reshape(-1, 2)
+    rays = np.zeros((len(xy), 6), dtype=np.float64)
+    fov = np.zeros(2, dtype=np.float64)
+    cam = pt_camera()
+    rc = _scotty().scotty_camera_place(_d(info), width, height, _d(tgt), phi, theta, r, min_r, max_r,
+                                       C.byref(cam), len(xy), _d(xy) if len(xy) else None,
+                                       _d(rays) if len(xy) else None, _d(fov))
+    if rc:
+        raise PTError(rc, "scotty_camera_place")
+    return cam, rays, (float(fov[0]), float(fov[1]))
+
+
+class ScottyBVH:
+    """StaticScene::BVHAccel(primitives, max_leaf_size) on the GPU over Scotty3D
+    primitives (scotty_bvh_create): one Mesh's triangles (positions (v, 3),
+    vertex normals (v, 3), indices (t, 3)) then spheres (s, 4)."""
+
+    def __init__(self, positions, normals, indices, spheres=None, max_leaf=32, device=0):
+        pos = np.ascontiguousarray(positions, dtype=np.float64).reshape(-1, 3)
+        nrm = np.ascontiguousarray(normals, dtype=np.float64).reshape(-1, 3)
+        idx = np.ascontiguousarray(indices, dtype=np.int32).reshape(-1, 3)
+        sph = np.zeros((0, 4)) if spheres is None else np.ascontiguousarray(spheres, dtype=np.float64).reshape(-1, 4)
+        self.h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = _scotty().scotty_bvh_create(_d(pos), _d(nrm), len(pos), idx.ctypes.data_as(C.POINTER(C.c_int32)),
+                                         len(idx), _d(sph) if len(sph) else None, len(sph), max_leaf, device,
+                                         C.byref(self.h), err, len(err))
+        if rc:
+            raise PTError(rc, err.value.decode(errors="replace"))
+
+    def intersect(self, rays, single=False):
+        """rays (n, 8) float64 = o, d, min_t, max_t -> (hit bool, t, prim index, normal (n, 3))."""
+        rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
+        n = len(rays)
+        hit = np.zeros(n, dtype=np.int32)
+        t = np.zeros(n, dtype=np.float64)
+        prim = np.zeros(n, dtype=np.int32)
+        nrm = np.zeros((n, 3), dtype=np.float64)
+        rc = _scotty().scotty_bvh_intersect(self.h, _d(rays), n, 1 if single else 0,
+                                            hit.ctypes.data_as(C.POINTER(C.c_int32)), _d(t),
+                                            prim.ctypes.data_as(C.POINTER(C.c_int32)), _d(nrm))
+        if rc:
+            raise PTError(rc, "scotty_bvh_intersect")
+        return hit.astype(bool), t, prim, nrm
+
+    def occluded(self, rays):
+        rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
+        hit = np.zeros(len(rays), dtype=np.int32)
+        rc = _scotty().scotty_bvh_occluded(self.h, _d(rays), len(rays), hit.ctypes.data_as(C.POINTER(C.c_int32)))
+        if rc:
+            raise PTError(rc, "scotty_bvh_occluded")
+        return hit.astype(bool)
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value and _SCOTTY is not None:
+            _SCOTTY.scotty_bvh_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        self.close()

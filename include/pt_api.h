@@ -192,6 +192,9 @@ typedef struct pt_mesh_desc {
   const pt_camera* camera;  /* NULL: default                                  */
 } pt_mesh_desc;
 int pt_scene_from_mesh(const pt_mesh_desc* mesh, pt_scene** out);
+/* The same with the reference builder's leaf size (BVHAccel(primitives,
+ * max_leaf_size), bvh.h:111; 0 = 32, the reference default). */
+int pt_scene_from_mesh_ex(const pt_mesh_desc* mesh, int32_t max_leaf, pt_scene** out);
 /* The same input built on GPU `device`: a binary BVH
  * on the device collapsed to the 4-wide, level-major layout (wide leaves hold
  * <= max_leaf primitives; the reference's host SAH build, bvh.cpp:48-337, is
@@ -328,9 +331,11 @@ int pt_write_png(const char* path, const uint8_t* rgba8, int32_t width, int32_t 
 int pt_write_pfm(const char* path, const float* rgba, int32_t width, int32_t height);
 
 /* Closest-hit query through the breadth-first traversal.  rays: n records of
- * 8 floats (o.xyz, tmax, d.xyz, unused).  hits: n records of
- * (uint64) ((float bits of t) << 32 | sorted prim index), or
- * PT_HIT_NONE when nothing is hit with t <= tmax. */
+ * 8 floats (o.xyz, tmax, d.xyz, tmin): a hit counts when tmin <= t <= tmax,
+ * both ends inclusive (Ray::min_t / max_t as Triangle::intersect tests them,
+ * triangle.cpp:189; a tmin <= 0 means 0, a NaN tmin is PT_E_INVALID).  hits:
+ * n records of (uint64) ((float bits of t) << 32 | sorted prim index), the
+ * closest such hit (ties to the lowest index), or PT_HIT_NONE. */
 #define PT_HIT_NONE 0xFFFFFFFFFFFFFFFFull
 int pt_intersect(pt_ctx* ctx, const float* rays, int32_t n, uint64_t* hits);
 /* The same with render flags: PT_FLAG_REF_ARITH selects the reference's

@@ -175,7 +175,8 @@ static float pto_tri_ref(v3 o, v3 d, const float* q) {
   if (dot(N, cross(sub(v0, v2), sub(P, v2))) < 0.0f) return -1.0f;
   return t == 0.0f ? 0.0f : t;
 }
-static float pto_sphere(v3 o, v3 d, const float* q) {
+/* nearest root with t >= tlo (the ray's t_min, >= 0) */
+static float pto_sphere(v3 o, v3 d, const float* q, float tlo) {
   v3 oc = mk(o.x - q[0], o.y - q[1], o.z - q[2]);
   float b = fdot(oc.x, oc.y, oc.z, d.x, d.y, d.z);
   float cc = fdot(oc.x, oc.y, oc.z, oc.x, oc.y, oc.z) - q[5];
@@ -183,16 +184,22 @@ static float pto_sphere(v3 o, v3 d, const float* q) {
   if (disc < 0.0f) return -1.0f;
   float sq = sqrtf(disc);
   float t0 = -b - sq, t1 = -b + sq;
-  float t = (t0 >= 0.0f) ? t0 : t1;
-  if (t < 0.0f) return -1.0f;
+  float t = (t0 >= tlo) ? t0 : t1;
+  if (t < tlo) return -1.0f;
   return t == 0.0f ? 0.0f : t;
 }
-static inline float prim_test(const pt_prim* p, v3 o, v3 d, int ref) {
+/* t of the primitive's hit with t >= tlo, or -1 */
+static inline float prim_test(const pt_prim* p, v3 o, v3 d, int ref, float tlo) {
   uint32_t meta;
   memcpy(&meta, &p->q[3], 4);
-  if ((meta >> 28) == PT_PRIM_SPHERE) return pto_sphere(o, d, p->q);
-  return ref ? pto_tri_ref(o, d, p->q) : pto_tri(o, d, p->q);
+  if ((meta >> 28) == PT_PRIM_SPHERE) return pto_sphere(o, d, p->q, tlo);
+  const float t = ref ? pto_tri_ref(o, d, p->q) : pto_tri(o, d, p->q);
+  return t >= tlo ? t : -1.0f;
 }
+/* A ray record: o.xyz, tmax, d.xyz, t_min (BVHAccel's Ray::min_t; pt_api.h
+ * pt_intersect).  Valid hits have t in [max(t_min, 0), tmax], both ends
+ * inclusive (triangle.cpp:189 rejects t < r.min_t and t > r.max_t). */
+static inline float ray_tlo(const float* ray) { return ray[7] > 0.0f ? ray[7] : 0.0f; }
 static inline uint64_t key(float t, uint32_t prim) {
   uint32_t b;
   memcpy(&b, &t, 4);
@@ -202,10 +209,10 @@ static inline uint64_t key(float t, uint32_t prim) {
 /* Closest hit by brute force: min over all primitives of (t, index), t <= tmax. */
 static uint64_t closest_brute(const pt_scene_desc* S, const float* ray, int ref) {
   v3 o = mk(ray[0], ray[1], ray[2]), d = mk(ray[4], ray[5], ray[6]);
-  float tmax = ray[3];
+  float tmax = ray[3], tlo = ray_tlo(ray);
   uint64_t best = PT_HIT_NONE;
   for (int i = 0; i < S->n_prims; ++i) {
-    float t = prim_test(&S->prims[i], o, d, ref);
+    float t = prim_test(&S->prims[i], o, d, ref, tlo);
     if (t >= 0.0f && t <= tmax) {
       uint64_t k = key(t, (uint32_t)i);
       if (k < best) best = k;
@@ -242,7 +249,7 @@ static int box_hit_d(const pt_node* nd, int c, v3 o, v3 d, double tmax) {
 }
 static uint64_t closest_bvh(const pt_scene_desc* S, const float* ray, int ref) {
   v3 o = mk(ray[0], ray[1], ray[2]), d = mk(ray[4], ray[5], ray[6]);
-  float tmax = ray[3];
+  float tmax = ray[3], tlo = ray_tlo(ray);
   uint64_t best = PT_HIT_NONE;
   int stack[256];
   int sp = 0;
@@ -252,7 +259,7 @@ static uint64_t closest_bvh(const pt_scene_desc* S, const float* ray, int ref) {
     if (nd->prim_count > 0) {
       for (int k = 0; k < nd->prim_count; ++k) {
         int i = nd->prim_start + k;
-        float t = prim_test(&S->prims[i], o, d, ref);
+        float t = prim_test(&S->prims[i], o, d, ref, tlo);
         if (t >= 0.0f && t <= tmax) {
           uint64_t kk = key(t, (uint32_t)i);
           if (kk < best) best = kk;
@@ -422,6 +429,36 @@ static int nee_ref(const pt_scene_desc* S, v3 T, v3 alb, v3 n, v3 pt, float ux, 
   return 0;
 }
 
+/* Camera ray through sensor point (ssx = row + jitter, ssy = column + jitter)
+ * of a W x H frame, kernelPrimaryRays cu:338-354 (direction; the origin is
+ * the camera's). */
+static v3 camera_dir(const pt_camera* cam, int W, int H, float ssx, float ssy, int refa) {
+  float kx = ssy / (float)W - 0.5f;
+  float ky = -(ssx / (float)H - 0.5f);
+  float kz = 1.0f;
+  float len = sqrtf(kx * kx + ky * ky + kz * kz);
+  kx = kx / len;
+  ky = ky / len;
+  kz = kz / len;
+  v3 Lf = ld3(cam->left), Up = ld3(cam->up), K = ld3(cam->look_at);
+  if (refa) { /* cu:347-354: k = k / length(k); dir = k.x left + k.y up + k.z lookAt */
+    v3 k = mk(ssy / (float)W - 0.5f, -(ssx / (float)H - 0.5f), 1.0f);
+    k = scl(k, 1.0f / len3(k));
+    return mk(dot(k, mk(Lf.x, Up.x, K.x)), dot(k, mk(Lf.y, Up.y, K.y)), dot(k, mk(Lf.z, Up.z, K.z)));
+  }
+  return nrm(mk(kx * Lf.x + ky * Up.x + kz * K.x, kx * Lf.y + ky * Up.y + kz * K.y, kx * Lf.z + ky * Up.z + kz * K.z));
+}
+/* The camera ray of sensor point (ssx, ssy) as out[6] = o.xyz, d.xyz. */
+void pto_camera_ray(const pt_camera* cam, int W, int H, float ssx, float ssy, uint32_t flags, float* out) {
+  v3 d = camera_dir(cam, W, H, ssx, ssy, (flags & PT_FLAG_REF_ARITH) != 0);
+  out[0] = cam->origin[0];
+  out[1] = cam->origin[1];
+  out[2] = cam->origin[2];
+  out[3] = d.x;
+  out[4] = d.y;
+  out[5] = d.z;
+}
+
 static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays) {
   const pt_scene_desc* S = J->S;
   const float EPS = 1e-3f;
@@ -432,23 +469,8 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
   /* camera ray, cu:338-354 */
   float ssx = (float)row + u01(u.v[0]);
   float ssy = (float)col + u01(u.v[1]);
-  float kx = ssy / (float)J->W - 0.5f;
-  float ky = -(ssx / (float)J->H - 0.5f);
-  float kz = 1.0f;
-  float len = sqrtf(kx * kx + ky * ky + kz * kz);
-  kx = kx / len;
-  ky = ky / len;
-  kz = kz / len;
-  v3 Lf = ld3(S->camera.left), Up = ld3(S->camera.up), K = ld3(S->camera.look_at);
   const int refa = (J->flags & PT_FLAG_REF_ARITH) != 0;
-  v3 d;
-  if (refa) { /* cu:347-354: k = k / length(k); dir = k.x left + k.y up + k.z lookAt */
-    v3 k = mk(ssy / (float)J->W - 0.5f, -(ssx / (float)J->H - 0.5f), 1.0f);
-    k = scl(k, 1.0f / len3(k));
-    d = mk(dot(k, mk(Lf.x, Up.x, K.x)), dot(k, mk(Lf.y, Up.y, K.y)), dot(k, mk(Lf.z, Up.z, K.z)));
-  } else {
-    d = nrm(mk(kx * Lf.x + ky * Up.x + kz * K.x, kx * Lf.y + ky * Up.y + kz * K.y, kx * Lf.z + ky * Up.z + kz * K.z));
-  }
+  v3 d = camera_dir(&S->camera, J->W, J->H, ssx, ssy, refa);
   v3 o = ld3(S->camera.origin);
   v3 T = mk(1.0f, 1.0f, 1.0f), L = mk(0.0f, 0.0f, 0.0f);
   int spec = 0;

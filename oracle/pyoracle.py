@@ -45,6 +45,8 @@ def _load():
                                C.c_uint32, C.POINTER(C.c_float)]
     lib.pto_philox.restype = None
     lib.pto_philox.argtypes = [C.c_uint32] * 6 + [C.POINTER(C.c_uint32)]
+    lib.pto_camera_ray.restype = None
+    lib.pto_camera_ray.argtypes = [P, C.c_int, C.c_int, C.c_float, C.c_float, C.c_uint32, C.POINTER(C.c_float)]
     lib.pto_sincos2pi.restype = None
     lib.pto_sincos2pi.argtypes = [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
     return lib
@@ -121,6 +123,14 @@ def philox(c, k):
     out = (C.c_uint32 * 4)()
     LIB.pto_philox(*[int(x) & 0xFFFFFFFF for x in c], *[int(x) & 0xFFFFFFFF for x in k], out)
     return list(out)
+
+
+def camera_ray(cam, width, height, ssx, ssy, flags=0):
+    """The kernels' camera ray (cu:338-354) through sensor point (ssx = row +
+    jitter, ssy = column + jitter): (o.xyz, d.xyz) float32."""
+    out = (C.c_float * 6)()
+    LIB.pto_camera_ray(C.addressof(cam), width, height, ssx, ssy, flags, out)
+    return np.array(out, dtype=np.float32)
 
 
 def sincos2pi(u):

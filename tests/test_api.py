@@ -58,11 +58,15 @@ def test_scotty_surface_library_exports():
     lib = ptrace._scotty()
     header = (ROOT / "include" / "scotty_capi.h").read_text()
     declared = set(re.findall(r"\b(scotty_[a-z_]+)\s*\(", header))
-    assert declared == {"scotty_render", "scotty_viewer"}
+    assert {"scotty_render", "scotty_viewer", "scotty_generate_rays", "scotty_camera_place", "scotty_bvh_create",
+            "scotty_bvh_intersect", "scotty_bvh_occluded", "scotty_bvh_destroy"} <= declared
     for name in declared:
         assert hasattr(lib, name), name
     if have_gpu():
         return
+    with pytest.raises(ptrace.PTError) as e:
+        ptrace.ScottyBVH(np.eye(3), np.eye(3), [[0, 1, 2]])
+    assert e.value.code in (ptrace.PT_E_NODEVICE, ptrace.PT_E_HIP)
     scene = ptrace.ArrayScene.load(ROOT / "tests" / "golden" / "scenes" / "CBempty.npz")
     with pytest.raises(ptrace.PTError) as e:
         ptrace.scotty_render(scene, 8, 8, 1, 2, threads=2)

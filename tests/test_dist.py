@@ -90,3 +90,17 @@ def test_gather_layout_reused_across_frames(tmp_path):
         assert np.array_equal(frames[f][..., 0], v / 2)
         assert np.array_equal(frames[f][..., 2], 3 * v / 2)
         assert np.all(frames[f][..., 3] == 1.0)
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """bench.py --gpus N launches N ranks itself, but not onto GPUs that are
+    not there (no GPU in this container)."""
+    import subprocess
+    import sys
+    from conftest import ROOT, have_gpu
+    if have_gpu():
+        pytest.skip("GPU box: covered by test_gpu_regress.py")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    assert "needs 2 visible GPUs" in r.stderr

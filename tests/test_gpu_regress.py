@@ -1,0 +1,105 @@
+"""Deterministic regression tests for two memory-safety fixes of round 2, each
+on a fresh context of its own (not dependent on the session context's scene
+order), and the bench's own rank launcher.
+
+* 6881d6f (host heap corruption): the root table's detached leaves of a
+  scene were applied to the next scene loaded after a single-leaf scene.
+  CBbunny -> CBempty -> CBbunny on one context must trace and render exactly
+  as the oracle does.
+* 6f3f032 (device buffer overrun): ensure_paths allocated fewer path slots
+  than pt_render then launched, after a queue overflow doubled the queue
+  factor on a context holding a 3-slot reference-schedule pool.  A
+  reference-schedule render, then an overflowing 16.8 M-path render on the
+  same context must give the fresh context's image bit for bit."""
+import json
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import ptrace
+import pyoracle
+from conftest import ROOT, load_fixture
+from rays import camera_rays, interior_rays
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    from conftest import have_gpu
+    if not have_gpu():
+        pytest.skip("no GPU")
+
+
+def test_scene_reload_after_single_leaf_scene():
+    ctx = ptrace.Context(0)
+    try:
+        for name in ("CBbunny", "CBempty", "CBbunny", "CBempty"):
+            sc = load_fixture(name)
+            d = sc.desc()
+            ctx.load_scene(sc)
+            rays = np.concatenate([camera_rays(d, 3000, seed=1), interior_rays(d, 3000, seed=2)])
+            assert np.array_equal(ctx.intersect(rays), pyoracle.intersect(d, rays, use_bvh=True)), name
+            ctx.clear()
+            ctx.render(40, 32, 2, max_bounces=5)
+            o, _ = pyoracle.image(d, 40, 32, 2, max_bounces=5)
+            assert np.array_equal(ctx.get_image(), o), name
+    finally:
+        ctx.close()
+
+
+def _soup():
+    rng = np.random.default_rng(11)
+    c = rng.random((3000, 1, 3), dtype=np.float32)
+    return ptrace.Scene.from_triangles((c + 0.6 * (rng.random((3000, 3, 3), dtype=np.float32) - 0.5)).reshape(-1, 9))
+
+
+def test_overflow_rerun_after_reference_schedule_pool():
+    sc = _soup()
+    W = H = 1024
+    spp = 16  # 16.8 M paths: more than a 3-slot pool holds once the queue factor doubles
+    ref_ctx = ptrace.Context(0)
+    try:
+        ref_ctx.load_scene(sc)
+        ref_ctx.render(W, H, spp, max_bounces=2, seed=15618)
+        ref = ref_ctx.get_image()
+        assert ref_ctx.stats().queue_factor > 4  # the soup overflows the default factor
+    finally:
+        ref_ctx.close()
+    ctx = ptrace.Context(0)
+    try:
+        ctx.load_scene(sc)
+        ctx.render(64, 64, 2, max_bounces=2, seed=15618, flags=ptrace.PT_FLAG_REF_SCHEDULE)  # 3 ray slots per path
+        ctx.clear()
+        ctx.reset_stats()
+        ctx.render(W, H, spp, max_bounces=2, seed=15618)
+        assert ctx.stats().queue_factor > 4
+        assert np.array_equal(ctx.get_image(), ref)
+    finally:
+        ctx.close()
+
+
+def _bench(tmp_path, gpus, tag):
+    out = tmp_path / f"frame{tag}.npy"
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(gpus), "--backend", "gloo", "--steps", "1",
+           "--warmup", "0", "--configs", "none", "--config5", "off", "--ref-arith", "none", "--no-cpu",
+           "--no-1spp", "--width", "96", "--height", "64", "--spp", "4", "--bounces", "4", "--batch", "8192",
+           "--save-frame", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    return line, np.load(out)
+
+
+def test_bench_launches_ranks_itself(tmp_path):
+    """bench.py --gpus 2 (no launcher around it) starts two ranks; both render
+    their tiles and the gathered frame equals the one-rank frame bit for bit
+    (gloo: both ranks share this box's GPU)."""
+    one, f1 = _bench(tmp_path, 1, "1")
+    two, f2 = _bench(tmp_path, 2, "2")
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert one["rays_per_frame"] == two["rays_per_frame"]
+    assert np.array_equal(f1, f2)
+    assert f1[..., :3].mean() > 0

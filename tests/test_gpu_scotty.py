@@ -55,10 +55,14 @@ def test_viewer_loop_matches_progressive_render(gpu_ctx, keys, frames_after_move
 
 
 def test_viewer_pause():
-    """'p' pauses: renderPicture shows the frame without rendering more
-    samples; a second 'p' resumes."""
+    """'p' toggles pauseSim, which display.cpp's renderPicture never reads
+    (display.cpp:145-174 clears the update flag and renders regardless): every
+    displayed frame renders samples_per_frame more samples, paused or not, and
+    the frames equal those of a loop without the key."""
     scene = load_fixture("CBgems")
-    _, n = ptrace.scotty_viewer(scene, W, H, 2, "..p..")
-    assert n == 4
+    img_p, n = ptrace.scotty_viewer(scene, W, H, 2, "..p..")
+    assert n == 2 * 5
+    img, n2 = ptrace.scotty_viewer(scene, W, H, 2, ".....")
+    assert n2 == n and np.array_equal(img_p, img)
     _, n = ptrace.scotty_viewer(scene, W, H, 2, ".p.p.")
-    assert n == 6  # frames 1, 4 (resumed at 'p') and 5 render
+    assert n == 2 * 5
