@@ -1042,7 +1042,12 @@ __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wst
 // in registers (no ray records, hit words or path state in HBM).  Closest hits
 // use the same primitive tests and tie rule as the leaf code of
 // process_item (trace.hip); results are bit-identical to the wavefront path.
-template <bool REFA>
+// PT_PATH_TRI_BR: tri_test's branch mode in the single-leaf kernel (trace.hip)
+#ifndef PT_PATH_TRI_BR
+#define PT_PATH_TRI_BR 0
+#endif
+// SPH: the leaf may hold spheres (else the sphere branch is not compiled in)
+template <bool REFA, bool SPH = true>
 __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, int pcount, const RayV& r,
                                              uint32_t& prim, float& t) {
   float bt = r.tmax;
@@ -1055,12 +1060,12 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
     const float4 q0 = f4(P[0]), q1 = f4(P[1]), q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
     asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q2.x), "s"(q3.x), "s"(q4.x), "s"(q5.x));
     float tt;
-    if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
+    if (SPH && (__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
       tt = sphere_test(r.o, r.d, q0, q1);
     } else {
       // (a tri_outside pre-test does not pay here: extension rays of one wave
       // rarely all miss a plane, measured -7 % on CBempty)
-      tt = tri_test<REFA>(r.o, r.d, q0, q1, q2, q3, q4, q5, bt);
+      tt = tri_test<REFA, PT_PATH_TRI_BR>(r.o, r.d, q0, q1, q2, q3, q4, q5, bt);
     }
     if (tt >= 0.0f && (tt < bt || (tt == bt && bp < 0))) {
       bt = tt;
@@ -1074,7 +1079,7 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
 // any primitive at t in [0, tmax]; triangles whose plane hit is certainly
 // outside [0, tmax] for every lane (tri_outside: shadow rays toward the light
 // mostly point away from the walls or end before them) cost no division
-template <bool REFA>
+template <bool REFA, bool SPH = true>
 __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, int pcount, const RayV& r) {
   const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * 6);
   bool hit = false;
@@ -1084,12 +1089,13 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
     const float4 q0 = f4(P[0]), q1 = f4(P[1]), q3 = f4(P[3]);
     asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q3.x));
     float tt = -1.0f;
-    if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
+    if (SPH && (__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
       tt = sphere_test(r.o, r.d, q0, q1);
     } else {
       const float ndd = fdot(q3.x, q3.y, q3.z, r.d.x, r.d.y, r.d.z);
       const float num = q1.w - fdot(q3.x, q3.y, q3.z, r.o.x, r.o.y, r.o.z);
-      if (!tri_outside(ndd, num, r.tmax)) tt = tri_test<REFA>(r.o, r.d, q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), r.tmax);
+      if (!tri_outside(ndd, num, r.tmax))
+        tt = tri_test<REFA, PT_PATH_TRI_BR>(r.o, r.d, q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), r.tmax);
     }
     hit = hit || (tt >= 0.0f && tt <= r.tmax);
     if (!__any(!hit)) break;  // every active lane is occluded
@@ -1199,7 +1205,9 @@ static __device__ unsigned long long g_path_timing[PT_TIMING_WAVES * 8];
 // (35.9 -> 36.8 ms), while it shortens the tail of small chunks (a 1/8 share:
 // 5.05 -> 4.89 ms): the host takes it only when the chunk is small against the
 // resident lanes (PT_PATH_GUIDED_BELOW paths per lane, default 128).
-template <int NSH, bool REFA, bool GUIDED>
+// SPH: the leaf holds spheres (false: the sphere test is not compiled in; the
+// host picks the variant, pt_ctx::has_sphere)
+template <int NSH, bool REFA, bool GUIDED, bool SPH = true>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
     uint32_t* __restrict__ work, uint32_t nreg, uint32_t tail_unit) {
@@ -1317,7 +1325,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       float t = 0.0f;
       if (st.flags & F_EXT) {
         // (extension rays have tmax = inf: not carried across iterations)
-        leaf_closest<REFA>(S.prims, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t);
+        leaf_closest<REFA, SPH>(S.prims, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t);
         nrays++;
       }
       bool clear[NSH];
@@ -1334,7 +1342,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
             shr[s] = RayV{mk(q[0], q[TPB], q[2 * TPB]), mk(q[3 * TPB], q[4 * TPB], q[5 * TPB]), q[6 * TPB]};
             C[s] = mk(q[7 * TPB], q[8 * TPB], q[9 * TPB]);
           }
-          clear[s] = !leaf_occluded<REFA>(S.prims, pstart, pcount, shr[s]);
+          clear[s] = !leaf_occluded<REFA, SPH>(S.prims, pstart, pcount, shr[s]);
           nrays++;
         }
       }

@@ -60,10 +60,27 @@ __device__ __forceinline__ float edge_ref(const float4 N, float ex, float ey, fl
   const f3 C = cross(mk(ex, ey, ez), mk(P.x - v.x, P.y - v.y, P.z - v.z));
   return fdot(N.x, N.y, N.z, C.x, C.y, C.z);
 }
-template <bool REFA = false>
+// BR: how the per-lane rejections branch.  0: a branch after each test (a
+// wave skips the rest when every lane has rejected); 1: one branch after the
+// plane hit (t outside [tlo, tbest] or flat), the three edge tests
+// predicated; 2: no branch.  The same operations and result in every mode.
+template <bool REFA = false, int BR = 0>
 __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q0, const float4 q1,
                                           const float4 q2, const float4 q3, const float4 q4,
                                           const float4 q5, const float tbest, const float tlo = 0.0f) {
+  if constexpr (BR != 0 && !REFA) {
+    const float ndd = fdot(q3.x, q3.y, q3.z, d.x, d.y, d.z);
+    const bool flat = fabsf(ndd) < 1e-6f;
+    const float t = (q1.w - fdot(q3.x, q3.y, q3.z, o.x, o.y, o.z)) / ndd;
+    const bool out = flat | (t < tlo) | (t > tbest);
+    if (BR == 1 && out) return -1.0f;
+    const f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
+    const float e0 = fdot(q2.w, q3.w, q4.w, P.x - q0.x, P.y - q0.y, P.z - q0.z);
+    const float e1 = fdot(q4.x, q4.y, q4.z, P.x - q1.x, P.y - q1.y, P.z - q1.z);
+    const float e2 = fdot(q5.x, q5.y, q5.z, P.x - q2.x, P.y - q2.y, P.z - q2.z);
+    const bool miss = out | (e0 < 0.0f) | (e1 < 0.0f) | (e2 < 0.0f);
+    return miss ? -1.0f : t + 0.0f;  // (t + 0 maps -0 to +0, as t == 0 ? 0 : t)
+  }
   float ndd = fdot(q3.x, q3.y, q3.z, d.x, d.y, d.z);
   if (REFA ? fabsf(ndd) <= 1e-6f : fabsf(ndd) < 1e-6f) return -1.0f;
   float t = (q1.w - fdot(q3.x, q3.y, q3.z, o.x, o.y, o.z)) / ndd;

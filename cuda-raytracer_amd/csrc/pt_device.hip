@@ -699,8 +699,8 @@ int pt_create(pt_ctx** out, int device) {
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[0], k_path_leaf<1, false, true>, TPB, 0);
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[1], k_path_leaf<2, false, true>, TPB, 0);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[2], k_path_leaf<1, true, true>, TPB, 0);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[3], k_path_leaf<2, true, true>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[2], k_path_leaf<1, true, true, false>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[3], k_path_leaf<2, true, true, false>, TPB, 0);
     for (int i = 0; i < 4; ++i) c->path_grid[i] = std::max(1, ncu * std::max(1, nb[i]));
   }
   *out = c;
@@ -981,10 +981,14 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       const uint32_t blocks = std::min<uint32_t>(want, c->path_grid[kv]);
       // guided grabs only for chunks that are small against the resident lanes
       const bool guided = (uint64_t)M < (uint64_t)c->path_guided_below * blocks * TPB;
-      auto kpath = guided ? (kv == 0 ? k_path_leaf<1, false, true> : kv == 1 ? k_path_leaf<2, false, true>
-                             : kv == 2 ? k_path_leaf<1, true, true> : k_path_leaf<2, true, true>)
-                          : (kv == 0 ? k_path_leaf<1, false, false> : kv == 1 ? k_path_leaf<2, false, false>
-                             : kv == 2 ? k_path_leaf<1, true, false> : k_path_leaf<2, true, false>);
+      // (spheres: the sphere test compiled in; the reference arithmetic has none)
+      const bool sph = c->has_sphere;
+      auto kpath = guided ? (kv == 0 ? (sph ? k_path_leaf<1, false, true, true> : k_path_leaf<1, false, true, false>)
+                             : kv == 1 ? (sph ? k_path_leaf<2, false, true, true> : k_path_leaf<2, false, true, false>)
+                             : kv == 2 ? k_path_leaf<1, true, true, false> : k_path_leaf<2, true, true, false>)
+                          : (kv == 0 ? (sph ? k_path_leaf<1, false, false, true> : k_path_leaf<1, false, false, false>)
+                             : kv == 1 ? (sph ? k_path_leaf<2, false, false, true> : k_path_leaf<2, false, false, false>)
+                             : kv == 2 ? k_path_leaf<1, true, false, false> : k_path_leaf<2, true, false, false>);
       // guided grabs from nreg path regions (k_path_leaf path_grab): each
       // region's tail phases begin path_guide chunks per wave before its end
       const uint32_t nreg = (uint32_t)std::max(1, std::min<int>(c->path_regions, (int)std::min<uint32_t>(blocks, PATH_REGIONS_MAX)));

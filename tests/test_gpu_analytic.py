@@ -175,13 +175,16 @@ def test_closed_emissive_box_ref_arith(gpu_ctx, split):
 # ---- area light over a diffuse plane ---------------------------------------------------
 A_SIDE, HGT = 1.2, 0.9   # light edge, height over the plane
 LIGHT_C = np.array([0.2, 0.0, -0.3])
+# The estimator shades the hit point moved back along the ray by 1e-3
+# (its.pt += -r->d * 1e-3, cu:1224): the camera looks straight down, so NEE
+# starts 1e-3 above the plane (0.15 % more irradiance at this height).
+HIT_OFFSET = 1e-3
 
 
-def _light_integral(px, pz, power):
-    """integral over the light of cos_n cos_l / r^power dA for the plane point
-    (px, 0, pz) (both cosines = h / r for a parallel light)."""
+def _light_integral(px, pz, power, h=HGT - HIT_OFFSET):
+    """integral over the light of cos_n cos_l / r^power dA for the point
+    (px, HGT - h, pz) (both cosines = h / r for a parallel light)."""
     from scipy import integrate
-    h = HGT
     x0, z0 = LIGHT_C[0] - A_SIDE / 2 - px, LIGHT_C[2] - A_SIDE / 2 - pz
     f = lambda z, x: h * h / (x * x + z * z + h * h) ** (1 + power / 2)
     v, err = integrate.dblquad(f, x0, x0 + A_SIDE, z0, z0 + A_SIDE, epsabs=1e-13, epsrel=1e-11)
@@ -224,6 +227,6 @@ def test_light_integral_closed_forms():
     a, b = X / h, Y / h
     F = (a / math.sqrt(1 + a * a) * math.atan(b / math.sqrt(1 + a * a))
          + b / math.sqrt(1 + b * b) * math.atan(a / math.sqrt(1 + b * b))) / (2 * math.pi)
-    assert abs(_light_integral(LIGHT_C[0], LIGHT_C[2], 2) - 4 * math.pi * F) < 1e-10
+    assert abs(_light_integral(LIGHT_C[0], LIGHT_C[2], 2, h=h) - 4 * math.pi * F) < 1e-10
     g = h * math.atan(X * Y / (h * math.sqrt(h * h + X * X + Y * Y)))
-    assert abs(_light_integral(LIGHT_C[0], LIGHT_C[2], 1) - 4 * g) < 1e-10
+    assert abs(_light_integral(LIGHT_C[0], LIGHT_C[2], 1, h=h) - 4 * g) < 1e-10
