@@ -33,6 +33,7 @@ constexpr float INV_PI = 0.318309886183790671f;
 constexpr float REF_DIFFUSE_MULT = 0.3183f;  // BSDF_DIFFUSE_MULTIPLIER, cu:272
 constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
 constexpr int SHADE_REC = 5;  // float4 per hit-shading record (ShadeArgs::shade)
+constexpr uint32_t ERR_KERNARG = 2u;  // pt_ctx::d_err bit: k_path_leaf's kernel-argument layout check failed
 
 struct ShadeArgs {
   float4* ray;  // ray records (trace.h): ext ray of path p in slot p, shadow ray s in slot (1+s)N + p
@@ -128,6 +129,7 @@ struct RayV {
 // KR: re-read the light from the kernel argument segment at each use (only in
 // a kernel whose first argument is the ShadeArgs): its 16 SGPRs are then not
 // held, and spilled, across the whole path loop.
+// (KR = true only in k_path_leaf, which checks the layout at launch)
 template <bool KR>
 __device__ __forceinline__ pt_light light_of(const ShadeArgs& S) {
   if (KR) {
@@ -999,9 +1001,11 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   count_rays(S.rcount, n, sh + MAX_ROOT_TARGETS * 8);
 }
 
-// Work left (the host polls it: 0 = the chunk is done): live slots over all
-// workgroups plus the blocks no dispenser has handed out yet; with stats, also
-// the chunk's shaded vertices (stats[STAT_SHADED]).  A grid of LIVE_SUM_BLOCKS
+// Work left in paths (the host polls it: 0 = the chunk is done): live slots
+// over all workgroups, the unstarted rest of each workgroup's current block,
+// and POOL_BLOCK paths for every block no dispenser has handed out yet (the
+// chunk's last block may hold fewer: an upper bound); with stats, also the
+// chunk's shaded vertices (stats[STAT_SHADED]).  A grid of LIVE_SUM_BLOCKS
 // workgroups, one atomic each into the zeroed *live.
 constexpr int LIVE_SUM_BLOCKS = 64;
 __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wstate, uint32_t G, const uint32_t* pool,
@@ -1010,12 +1014,12 @@ __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wst
   unsigned long long v = 0, sh = 0;
   for (uint32_t b = blockIdx.x * 1024 + threadIdx.x; b < G; b += gridDim.x * 1024) {
     const uint4 w = wstate[b];
-    v += w.z;
+    v += w.z + (w.y > w.x ? w.y - w.x : 0u);
     sh += w.w;
   }
   if (blockIdx.x == 0 && threadIdx.x < POOLS) {
     const uint32_t lim = pool_limit(nblocks, threadIdx.x), c = pool[(size_t)threadIdx.x * CSTRIDE];
-    v += c < lim ? lim - c : 0u;
+    v += c < lim ? (unsigned long long)(lim - c) * POOL_BLOCK : 0ull;
   }
   v = wave_sum64(v);
   sh = wave_sum64(sh);
@@ -1030,7 +1034,7 @@ __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wst
       t += part[0][w];
       u += part[1][w];
     }
-    if (t) atomicAdd(live, (uint32_t)t);
+    if (t) atomicAdd(live, (uint32_t)min(t, 0xFFFFFFFFull));
     if (shaded && u) atomicAdd(shaded, u);
   }
 }
@@ -1210,11 +1214,12 @@ static __device__ unsigned long long g_path_timing[PT_TIMING_WAVES * 8];
 template <int NSH, bool REFA, bool GUIDED, bool SPH = true>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
-    uint32_t* __restrict__ work, uint32_t nreg, uint32_t tail_unit) {
+    uint32_t* __restrict__ work, uint32_t nreg, uint32_t tail_unit, uint32_t* __restrict__ err) {
   const uint32_t lid = lane_id();
-#ifdef PT_DBG_BOUNDS
   // light_of<true> reads the light at offsetof(ShadeArgs, light) of the
-  // kernel-argument segment: S must be this kernel's first parameter
+  // kernel-argument segment, so S must stay this kernel's FIRST parameter:
+  // checked at every launch (wave-uniform, a few cached scalar loads); a
+  // mismatch sets ERR_KERNARG and the kernel does nothing (pt_render fails)
   if (PT_PATH_LIGHT_RELOAD) {
     const pt_light a = light_of<true>(S), b = S.light;
     uint32_t wa[sizeof a / 4], wb[sizeof b / 4];
@@ -1223,9 +1228,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
     bool same = true;
 #pragma unroll
     for (uint32_t i = 0; i < sizeof a / 4; ++i) same = same && wa[i] == wb[i];
-    if (!same && blockIdx.x == 0 && threadIdx.x == 0) printf("PT_DBG_BOUNDS k_path_leaf: ShadeArgs is not at kernarg 0\n");
+    if (!same) {
+      if (threadIdx.x == 0) atomicOr(err, ERR_KERNARG);
+      return;
+    }
   }
-#endif
   uint32_t nrays = 0;
   // wave-uniform: the path region this wave grabs from (its workgroup's, then
   // the next ones as they run out) and how many regions it has found empty

@@ -736,6 +736,18 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
 #ifndef PT_LEAF_PAIR
 #define PT_LEAF_PAIR 0
 #endif
+// PT_LEAF_LDS (leaf-only level kernel): a leaf's records (<= LEAF_LDS_MAX
+// primitives, 96 B each) are staged in the wave's LDS region with coalesced
+// vector loads -- one memory round trip for the whole leaf, as the reference
+// stages <= 32 triangles in shared memory (cu:1128-1142) -- and each record is
+// read back with uniform-address LDS loads (then moved to SGPRs) instead of
+// one scalar round trip per primitive.
+#ifndef PT_LEAF_LDS
+#define PT_LEAF_LDS 0
+#endif
+constexpr int LEAF_LDS_MAX = 32;
+__device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+__device__ __forceinline__ float4 rfl4(const float4 v) { return make_float4(rfl(v.x), rfl(v.y), rfl(v.z), rfl(v.w)); }
 template <bool REFA = false, bool LEAF = false, bool TMIN = false>
 __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane, bool ids,
                                              bool out_ids, bool two_level) {
@@ -803,7 +815,33 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
         }
       }
     };
-    if constexpr (LEAF && PT_LEAF_PAIR) {
+    if constexpr (LEAF && PT_LEAF_LDS) {
+      // (leaves larger than LEAF_LDS_MAX go through in chunks of it)
+      __shared__ float4 s_leaf[TPB / 64][LEAF_LDS_MAX * 6];
+      float4* const Ls = s_leaf[threadIdx.x >> 6];
+      for (int c0 = 0; c0 < pcount; c0 += LEAF_LDS_MAX) {
+        const int nc = min(LEAF_LDS_MAX, pcount - c0);
+        const float4* __restrict__ G = A.prims + (size_t)(pstart + c0) * 6;
+        const int nv = nc * 6;
+        // (the last chunk's LDS reads are done: every lane passed its loop)
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const int i0 = (int)lid, i1 = 64 + (int)lid, i2 = 128 + (int)lid;
+        float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0, v2 = v0;
+        if (i0 < nv) v0 = G[i0];
+        if (i1 < nv) v1 = G[i1];
+        if (i2 < nv) v2 = G[i2];
+        if (i0 < nv) Ls[i0] = v0;
+        if (i1 < nv) Ls[i1] = v1;
+        if (i2 < nv) Ls[i2] = v2;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        for (int k = 0; k < nc; ++k) {
+          const float4* R = Ls + k * 6;
+          const float4 q0 = rfl4(R[0]), q1 = rfl4(R[1]), q2 = rfl4(R[2]), q3 = rfl4(R[3]), q4 = rfl4(R[4]),
+                       q5 = rfl4(R[5]);
+          test_prim(c0 + k, q0, q1, q2, q3, q4, q5);
+        }
+      }
+    } else if constexpr (LEAF && PT_LEAF_PAIR) {
       // two records per scalar round trip (leaf records come from L2, not the
       // scalar cache: the round trip, not the tests, bounds a leaf visit)
       for (int k = 0; k < pcount; k += 2, P += 12) {

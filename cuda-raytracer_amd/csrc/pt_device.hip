@@ -65,6 +65,12 @@ struct pt_ctx {
   std::vector<pt_node> nodes_host;
   pt_light light{};
   pt_camera camera{};
+  // The stored BVH boxes carry a guard band G = 2^-17 M (scene_internal.h
+  // box_guard) that keeps the fp32 slab test conservative for ray origins
+  // with |coordinates| up to ~22 M (M: the scene's largest coordinate
+  // magnitude); camera and query-ray origins beyond origin_bound = 16 M are
+  // refused (PT_E_UNSUPPORTED) rather than risking a culled grazing hit.
+  double origin_bound = INFINITY;
   pt_node* d_nodes = nullptr;
   float4* d_prims = nullptr;
   float4* d_prims_ref = nullptr;  // PT_FLAG_REF_ARITH records (ref_prim_records)
@@ -841,6 +847,29 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   HIPCHK(c, hipMemset(c->d_qoff, 0, (size_t)s->n_nodes * NLANE * 4));
   c->light = s->light;
   c->camera = s->camera;
+  {  // origin_bound: 16 x the largest magnitude of the scene's vertices, sphere extents, camera, light
+    double m = 0.0;
+    auto upd = [&](double v) { m = std::max(m, std::fabs(v)); };
+    for (int i = 0; i < s->n_prims; ++i) {
+      const float* q = s->prims[i].q;
+      uint32_t meta;
+      memcpy(&meta, &q[3], 4);
+      if ((meta >> 28) == PT_PRIM_SPHERE) {
+        for (int k = 0; k < 3; ++k) upd(std::fabs(q[k]) + q[4]);
+      } else {
+        for (int k = 0; k < 3; ++k) {
+          upd(q[k]);
+          upd(q[4 + k]);
+          upd(q[8 + k]);
+        }
+      }
+    }
+    for (int k = 0; k < 3; ++k) {
+      upd(s->camera.origin[k]);
+      upd(s->light.position[k]);
+    }
+    c->origin_bound = 16.0 * m;
+  }
   c->have_scene = true;
   c->cap_paths = 0;  // force re-derivation of root queue offsets
   c->cap_spp = 0;
@@ -849,6 +878,9 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
 
 int pt_set_camera(pt_ctx* c, const pt_camera* cam) {
   if (!c || !cam) return PT_E_INVALID;
+  for (int k = 0; k < 3; ++k)
+    if (!(std::fabs((double)cam->origin[k]) <= c->origin_bound))
+      return fail(c, PT_E_UNSUPPORTED, "pt_set_camera: origin beyond 16x the scene's extent (conservative box guard)");
   c->camera = *cam;
   return pt_clear(c);
 }
@@ -931,7 +963,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
 
   hipEvent_t t0 = c->ev[6], t1 = c->ev[7];
   HIPCHK(c, hipEventRecord(t0, c->stream));
-  bool first = true;
+  bool first = true, path_err = false;
   // chunks of spp_c samples of every owned pixel: M = npix * spp_c paths, each
   // path's radiance lands in res[j * npix + q] and is summed in sample order
   for (int done = 0; done < P->spp;) {
@@ -996,7 +1028,9 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
           ((uint64_t)blocks * (TPB / 64) + nreg - 1) / nreg * (uint64_t)c->path_guide, 1u << 22);
       HIPCHK(c, hipMemsetAsync(c->d_work, 0, (size_t)nreg * PATH_CTR_STRIDE * 4, c->stream));
       c->launch(pt_ctx::K_PATH, 0, kpath, dim3(blocks), dim3(TPB), S,
-                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work, nreg, tail_unit);
+                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work, nreg, tail_unit, c->d_err);
+      HIPCHK(c, hipMemcpyAsync(c->h_poll, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+      path_err = true;
       c->stats.passes += passes;
       if (first) c->stats.batch_paths = (int32_t)M;
     } else {
@@ -1081,7 +1115,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
           finished = true;
           break;
         }
-        // live slots + unstarted paths below 1/16 of the pool: the chunk's tail
+        // paths left (live slots + unstarted paths, k_live_sum) below 1/16
+        // of the pool: the chunk's tail, one pass per poll
         const int np = (uint64_t)nlive * 16 < N ? 1 : POLL_GROUP;
         if ((rc = enqueue_group(g + 2, np))) return rc;
         queued += (uint64_t)np;
@@ -1110,6 +1145,10 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   }
   HIPCHK(c, hipEventRecord(t1, c->stream));
   HIPCHK(c, hipEventSynchronize(t1));
+  if (path_err && (c->h_poll[0] & ERR_KERNARG)) {
+    c->timing = false;
+    return fail(c, PT_E_HIP, "k_path_leaf: ShadeArgs is not the kernel's first argument (light_of<true>)");
+  }
   float total = 0;
   hipEventElapsedTime(&total, t0, t1);
   c->stats.ms_total = total;
@@ -1224,7 +1263,11 @@ int pt_intersect_ex(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits, uin
   // render kernels' traversal unchanged
   std::vector<float> tmin;
   for (int32_t i = 0; i < n; ++i) {
-    const float t = rays[(size_t)8 * i + 7];
+    const float* r = rays + (size_t)8 * i;
+    if (!(std::fabs((double)r[0]) <= c->origin_bound && std::fabs((double)r[1]) <= c->origin_bound &&
+          std::fabs((double)r[2]) <= c->origin_bound))
+      return fail(c, PT_E_UNSUPPORTED, "pt_intersect: ray origin beyond 16x the scene's extent (conservative box guard)");
+    const float t = r[7];
     if (t != t) return fail(c, PT_E_INVALID, "pt_intersect: t_min is NaN");
     if (t > 0.0f) {
       if (tmin.empty()) tmin.assign((size_t)n, 0.0f);

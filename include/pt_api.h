@@ -235,6 +235,11 @@ const char* pt_last_error(const pt_ctx* ctx);
 int pt_device_count(int* n);
 
 int pt_load_scene(pt_ctx* ctx, const pt_scene_desc* scene);
+/* PT_E_UNSUPPORTED when the origin lies beyond 16 x the scene's largest
+ * coordinate magnitude M (vertices, sphere extents, the scene's camera and
+ * light): the stored boxes' guard band keeps the fp32 box test conservative
+ * only for origins within ~22 M.  pt_intersect applies the same bound to its
+ * ray origins. */
 int pt_set_camera(pt_ctx* ctx, const pt_camera* camera);
 
 /* Render parameters. */

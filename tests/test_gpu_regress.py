@@ -103,3 +103,24 @@ def test_bench_launches_ranks_itself(tmp_path):
     assert one["rays_per_frame"] == two["rays_per_frame"]
     assert np.array_equal(f1, f2)
     assert f1[..., :3].mean() > 0
+
+
+def test_origin_bound(gpu_ctx):
+    """Camera and query-ray origins beyond 16x the scene's extent are refused
+    (the boxes' guard band keeps the fp32 box test conservative only within
+    ~22x); origins inside still work."""
+    sc = load_fixture("CBbunny")
+    d = sc.desc()
+    gpu_ctx.load_scene(sc)
+    cam = ptrace.pt_camera.from_buffer_copy(bytes(d.camera))
+    cam.origin[2] = 1e4
+    with pytest.raises(ptrace.PTError) as e:
+        gpu_ctx.set_camera(cam)
+    assert e.value.code == ptrace.PT_E_UNSUPPORTED
+    rays = camera_rays(d, 100, seed=3)
+    rays[7, 0] = -1e5
+    with pytest.raises(ptrace.PTError) as e:
+        gpu_ctx.intersect(rays)
+    assert e.value.code == ptrace.PT_E_UNSUPPORTED
+    rays[7, 0] = 20.0  # CBbunny's extent is ~1.5: 16 x is 24
+    assert np.array_equal(gpu_ctx.intersect(rays), pyoracle.intersect(d, rays, use_bvh=True))
