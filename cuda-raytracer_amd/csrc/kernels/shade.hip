@@ -1046,31 +1046,20 @@ __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wst
 // in registers (no ray records, hit words or path state in HBM).  Closest hits
 // use the same primitive tests and tie rule as the leaf code of
 // process_item (trace.hip); results are bit-identical to the wavefront path.
-// PT_PATH_TRI_BR: tri_test's branch mode in the single-leaf kernel (trace.hip)
-#ifndef PT_PATH_TRI_BR
-#define PT_PATH_TRI_BR 0
-#endif
 // SPH: the leaf may hold spheres (else the sphere branch is not compiled in)
 template <bool REFA, bool SPH = true>
 __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, int pcount, const RayV& r,
                                              uint32_t& prim, float& t) {
   float bt = r.tmax;
   int bp = -1;
-  const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * 6);
-  for (int k = 0; k < pcount; ++k, P += 6) {
-    // the whole 96-B record in one scalar round trip: the empty use pins the
-    // loads above the sphere/triangle branch, which the compiler would wait on
-    // before issuing the rest (CBempty +0.8 %, CBspheres +0.4 %)
-    const float4 q0 = f4(P[0]), q1 = f4(P[1]), q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
-    asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q2.x), "s"(q3.x), "s"(q4.x), "s"(q5.x));
-    float tt;
-    if (SPH && (__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
-      tt = sphere_test(r.o, r.d, q0, q1);
-    } else {
-      // (a tri_outside pre-test does not pay here: extension rays of one wave
-      // rarely all miss a plane, measured -7 % on CBempty)
-      tt = tri_test<REFA, PT_PATH_TRI_BR>(r.o, r.d, q0, q1, q2, q3, q4, q5, bt);
-    }
+  constexpr int PS = prim_stride<REFA>();
+  const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * PS);
+  for (int k = 0; k < pcount; ++k, P += PS) {
+    // the whole record in one scalar round trip (load_prim)
+    const Prim q = load_prim<REFA>(P);
+    // (a tri_outside pre-test does not pay here: extension rays of one wave
+    // rarely all miss a plane, measured -7 % on CBempty)
+    const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1) : tri_test<REFA>(r.o, r.d, q, bt);
     if (tt >= 0.0f && (tt < bt || (tt == bt && bp < 0))) {
       bt = tt;
       bp = pstart + k;
@@ -1085,21 +1074,18 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
 // mostly point away from the walls or end before them) cost no division
 template <bool REFA, bool SPH = true>
 __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, int pcount, const RayV& r) {
-  const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * 6);
+  constexpr int PS = prim_stride<REFA>();
+  const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * PS);
   bool hit = false;
-  for (int k = 0; k < pcount; ++k, P += 6) {
-    // q0, q1 and q3 (the pre-test's operands) in one round trip; loading all
-    // six here as well measured -0.7 % (CBempty, CBspheres)
-    const float4 q0 = f4(P[0]), q1 = f4(P[1]), q3 = f4(P[3]);
-    asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q3.x));
+  for (int k = 0; k < pcount; ++k, P += PS) {
+    const Prim q = load_prim<REFA>(P);
     float tt = -1.0f;
-    if (SPH && (__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
-      tt = sphere_test(r.o, r.d, q0, q1);
+    if (SPH && prim_sphere<REFA>(q)) {
+      tt = sphere_test(r.o, r.d, q.q0, q.q1);
     } else {
-      const float ndd = fdot(q3.x, q3.y, q3.z, r.d.x, r.d.y, r.d.z);
-      const float num = q1.w - fdot(q3.x, q3.y, q3.z, r.o.x, r.o.y, r.o.z);
-      if (!tri_outside(ndd, num, r.tmax))
-        tt = tri_test<REFA, PT_PATH_TRI_BR>(r.o, r.d, q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), r.tmax);
+      float ndd, num;
+      plane_nd<REFA>(r.o, r.d, q, ndd, num);
+      if (!tri_outside<REFA>(ndd, num, r.tmax)) tt = tri_test<REFA>(r.o, r.d, q, r.tmax);
     }
     hit = hit || (tt >= 0.0f && tt <= r.tmax);
     if (!__any(!hit)) break;  // every active lane is occluded

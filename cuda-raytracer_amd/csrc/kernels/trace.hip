@@ -35,18 +35,76 @@
 
 namespace pt {
 
-// ---- primitive tests ----------------------------------------------------------
-
-// Reference triangle test intersectRayTriangle (cu:217-270) on precomputed
-// operands (pt_api.h pt_prim): plane hit, then the three edge-side tests, each
-// dot(m_k, P - v_k) with m_k = N x e_k (the reference's dot(N, cross(e_k,
-// P - v_k)) without its per-ray cross products).  Dot products and P = o + t d
-// are FMA chains (what nvcc makes of the reference's expressions under its
-// default --fmad=true): dot(a, b) = fma(a.z, b.z, fma(a.y, b.y, a.x * b.x)).
-// Returns t >= 0 or -1 on a miss.  t = -0 is returned as +0 so that the
+// ---- primitive records and tests ------------------------------------------------
+//
+// Device primitive records (built by pt_load_scene from the pt_api.h pt_prim
+// format).  Default arithmetic: PREC = 4 float4 per primitive --
+//   triangle: rows U, V, W of its Baldwin-Weber transform (Baldwin & Weber,
+//     JCGT 5(3) 2016): the affine map taking world space to the triangle's
+//     barycentric frame (v0 -> 0, v1 -> (1,0,0), v2 -> (0,1,0), the plane to
+//     w = 0), computed in double from the fp32 vertices, stored as fp32 rows
+//     {a, b, c, d} (value = a x + b y + c z + d), then {meta, 0, 0, 0};
+//   sphere: {centre, 0}, {radius, radius^2, 0, 0}, 0, {meta, 0, 0, 0}.
+// The ray's plane hit is t = -W(o) / W(d) and it hits the triangle iff
+// u = U(o) + t U(d) >= 0, v = V(o) + t V(d) >= 0 and u + v <= 1 -- the
+// reference's plane hit + inside test (intersectRayTriangle, cu:217-270) in
+// 6 multiply-adds fewer per test than its per-ray edge cross products, and
+// no vertex data.  PT_FLAG_REF_ARITH (REFA): 6 float4 per primitive, the
+// reference's literal operands (ref_prim_records) and test (tri_test).
+// Dot products and FMA chains: dot(a, b) = fma(a.z, b.z, fma(a.y, b.y,
+// a.x * b.x)) (what nvcc makes of the reference's expressions under its
+// default --fmad=true); the oracle (ptoracle.c) spells every one with fmaf.
+// Tests return t >= 0 or -1 on a miss; t = -0 is returned as +0 so that the
 // {t bits, id} key orders correctly.
 __device__ __forceinline__ float fdot(float ax, float ay, float az, float bx, float by, float bz) {
   return __builtin_fmaf(az, bz, __builtin_fmaf(ay, by, ax * bx));
+}
+template <bool REFA>
+constexpr int prim_stride() {
+  return REFA ? 6 : 4;
+}
+struct Prim {
+  float4 q0, q1, q2, q3, q4, q5;  // (q4, q5: REFA records only)
+};
+// a primitive's record in SGPRs, one scalar round trip (the empty use pins
+// every load above the sphere/triangle branch; the compiler would otherwise
+// wait on the meta word before issuing the rest)
+template <bool REFA>
+__device__ __forceinline__ Prim load_prim(const CPTR(f4v) P) {
+  Prim r;
+  r.q0 = f4(P[0]);
+  r.q1 = f4(P[1]);
+  r.q2 = f4(P[2]);
+  r.q3 = f4(P[3]);
+  if constexpr (REFA) {
+    r.q4 = f4(P[4]);
+    r.q5 = f4(P[5]);
+    asm volatile("" ::"s"(r.q0.w), "s"(r.q1.x), "s"(r.q2.x), "s"(r.q3.x), "s"(r.q4.x), "s"(r.q5.x));
+  } else {
+    r.q4 = r.q5 = make_float4(0.f, 0.f, 0.f, 0.f);
+    asm volatile("" ::"s"(r.q0.x), "s"(r.q1.x), "s"(r.q2.x), "s"(r.q3.x));
+  }
+  return r;
+}
+template <bool REFA>
+__device__ __forceinline__ bool prim_sphere(const Prim& q) {
+  return !REFA && (__float_as_uint(q.q3.x) >> 28) == PT_PRIM_SPHERE;
+}
+// Baldwin-Weber triangle test (default arithmetic): one branch after the
+// plane hit (a wave skips the inside test when no lane has t in [tlo, tbest]),
+// the inside test predicated.  A ray parallel to the plane has t = +-inf or
+// NaN and misses.
+__device__ __forceinline__ float bw_plane(const f3 o, const float4 W) {
+  return __builtin_fmaf(W.z, o.z, __builtin_fmaf(W.y, o.y, __builtin_fmaf(W.x, o.x, W.w)));
+}
+__device__ __forceinline__ float bw_test(const f3 o, const f3 d, const float4 U, const float4 V, const float4 W,
+                                         float tbest, float tlo = 0.0f) {
+  const float t = -bw_plane(o, W) / fdot(W.x, W.y, W.z, d.x, d.y, d.z);
+  if (!(t >= tlo) | (t > tbest)) return -1.0f;
+  const float u = __builtin_fmaf(t, fdot(U.x, U.y, U.z, d.x, d.y, d.z), bw_plane(o, U));
+  const float v = __builtin_fmaf(t, fdot(V.x, V.y, V.z, d.x, d.y, d.z), bw_plane(o, V));
+  const bool miss = (u < 0.0f) | (v < 0.0f) | (u + v > 1.0f);
+  return miss ? -1.0f : t + 0.0f;  // (t + 0 maps -0 to +0)
 }
 // PT_FLAG_REF_ARITH (REFA): the literal edge test of cu:251-267,
 // dot(N, cross(e_k, P - v_k)) < 0, on the reference-arithmetic primitive
@@ -60,47 +118,39 @@ __device__ __forceinline__ float edge_ref(const float4 N, float ex, float ey, fl
   const f3 C = cross(mk(ex, ey, ez), mk(P.x - v.x, P.y - v.y, P.z - v.z));
   return fdot(N.x, N.y, N.z, C.x, C.y, C.z);
 }
-// BR: how the per-lane rejections branch.  0: a branch after each test (a
-// wave skips the rest when every lane has rejected); 1: one branch after the
-// plane hit (t outside [tlo, tbest] or flat), the three edge tests
-// predicated; 2: no branch.  The same operations and result in every mode.
-template <bool REFA = false, int BR = 0>
-__device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q0, const float4 q1,
-                                          const float4 q2, const float4 q3, const float4 q4,
-                                          const float4 q5, const float tbest, const float tlo = 0.0f) {
-  if constexpr (BR != 0 && !REFA) {
-    const float ndd = fdot(q3.x, q3.y, q3.z, d.x, d.y, d.z);
-    const bool flat = fabsf(ndd) < 1e-6f;
-    const float t = (q1.w - fdot(q3.x, q3.y, q3.z, o.x, o.y, o.z)) / ndd;
-    const bool out = flat | (t < tlo) | (t > tbest);
-    if (BR == 1 && out) return -1.0f;
-    const f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
-    const float e0 = fdot(q2.w, q3.w, q4.w, P.x - q0.x, P.y - q0.y, P.z - q0.z);
-    const float e1 = fdot(q4.x, q4.y, q4.z, P.x - q1.x, P.y - q1.y, P.z - q1.z);
-    const float e2 = fdot(q5.x, q5.y, q5.z, P.x - q2.x, P.y - q2.y, P.z - q2.z);
-    const bool miss = out | (e0 < 0.0f) | (e1 < 0.0f) | (e2 < 0.0f);
-    return miss ? -1.0f : t + 0.0f;  // (t + 0 maps -0 to +0, as t == 0 ? 0 : t)
-  }
+// The reference's literal test (REFA records): plane hit, then the three edge
+// tests dot(N, cross(e_k, P - v_k)) < 0 (cu:223-267).
+__device__ __forceinline__ float tri_test_ref(const f3 o, const f3 d, const float4 q0, const float4 q1,
+                                              const float4 q2, const float4 q3, const float4 q4, const float4 q5,
+                                              const float tbest, const float tlo = 0.0f) {
   float ndd = fdot(q3.x, q3.y, q3.z, d.x, d.y, d.z);
-  if (REFA ? fabsf(ndd) <= 1e-6f : fabsf(ndd) < 1e-6f) return -1.0f;
+  if (fabsf(ndd) <= 1e-6f) return -1.0f;
   float t = (q1.w - fdot(q3.x, q3.y, q3.z, o.x, o.y, o.z)) / ndd;
   // t > tbest cannot win (ties need t == tbest): skip the edge tests; hits
   // before the ray's t_min (tlo >= 0, pt_intersect) do not count
   if (t < tlo || t > tbest) return -1.0f;
   f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
-  if constexpr (REFA) {
-    if (edge_ref(q3, q2.w, q3.w, q4.w, P, q0) < 0.0f) return -1.0f;
-    if (edge_ref(q3, q4.x, q4.y, q4.z, P, q1) < 0.0f) return -1.0f;
-    if (edge_ref(q3, q5.x, q5.y, q5.z, P, q2) < 0.0f) return -1.0f;
-    return t == 0.0f ? 0.0f : t;
-  }
-  // edge 0 (v0 -> v1)
-  if (fdot(q2.w, q3.w, q4.w, P.x - q0.x, P.y - q0.y, P.z - q0.z) < 0.0f) return -1.0f;
-  // edge 1 (v1 -> v2)
-  if (fdot(q4.x, q4.y, q4.z, P.x - q1.x, P.y - q1.y, P.z - q1.z) < 0.0f) return -1.0f;
-  // edge 2 (v2 -> v0)
-  if (fdot(q5.x, q5.y, q5.z, P.x - q2.x, P.y - q2.y, P.z - q2.z) < 0.0f) return -1.0f;
+  if (edge_ref(q3, q2.w, q3.w, q4.w, P, q0) < 0.0f) return -1.0f;
+  if (edge_ref(q3, q4.x, q4.y, q4.z, P, q1) < 0.0f) return -1.0f;
+  if (edge_ref(q3, q5.x, q5.y, q5.z, P, q2) < 0.0f) return -1.0f;
   return t == 0.0f ? 0.0f : t;
+}
+// A triangle's closest-hit test in the record's arithmetic.
+template <bool REFA>
+__device__ __forceinline__ float tri_test(const f3 o, const f3 d, const Prim& q, float tbest, float tlo = 0.0f) {
+  if constexpr (REFA) return tri_test_ref(o, d, q.q0, q.q1, q.q2, q.q3, q.q4, q.q5, tbest, tlo);
+  else return bw_test(o, d, q.q0, q.q1, q.q2, tbest, tlo);
+}
+// The plane hit as t = num / ndd, for the division-free pre-test.
+template <bool REFA>
+__device__ __forceinline__ void plane_nd(const f3 o, const f3 d, const Prim& q, float& ndd, float& num) {
+  if constexpr (REFA) {
+    ndd = fdot(q.q3.x, q.q3.y, q.q3.z, d.x, d.y, d.z);
+    num = q.q1.w - fdot(q.q3.x, q.q3.y, q.q3.z, o.x, o.y, o.z);
+  } else {
+    ndd = fdot(q.q2.x, q.q2.y, q.q2.z, d.x, d.y, d.z);
+    num = -bw_plane(o, q.q2);
+  }
 }
 
 // Division-free early rejection: true only when the plane hit of tri_test is
@@ -111,9 +161,12 @@ __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const float4 q
 //  * same signs, tmax >= 2^-60: x = RN(RN(tmax |ndd|) (1 + 2^-20)) exceeds
 //    tmax |ndd| (1 + 2^-21), so |num| > x gives q > tmax (1 + 2^-21), which
 //    rounds above tmax (tmax = inf never rejects).
+// (FLAT: the test rejects |ndd| <= 1e-6 as parallel, REFA; the Baldwin-Weber
+// test has no such rejection)
+template <bool FLAT = true>
 __device__ __forceinline__ bool tri_outside(float ndd, float num, float tmax) {
   const float an = fabsf(num), ad = fabsf(ndd);
-  const bool flat = ad < 1e-6f;
+  const bool flat = FLAT && ad <= 1e-6f;
   const bool behind = ((num < 0.0f) != (ndd < 0.0f)) & (an > 0x1p-60f) & (ad < 0x1p60f);
   const bool beyond = ((num < 0.0f) == (ndd < 0.0f)) & (tmax >= 0x1p-60f) & (an > (tmax * ad) * (1.0f + 0x1p-20f));
   return flat | behind | beyond;
@@ -136,11 +189,6 @@ __device__ __forceinline__ f2v fdot2(const f3x2& a, const f3x2& b) {
   return fma2(a.z, b.z, fma2(a.y, b.y, a.x * b.x));
 }
 
-// dot(m, P - v) on two lanes: the edge-side test
-__device__ __forceinline__ f2v edge_side2(const f3x2& P, const f3x2& v, const f3x2& m) {
-  return fma2(m.z, P.z - v.z, fma2(m.y, P.y - v.y, m.x * (P.x - v.x)));
-}
-
 // dot(N, cross(e, P - v)) on two lanes (REFA: edge_ref, element for element)
 __device__ __forceinline__ f2v edge_ref2(const f3x2& N, const f3x2& P, const f3x2& v, const f3x2& e) {
   const f3x2 w{P.x - v.x, P.y - v.y, P.z - v.z};
@@ -148,18 +196,18 @@ __device__ __forceinline__ f2v edge_ref2(const f3x2& N, const f3x2& P, const f3x
   return fdot2(N, C);
 }
 
-// N: normal, pd: plane offset, v0..v2: vertices, m0..m2: edge normals (pt_prim
-// layout; under REFA the edges e0..e2, see tri_test)
-template <bool REFA = false>
-__device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const f3x2& N, f2v pd, const f3x2& v0,
-                                         const f3x2& v1, const f3x2& v2, const f3x2& m0, const f3x2& m1,
-                                         const f3x2& m2, f2v tbest, f2v tlo = f2v{0.0f, 0.0f}) {
+// REFA: N normal, pd plane offset, v0..v2 vertices, e0..e2 edges (the
+// reference's operands, tri_test_ref); element i is tri_test_ref of ray i
+template <bool REFA = true>
+__device__ __forceinline__ f2v tri_test2_ref(const f3x2& o, const f3x2& d, const f3x2& N, f2v pd, const f3x2& v0,
+                                             const f3x2& v1, const f3x2& v2, const f3x2& m0, const f3x2& m1,
+                                             const f3x2& m2, f2v tbest, f2v tlo = f2v{0.0f, 0.0f}) {
   const f2v ndd = fdot2(N, d);
   const f2v t = (pd - fdot2(N, o)) / ndd;
   const f3x2 P{fma2(t, d.x, o.x), fma2(t, d.y, o.y), fma2(t, d.z, o.z)};
-  const f2v s0 = REFA ? edge_ref2(N, P, v0, m0) : edge_side2(P, v0, m0);
-  const f2v s1 = REFA ? edge_ref2(N, P, v1, m1) : edge_side2(P, v1, m1);
-  const f2v s2 = REFA ? edge_ref2(N, P, v2, m2) : edge_side2(P, v2, m2);
+  const f2v s0 = edge_ref2(N, P, v0, m0);
+  const f2v s1 = edge_ref2(N, P, v1, m1);
+  const f2v s2 = edge_ref2(N, P, v2, m2);
   // t + 0 maps -0 to +0 and leaves every other value unchanged (strict fp:
   // the add is not folded away)
   const f2v tz = t + sp(0.0f);
@@ -167,11 +215,42 @@ __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const f3x
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     // non-short-circuit: every comparison is one v_cmp, combined on the SALU
-    const bool flat = REFA ? fabsf(ndd[i]) <= 1e-6f : fabsf(ndd[i]) < 1e-6f;
+    const bool flat = fabsf(ndd[i]) <= 1e-6f;
     const bool miss = flat | (t[i] < tlo[i]) | (t[i] > tbest[i]) | (s0[i] < 0.0f) | (s1[i] < 0.0f) | (s2[i] < 0.0f);
     r[i] = miss ? -1.0f : tz[i];
   }
   return r;
+}
+// Baldwin-Weber on two rays (element i is bw_test of ray i, branch-free)
+__device__ __forceinline__ f2v bw_plane2(const f3x2& o, const float4 R) {
+  return fma2(sp(R.z), o.z, fma2(sp(R.y), o.y, fma2(sp(R.x), o.x, sp(R.w))));
+}
+__device__ __forceinline__ f2v bw_test2(const f3x2& o, const f3x2& d, const float4 U, const float4 V, const float4 W,
+                                        f2v tbest, f2v tlo) {
+  const f2v t = -bw_plane2(o, W) / fdot2(sp3(W.x, W.y, W.z), d);
+  const f2v u = fma2(t, fdot2(sp3(U.x, U.y, U.z), d), bw_plane2(o, U));
+  const f2v v = fma2(t, fdot2(sp3(V.x, V.y, V.z), d), bw_plane2(o, V));
+  const f2v uv = u + v;
+  const f2v tz = t + sp(0.0f);
+  f2v r;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const bool miss = !(t[i] >= tlo[i]) | (t[i] > tbest[i]) | (u[i] < 0.0f) | (v[i] < 0.0f) | (uv[i] > 1.0f);
+    r[i] = miss ? -1.0f : tz[i];
+  }
+  return r;
+}
+// Two rays (pair j, j + 1) against triangle q in the record's arithmetic.
+template <bool REFA>
+__device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const Prim& q, f2v tbest, f2v tlo) {
+  if constexpr (REFA) {
+    const float4 q0 = q.q0, q1 = q.q1, q2 = q.q2, q3 = q.q3, q4 = q.q4, q5 = q.q5;
+    return tri_test2_ref(o, d, sp3(q3.x, q3.y, q3.z), sp(q1.w), sp3(q0.x, q0.y, q0.z), sp3(q1.x, q1.y, q1.z),
+                         sp3(q2.x, q2.y, q2.z), sp3(q2.w, q3.w, q4.w), sp3(q4.x, q4.y, q4.z),
+                         sp3(q5.x, q5.y, q5.z), tbest, tlo);
+  } else {
+    return bw_test2(o, d, q.q0, q.q1, q.q2, tbest, tlo);
+  }
 }
 
 // Ray-sphere (the reference has none: spheres are reinterpret_cast to
@@ -384,38 +463,23 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
                                   bt))
           continue;
         const int pstart = T.istart[i];
-        const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);
-        for (int kk = 0; kk < T.icount[i]; ++kk, P += 6) {
-          const float4 q0 = f4(P[0]), q1 = f4(P[1]);
-          // one scalar round trip: the operands the ray kind needs, issued
-          // with q0, q1 before the sphere/triangle branch (shade ms -0.3 to
-          // -1 % on CBbunny / the dragon proxy, frame time within noise)
-          const float4 q3p = f4(P[3]);
-          if (anyhit[j]) {
-            asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q3p.x));
-          } else {
-            const float4 q2p = f4(P[2]), q4p = f4(P[4]), q5p = f4(P[5]);
-            asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q2p.x), "s"(q3p.x), "s"(q4p.x), "s"(q5p.x));
-          }
+        constexpr int PS = prim_stride<REFA>();
+        const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * PS);
+        for (int kk = 0; kk < T.icount[i]; ++kk, P += PS) {
+          const Prim q = load_prim<REFA>(P);
           float tt;
-          if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE)
-            tt = sphere_test(o[j], d[j], q0, q1, tlo);
-          else if (anyhit[j]) {
+          if (prim_sphere<REFA>(q)) {
+            tt = sphere_test(o[j], d[j], q.q0, q.q1, tlo);
+          } else if (anyhit[j] || PT_ROOT_EXT_PRETEST) {
             // shadow rays: division-free pre-test (they mostly point away from
             // the walls or end before them, see tri_outside)
-            const float4 q3 = f4(P[3]);
-            const float ndd = fdot(q3.x, q3.y, q3.z, d[j].x, d[j].y, d[j].z);
-            const float num = q1.w - fdot(q3.x, q3.y, q3.z, o[j].x, o[j].y, o[j].z);
+            float ndd, num;
+            plane_nd<REFA>(o[j], d[j], q, ndd, num);
             tt = -1.0f;
-            if (!tri_outside(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), bt, tlo);
-          } else if (PT_ROOT_EXT_PRETEST) {
-            const float4 q3 = f4(P[3]);
-            const float ndd = fdot(q3.x, q3.y, q3.z, d[j].x, d[j].y, d[j].z);
-            const float num = q1.w - fdot(q3.x, q3.y, q3.z, o[j].x, o[j].y, o[j].z);
-            tt = -1.0f;
-            if (!tri_outside(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), q3, f4(P[4]), f4(P[5]), bt, tlo);
-          } else
-            tt = tri_test<REFA>(o[j], d[j], q0, q1, f4(P[2]), f4(P[3]), f4(P[4]), f4(P[5]), bt, tlo);
+            if (!tri_outside<REFA>(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q, bt, tlo);
+          } else {
+            tt = tri_test<REFA>(o[j], d[j], q, bt, tlo);
+          }
           // ties go to the lowest primitive across the inline leaves too
           // (their primitive ranges are not in increasing order)
           if (tt >= 0.0f && (tt < bt || (tt == bt && (bp < 0 || pstart + kk < bp)))) {
@@ -437,12 +501,6 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
   push_children<R, MAX_ROOT_TARGETS>(A, TableTargets{T}, lane, id, o, d, tm, pv, R, sh, false);
 }
 
-// the shared level kernel loads a leaf record in one round trip too (it now
-// fits its register budget: levels -0.3 to -0.5 ms per frame; round 1's
-// one-level kernel lost interior speed to it)
-#ifndef PT_SHARED_LEAF_LOAD1
-#define PT_SHARED_LEAF_LOAD1 1
-#endif
 // LEAF: the node is known to be a leaf (the leaf-only level kernel): the
 // interior code is not compiled in (fewer registers, more waves)
 template <bool IMPLICIT, bool REFA = false, bool LEAF = false, bool TMIN = false>
@@ -503,34 +561,26 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
       bt[j] = tmax[j];
       bp[j] = -1;
     }
-    const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);
-    for (int k = 0; k < pcount; ++k, P += 6) {
-      const float4 q0 = f4(P[0]), q1 = f4(P[1]);
-      if constexpr (LEAF) {  // one scalar round trip per record (see process_wave)
-        const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
-        asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q2.x), "s"(q3.x), "s"(q4.x), "s"(q5.x));
-      }
-      const uint32_t meta = __float_as_uint(q0.w);
-      if ((meta >> 28) == PT_PRIM_SPHERE) {
+    constexpr int PS = prim_stride<REFA>();
+    const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * PS);
+    for (int k = 0; k < pcount; ++k, P += PS) {
+      const Prim q = load_prim<REFA>(P);
+      if (prim_sphere<REFA>(q)) {
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {
           if (j >= nj) break;
-          float t = sphere_test(o[j], d[j], q0, q1, tlo[j]);
+          float t = sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]);
           if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
             bt[j] = t;
             bp[j] = pstart + k;
           }
         }
       } else {
-        const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
-        const f3x2 N = sp3(q3.x, q3.y, q3.z), v0 = sp3(q0.x, q0.y, q0.z), v1 = sp3(q1.x, q1.y, q1.z),
-                   v2 = sp3(q2.x, q2.y, q2.z), e0 = sp3(q2.w, q3.w, q4.w), e1 = sp3(q4.x, q4.y, q4.z),
-                   e2 = sp3(q5.x, q5.y, q5.z);  // edge normals m0, m1, m2
 #pragma unroll
         for (int j = 0; j < RPT; j += 2) {
           if (j >= nj) break;
-          const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
-                                   e2, f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
+          const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{bt[j], bt[j + 1]},
+                                         f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const float t = t2[i];
@@ -733,21 +783,6 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
   }
 }
 
-#ifndef PT_LEAF_PAIR
-#define PT_LEAF_PAIR 0
-#endif
-// PT_LEAF_LDS (leaf-only level kernel): a leaf's records (<= LEAF_LDS_MAX
-// primitives, 96 B each) are staged in the wave's LDS region with coalesced
-// vector loads -- one memory round trip for the whole leaf, as the reference
-// stages <= 32 triangles in shared memory (cu:1128-1142) -- and each record is
-// read back with uniform-address LDS loads (then moved to SGPRs) instead of
-// one scalar round trip per primitive.
-#ifndef PT_LEAF_LDS
-#define PT_LEAF_LDS 0
-#endif
-constexpr int LEAF_LDS_MAX = 32;
-__device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
-__device__ __forceinline__ float4 rfl4(const float4 v) { return make_float4(rfl(v.x), rfl(v.y), rfl(v.z), rfl(v.w)); }
 template <bool REFA = false, bool LEAF = false, bool TMIN = false>
 __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane, bool ids,
                                              bool out_ids, bool two_level) {
@@ -781,108 +816,28 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
       bt[j] = tmax[j];
       bp[j] = -1;
     }
-    const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * 6);
-    // one primitive's tests against the wave's rays (its record in SGPRs)
-    auto test_prim = [&](int k, const float4& q0, const float4& q1, const float4& q2, const float4& q3,
-                         const float4& q4, const float4& q5) {
-      if ((__float_as_uint(q0.w) >> 28) == PT_PRIM_SPHERE) {
+    constexpr int PS = prim_stride<REFA>();
+    const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * PS);
+    // one primitive's tests against the wave's rays (its record in SGPRs,
+    // loaded in one scalar round trip)
+    for (int k = 0; k < pcount; ++k, P += PS) {
+      const Prim q = load_prim<REFA>(P);
+      if (prim_sphere<REFA>(q)) {
 #pragma unroll
         for (int j = 0; j < RPTW; ++j) {
           if (j >= nj) break;
-          float t = sphere_test(o[j], d[j], q0, q1, tlo[j]);
+          float t = sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]);
           if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
             bt[j] = t;
             bp[j] = pstart + k;
           }
         }
       } else {
-        const f3x2 N = sp3(q3.x, q3.y, q3.z), v0 = sp3(q0.x, q0.y, q0.z), v1 = sp3(q1.x, q1.y, q1.z),
-                   v2 = sp3(q2.x, q2.y, q2.z), e0 = sp3(q2.w, q3.w, q4.w), e1 = sp3(q4.x, q4.y, q4.z),
-                   e2 = sp3(q5.x, q5.y, q5.z);  // edge normals m0, m1, m2
 #pragma unroll
         for (int j = 0; j < RPTW; j += 2) {
           if (j >= nj) break;
-          const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
-                                         e2, f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const float t = t2[i];
-            if (valid[j + i] && t >= 0.0f && (t < bt[j + i] || (t == bt[j + i] && bp[j + i] < 0))) {
-              bt[j + i] = t;
-              bp[j + i] = pstart + k;
-            }
-          }
-        }
-      }
-    };
-    if constexpr (LEAF && PT_LEAF_LDS) {
-      // (leaves larger than LEAF_LDS_MAX go through in chunks of it)
-      __shared__ float4 s_leaf[TPB / 64][LEAF_LDS_MAX * 6];
-      float4* const Ls = s_leaf[threadIdx.x >> 6];
-      for (int c0 = 0; c0 < pcount; c0 += LEAF_LDS_MAX) {
-        const int nc = min(LEAF_LDS_MAX, pcount - c0);
-        const float4* __restrict__ G = A.prims + (size_t)(pstart + c0) * 6;
-        const int nv = nc * 6;
-        // (the last chunk's LDS reads are done: every lane passed its loop)
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        const int i0 = (int)lid, i1 = 64 + (int)lid, i2 = 128 + (int)lid;
-        float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0, v2 = v0;
-        if (i0 < nv) v0 = G[i0];
-        if (i1 < nv) v1 = G[i1];
-        if (i2 < nv) v2 = G[i2];
-        if (i0 < nv) Ls[i0] = v0;
-        if (i1 < nv) Ls[i1] = v1;
-        if (i2 < nv) Ls[i2] = v2;
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        for (int k = 0; k < nc; ++k) {
-          const float4* R = Ls + k * 6;
-          const float4 q0 = rfl4(R[0]), q1 = rfl4(R[1]), q2 = rfl4(R[2]), q3 = rfl4(R[3]), q4 = rfl4(R[4]),
-                       q5 = rfl4(R[5]);
-          test_prim(c0 + k, q0, q1, q2, q3, q4, q5);
-        }
-      }
-    } else if constexpr (LEAF && PT_LEAF_PAIR) {
-      // two records per scalar round trip (leaf records come from L2, not the
-      // scalar cache: the round trip, not the tests, bounds a leaf visit)
-      for (int k = 0; k < pcount; k += 2, P += 12) {
-        const CPTR(f4v) P2 = k + 1 < pcount ? P + 6 : P;  // (uniform; an odd tail reloads the last record)
-        const float4 q0 = f4(P[0]), q1 = f4(P[1]), q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
-        const float4 u0 = f4(P2[0]), u1 = f4(P2[1]), u2 = f4(P2[2]), u3 = f4(P2[3]), u4 = f4(P2[4]), u5 = f4(P2[5]);
-        asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q2.x), "s"(q3.x), "s"(q4.x), "s"(q5.x));
-        asm volatile("" ::"s"(u0.w), "s"(u1.x), "s"(u2.x), "s"(u3.x), "s"(u4.x), "s"(u5.x));
-        test_prim(k, q0, q1, q2, q3, q4, q5);
-        if (k + 1 < pcount) test_prim(k + 1, u0, u1, u2, u3, u4, u5);
-      }
-    } else
-    for (int k = 0; k < pcount; ++k, P += 6) {
-      const float4 q0 = f4(P[0]), q1 = f4(P[1]);
-      if constexpr (LEAF || PT_SHARED_LEAF_LOAD1) {
-        // the whole 96-B record in one scalar round trip (the compiler waits
-        // on q0, q1 for the sphere/triangle branch before issuing the rest)
-        const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
-        asm volatile("" ::"s"(q0.w), "s"(q1.x), "s"(q2.x), "s"(q3.x), "s"(q4.x), "s"(q5.x));
-      }
-      const uint32_t meta = __float_as_uint(q0.w);
-      if ((meta >> 28) == PT_PRIM_SPHERE) {
-#pragma unroll
-        for (int j = 0; j < RPTW; ++j) {
-          if (j >= nj) break;
-          float t = sphere_test(o[j], d[j], q0, q1, tlo[j]);
-          if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
-            bt[j] = t;
-            bp[j] = pstart + k;
-          }
-        }
-      } else {
-        const float4 q2 = f4(P[2]), q3 = f4(P[3]), q4 = f4(P[4]), q5 = f4(P[5]);
-        const f3x2 N = sp3(q3.x, q3.y, q3.z), v0 = sp3(q0.x, q0.y, q0.z), v1 = sp3(q1.x, q1.y, q1.z),
-                   v2 = sp3(q2.x, q2.y, q2.z), e0 = sp3(q2.w, q3.w, q4.w), e1 = sp3(q4.x, q4.y, q4.z),
-                   e2 = sp3(q5.x, q5.y, q5.z);  // edge normals m0, m1, m2
-#pragma unroll
-        for (int j = 0; j < RPTW; j += 2) {
-          if (j >= nj) break;
-          const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), N, sp(q1.w), v0, v1, v2, e0, e1,
-                                   e2, f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
+          const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{bt[j], bt[j + 1]},
+                                         f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const float t = t2[i];

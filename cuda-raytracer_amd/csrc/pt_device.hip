@@ -634,6 +634,68 @@ static std::vector<pt_prim> ref_prim_records(const pt_scene_desc* s) {
   return out;
 }
 
+// The default arithmetic's records (trace.hip, 4 float4 per primitive): a
+// triangle's Baldwin-Weber rows U, V, W and {meta, 0, 0, 0}.  From the fp32
+// vertices A, B, C in double: e1 = B - A, e2 = C - A, n = e1 x e2 (component
+// by component, in this order), and with k the axis of n's largest magnitude
+// (x if |n.x| > |n.y| and |n.x| > |n.z|, else y if |n.y| > |n.z|, else z)
+// the rows that map v -> (u, v, w) with w = dot(n, v - A) / n_k; each entry
+// one double division, rounded once to fp32 (oracle/ptoracle.c bw_rows
+// restates the same operations).  A sphere: {centre, 0}, {radius,
+// radius^2, 0, 0}, 0, {meta, 0, 0, 0}.
+static void bw_rows(const float* q, double r[12]) {
+  const double A[3] = {q[0], q[1], q[2]}, B[3] = {q[4], q[5], q[6]}, C[3] = {q[8], q[9], q[10]};
+  double e1[3], e2[3], n[3];
+  for (int k = 0; k < 3; ++k) {
+    e1[k] = B[k] - A[k];
+    e2[k] = C[k] - A[k];
+  }
+  n[0] = e1[1] * e2[2] - e1[2] * e2[1];
+  n[1] = e1[2] * e2[0] - e1[0] * e2[2];
+  n[2] = e1[0] * e2[1] - e1[1] * e2[0];
+  const double an = n[0] * A[0] + n[1] * A[1] + n[2] * A[2];
+  if (std::fabs(n[0]) > std::fabs(n[1]) && std::fabs(n[0]) > std::fabs(n[2])) {
+    const double x = n[0];
+    const double rr[12] = {0, e2[2] / x, -e2[1] / x, (C[1] * A[2] - C[2] * A[1]) / x,
+                           0, -e1[2] / x, e1[1] / x, -(B[1] * A[2] - B[2] * A[1]) / x,
+                           1, n[1] / x, n[2] / x, -an / x};
+    memcpy(r, rr, sizeof rr);
+  } else if (std::fabs(n[1]) > std::fabs(n[2])) {
+    const double y = n[1];
+    const double rr[12] = {-e2[2] / y, 0, e2[0] / y, (C[2] * A[0] - C[0] * A[2]) / y,
+                           e1[2] / y, 0, -e1[0] / y, -(B[2] * A[0] - B[0] * A[2]) / y,
+                           n[0] / y, 1, n[2] / y, -an / y};
+    memcpy(r, rr, sizeof rr);
+  } else {
+    const double z = n[2];
+    const double rr[12] = {e2[1] / z, -e2[0] / z, 0, (C[0] * A[1] - C[1] * A[0]) / z,
+                           -e1[1] / z, e1[0] / z, 0, -(B[0] * A[1] - B[1] * A[0]) / z,
+                           n[0] / z, n[1] / z, 1, -an / z};
+    memcpy(r, rr, sizeof rr);
+  }
+}
+static std::vector<float4> bw_prim_records(const pt_scene_desc* s) {
+  std::vector<float4> out((size_t)s->n_prims * prim_stride<false>(), make_float4(0.f, 0.f, 0.f, 0.f));
+  for (int i = 0; i < s->n_prims; ++i) {
+    const float* q = s->prims[i].q;
+    uint32_t meta;
+    memcpy(&meta, &q[3], 4);
+    float4* o = &out[(size_t)i * prim_stride<false>()];
+    if ((meta >> 28) == PT_PRIM_SPHERE) {
+      o[0] = make_float4(q[0], q[1], q[2], 0.f);
+      o[1] = make_float4(q[4], q[5], 0.f, 0.f);
+    } else {
+      double r[12];
+      bw_rows(q, r);
+      o[0] = make_float4((float)r[0], (float)r[1], (float)r[2], (float)r[3]);
+      o[1] = make_float4((float)r[4], (float)r[5], (float)r[6], (float)r[7]);
+      o[2] = make_float4((float)r[8], (float)r[9], (float)r[10], (float)r[11]);
+    }
+    o[3] = make_float4(q[3], 0.f, 0.f, 0.f);
+  }
+  return out;
+}
+
 static void build_owned_pixels(pt_ctx* c, int W, int H, int T, int rank, int nranks) {
   c->pix_of.clear();
   const int ntx = (W + T - 1) / T, nty = (H + T - 1) / T;
@@ -792,7 +854,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     HIPCHK(c, hipMemcpy(c->d_kmap, km.data(), KMAP_SIZE * 4, hipMemcpyHostToDevice));
   }
   if ((rc = dalloc(c, &c->d_nodes, s->n_nodes))) return rc;
-  if ((rc = dalloc(c, &c->d_prims, (size_t)s->n_prims * 6))) return rc;
+  if ((rc = dalloc(c, &c->d_prims, (size_t)s->n_prims * prim_stride<false>()))) return rc;
   if ((rc = dalloc(c, &c->d_prims_ref, (size_t)s->n_prims * 6))) return rc;
   if ((rc = dalloc(c, &c->d_shade, (size_t)s->n_prims * SHADE_REC))) return rc;
   if ((rc = dalloc(c, &c->d_bsdfs, std::max(1, s->n_bsdfs)))) return rc;
@@ -818,7 +880,10 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
           if (ch >= 0 && dn[ch].prim_count > 0) c->level_has_leaf[l + 1] = 1;  // (children sit one level down)
         }
   }
-  HIPCHK(c, hipMemcpy(c->d_prims, s->prims, sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));
+  {
+    const std::vector<float4> rec = bw_prim_records(s);
+    HIPCHK(c, hipMemcpy(c->d_prims, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice));
+  }
   {
     const std::vector<pt_prim> ref = ref_prim_records(s);
     HIPCHK(c, hipMemcpy(c->d_prims_ref, ref.data(), sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));

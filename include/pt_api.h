@@ -67,9 +67,11 @@ extern "C" {
 #define PT_PRIM_SPHERE 1u
 
 /* One intersectable primitive, 96 bytes = 6 x float4, in BVH-sorted order
- * (the order of BVHAccel::getSortedPrimitives(), bvh.cpp:384).  Triangles store
- * the operands of the reference triangle test (cu:217-270) in the form the
- * kernels evaluate it:
+ * (the order of BVHAccel::getSortedPrimitives(), bvh.cpp:384): the flattened
+ * scene's record (the device keeps its own forms of it: pt_load_scene derives
+ * the Baldwin-Weber rows the default test evaluates and the literal operands
+ * of PT_FLAG_REF_ARITH from the vertices).  Triangles store the
+ * operands of the reference triangle test (cu:217-270):
  *   q0 = v0.xyz, meta        q1 = v1.xyz, dN = dot(N, v0)
  *   q2 = v2.xyz, m0.x        q3 = N.xyz (= cross(v1-v0, v2-v0)), m0.y
  *   q4 = m1.xyz, m0.z        q5 = m2.xyz, 0

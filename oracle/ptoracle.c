@@ -6,7 +6,8 @@
  * checker.  The product path (libptcore.so) never links, loads or calls it.
  *
  * It restates, with the parity decisions of SURVEY.md §8(a):
- *   intersectRayTriangle         src/cudaRenderer.cu:217-270   -> pto_tri
+ *   intersectRayTriangle         src/cudaRenderer.cu:217-270   -> pto_tri (the build's
+ *                                Baldwin-Weber form) / pto_tri_ref (literal)
  *   kernelMergeIntersections     cu:515-540 (min over candidates) -> pto_closest_brute
  *   rayIntersectSingle leaf loop cu:1144-1169                   -> pto_closest_bvh
  *   kernelPrimaryRays            cu:312-376                     -> camera_ray
@@ -138,24 +139,66 @@ static void sincos2pi(float u, float* s, float* c) {
 void pto_sincos2pi(float u, float* s, float* c) { sincos2pi(u, s, c); }
 
 /* ---- primitive tests -------------------------------------------------------- */
-/* intersectRayTriangle, cu:217-270: plane hit then three edge sign tests,
- * dot(N, cross(e_k, P - v_k)) evaluated as dot(m_k, P - v_k) with the
- * precomputed edge normals m_k = N x e_k (pt_api.h pt_prim layout). */
-/* dot products and P = o + t d as FMA chains, exactly as trace.hip:
+/* dot products as FMA chains, exactly as trace.hip:
  * fdot(a, b) = fma(a.z, b.z, fma(a.y, b.y, a.x * b.x)) */
 static inline float fdot(float ax, float ay, float az, float bx, float by, float bz) {
   return fmaf(az, bz, fmaf(ay, by, ax * bx));
 }
-static float pto_tri(v3 o, v3 d, const float* q) {
-  float ndd = fdot(q[12], q[13], q[14], d.x, d.y, d.z);
-  if (fabsf(ndd) < 1e-6f) return -1.0f;
-  float t = (q[7] - fdot(q[12], q[13], q[14], o.x, o.y, o.z)) / ndd;
-  if (t < 0.0f) return -1.0f;
-  v3 P = mk(fmaf(t, d.x, o.x), fmaf(t, d.y, o.y), fmaf(t, d.z, o.z));
-  if (fdot(q[11], q[15], q[19], P.x - q[0], P.y - q[1], P.z - q[2]) < 0.0f) return -1.0f;
-  if (fdot(q[16], q[17], q[18], P.x - q[4], P.y - q[5], P.z - q[6]) < 0.0f) return -1.0f;
-  if (fdot(q[20], q[21], q[22], P.x - q[8], P.y - q[9], P.z - q[10]) < 0.0f) return -1.0f;
-  return t == 0.0f ? 0.0f : t;
+/* The build's triangle test (the default arithmetic; trace.hip bw_test): the
+ * reference's plane hit + inside test (intersectRayTriangle, cu:217-270) on
+ * the triangle's Baldwin-Weber transform (Baldwin & Weber, JCGT 5(3) 2016).
+ * bw_rows restates pt_device.hip's record builder: from the fp32 vertices in
+ * double, e1 = B - A, e2 = C - A, n = e1 x e2, k = the axis of n's largest
+ * magnitude, and rows U, V, W (value = a x + b y + c z + d) with W the plane
+ * scaled by 1 / n_k; each entry one double division rounded to fp32. */
+static void bw_rows(const float* q, float out[12]) {
+  const double A[3] = {q[0], q[1], q[2]}, B[3] = {q[4], q[5], q[6]}, C[3] = {q[8], q[9], q[10]};
+  double e1[3], e2[3], n[3], r[12];
+  for (int k = 0; k < 3; ++k) {
+    e1[k] = B[k] - A[k];
+    e2[k] = C[k] - A[k];
+  }
+  n[0] = e1[1] * e2[2] - e1[2] * e2[1];
+  n[1] = e1[2] * e2[0] - e1[0] * e2[2];
+  n[2] = e1[0] * e2[1] - e1[1] * e2[0];
+  const double an = n[0] * A[0] + n[1] * A[1] + n[2] * A[2];
+  if (fabs(n[0]) > fabs(n[1]) && fabs(n[0]) > fabs(n[2])) {
+    const double x = n[0];
+    r[0] = 0; r[1] = e2[2] / x; r[2] = -e2[1] / x; r[3] = (C[1] * A[2] - C[2] * A[1]) / x;
+    r[4] = 0; r[5] = -e1[2] / x; r[6] = e1[1] / x; r[7] = -(B[1] * A[2] - B[2] * A[1]) / x;
+    r[8] = 1; r[9] = n[1] / x; r[10] = n[2] / x; r[11] = -an / x;
+  } else if (fabs(n[1]) > fabs(n[2])) {
+    const double y = n[1];
+    r[0] = -e2[2] / y; r[1] = 0; r[2] = e2[0] / y; r[3] = (C[2] * A[0] - C[0] * A[2]) / y;
+    r[4] = e1[2] / y; r[5] = 0; r[6] = -e1[0] / y; r[7] = -(B[2] * A[0] - B[0] * A[2]) / y;
+    r[8] = n[0] / y; r[9] = 1; r[10] = n[2] / y; r[11] = -an / y;
+  } else {
+    const double z = n[2];
+    r[0] = e2[1] / z; r[1] = -e2[0] / z; r[2] = 0; r[3] = (C[0] * A[1] - C[1] * A[0]) / z;
+    r[4] = -e1[1] / z; r[5] = e1[0] / z; r[6] = 0; r[7] = -(B[0] * A[1] - B[1] * A[0]) / z;
+    r[8] = n[0] / z; r[9] = n[1] / z; r[10] = 1; r[11] = -an / z;
+  }
+  for (int i = 0; i < 12; ++i) out[i] = (float)r[i];
+}
+/* every triangle's rows (12 floats per primitive; spheres: zeros) */
+static float* bw_table(const pt_scene_desc* S) {
+  float* t = (float*)calloc((size_t)(S->n_prims > 0 ? S->n_prims : 1) * 12, sizeof(float));
+  for (int i = 0; i < S->n_prims; ++i) {
+    uint32_t meta;
+    memcpy(&meta, &S->prims[i].q[3], 4);
+    if ((meta >> 28) != PT_PRIM_SPHERE) bw_rows(S->prims[i].q, t + (size_t)12 * i);
+  }
+  return t;
+}
+static inline float bw_plane(const float* R, v3 o) { return fmaf(R[2], o.z, fmaf(R[1], o.y, fmaf(R[0], o.x, R[3]))); }
+/* t = -W(o) / W(d); a hit iff t >= tlo, u = U(o) + t U(d) >= 0, v >= 0, u + v <= 1 */
+static float pto_tri(v3 o, v3 d, const float* M, float tlo) {
+  const float t = -bw_plane(M + 8, o) / fdot(M[8], M[9], M[10], d.x, d.y, d.z);
+  if (!(t >= tlo)) return -1.0f;
+  const float u = fmaf(t, fdot(M[0], M[1], M[2], d.x, d.y, d.z), bw_plane(M, o));
+  const float v = fmaf(t, fdot(M[4], M[5], M[6], d.x, d.y, d.z), bw_plane(M + 4, o));
+  if (u < 0.0f || v < 0.0f || u + v > 1.0f) return -1.0f;
+  return t + 0.0f; /* (-0 -> +0) */
 }
 /* intersectRayTriangle, cu:217-270, literally (PT_FLAG_REF_ARITH): N and
  * dot(N, v0) per call, edge k rejected when dot(N, cross(e_k, P - v_k)) < 0,
@@ -188,12 +231,14 @@ static float pto_sphere(v3 o, v3 d, const float* q, float tlo) {
   if (t < tlo) return -1.0f;
   return t == 0.0f ? 0.0f : t;
 }
-/* t of the primitive's hit with t >= tlo, or -1 */
-static inline float prim_test(const pt_prim* p, v3 o, v3 d, int ref, float tlo) {
+/* t of primitive i's hit with t >= tlo, or -1 (bw: the scene's rows, bw_table) */
+static inline float prim_test(const pt_scene_desc* S, const float* bw, int i, v3 o, v3 d, int ref, float tlo) {
+  const pt_prim* p = &S->prims[i];
   uint32_t meta;
   memcpy(&meta, &p->q[3], 4);
   if ((meta >> 28) == PT_PRIM_SPHERE) return pto_sphere(o, d, p->q, tlo);
-  const float t = ref ? pto_tri_ref(o, d, p->q) : pto_tri(o, d, p->q);
+  if (!ref) return pto_tri(o, d, bw + (size_t)12 * i, tlo);
+  const float t = pto_tri_ref(o, d, p->q);
   return t >= tlo ? t : -1.0f;
 }
 /* A ray record: o.xyz, tmax, d.xyz, t_min (BVHAccel's Ray::min_t; pt_api.h
@@ -207,12 +252,12 @@ static inline uint64_t key(float t, uint32_t prim) {
 }
 
 /* Closest hit by brute force: min over all primitives of (t, index), t <= tmax. */
-static uint64_t closest_brute(const pt_scene_desc* S, const float* ray, int ref) {
+static uint64_t closest_brute(const pt_scene_desc* S, const float* bw, const float* ray, int ref) {
   v3 o = mk(ray[0], ray[1], ray[2]), d = mk(ray[4], ray[5], ray[6]);
   float tmax = ray[3], tlo = ray_tlo(ray);
   uint64_t best = PT_HIT_NONE;
   for (int i = 0; i < S->n_prims; ++i) {
-    float t = prim_test(&S->prims[i], o, d, ref, tlo);
+    float t = prim_test(S, bw, i, o, d, ref, tlo);
     if (t >= 0.0f && t <= tmax) {
       uint64_t k = key(t, (uint32_t)i);
       if (k < best) best = k;
@@ -247,7 +292,7 @@ static int box_hit_d(const pt_node* nd, int c, v3 o, v3 d, double tmax) {
   }
   return 1;
 }
-static uint64_t closest_bvh(const pt_scene_desc* S, const float* ray, int ref) {
+static uint64_t closest_bvh(const pt_scene_desc* S, const float* bw, const float* ray, int ref) {
   v3 o = mk(ray[0], ray[1], ray[2]), d = mk(ray[4], ray[5], ray[6]);
   float tmax = ray[3], tlo = ray_tlo(ray);
   uint64_t best = PT_HIT_NONE;
@@ -259,7 +304,7 @@ static uint64_t closest_bvh(const pt_scene_desc* S, const float* ray, int ref) {
     if (nd->prim_count > 0) {
       for (int k = 0; k < nd->prim_count; ++k) {
         int i = nd->prim_start + k;
-        float t = prim_test(&S->prims[i], o, d, ref, tlo);
+        float t = prim_test(S, bw, i, o, d, ref, tlo);
         if (t >= 0.0f && t <= tmax) {
           uint64_t kk = key(t, (uint32_t)i);
           if (kk < best) best = kk;
@@ -280,13 +325,25 @@ static uint64_t closest_bvh(const pt_scene_desc* S, const float* ray, int ref) {
   return best;
 }
 
-uint64_t pto_closest_brute(const pt_scene_desc* S, const float* ray) { return closest_brute(S, ray, 0); }
-uint64_t pto_closest_bvh(const pt_scene_desc* S, const float* ray) { return closest_bvh(S, ray, 0); }
+uint64_t pto_closest_brute(const pt_scene_desc* S, const float* ray) {
+  float* bw = bw_table(S);
+  const uint64_t h = closest_brute(S, bw, ray, 0);
+  free(bw);
+  return h;
+}
+uint64_t pto_closest_bvh(const pt_scene_desc* S, const float* ray) {
+  float* bw = bw_table(S);
+  const uint64_t h = closest_bvh(S, bw, ray, 0);
+  free(bw);
+  return h;
+}
 
 void pto_intersect_ex(const pt_scene_desc* S, const float* rays, int n, uint64_t* hits, int use_bvh, uint32_t flags) {
   const int ref = (flags & PT_FLAG_REF_ARITH) != 0;
+  float* bw = bw_table(S);
   for (int i = 0; i < n; ++i)
-    hits[i] = use_bvh ? closest_bvh(S, rays + 8 * i, ref) : closest_brute(S, rays + 8 * i, ref);
+    hits[i] = use_bvh ? closest_bvh(S, bw, rays + 8 * i, ref) : closest_brute(S, bw, rays + 8 * i, ref);
+  free(bw);
 }
 void pto_intersect(const pt_scene_desc* S, const float* rays, int n, uint64_t* hits, int use_bvh) {
   pto_intersect_ex(S, rays, n, hits, use_bvh, 0);
@@ -318,6 +375,7 @@ void pto_bfs_visits(const pt_scene_desc* S, const float* rays, int n, uint64_t* 
 /* ---- path tracing ------------------------------------------------------------ */
 typedef struct {
   const pt_scene_desc* S;
+  const float* bw; /* bw_table(S) */
   int W, H, spp, max_bounces, sample_offset, use_bvh;
   uint32_t seed, flags;
   int tile, rank, nranks;
@@ -331,7 +389,7 @@ typedef struct {
 static uint64_t trace(const job_t* J, v3 o, v3 d, float tmax) {
   float r[8] = {o.x, o.y, o.z, tmax, d.x, d.y, d.z, 0.0f};
   const int ref = (J->flags & PT_FLAG_REF_ARITH) != 0;
-  return J->use_bvh ? closest_bvh(J->S, r, ref) : closest_brute(J->S, r, ref);
+  return J->use_bvh ? closest_bvh(J->S, J->bw, r, ref) : closest_brute(J->S, J->bw, r, ref);
 }
 
 /* Radiance of sample s of pixel g: the per-path state machine of k_shade. */
@@ -698,6 +756,8 @@ uint64_t pto_render(const pt_scene_desc* S, int W, int H, int spp, int max_bounc
     if (t % nranks == rank) owned[no++] = (uint32_t)t;
   job_t J;
   J.S = S;
+  float* bw = bw_table(S);
+  J.bw = bw;
   J.W = W;
   J.H = H;
   J.spp = spp;
@@ -719,6 +779,7 @@ uint64_t pto_render(const pt_scene_desc* S, int W, int H, int spp, int max_bounc
   for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
   free(th);
   free(owned);
+  free(bw);
   return (uint64_t)atomic_load(&J.rays);
 }
 
@@ -728,6 +789,8 @@ void pto_sample(const pt_scene_desc* S, int W, int H, int max_bounces, uint32_t 
   job_t J;
   memset(&J, 0, sizeof(J));
   J.S = S;
+  float* bw = bw_table(S);
+  J.bw = bw;
   J.W = W;
   J.H = H;
   J.max_bounces = max_bounces;
@@ -736,6 +799,7 @@ void pto_sample(const pt_scene_desc* S, int W, int H, int max_bounces, uint32_t 
   J.use_bvh = 1;
   uint64_t nr = 0;
   v3 l = path_radiance(&J, g, s, &nr);
+  free(bw);
   out3[0] = l.x;
   out3[1] = l.y;
   out3[2] = l.z;
@@ -745,11 +809,16 @@ void pto_sample(const pt_scene_desc* S, int W, int H, int max_bounces, uint32_t 
  * of its spp samples in sample order, divided by spp; *rays += rays cast.
  * The per-pixel estimator of the Scotty3D-surface CPU renderer
  * (oracle/scotty_cpu.cpp, PathTracer::raytrace_pixel, pathtracer.cpp:499-508). */
-void pto_pixel(const pt_scene_desc* S, int W, int H, int spp, int max_bounces, uint32_t seed, uint32_t flags,
-               int sample_offset, uint32_t g, float* out4, uint64_t* rays) {
+float* pto_bw_table(const pt_scene_desc* S) { return bw_table(S); }
+void pto_free(void* p) { free(p); }
+/* bw: pto_bw_table(S), built once by the caller (the Scotty3D-surface
+ * estimator calls this per pixel) */
+void pto_pixel_bw(const pt_scene_desc* S, const float* bw, int W, int H, int spp, int max_bounces, uint32_t seed,
+                  uint32_t flags, int sample_offset, uint32_t g, float* out4, uint64_t* rays) {
   job_t J;
   memset(&J, 0, sizeof(J));
   J.S = S;
+  J.bw = bw;
   J.W = W;
   J.H = H;
   J.max_bounces = max_bounces;
@@ -770,6 +839,12 @@ void pto_pixel(const pt_scene_desc* S, int W, int H, int spp, int max_bounces, u
   out4[2] = az / ns;
   out4[3] = 1.0f;
   if (rays) *rays += nr;
+}
+void pto_pixel(const pt_scene_desc* S, int W, int H, int spp, int max_bounces, uint32_t seed, uint32_t flags,
+               int sample_offset, uint32_t g, float* out4, uint64_t* rays) {
+  float* bw = bw_table(S);
+  pto_pixel_bw(S, bw, W, H, spp, max_bounces, seed, flags, sample_offset, g, out4, rays);
+  free(bw);
 }
 
 /* ---- display filter: kernelMedianFilter, cu:773-842 --------------------------

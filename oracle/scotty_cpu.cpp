@@ -16,13 +16,17 @@
 
 #include "../cuda-raytracer_amd/scotty/scotty_pt.h"
 
-extern "C" void pto_pixel(const pt_scene_desc* S, int W, int H, int spp, int max_bounces, uint32_t seed,
-                          uint32_t flags, int sample_offset, uint32_t g, float* out4, uint64_t* rays);
+extern "C" float* pto_bw_table(const pt_scene_desc* S);
+extern "C" void pto_free(void* p);
+extern "C" void pto_pixel_bw(const pt_scene_desc* S, const float* bw, int W, int H, int spp, int max_bounces,
+                             uint32_t seed, uint32_t flags, int sample_offset, uint32_t g, float* out4, uint64_t* rays);
 
 namespace {
 
 struct OracleEstimator {
   const pt_scene_desc* S = nullptr;
+  float* bw = nullptr;  // the scene's triangle rows (pto_bw_table), built in begin()
+  ~OracleEstimator() { pto_free(bw); }
   uint32_t seed = 15618;
   int W = 0, H = 0, spp = 1, depth = 8;
   uint32_t flags = 0;
@@ -37,6 +41,8 @@ struct OracleEstimator {
     depth = (int)d;
     flags = f;
     rays = 0;
+    pto_free(bw);
+    bw = pto_bw_table(S);
   }
   void pixel(size_t x, size_t y, float rgba[4]) {
     const size_t ntx = ((size_t)W + 31) / 32;
@@ -45,7 +51,7 @@ struct OracleEstimator {
       return;
     }
     uint64_t n = 0;
-    pto_pixel(S, W, H, spp, depth, seed, flags, 0, (uint32_t)(y * (size_t)W + x), rgba, &n);
+    pto_pixel_bw(S, bw, W, H, spp, depth, seed, flags, 0, (uint32_t)(y * (size_t)W + x), rgba, &n);
     rays += n;
   }
 };

@@ -209,7 +209,7 @@ def test_closest_hit_ref_arith_bit_exact(gpu_ctx, name):
     dot(N, cross(e_k, P - v_k)), N and N.v0 per the reference) through the
     breadth-first traversal equals the oracle's per-call restatement, on the
     fixture rays and on rays aimed at triangle edges (where the literal and
-    edge-normal forms disagree: see DESIGN.md §2)."""
+    the default Baldwin-Weber forms disagree: see DESIGN.md §2)."""
     sc = load_fixture(name)
     d = sc.desc()
     gpu_ctx.load_scene(sc)
@@ -219,7 +219,7 @@ def test_closest_hit_ref_arith_bit_exact(gpu_ctx, name):
     assert (o != ptrace.PT_HIT_NONE).sum() > 1000
     bad = np.nonzero(g != o)[0]
     assert len(bad) == 0, f"{len(bad)} mismatching hits, first {bad[:5]}: gpu {g[bad[:5]]} oracle {o[bad[:5]]}"
-    # the default (edge-normal) test differs from it on edge-aimed rays only
+    # the default (Baldwin-Weber) test differs from it on edge-aimed rays only
     dflt = gpu_ctx.intersect(rays)
     assert np.array_equal(dflt, pyoracle.intersect(d, rays, use_bvh=True))
 

@@ -90,8 +90,8 @@ def test_oracle_quirk_modes():
 
 def test_ref_arith_oracle_consistent():
     """PT_FLAG_REF_ARITH in the oracle: the literal triangle test's BVH walk
-    equals its brute force, it finds the same primitives as the edge-normal
-    form on generic rays, and a full reference-mode render is finite."""
+    equals its brute force, it finds the same primitives as the default
+    Baldwin-Weber form on generic rays, and a full reference-mode render is finite."""
     import ptrace
     from conftest import load_fixture
     from rays import camera_rays, edge_rays, interior_rays
