@@ -1060,10 +1060,7 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
     // (a tri_outside pre-test does not pay here: extension rays of one wave
     // rarely all miss a plane, measured -7 % on CBempty)
     const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1) : tri_test<REFA>(r.o, r.d, q, bt);
-    if (tt >= 0.0f && (tt < bt || (tt == bt && bp < 0))) {
-      bt = tt;
-      bp = pstart + k;
-    }
+    take_hit(tt, pstart + k, bt, bp);
   }
   prim = bp < 0 ? PT_PRIM_NONE : (uint32_t)bp;
   t = bt;

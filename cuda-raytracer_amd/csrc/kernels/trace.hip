@@ -103,7 +103,9 @@ __device__ __forceinline__ float bw_test(const f3 o, const f3 d, const float4 U,
   if (!(t >= tlo) | (t > tbest)) return -1.0f;
   const float u = __builtin_fmaf(t, fdot(U.x, U.y, U.z, d.x, d.y, d.z), bw_plane(o, U));
   const float v = __builtin_fmaf(t, fdot(V.x, V.y, V.z, d.x, d.y, d.z), bw_plane(o, V));
-  const bool miss = (u < 0.0f) | (v < 0.0f) | (u + v > 1.0f);
+  // (unordered compares: a NaN u or v -- a ray parallel to the plane, t =
+  // +-inf -- is a miss)
+  const bool miss = !(u >= 0.0f) | !(v >= 0.0f) | !(u + v <= 1.0f);
   return miss ? -1.0f : t + 0.0f;  // (t + 0 maps -0 to +0)
 }
 // PT_FLAG_REF_ARITH (REFA): the literal edge test of cu:251-267,
@@ -235,7 +237,7 @@ __device__ __forceinline__ f2v bw_test2(const f3x2& o, const f3x2& d, const floa
   f2v r;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const bool miss = !(t[i] >= tlo[i]) | (t[i] > tbest[i]) | (u[i] < 0.0f) | (v[i] < 0.0f) | (uv[i] > 1.0f);
+    const bool miss = !(t[i] >= tlo[i]) | (t[i] > tbest[i]) | !(u[i] >= 0.0f) | !(v[i] >= 0.0f) | !(uv[i] <= 1.0f);
     r[i] = miss ? -1.0f : tz[i];
   }
   return r;
@@ -251,6 +253,27 @@ __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const Pri
   } else {
     return bw_test2(o, d, q.q0, q.q1, q.q2, tbest, tlo);
   }
+}
+
+// Closest-hit update of a leaf loop: take t when it is a hit (t >= 0) that
+// beats {bt, bp} -- nearer, or as near as the incoming key while this leaf has
+// no hit yet (its primitives are tested in increasing index order, so the
+// first of equal hits is the lowest).  A lane without a ray has bt < 0 and
+// takes nothing.  PT_SELECT_UPDATE: as two selects (no exec-mask branch).
+#ifndef PT_SELECT_UPDATE
+#define PT_SELECT_UPDATE 0  // (selects: leaf levels -3 to -7 %, CBempty -0.5 %)
+#endif
+__device__ __forceinline__ void take_hit(float t, int k, float& bt, int& bp) {
+#if PT_SELECT_UPDATE
+  const bool take = (t >= 0.0f) & ((t < bt) | ((t == bt) & (bp < 0)));
+  bt = take ? t : bt;
+  bp = take ? k : bp;
+#else
+  if (t >= 0.0f && (t < bt || (t == bt && bp < 0))) {
+    bt = t;
+    bp = k;
+  }
+#endif
 }
 
 // Ray-sphere (the reference has none: spheres are reinterpret_cast to
@@ -569,11 +592,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {
           if (j >= nj) break;
-          float t = sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]);
-          if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
-            bt[j] = t;
-            bp[j] = pstart + k;
-          }
+          take_hit(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
         }
       } else {
 #pragma unroll
@@ -582,13 +601,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
           const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{bt[j], bt[j + 1]},
                                          f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const float t = t2[i];
-            if (valid[j + i] && t >= 0.0f && (t < bt[j + i] || (t == bt[j + i] && bp[j + i] < 0))) {
-              bt[j + i] = t;
-              bp[j + i] = pstart + k;
-            }
-          }
+          for (int i = 0; i < 2; ++i) take_hit(t2[i], pstart + k, bt[j + i], bp[j + i]);
         }
       }
     }
@@ -826,11 +839,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 #pragma unroll
         for (int j = 0; j < RPTW; ++j) {
           if (j >= nj) break;
-          float t = sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]);
-          if (valid[j] && t >= 0.0f && (t < bt[j] || (t == bt[j] && bp[j] < 0))) {
-            bt[j] = t;
-            bp[j] = pstart + k;
-          }
+          take_hit(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
         }
       } else {
 #pragma unroll
@@ -839,13 +848,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
           const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{bt[j], bt[j + 1]},
                                          f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const float t = t2[i];
-            if (valid[j + i] && t >= 0.0f && (t < bt[j + i] || (t == bt[j + i] && bp[j + i] < 0))) {
-              bt[j + i] = t;
-              bp[j + i] = pstart + k;
-            }
-          }
+          for (int i = 0; i < 2; ++i) take_hit(t2[i], pstart + k, bt[j + i], bp[j + i]);
         }
       }
     }
@@ -1025,6 +1028,141 @@ __device__ __forceinline__ void trace_level_body(const TraceArgs& A, const Level
     const int n = (int)min((uint32_t)WTILE, c - i * WTILE);
     process_wave<REFA, LEAF, TMIN>(A, node, __builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n), lane,
                        L.ids != 0, L.out_ids != 0, L.two_level != 0);
+  }
+}
+
+// ---- depth-first subtree traversal below the DFS cut level -----------------------
+// The rays of the cut level's (node, lane) queues are gathered once and each
+// lane walks its ray through the node's whole subtree: nearest child first,
+// the others on a per-lane LDS stack; node and primitive records through
+// vector loads (a subtree's records stay L2-resident while its queue is
+// processed).  Same closest-hit rules as the level kernels (min of the {t,
+// prim} key, ties to the lowest primitive; a shadow ray stops at its first
+// occluder), so the result does not depend on the traversal order.
+#ifndef PT_DFS_STACK
+#define PT_DFS_STACK 32
+#endif
+constexpr int DFS_STACK = PT_DFS_STACK;  // per-lane stack entries (the host checks 3 x subtree depth fits)
+__device__ __forceinline__ bool box_hit_t(float bx0, float bx1, float by0, float by1, float bz0, float bz1,
+                                          const f3 oi, const f3 inv, float tmax, float& tn) {
+  float tx0 = __builtin_fmaf(bx0, inv.x, -oi.x), tx1 = __builtin_fmaf(bx1, inv.x, -oi.x);
+  float ty0 = __builtin_fmaf(by0, inv.y, -oi.y), ty1 = __builtin_fmaf(by1, inv.y, -oi.y);
+  float tz0 = __builtin_fmaf(bz0, inv.z, -oi.z), tz1 = __builtin_fmaf(bz1, inv.z, -oi.z);
+  tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+  float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+  return tn <= tf;
+}
+template <bool REFA, bool TMIN>
+__device__ __forceinline__ void dfs_ray(const TraceArgs& A, int root, uint32_t id, const f3 o, const f3 d,
+                                        float tmax, int* __restrict__ stk) {
+  const float tlo = TMIN ? A.tmin[id] : 0.0f;
+  const bool anyhit = id >= A.shadow_base;
+  const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d.x)), __builtin_amdgcn_rcpf(safe_dir(d.y)),
+                    __builtin_amdgcn_rcpf(safe_dir(d.z)));
+  const f3 oi = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+  float bt = tmax;
+  int bp = -1;
+  int sp = 0;
+  int node = root;
+  constexpr int PS = prim_stride<REFA>();
+  while (true) {
+    if (node < 0) {
+      if (sp == 0) break;
+      --sp;
+      node = stk[sp * TPB];
+    }
+    const float4* nv = reinterpret_cast<const float4*>(A.nodes + node);
+    const int4 lk = reinterpret_cast<const int4*>(nv)[6];  // child[4]
+    const int4 pr = reinterpret_cast<const int4*>(nv)[7];  // prim_start, prim_count, ...
+    if (pr.y > 0) {
+      const float4* P = A.prims + (size_t)pr.x * PS;
+      bool stop = false;
+      for (int k = 0; k < pr.y; ++k, P += PS) {
+        Prim q;
+        q.q0 = P[0];
+        q.q1 = P[1];
+        q.q2 = P[2];
+        q.q3 = P[3];
+        if constexpr (REFA) {
+          q.q4 = P[4];
+          q.q5 = P[5];
+        }
+        const float t = prim_sphere<REFA>(q) ? sphere_test(o, d, q.q0, q.q1, tlo) : tri_test<REFA>(o, d, q, bt, tlo);
+        const int pi = pr.x + k;
+        if (t >= 0.0f && t <= bt && (t < bt || bp < 0 || pi < bp)) {
+          bt = t;
+          bp = pi;
+          if (anyhit) {
+            stop = true;
+            break;
+          }
+        }
+      }
+      node = -1;
+      if (stop) break;
+      continue;
+    }
+    const float4 bx0 = nv[0], bx1 = nv[1], by0 = nv[2], by1 = nv[3], bz0 = nv[4], bz1 = nv[5];
+    node = -1;
+    float best = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int ch = c == 0 ? lk.x : c == 1 ? lk.y : c == 2 ? lk.z : lk.w;
+      float tn;
+      const bool h = ch >= 0 && box_hit_t(f4c(bx0, c), f4c(bx1, c), f4c(by0, c), f4c(by1, c), f4c(bz0, c),
+                                          f4c(bz1, c), oi, inv, bt, tn);
+      if (h) {
+        if (node < 0) {
+          node = ch;
+          best = tn;
+        } else {
+          const bool nearer = tn < best;
+          stk[sp * TPB] = nearer ? node : ch;
+          ++sp;
+          node = nearer ? ch : node;
+          best = nearer ? tn : best;
+        }
+      }
+    }
+  }
+  if (bp >= 0) report_hit(A.ray, A.shadow_base, id, bt, (uint32_t)bp);
+}
+// The DFS cut level: wave items of 256 rays (the scan runs it in wave mode),
+// each lane's rays one after another through dfs_ray.
+template <bool REFA, bool TMIN = false>
+__global__ __launch_bounds__(TPB) void k_trace_dfs(TraceArgs A, LevelArgs L) {
+  __shared__ int stk[DFS_STACK * TPB];
+  const int lane = blockIdx.x & (NLANE - 1);
+  const uint32_t lid = lane_id();
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t* __restrict__ ep = L.iprefix + (size_t)lane * (L.maxln + 1);
+  const uint32_t M = ep[L.nl];
+  const uint32_t stride = (gridDim.x / NLANE) * (TPB / 64);
+  for (uint32_t m = (blockIdx.x / NLANE) * (TPB / 64) + wave; m < M; m += stride) {
+    int lo = 0, hi = L.nl;
+    while (hi - lo > 1) {
+      const int step = (hi - lo + 63) >> 6;
+      const int idx = lo + (int)lid * step;
+      const bool le = idx < hi && ep[idx] <= m;
+      const unsigned long long msk = __ballot(le);
+      lo = lo + (63 - __clzll(msk)) * step;
+      hi = min(lo + step, hi);
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    const int node = L.first + lo;
+    const uint32_t i = m - ep[lo];
+    const uint32_t c = L.icnt[(size_t)lane * (L.maxln + 1) + lo];
+    const uint32_t base = __builtin_amdgcn_readfirstlane(A.qoff[(size_t)node * NLANE + lane] + i * WTILE);
+    const int n = __builtin_amdgcn_readfirstlane((int)min((uint32_t)WTILE, c - i * WTILE));
+    for (int j = 0; j < RPTW; ++j) {
+      const int r = j * 64 + (int)lid;
+      if (r >= n) break;
+      uint32_t id;
+      f3 o, d;
+      float tmax;
+      load_ray(A, L.ids != 0, base + (uint32_t)r, id, o, d, tmax);
+      if (tmax >= 0.0f) dfs_ray<REFA, TMIN>(A, node, id, o, d, tmax, stk + threadIdx.x);
+    }
   }
 }
 

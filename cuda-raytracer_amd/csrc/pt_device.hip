@@ -102,6 +102,7 @@ struct pt_ctx {
   uint32_t* d_icnt = nullptr;
   uint32_t* d_scan_aux = nullptr;  // multi-workgroup scan: partials + per-node target counts
   int scan_multi_min = 0;          // levels with more nodes use k_scan_count + k_scan_alloc
+  int dfs_level = 1 << 20;         // the DFS cut: this real level's rays finish their subtrees depth-first
   unsigned long long* d_rcount = nullptr;  // valid root rays: RCOUNT_SLOTS counters, one 128-B line each
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
@@ -404,6 +405,17 @@ static void build_root_table(pt_ctx* c) {
   // levels wider than this scan with many workgroups (PT_SCAN_MULTI_MIN nodes)
   const char* sm = getenv("PT_SCAN_MULTI_MIN");
   c->scan_multi_min = sm ? atoi(sm) : SCAN_MULTI_MIN_DEFAULT;
+  // depth-first below the k-th real level (PT_DFS_LEVEL=k, 0 = the root
+  // targets' level; negative: off), when its per-lane stack fits the deepest
+  // subtree (3 entries per level below the cut)
+  const char* dl = getenv("PT_DFS_LEVEL");
+  const int dk = dl ? atoi(dl) : -1;
+  c->dfs_level = 1 << 20;
+  if (dk >= 0 && !c->root_leaf) {
+    const int l0 = skip ? 2 : 1;
+    const int ls = l0 + (c->two_level ? 2 : 1) * dk;
+    if (ls < c->n_levels && 3 * (c->n_levels - 1 - ls) + 1 <= DFS_STACK) c->dfs_level = ls;
+  }
 }
 
 // Queue offsets of the root's targets: each gets root_per_lane ids in every
@@ -460,9 +472,11 @@ static int trace_levels(pt_ctx* c) {
   for (int l = l0; l < c->n_levels; ++l) {
     const bool real = !c->two_level || ((l - l0) & 1) == 0;
     if (!real && !c->level_has_leaf[l]) continue;
+    const bool dfs = l == c->dfs_level;
     LevelArgs L;
-    L.real = real;
-    L.two_level = c->two_level && real;
+    // the DFS level allocates no targets (real = 0) and runs wave items
+    L.real = real && !dfs;
+    L.two_level = (c->two_level && real) || dfs;
     L.first = c->level_start[l];
     L.nl = c->level_start[l + 1] - c->level_start[l];
     L.maxln = c->max_level_nodes;
@@ -501,6 +515,12 @@ static int trace_levels(pt_ctx* c) {
                                                                                      : k_trace_level<false, true>))
               : (c->refa ? (leaves ? k_trace_leaves<true> : wave_only ? k_trace_real<true> : k_trace_level<true>)
                          : (leaves ? k_trace_leaves<false> : wave_only ? k_trace_real<false> : k_trace_level<false>));
+    if (dfs) {
+      auto kd = c->tmin ? (c->refa ? k_trace_dfs<true, true> : k_trace_dfs<false, true>)
+                        : (c->refa ? k_trace_dfs<true> : k_trace_dfs<false>);
+      c->launch(pt_ctx::K_LEVEL, l, kd, dim3(LEVEL_GRID), dim3(TPB), A, L);
+      break;  // nothing is queued below the cut
+    }
     c->launch(pt_ctx::K_LEVEL, l, kl, dim3(LEVEL_GRID), dim3(TPB), A, L);
   }
   HIPCHK(c, hipGetLastError());

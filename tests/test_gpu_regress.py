@@ -124,3 +124,41 @@ def test_origin_bound(gpu_ctx):
     assert e.value.code == ptrace.PT_E_UNSUPPORTED
     rays[7, 0] = 20.0  # CBbunny's extent is ~1.5: 16 x is 24
     assert np.array_equal(gpu_ctx.intersect(rays), pyoracle.intersect(d, rays, use_bvh=True))
+
+
+def _in_plane_scene():
+    """Axis-aligned right triangles in the planes z = 0, y = 0.5 and x = 0.25,
+    and rays lying in or parallel to those planes (W.d = 0: t = NaN or +-inf;
+    with t = +inf and the ray's tmax = inf, the ordered inside test of round 3's
+    first Baldwin-Weber build took u = inf, v = NaN for a hit at t = inf)."""
+    P = np.array([[0, 0, 0, 1, 0, 0, 0, 1, 0],
+                  [1, 1, 0, 0, 1, 0, 1, 0, 0],
+                  [0, 0.5, 0, 1, 0.5, 0, 0, 0.5, 1],
+                  [0.25, 0, 0, 0.25, 1, 0, 0.25, 0, 1]], np.float32)
+    bsdf = ptrace.pt_bsdf()
+    bsdf.type = ptrace.PT_BSDF_DIFFUSE
+    sc = ptrace.Scene.from_mesh(P, [bsdf], tri_bsdf=np.zeros(len(P), np.int32))
+    rays = []
+    for o, d in [((-1, 0.25, 0), (1, 0, 0)), ((0.3, -1, 0), (0, 1, 0)), ((-1, -1, 0), (0.6, 0.8, 0)),
+                 ((-1, 0.5, 0.3), (1, 0, 0)), ((0.2, 0.5, -1), (0, 0, 1)), ((0.25, -1, 0.5), (0, 1, 0)),
+                 ((0.25, 0.3, -1), (0, 0, 1)), ((0.25, 0.0, 0.0), (0, 0.6, 0.8)),
+                 # parallel to a plane just off it: t = +inf on one side
+                 ((-1, 0.25, -0.3), (1, 0, 0)), ((-1, 0.25, 0.3), (1, 0, 0)), ((0.3, -1, -0.2), (0, 1, 0)),
+                 ((0.2, 0.3, -1), (0, 0, 1)), ((0.2, 0.7, -1), (0, 0, 1)), ((0.05, -1, 0.5), (0, 1, 0)),
+                 ((0.45, -1, 0.5), (0, 1, 0))]:
+        rays.append([*o, np.inf, *d, 0.0])
+    return sc, np.array(rays, np.float32)
+
+
+def test_rays_in_a_triangle_plane_miss_it(gpu_ctx):
+    """A ray lying in a triangle's plane has no plane hit (the reference
+    rejects |N.d| < 1e-6, cu:230): the Baldwin-Weber test's t = +-inf / NaN
+    must not become a hit at t = inf (unordered inside test, trace.hip
+    bw_test), on the GPU and in the oracle alike."""
+    sc, rays = _in_plane_scene()
+    d = sc.desc()
+    gpu_ctx.load_scene(sc)
+    o = pyoracle.intersect(d, rays, use_bvh=False)
+    assert np.array_equal(gpu_ctx.intersect(rays), o)
+    t = ptrace.hit_t(o)
+    assert not np.isinf(t[o != ptrace.PT_HIT_NONE]).any()

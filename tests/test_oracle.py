@@ -123,3 +123,16 @@ def test_oracle_bvh_walk_equals_brute_force_on_grazing_rays(name):
         rays.append(sphere_tangent_rays(d, 2000, seed=3))
     rays = np.concatenate(rays)
     assert np.array_equal(pyoracle.intersect(d, rays, use_bvh=True), pyoracle.intersect(d, rays, use_bvh=False))
+
+
+def test_oracle_in_plane_rays_do_not_hit_at_infinity():
+    """The oracle's Baldwin-Weber test (ptoracle.c pto_tri): rays lying in a
+    triangle's plane never report a hit at t = inf (tests/test_gpu_regress.py
+    checks the GPU against the same rays)."""
+    import ptrace
+    from test_gpu_regress import _in_plane_scene
+    sc, rays = _in_plane_scene()
+    o = pyoracle.intersect(sc.desc(), rays, use_bvh=False)
+    t = ptrace.hit_t(o)
+    hit = o != ptrace.PT_HIT_NONE
+    assert np.isfinite(t[hit]).all()
