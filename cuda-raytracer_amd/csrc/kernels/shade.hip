@@ -1216,6 +1216,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       return;
     }
   }
+  // rays traced by the wave (wave-uniform, counted from ballots: no VGPR)
   uint32_t nrays = 0;
   // wave-uniform: the path region this wave grabs from (its workgroup's, then
   // the next ones as they run out) and how many regions it has found empty
@@ -1230,7 +1231,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
   uint32_t next = 0, end = 0;
   bool drained = false;
   bool active = false;
-  uint32_t p = 0;
+  // the lane's path index lives in LDS between its uses (camera ray, sample
+  // index, result): one VGPR less across the vertex loop
+  __shared__ uint32_t sh_p[TPB];
   PathState st{mk(0, 0, 0), 0u, mk(0, 0, 0), 0u};
   RayV ext{mk(0, 0, 0), mk(0, 0, 1), -1.0f}, shr[NSH];
   f3 C[NSH];
@@ -1287,7 +1290,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       const uint32_t r = mbcnt64(idle);
       const uint32_t avail = end - next;
       if (!active && r < avail) {
-        p = next + r;
+        const uint32_t p = next + r;
+        sh_p[threadIdx.x] = p;
         active = true;
         const f3 dir = camera_dir<PT_PATH_MAD64, REFA>(S, p, st.g);
         st.T = mk(1.0f, 1.0f, 1.0f);
@@ -1310,13 +1314,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       continue;  // (pool was empty: the next iteration grabs a chunk)
     }
     // ---- one vertex of every active path: leaf tests, then shade
+    nrays += (uint32_t)__popcll(__ballot(active && (st.flags & F_EXT)));
+#pragma unroll
+    for (int s = 0; s < NSH; ++s) nrays += (uint32_t)__popcll(__ballot(active && (st.flags & sh_bit(s))));
     if (active) {
       uint32_t prim = PT_PRIM_NONE;
       float t = 0.0f;
       if (st.flags & F_EXT) {
         // (extension rays have tmax = inf: not carried across iterations)
         leaf_closest<REFA, SPH>(S.prims, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t);
-        nrays++;
       }
       bool clear[NSH];
 #pragma unroll
@@ -1333,16 +1339,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
             C[s] = mk(q[7 * TPB], q[8 * TPB], q[9 * TPB]);
           }
           clear[s] = !leaf_occluded<REFA, SPH>(S.prims, pstart, pcount, shr[s]);
-          nrays++;
         }
       }
       bool new_ext, new_sh[NSH];
       RayV e2, s2[NSH];
       // (the sample index is recomputed, not carried: one register less)
       shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD, REFA, PT_PATH_LDS_SH>(
-          S, S.sample_base + udiv_q(p, S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2, new_sh, s2,
+          S, S.sample_base + udiv_q(sh_p[threadIdx.x], S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2, new_sh, s2,
           sh_lds);
-      if (new_ext) ext = e2;
+      // (unconditional: without a new extension ray F_EXT is clear and ext is
+      // not read again before the lane's next camera ray -- the old ray need
+      // not stay live through shade_vertex)
+      ext = e2;
       if constexpr (!PT_PATH_LDS_SH) {
 #pragma unroll
         for (int s = 0; s < NSH; ++s)
@@ -1353,13 +1361,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       const uint32_t done = ((st.flags >> 8) & 0xffu) - 1u;
       if (!(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || done >= (uint32_t)passes) {
         if constexpr (PT_PATH_LDS_SH) st.L = mk(Lq[0], Lq[TPB], Lq[2 * TPB]);
-        put_res(S.ps1, p, st.L);
+        put_res(S.ps1, sh_p[threadIdx.x], st.L);
         active = false;
       }
     }
   }
   // rays traced (R): one fire-and-forget atomic per wave into its lane's counter
-  const uint32_t w = wave_sum(nrays);
+  const uint32_t w = __builtin_amdgcn_readfirstlane(nrays);
   if (lid == 0 && w)
     atomicAdd(rcount + (size_t)((blockIdx.x * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16,
               (unsigned long long)w);
