@@ -33,6 +33,7 @@ constexpr float INV_PI = 0.318309886183790671f;
 constexpr float REF_DIFFUSE_MULT = 0.3183f;  // BSDF_DIFFUSE_MULTIPLIER, cu:272
 constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
 constexpr int SHADE_REC = 5;  // float4 per hit-shading record (ShadeArgs::shade)
+constexpr uint32_t SHADE_SMOOTH = 1u << 27;  // shading-record meta bit: a triangle with distinct vertex normals
 constexpr uint32_t ERR_KERNARG = 2u;  // pt_ctx::d_err bit: k_path_leaf's kernel-argument layout check failed
 
 struct ShadeArgs {
@@ -312,23 +313,26 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
     if (prim != PT_PRIM_NONE) {
       const f3 P = REFA ? mk(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z))
                         : mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+      // the record's first 16 B answer spheres ({centre, meta}) and flat
+      // triangles ({n0, meta}); the rest is read only for a triangle with
+      // distinct vertex normals (or the reference arithmetic's blend)
       const float4* Q = S.shade + (size_t)prim * SHADE_REC;
-      // the whole record in one round trip (a sphere needs only q0)
-      const float4 q0 = Q[0], q1 = Q[1], q2 = Q[2], q3 = Q[3], q4 = Q[4];
-      asm volatile("" ::"v"(q0.w), "v"(q1.x), "v"(q2.x), "v"(q3.x), "v"(q4.w));
-      const uint32_t meta = __float_as_uint(q0.w);
+      const float4 q0 = Q[0];
+      const uint32_t meta = __float_as_uint(q0.w) & ~SHADE_SMOOTH;
       f3 ns;
       if ((meta >> 28) == PT_PRIM_SPHERE) {
         ns = normalize(mk(P.x - q0.x, P.y - q0.y, P.z - q0.z));
       } else {
-        const f3 n0 = mk(q1.w, q2.w, q3.x), n1 = mk(q3.y, q3.z, q3.w), n2 = mk(q4.x, q4.y, q4.z);
-        if (!REFA && q4.w != 0.0f) {
+        const f3 n0 = xyz(q0);
+        if (!REFA && !(__float_as_uint(q0.w) & SHADE_SMOOTH)) {
           // flat triangle (n0 == n1 == n2): the barycentric blend is a
           // positive multiple of n0, so its normalisation is normalize(n0)
           ns = normalize(n0);
         } else {
+          const float4 q1 = Q[1], q2 = Q[2], q3 = Q[3], q4 = Q[4];
+          const f3 n1 = mk(q1.w, q2.w, q3.w), n2 = xyz(q4);
           // barycentric shading normal (cu:1213-1221)
-          const f3 A = xyz(q0), B = xyz(q1), Cv = xyz(q2);
+          const f3 A = xyz(q1), B = xyz(q2), Cv = xyz(q3);
           float total = length(cross(A - B, B - Cv));
           float bC = length(cross(A - P, B - P)) / total;
           float bA = length(cross(B - P, Cv - P)) / total;

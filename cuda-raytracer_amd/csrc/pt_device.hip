@@ -842,6 +842,8 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     uint32_t meta;
     memcpy(&meta, &s->prims[i].q[3], 4);
     if ((int)(meta & 0x0FFFFFFFu) >= s->n_bsdfs) return fail(c, PT_E_INVALID, "primitive bsdf out of range");
+    // (bit 27 of a device shading record's meta word is its SHADE_SMOOTH flag)
+    if ((meta & 0x0FFFFFFFu) >= SHADE_SMOOTH) return fail(c, PT_E_UNSUPPORTED, "more than 2^27 bsdfs");
     if ((meta >> 28) == PT_PRIM_SPHERE) c->has_sphere = true;
   }
   for (int i = 0; i < s->n_bsdfs; ++i)
@@ -909,20 +911,32 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     HIPCHK(c, hipMemcpy(c->d_prims_ref, ref.data(), sizeof(pt_prim) * s->n_prims, hipMemcpyHostToDevice));
   }
   {
-    // {A, meta}{B, n0.x}{C, n0.y}{n0.z, n1}{n2, flat} (shade.hip ShadeArgs::shade)
+    // shade.hip ShadeArgs::shade: triangle {n0, meta'}{A, n1.x}{B, n1.y}{C, n1.z}{n2, 0},
+    // sphere {centre, meta'}; meta' = meta | SHADE_SMOOTH unless the triangle is
+    // flat (identical vertex normals: its shading normal is normalize(n0), so
+    // a hit on it reads the first 16 B only)
     std::vector<float4> rec((size_t)s->n_prims * SHADE_REC);
     for (int i = 0; i < s->n_prims; ++i) {
       const float* q = s->prims[i].q;
       const float *n0 = s->shading[i].n0, *n1 = s->shading[i].n1, *n2 = s->shading[i].n2;
       float4* r = &rec[(size_t)i * SHADE_REC];
-      r[0] = make_float4(q[0], q[1], q[2], q[3]);
-      r[1] = make_float4(q[4], q[5], q[6], n0[0]);
-      r[2] = make_float4(q[8], q[9], q[10], n0[1]);
-      r[3] = make_float4(n0[2], n1[0], n1[1], n1[2]);
-      // flat: identical vertex normals (the shading normal is normalize(n0))
+      uint32_t meta;
+      memcpy(&meta, &q[3], 4);
+      if ((meta >> 28) == PT_PRIM_SPHERE) {
+        r[0] = make_float4(q[0], q[1], q[2], q[3]);
+        r[1] = r[2] = r[3] = r[4] = make_float4(0.f, 0.f, 0.f, 0.f);
+        continue;
+      }
       const bool flat = n0[0] == n1[0] && n0[1] == n1[1] && n0[2] == n1[2] && n1[0] == n2[0] && n1[1] == n2[1] &&
                         n1[2] == n2[2];
-      r[4] = make_float4(n2[0], n2[1], n2[2], flat ? 1.0f : 0.0f);
+      const uint32_t m2 = meta | (flat ? 0u : SHADE_SMOOTH);
+      float mf;
+      memcpy(&mf, &m2, 4);
+      r[0] = make_float4(n0[0], n0[1], n0[2], mf);
+      r[1] = make_float4(q[0], q[1], q[2], n1[0]);
+      r[2] = make_float4(q[4], q[5], q[6], n1[1]);
+      r[3] = make_float4(q[8], q[9], q[10], n1[2]);
+      r[4] = make_float4(n2[0], n2[1], n2[2], 0.0f);
     }
     HIPCHK(c, hipMemcpy(c->d_shade, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice));
   }
