@@ -74,7 +74,9 @@ VALU_PEAK_TFLOPS = 157.3    # MI355X FP32 vector peak, same guide
 # the plane offset 6, the division 1, P = o + t d 6, three edge tests 8 each;
 # sphere_test: o - c 3, b 5, c 6, disc 2, sqrt 1, the two roots 2)
 FLOP_TRI, FLOP_SPHERE = 42, 19
-PMC_DIR = ROOT / "profiles" / "r02"
+# the newest round's PMC summaries (scripts/profile_round.sh -> profiles/rNN/)
+PMC_DIR = max((d for d in (ROOT / "profiles").glob("r[0-9][0-9]") if any(d.glob("pmc_*.json"))),
+              default=ROOT / "profiles" / "r02")
 
 
 def parse():

@@ -41,7 +41,7 @@ def main():
         if not files:
             continue
         cfg = f"{sc} 1024x1024 256spp 8 bounces, bench.py --scene {sc} --configs none --config5 off --steps 1 " \
-              f"--warmup 0 --no-cpu --no-1spp (2 frames)"
+              f"--warmup 0 --no-cpu --no-1spp --ref-arith none (2 frames)"
         subprocess.run([sys.executable, str(ROOT / "scripts" / "pmc_summary.py"), *files, "--json",
                         str(dst / f"pmc_{sc}.json"), "--config", cfg], check=True, stdout=subprocess.DEVNULL)
         print("pmc", sc, len(files), "passes")
