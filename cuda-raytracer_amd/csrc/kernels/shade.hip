@@ -683,10 +683,13 @@ __device__ __forceinline__ uint32_t block_key_rank(uint32_t key, bool act, uint3
 // PT_SORT_WAVE its place in the key order of the wave (1) or workgroup (2)).
 // Every thread of the workgroup calls this; act = the thread has a slot
 // (p < N).  kc: LDS for block_key_rank.
+// sparse (workgroup-uniform): most of the workgroup's slots are free (the tail
+// of a chunk): the flags word is read first and only live slots read the rest
+// (a second, dependent round trip instead of ~100 B of loads per free slot)
 template <int NSH, bool REFA = false>
 __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool act, uint32_t& q, bool& new_ext,
                                           RayV& ext, bool (&new_sh)[NSH], RayV (&shr)[NSH], uint32_t (*kc)[4],
-                                          uint32_t* bins) {
+                                          uint32_t* bins, bool sparse = false) {
   new_ext = false;
 #pragma unroll
   for (int s = 0; s < NSH; ++s) new_sh[s] = false;
@@ -697,19 +700,37 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
   // pending contributions); words the flags do not cover are stale and only
   // pass through selects
   const float4 s0 = S.ps0[p];
-  const float4 s1 = S.ps1[p];
-  const float4 r0 = S.ray[RSTRIDE * p], r1 = S.ray[RSTRIDE * p + 1];
-  float4 hs[NSH], cs[NSH];
+  float4 s1, r0, r1, hs[NSH], cs[NSH];
+  auto load_rest = [&]() {
+    s1 = S.ps1[p];
+    r0 = S.ray[RSTRIDE * p];
+    r1 = S.ray[RSTRIDE * p + 1];
 #pragma unroll
-  for (int s = 0; s < NSH; ++s) {
-    hs[s] = S.ray[RSTRIDE * ((1 + s) * S.N + p) + 1];
-    cs[s] = (s ? S.ps3 : S.ps2)[p];
+    for (int s = 0; s < NSH; ++s) {
+      hs[s] = S.ray[RSTRIDE * ((1 + s) * S.N + p) + 1];
+      cs[s] = (s ? S.ps3 : S.ps2)[p];
+    }
+  };
+  if (!sparse) {
+    load_rest();
+    // (the compiler would sink each load into the branch that uses it, i.e.
+    // behind the previous load's wait: pin them all here)
+    asm volatile("" ::"v"(s0.w), "v"(s1.w), "v"(r0.x), "v"(r1.x));
+#pragma unroll
+    for (int s = 0; s < NSH; ++s) asm volatile("" ::"v"(hs[s].z), "v"(cs[s].x));
+  } else {
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    s1 = r0 = z;
+    r1 = make_float4(0.f, 0.f, __uint_as_float(PT_PRIM_NONE), 0.f);
+#pragma unroll
+    for (int s = 0; s < NSH; ++s) hs[s] = cs[s] = z;
+    if (act && (__float_as_uint(s0.w) & (F_EXT | F_SHADOW | F_SHADOW2))) {
+      load_rest();
+      asm volatile("" ::"v"(s1.w), "v"(r0.x), "v"(r1.x));
+#pragma unroll
+      for (int s = 0; s < NSH; ++s) asm volatile("" ::"v"(hs[s].z), "v"(cs[s].x));
+    }
   }
-  // (the compiler would sink each load into the branch that uses it, i.e.
-  // behind the previous load's wait: pin them all here)
-  asm volatile("" ::"v"(s0.w), "v"(s1.w), "v"(r0.x), "v"(r1.x));
-#pragma unroll
-  for (int s = 0; s < NSH; ++s) asm volatile("" ::"v"(hs[s].z), "v"(cs[s].x));
   const uint32_t flags = act ? __float_as_uint(s0.w) : 0u;
   if constexpr (PT_SORT_WAVE == 1 || PT_SORT_WAVE == 2) {
     // (every load above has completed -- the asm uses -- before any thread
@@ -876,11 +897,15 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
 #define PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(7, 8)))
 #endif
 template <int NSH, bool REFA>
+// a workgroup with fewer live slots than this reads its slots sparsely (shade_slot)
+#ifndef PT_SPARSE_LIVE
+#define PT_SPARSE_LIVE 128
+#endif
 __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
   __shared__ uint32_t s_free[4], s_live[4], s_busy[4], s_next, s_end, s_shaded, s_nb, s_nbn;
   __shared__ float s_dir[3][TPB];
-  __shared__ int s_skip;
+  __shared__ int s_skip, s_sparse;
   const int tid = threadIdx.x, wave = tid >> 6;
   const uint32_t nblocks = (S.M + POOL_BLOCK - 1) / POOL_BLOCK;
   if (tid == 0) {
@@ -889,6 +914,8 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     s_end = ws.y;
     s_shaded = ws.w;
     s_skip = ws.z == 0 && ws.x >= ws.y;  // idle: unless a dispenser is still open (below)
+    // (ws.z: the slots live after the last pass's regeneration)
+    s_sparse = ws.z < (uint32_t)PT_SPARSE_LIVE;
   }
   __syncthreads();
   if (s_skip) {  // (uniform: every thread has read it before the barrier below)
@@ -915,7 +942,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t s_bins[PT_SORT_WAVE == 3 ? 4 * HIST_BINS : 1];
   uint32_t q = p;  // where this lane's path state and new rays go
   int state = shade_slot<NSH, REFA>(S, p, p < S.N, q, new_ext, ext, new_sh, shr, s_kc,
-                                    s_bins + (PT_SORT_WAVE == 3 ? wave * HIST_BINS : 0));
+                                    s_bins + (PT_SORT_WAVE == 3 ? wave * HIST_BINS : 0), s_sparse != 0);
   // ---- regeneration: free slots take the next paths in rank order, from the
   // current block and then from a newly claimed one
   const bool fr = p < S.N && state != SLOT_LIVE;
