@@ -41,6 +41,8 @@ REGION = {
                      "prim_sphere", "take_hit", "box_hit", "fdot2", "fma2"],
     "rng": ["philox", "philox_round", "rng", "rng_nee2", "u01", "mulhilo", "mad64", "philox10"],
     "camera": ["camera_dir", "camera_dir_ref"],
+    "rootpass": ["root_pass", "push_children", "push_ray", "count_rays", "wave_sum"],
+    "slots": ["shade_slot", "wave_hist_rank", "wave_key_rank", "claim_block", "block_range", "path_pixel", "put_res"],
     "nee": ["nee_sample", "light_of", "light_sample"],
     "shading": ["shade_vertex", "normalize", "cross", "dot", "length", "sincos2pi", "mulv", "xyz", "mk", "ld3"],
 }
