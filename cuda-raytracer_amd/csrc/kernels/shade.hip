@@ -846,6 +846,8 @@ __device__ __forceinline__ void count_rays(unsigned long long* rcount, uint32_t 
 // paths early while others still hold many (a static split of the chunk by
 // pixel region leaves a long tail: regions differ in mean path length).
 constexpr uint32_t POOL_BLOCK = TPB, POOLS = 64;
+// wstate {next, end} of a workgroup that found every dispenser exhausted
+constexpr uint32_t WS_EXHAUSTED = 0xFFFFFFFFu;
 // Paths [b, e) of block c (ShadeArgs::pblock / pbig).
 __device__ __forceinline__ void block_range(const ShadeArgs& S, uint32_t c, uint32_t& b, uint32_t& e) {
   const uint32_t big = S.pbig * S.pblock;
@@ -862,8 +864,8 @@ __device__ __forceinline__ uint32_t pool_limit(uint32_t nblocks, uint32_t s) {
 }
 // Wave 0 of a workgroup: claim one block, trying dispenser (b + k) % POOLS in
 // order among those not yet exhausted (all 64 peeked at once, one lane each).
-// Returns the block index, or -1 when every dispenser is exhausted (or lost
-// the race for its last block).
+// Returns the block index, -2 when every dispenser is exhausted, -1 when it
+// lost the race for the last block of the one it tried (others may be open).
 __device__ __forceinline__ int claim_block(const ShadeArgs& S, uint32_t nblocks) {
   const uint32_t ln = lane_id();
   const uint32_t sd = (blockIdx.x + ln) & (POOLS - 1);
@@ -871,7 +873,7 @@ __device__ __forceinline__ int claim_block(const ShadeArgs& S, uint32_t nblocks)
       __hip_atomic_load(S.pool + (size_t)sd * CSTRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
       pool_limit(nblocks, sd);
   const unsigned long long mo = __ballot(open);
-  if (!mo) return -1;
+  if (!mo) return -2;
   const uint32_t k = (uint32_t)__builtin_ctzll(mo);
   int c = -1;
   if (ln == k) {
@@ -945,11 +947,16 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     s_next = ws.x;
     s_end = ws.y;
     s_shaded = ws.w;
-    s_skip = ws.z == 0 && ws.x >= ws.y;  // idle: unless a dispenser is still open (below)
+    // idle: unless a dispenser is still open (below); with next = WS_EXHAUSTED
+    // this workgroup has found every dispenser exhausted, which stays so for
+    // the rest of the chunk: no peek (in a chunk's tail the 64 dispenser
+    // words, peeked by every idle workgroup of every pass, are a hot spot)
+    s_skip = ws.z == 0 && ws.x >= ws.y ? (ws.x == WS_EXHAUSTED ? 2 : 1) : 0;
     // (ws.z: the slots live after the last pass's regeneration)
     s_sparse = ws.z < (uint32_t)PT_SPARSE_LIVE;
   }
   __syncthreads();
+  if (s_skip == 2) return;
   if (s_skip) {  // (uniform: every thread has read it before the barrier below)
     __syncthreads();
     if (wave == 0) {
@@ -1000,14 +1007,16 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   for (int round = 0; round < (S.cull ? PT_CULL_ROUNDS : 2) && placed < nf; ++round) {
     if (next >= end) {
       // (wave 0 claims one block; uniform: every thread reads s_nb after the barrier)
+      if (next == WS_EXHAUSTED) break;
       if (wave == 0) {
         const int c = claim_block(S, nblocks);
-        if (tid == 0) s_nb = c >= 0 ? (uint32_t)c : 0xFFFFFFFFu;
+        if (tid == 0) s_nb = c >= 0 ? (uint32_t)c : c == -2 ? WS_EXHAUSTED : 0xFFFFFFFEu;
       }
       __syncthreads();
       const uint32_t nb = s_nb;
       __syncthreads();  // (s_nb is written again by the next round)
-      if (nb == 0xFFFFFFFFu) break;
+      if (nb == WS_EXHAUSTED) next = end = WS_EXHAUSTED;
+      if (nb >= 0xFFFFFFFEu) break;
       block_range(S, nb, next, end);
     }
     const uint32_t need = nf - placed;
