@@ -75,21 +75,6 @@ struct ShadeArgs {
   // target whose subtree holds the primitive (KMAP_SIZE entries)
   const uint32_t* __restrict__ kmap;
   uint32_t kmshift;
-  // camera-ray culling at path start (k_shade_push): a camera ray that misses
-  // the scene box (the union of the root's child boxes, conservative) is a
-  // miss -- its path ends with radiance 0 without taking a slot.  cull = 0:
-  // off (the host turns it on when a sample of the image's camera rays misses
-  // the box, e.g. bunny.dae; the Cornell scenes' camera rays all enter it)
-  float sbox[6];  // {min x, max x, min y, max y, min z, max z}
-  uint32_t cull;
-  // path blocks: the first pbig blocks hold pblock paths each, the rest
-  // POOL_BLOCK (block_range).  Without cull every block is POOL_BLOCK; with
-  // it, a workgroup takes ~2.4 candidates per free slot, and large blocks
-  // early in the chunk let it claim about once per pass instead of once per
-  // candidate round (a claim's dispenser atomics go to the memory side of the
-  // 8 XCDs), while the small blocks at the end keep the chunk's tail short (no
-  // workgroup is left holding many unstarted paths)
-  uint32_t pblock, pbig;
 };
 
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -846,26 +831,13 @@ __device__ __forceinline__ void count_rays(unsigned long long* rcount, uint32_t 
 // paths early while others still hold many (a static split of the chunk by
 // pixel region leaves a long tail: regions differ in mean path length).
 constexpr uint32_t POOL_BLOCK = TPB, POOLS = 64;
-// wstate {next, end} of a workgroup that found every dispenser exhausted
-constexpr uint32_t WS_EXHAUSTED = 0xFFFFFFFFu;
-// Paths [b, e) of block c (ShadeArgs::pblock / pbig).
-__device__ __forceinline__ void block_range(const ShadeArgs& S, uint32_t c, uint32_t& b, uint32_t& e) {
-  const uint32_t big = S.pbig * S.pblock;
-  b = c < S.pbig ? c * S.pblock : big + (c - S.pbig) * POOL_BLOCK;
-  b = min(b, S.M);
-  e = min(S.M, b + (c < S.pbig ? S.pblock : POOL_BLOCK));
-}
-__host__ __device__ inline uint32_t num_blocks(uint32_t M, uint32_t pblock, uint32_t pbig) {
-  const uint64_t big = (uint64_t)pbig * pblock;
-  return big >= M ? (uint32_t)((M + pblock - 1) / pblock) : pbig + (uint32_t)((M - big + POOL_BLOCK - 1) / POOL_BLOCK);
-}
 __device__ __forceinline__ uint32_t pool_limit(uint32_t nblocks, uint32_t s) {
   return nblocks > s ? (nblocks - s + POOLS - 1) / POOLS : 0u;
 }
 // Wave 0 of a workgroup: claim one block, trying dispenser (b + k) % POOLS in
 // order among those not yet exhausted (all 64 peeked at once, one lane each).
-// Returns the block index, -2 when every dispenser is exhausted, -1 when it
-// lost the race for the last block of the one it tried (others may be open).
+// Returns the block index, or -1 when every dispenser is exhausted (or lost
+// the race for its last block).
 __device__ __forceinline__ int claim_block(const ShadeArgs& S, uint32_t nblocks) {
   const uint32_t ln = lane_id();
   const uint32_t sd = (blockIdx.x + ln) & (POOLS - 1);
@@ -873,7 +845,7 @@ __device__ __forceinline__ int claim_block(const ShadeArgs& S, uint32_t nblocks)
       __hip_atomic_load(S.pool + (size_t)sd * CSTRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
       pool_limit(nblocks, sd);
   const unsigned long long mo = __ballot(open);
-  if (!mo) return -2;
+  if (!mo) return -1;
   const uint32_t k = (uint32_t)__builtin_ctzll(mo);
   int c = -1;
   if (ln == k) {
@@ -891,8 +863,7 @@ template <int NSH, bool REFA>
 __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
   const uint32_t p = blockIdx.x * TPB + threadIdx.x;
-  uint32_t base, end;
-  block_range(S, blockIdx.x, base, end);
+  const uint32_t base = blockIdx.x * POOL_BLOCK, end = min(S.M, base + POOL_BLOCK);
   const uint32_t slots = min((uint32_t)TPB, S.N - blockIdx.x * TPB);  // (the last workgroup may be partial)
   const uint32_t n0 = end > base ? min(slots, end - base) : 0u;
   const bool live = threadIdx.x < n0;
@@ -930,33 +901,23 @@ template <int NSH, bool REFA>
 #ifndef PT_SPARSE_LIVE
 #define PT_SPARSE_LIVE 128
 #endif
-// candidate rounds of the regeneration when camera rays are culled (S.cull)
-#ifndef PT_CULL_ROUNDS
-#define PT_CULL_ROUNDS 4
-#endif
 __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
-  __shared__ uint32_t s_free[4], s_live[4], s_busy[4], s_next, s_end, s_shaded, s_nb;
+  __shared__ uint32_t s_free[4], s_live[4], s_busy[4], s_next, s_end, s_shaded, s_nb, s_nbn;
   __shared__ float s_dir[3][TPB];
-  __shared__ uint32_t s_pix[TPB];  // the paths the free slots start, in rank order
   __shared__ int s_skip, s_sparse;
   const int tid = threadIdx.x, wave = tid >> 6;
-  const uint32_t nblocks = num_blocks(S.M, S.pblock, S.pbig);
+  const uint32_t nblocks = (S.M + POOL_BLOCK - 1) / POOL_BLOCK;
   if (tid == 0) {
     const uint4 ws = S.wstate[blockIdx.x];
     s_next = ws.x;
     s_end = ws.y;
     s_shaded = ws.w;
-    // idle: unless a dispenser is still open (below); with next = WS_EXHAUSTED
-    // this workgroup has found every dispenser exhausted, which stays so for
-    // the rest of the chunk: no peek (in a chunk's tail the 64 dispenser
-    // words, peeked by every idle workgroup of every pass, are a hot spot)
-    s_skip = ws.z == 0 && ws.x >= ws.y ? (ws.x == WS_EXHAUSTED ? 2 : 1) : 0;
+    s_skip = ws.z == 0 && ws.x >= ws.y;  // idle: unless a dispenser is still open (below)
     // (ws.z: the slots live after the last pass's regeneration)
     s_sparse = ws.z < (uint32_t)PT_SPARSE_LIVE;
   }
   __syncthreads();
-  if (s_skip == 2) return;
   if (s_skip) {  // (uniform: every thread has read it before the barrier below)
     __syncthreads();
     if (wave == 0) {
@@ -983,7 +944,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   int state = shade_slot<NSH, REFA>(S, p, p < S.N, q, new_ext, ext, new_sh, shr, s_kc,
                                     s_bins + (PT_SORT_WAVE == 3 ? wave * HIST_BINS : 0), s_sparse != 0);
   // ---- regeneration: free slots take the next paths in rank order, from the
-  // current block and then from newly claimed ones
+  // current block and then from a newly claimed one
   const bool fr = p < S.N && state != SLOT_LIVE;
   const unsigned long long mf = __ballot(fr), ml = __ballot(p < S.N && state == SLOT_LIVE),
                            mb = __ballot(p < S.N && state != SLOT_FREE);
@@ -994,84 +955,48 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   }
   __syncthreads();
   const uint32_t nf = s_free[0] + s_free[1] + s_free[2] + s_free[3];
-  // Candidate rounds: the workgroup computes the camera rays of the next paths
-  // (whole waves: ceil(cand / 64) of them run the camera code) and hands them
-  // to the free slots through LDS in rank order.  With S.cull, a camera ray
-  // that misses the scene box ends its path right here (radiance 0, one ray
-  // traced) and takes no slot, so a round takes a whole block's worth of
-  // candidates and the rounds go on until the free slots are filled (at most
-  // PT_CULL_ROUNDS); without it the first round fills them (every candidate
-  // survives).  Paths are consumed in order: a round stops after the survivor
-  // that fills the last free slot, the rest stay unstarted.
-  uint32_t next = s_next, end = s_end, placed = 0, nmiss = 0;
-  for (int round = 0; round < (S.cull ? PT_CULL_ROUNDS : 2) && placed < nf; ++round) {
-    if (next >= end) {
-      // (wave 0 claims one block; uniform: every thread reads s_nb after the barrier)
-      if (next == WS_EXHAUSTED) break;
-      if (wave == 0) {
-        const int c = claim_block(S, nblocks);
-        if (tid == 0) s_nb = c >= 0 ? (uint32_t)c : c == -2 ? WS_EXHAUSTED : 0xFFFFFFFEu;
+  const uint32_t next = s_next, end = s_end;
+  const uint32_t avail = end > next ? end - next : 0u;
+  const uint32_t t1 = min(nf, avail);
+  if (wave == 0) {
+    // (nf <= 256 = POOL_BLOCK: one new block always covers the rest)
+    int c = -1;
+    if (nf > t1) c = claim_block(S, nblocks);
+    if (tid == 0) {
+      uint32_t nb = 0, nbn = 0, nnext = next + t1, nend = end;
+      if (c >= 0) {
+        nb = (uint32_t)c * POOL_BLOCK;
+        const uint32_t nbend = min(S.M, nb + POOL_BLOCK);
+        nbn = min(nf - t1, nbend - nb);
+        nnext = nb + nbn;
+        nend = nbend;
       }
-      __syncthreads();
-      const uint32_t nb = s_nb;
-      __syncthreads();  // (s_nb is written again by the next round)
-      if (nb == WS_EXHAUSTED) next = end = WS_EXHAUSTED;
-      if (nb >= 0xFFFFFFFEu) break;
-      block_range(S, nb, next, end);
+      s_nb = nb;
+      s_nbn = nbn;
+      S.wstate[blockIdx.x] = make_uint4(nnext, nend, s_live[0] + s_live[1] + s_live[2] + s_live[3] + t1 + nbn,
+                                        s_shaded + s_busy[0] + s_busy[1] + s_busy[2] + s_busy[3]);
     }
-    const uint32_t need = nf - placed;
-    const uint32_t cand = min(end - next, S.cull ? (uint32_t)TPB : need);
-    const uint32_t P = next + (uint32_t)tid;
-    bool keep = false;
-    f3 dir = mk(0.f, 0.f, 1.f);
-    if ((uint32_t)tid < cand) {
-      uint32_t g;
-      dir = camera_dir<PT_SHADE_MAD64, REFA>(S, P, g);
-      keep = true;
-      if (S.cull) {
-        const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(dir.x)), __builtin_amdgcn_rcpf(safe_dir(dir.y)),
-                          __builtin_amdgcn_rcpf(safe_dir(dir.z)));
-        const f3 co = ld3(S.cam.origin);
-        keep = box_hit(S.sbox[0], S.sbox[1], S.sbox[2], S.sbox[3], S.sbox[4], S.sbox[5],
-                       mk(co.x * inv.x, co.y * inv.y, co.z * inv.z), inv, __builtin_inff());
-      }
-    }
-    const unsigned long long mk_ = __ballot(keep);
-    if ((tid & 63) == 0) s_kc[0][wave] = (uint32_t)__popcll(mk_);
-    __syncthreads();
-    uint32_t kr = mbcnt64(mk_);
-    for (int w = 0; w < wave; ++w) kr += s_kc[0][w];
-    const uint32_t nkeep = s_kc[0][0] + s_kc[0][1] + s_kc[0][2] + s_kc[0][3];
-    if (tid == 0) s_kc[1][0] = cand;
-    __syncthreads();
-    // the survivor that fills the last free slot ends the round
-    if (keep && nkeep > need && kr == need - 1) s_kc[1][0] = (uint32_t)tid + 1u;
-    __syncthreads();
-    const uint32_t cut = s_kc[1][0];
-    if ((uint32_t)tid < cut) {
-      if (keep) {
-        s_pix[placed + kr] = P;
-        s_dir[0][placed + kr] = dir.x;
-        s_dir[1][placed + kr] = dir.y;
-        s_dir[2][placed + kr] = dir.z;
-      } else {
-        put_res(S.res, P, mk(0.f, 0.f, 0.f));
-        ++nmiss;
-      }
-    }
-    next += cut;
-    placed += min(nkeep, need);
-    __syncthreads();  // (s_kc is written again by the next round)
   }
-  if (tid == 0)
-    S.wstate[blockIdx.x] = make_uint4(next, end, s_live[0] + s_live[1] + s_live[2] + s_live[3] + placed,
-                                      s_shaded + s_busy[0] + s_busy[1] + s_busy[2] + s_busy[3]);
+  __syncthreads();
+  // camera rays of the paths that start here, computed by the first ns threads
+  // of the workgroup (whole waves, not one lane in four of every wave: the
+  // camera code then runs in ceil(ns / 64) waves instead of all four), handed
+  // to the free slots through LDS in rank order
+  const uint32_t ns = min(nf, t1 + s_nbn);
+  if ((uint32_t)tid < ns) {
+    const uint32_t P = (uint32_t)tid < t1 ? next + (uint32_t)tid : s_nb + (uint32_t)tid - t1;
+    uint32_t g;
+    const f3 dir = camera_dir<PT_SHADE_MAD64, REFA>(S, P, g);
+    s_dir[0][tid] = dir.x;
+    s_dir[1][tid] = dir.y;
+    s_dir[2][tid] = dir.z;
+  }
   __syncthreads();
   if (fr) {
     uint32_t rank = mbcnt64(mf);
     for (int w = 0; w < wave; ++w) rank += s_free[w];
-    if (rank < placed) {
-      const uint32_t P = s_pix[rank];
+    if (rank < ns) {
+      const uint32_t P = rank < t1 ? next + rank : s_nb + rank - t1;
       S.ps0[q] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
       S.ps1[q] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
       ext = RayV{ld3(S.cam.origin), mk(s_dir[0][rank], s_dir[1][rank], s_dir[2][rank]), __builtin_inff()};
@@ -1092,7 +1017,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   tm[0] = __builtin_inff();
   valid[0] = new_ext;
   anyhit[0] = false;
-  uint32_t n = (new_ext ? 1u : 0u) + nmiss;
+  uint32_t n = new_ext ? 1u : 0u;
 #pragma unroll
   for (int s = 0; s < NSH; ++s) {
     id[1 + s] = (1 + s) * S.N + q;
@@ -1109,14 +1034,13 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
 
 // Work left in paths (the host polls it: 0 = the chunk is done): live slots
 // over all workgroups, the unstarted rest of each workgroup's current block,
-// and pblock paths for every block no dispenser has handed out yet (blocks
-// after the first pbig and the chunk's last block hold fewer: an upper bound); with stats, also the
+// and POOL_BLOCK paths for every block no dispenser has handed out yet (the
+// chunk's last block may hold fewer: an upper bound); with stats, also the
 // chunk's shaded vertices (stats[STAT_SHADED]).  A grid of LIVE_SUM_BLOCKS
 // workgroups, one atomic each into the zeroed *live.
 constexpr int LIVE_SUM_BLOCKS = 64;
 __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wstate, uint32_t G, const uint32_t* pool,
-                                                   uint32_t nblocks, uint32_t pblock, uint32_t* live,
-                                                   unsigned long long* shaded) {
+                                                   uint32_t nblocks, uint32_t* live, unsigned long long* shaded) {
   __shared__ unsigned long long part[2][16];
   unsigned long long v = 0, sh = 0;
   for (uint32_t b = blockIdx.x * 1024 + threadIdx.x; b < G; b += gridDim.x * 1024) {
@@ -1126,7 +1050,7 @@ __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wst
   }
   if (blockIdx.x == 0 && threadIdx.x < POOLS) {
     const uint32_t lim = pool_limit(nblocks, threadIdx.x), c = pool[(size_t)threadIdx.x * CSTRIDE];
-    v += c < lim ? (unsigned long long)(lim - c) * pblock : 0ull;
+    v += c < lim ? (unsigned long long)(lim - c) * POOL_BLOCK : 0ull;
   }
   v = wave_sum64(v);
   sh = wave_sum64(sh);

@@ -318,55 +318,6 @@ static void box_row(float (&b)[6][W], int i, const pt_node& parent, int k) {
   b[5][i] = parent.bmax_z[k];
 }
 
-// Camera-ray culling (ShadeArgs::cull, a measured option): the scene box is
-// the union of the root's child boxes (each conservative, so the union is);
-// culling can pay only when the camera sees past the scene, judged from a
-// 32 x 32 grid of pixel-centre rays in double (the kernels' camera model,
-// camera_dir): on when at least 1/16 of them miss the box.
-static bool camera_cull(const pt_ctx* c, float sbox[6]) {
-  const pt_node& r = c->nodes_host[0];
-  for (int a = 0; a < 3; ++a) {
-    sbox[2 * a] = INFINITY;
-    sbox[2 * a + 1] = -INFINITY;
-  }
-  for (int k = 0; k < 4; ++k) {
-    if (r.child[k] < 0) continue;
-    const float lo[3] = {r.bmin_x[k], r.bmin_y[k], r.bmin_z[k]}, hi[3] = {r.bmax_x[k], r.bmax_y[k], r.bmax_z[k]};
-    for (int a = 0; a < 3; ++a) {
-      sbox[2 * a] = std::min(sbox[2 * a], lo[a]);
-      sbox[2 * a + 1] = std::max(sbox[2 * a + 1], hi[a]);
-    }
-  }
-  // opt-in (PT_CULL_CAMERA=1): on bunny.dae it removes 40 % of the shaded
-  // vertices and 4 of 23 passes, but the frame is no faster (56.4 -> 57.3 ms:
-  // a missed camera ray's vertex was cheap to shade, and the candidate rounds
-  // cost as much; larger early blocks lengthen the tail, 1024: 62 ms)
-  const char* e = getenv("PT_CULL_CAMERA");
-  if (!e || atoi(e) == 0) return false;
-  const pt_camera& cam = c->camera;
-  int miss = 0;
-  constexpr int G = 32;
-  for (int i = 0; i < G; ++i)
-    for (int j = 0; j < G; ++j) {
-      const double kx = (j + 0.5) / G - 0.5, ky = -((i + 0.5) / G - 0.5);
-      double tn = 0.0, tf = INFINITY;
-      for (int a = 0; a < 3; ++a) {
-        const double d = kx * cam.left[a] + ky * cam.up[a] + cam.look_at[a];
-        const double o = cam.origin[a];
-        if (d == 0.0) {
-          if (o < sbox[2 * a] || o > sbox[2 * a + 1]) tf = -1.0;
-          continue;
-        }
-        double t0 = (sbox[2 * a] - o) / d, t1 = (sbox[2 * a + 1] - o) / d;
-        if (t0 > t1) std::swap(t0, t1);
-        tn = std::max(tn, t0);
-        tf = std::min(tf, t1);
-      }
-      miss += tn > tf;
-    }
-  return miss * 16 >= G * G;
-}
-
 static void build_root_table(pt_ctx* c) {
   RootTable& T = c->rt;
   memset(&T, 0, sizeof(T));
@@ -1148,10 +1099,6 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     }
     S.kmap = c->d_kmap;
     S.kmshift = c->kmap_shift;
-    memset(S.sbox, 0, sizeof S.sbox);
-    S.cull = !c->root_leaf && camera_cull(c, S.sbox) ? 1u : 0u;
-    S.pblock = POOL_BLOCK;
-    S.pbig = 0;
     if (c->root_leaf) {
       // single-leaf tree: every path runs to completion in one kernel
       // (persistent waves with path regeneration, output res[P])
@@ -1215,13 +1162,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       S.wstate = c->d_wstate;
       S.pool = c->d_pool;
       // dispensers: the first fill runs blocks 0 .. G-1 (workgroup b block b)
-      if (S.cull) {
-        // large blocks except for the chunk's last 2 N paths (PT_CULL_BLOCK)
-        const char* pb = getenv("PT_CULL_BLOCK");
-        S.pblock = (uint32_t)std::max(TPB, pb ? atoi(pb) : 1024);
-        S.pbig = M > 2ull * N ? (uint32_t)((M - 2ull * N) / S.pblock) : 0u;
-      }
-      const uint32_t nblocks = num_blocks(M, S.pblock, S.pbig);
+      const uint32_t nblocks = (M + POOL_BLOCK - 1) / POOL_BLOCK;
       {
         std::vector<uint32_t> init((size_t)POOLS * CSTRIDE, 0u);
         for (uint32_t k = 0; k < POOLS; ++k) init[(size_t)k * CSTRIDE] = G > k ? (G - k + POOLS - 1) / POOLS : 0u;
@@ -1249,7 +1190,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         }
         HIPCHK(c, hipMemsetAsync(c->d_live, 0, 4, c->stream));
         hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G,
-                           (const uint32_t*)c->d_pool, nblocks, S.pblock, c->d_live, (unsigned long long*)nullptr);
+                           (const uint32_t*)c->d_pool, nblocks, c->d_live, (unsigned long long*)nullptr);
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1), c->d_live, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1) + 1, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->ev_poll[g & 1], c->stream));
@@ -1292,7 +1233,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       if (!finished) return fail(c, PT_E_HIP, "paths did not finish within the pass bound");
       if (timed)  // shaded vertices of the chunk (stats only)
         hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G,
-                           (const uint32_t*)c->d_pool, nblocks, S.pblock, c->d_live, c->d_stats + STAT_SHADED);
+                           (const uint32_t*)c->d_pool, nblocks, c->d_live, c->d_stats + STAT_SHADED);
     }
     c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_res,
               c->d_accum, npix, spp_c);

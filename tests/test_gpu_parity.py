@@ -345,30 +345,3 @@ def test_scotty_camera_render(gpu_ctx):
     o, _ = pyoracle.image(d, 64, 48, 2, max_bounces=6)
     assert np.array_equal(g, o) and o[..., :3].mean() > 0.01
 
-
-@pytest.mark.parametrize("batch", [None, 1000])
-def test_camera_cull_matches_oracle(gpu_ctx, batch, monkeypatch):
-    """Camera-ray culling at path start (k_shade_push, ShadeArgs::cull; an
-    option, PT_CULL_CAMERA=1): on bunny.dae most camera rays miss the scene
-    box and end right at generation (radiance 0, one ray counted).  The image
-    and the ray count equal the oracle's with culling on and off, also with a
-    1000-slot pool (many regeneration rounds per workgroup, dispensers
-    exhausted mid-round) and with large early path blocks (PT_CULL_BLOCK)."""
-    import scenes
-    sc = scenes.bunny_lit()
-    d = sc.desc()
-    gpu_ctx.load_scene(sc)
-    W, H, SPP = 48, 40, 3
-    oi, orays = pyoracle.image(d, W, H, SPP, max_bounces=8, seed=15618)
-    out = {}
-    for cull in ("1", "0", "1/1024"):
-        monkeypatch.setenv("PT_CULL_CAMERA", cull[0])
-        monkeypatch.setenv("PT_CULL_BLOCK", cull[2:] or "256")
-        gpu_ctx.clear()
-        gpu_ctx.reset_stats()
-        kw = {} if batch is None else {"batch_paths": batch}
-        gpu_ctx.render(W, H, SPP, max_bounces=8, seed=15618, **kw)
-        out[cull] = (gpu_ctx.get_image(), gpu_ctx.stats().rays)
-    for cull, (img, rays) in out.items():
-        assert np.array_equal(img, oi), cull
-        assert rays == orays, (cull, rays, orays)
