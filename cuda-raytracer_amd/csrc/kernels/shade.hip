@@ -75,6 +75,11 @@ struct ShadeArgs {
   // target whose subtree holds the primitive (KMAP_SIZE entries)
   const uint32_t* __restrict__ kmap;
   uint32_t kmshift;
+  // dense pass (set by the host while the chunk has more than 2 N paths of
+  // work left, i.e. nearly every slot is live): k_shade_push issues every
+  // slot's loads at entry, in the same memory round trip as its workgroup's
+  // wstate word, instead of after the barrier that shares the wstate
+  uint32_t dense;
 };
 
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -686,10 +691,33 @@ __device__ __forceinline__ uint32_t block_key_rank(uint32_t key, bool act, uint3
 // sparse (workgroup-uniform): most of the workgroup's slots are free (the tail
 // of a chunk): the flags word is read first and only live slots read the rest
 // (a second, dependent round trip instead of ~100 B of loads per free slot)
+// Every word a slot may need (shade_slot), loaded in one round trip.
+// (plain members, no arrays: the struct must stay in registers)
+template <int NSH>
+struct SlotLoad {
+  float4 s0, s1, r0, r1, h0, c0, h1, c1;
+};
+template <int NSH>
+__device__ __forceinline__ SlotLoad<NSH> load_slot(const ShadeArgs& S, uint32_t p) {
+  SlotLoad<NSH> L;
+  L.s0 = S.ps0[p];
+  L.s1 = S.ps1[p];
+  L.r0 = S.ray[RSTRIDE * p];
+  L.r1 = S.ray[RSTRIDE * p + 1];
+  L.h0 = S.ray[RSTRIDE * (S.N + p) + 1];
+  L.c0 = S.ps2[p];
+  if (NSH > 1) {
+    L.h1 = S.ray[RSTRIDE * (2 * S.N + p) + 1];
+    L.c1 = S.ps3[p];
+  } else {
+    L.h1 = L.c1 = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  return L;
+}
 template <int NSH, bool REFA = false>
 __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool act, uint32_t& q, bool& new_ext,
                                           RayV& ext, bool (&new_sh)[NSH], RayV (&shr)[NSH], uint32_t (*kc)[4],
-                                          uint32_t* bins, bool sparse = false) {
+                                          uint32_t* bins, bool sparse, bool use_pre, const SlotLoad<NSH> pre) {
   new_ext = false;
 #pragma unroll
   for (int s = 0; s < NSH; ++s) new_sh[s] = false;
@@ -699,8 +727,20 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
   // instead of three dependent ones: flags, then records, then the ray and the
   // pending contributions); words the flags do not cover are stale and only
   // pass through selects
-  const float4 s0 = S.ps0[p];
-  float4 s1, r0, r1, hs[NSH], cs[NSH];
+  float4 s0, s1, r0, r1, hs[NSH], cs[NSH];
+  if (use_pre) {  // (dense pass: loaded at kernel entry)
+    s0 = pre.s0;
+    s1 = pre.s1;
+    r0 = pre.r0;
+    r1 = pre.r1;
+#pragma unroll
+    for (int s = 0; s < NSH; ++s) {
+      hs[s] = s ? pre.h1 : pre.h0;
+      cs[s] = s ? pre.c1 : pre.c0;
+    }
+  } else {
+    s0 = S.ps0[p];
+  }
   auto load_rest = [&]() {
     s1 = S.ps1[p];
     r0 = S.ray[RSTRIDE * p];
@@ -711,7 +751,11 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
       cs[s] = (s ? S.ps3 : S.ps2)[p];
     }
   };
-  if (!sparse) {
+  if (use_pre) {
+    asm volatile("" ::"v"(s0.w), "v"(s1.w), "v"(r0.x), "v"(r1.x));
+#pragma unroll
+    for (int s = 0; s < NSH; ++s) asm volatile("" ::"v"(hs[s].z), "v"(cs[s].x));
+  } else if (!sparse) {
     load_rest();
     // (the compiler would sink each load into the branch that uses it, i.e.
     // behind the previous load's wait: pin them all here)
@@ -908,6 +952,9 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   __shared__ int s_skip, s_sparse;
   const int tid = threadIdx.x, wave = tid >> 6;
   const uint32_t nblocks = (S.M + POOL_BLOCK - 1) / POOL_BLOCK;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  SlotLoad<NSH> pre{z4, z4, z4, z4, z4, z4, z4, z4};
+  if (S.dense) pre = load_slot<NSH>(S, blockIdx.x * TPB + tid < S.N ? blockIdx.x * TPB + tid : 0u);
   if (tid == 0) {
     const uint4 ws = S.wstate[blockIdx.x];
     s_next = ws.x;
@@ -942,7 +989,8 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t s_bins[PT_SORT_WAVE == 3 ? 4 * HIST_BINS : 1];
   uint32_t q = p;  // where this lane's path state and new rays go
   int state = shade_slot<NSH, REFA>(S, p, p < S.N, q, new_ext, ext, new_sh, shr, s_kc,
-                                    s_bins + (PT_SORT_WAVE == 3 ? wave * HIST_BINS : 0), s_sparse != 0);
+                                    s_bins + (PT_SORT_WAVE == 3 ? wave * HIST_BINS : 0), s_sparse != 0,
+                                    S.dense != 0, pre);
   // ---- regeneration: free slots take the next paths in rank order, from the
   // current block and then from a newly claimed one
   const bool fr = p < S.N && state != SLOT_LIVE;

@@ -1177,6 +1177,11 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       // (np passes; the tail of a chunk polls after every pass: a pass queued
       // after the last path ended still costs ~150 us of empty level and scan
       // launches)
+      // dense passes (ShadeArgs::dense) while more than 2 N paths of work are
+      // left at the last poll (PT_DENSE=0: never)
+      const char* de = getenv("PT_DENSE");
+      const bool dense_ok = !(de && atoi(de) == 0);
+      S.dense = dense_ok ? 1u : 0u;
       auto enqueue_group = [&](int g, int np) -> int {
         for (int k = 0; k < np; ++k) {
           int r = trace_levels(c);
@@ -1217,6 +1222,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         // paths left (live slots + unstarted paths, k_live_sum) below 1/16
         // of the pool: the chunk's tail, one pass per poll
         const int np = (uint64_t)nlive * 16 < N ? 1 : POLL_GROUP;
+        S.dense = dense_ok && (uint64_t)nlive > 2ull * N ? 1u : 0u;
         if ((rc = enqueue_group(g + 2, np))) return rc;
         queued += (uint64_t)np;
       }
