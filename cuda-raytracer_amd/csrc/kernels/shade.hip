@@ -75,6 +75,22 @@ struct ShadeArgs {
   // target whose subtree holds the primitive (KMAP_SIZE entries)
   const uint32_t* __restrict__ kmap;
   uint32_t kmshift;
+  // Tail compaction (pt_render): once every path of the chunk has started and
+  // few slots are still live, one shade pass writes the continuing paths'
+  // state and new rays densely into a second set of buffers (slot from the
+  // counter *compact), and the passes after it launch ceil(n / 256)
+  // workgroups over slots [0, *nact) of that set.  A shade workgroup's time is
+  // mostly a chain of dependent memory round trips, nearly the same for 20
+  // live slots as for 256, so without this the tail's passes cost almost as
+  // much as full ones.  The slots are read from the *_in buffers (and S.ray)
+  // and written to ps0..ps3 and A.ray: the same arrays except in a
+  // compaction pass.
+  const float4* ps0_in;
+  const float4* ps1_in;
+  const float4* ps2_in;
+  const float4* ps3_in;
+  uint32_t* compact;     // compaction pass: the output buffers' slot counter (zeroed); else null
+  const uint32_t* nact;  // after a compaction: the live slots are [0, *nact); else null ([0, N))
   // dense pass (set by the host while the chunk has more than 2 N paths of
   // work left, i.e. nearly every slot is live): k_shade_push issues every
   // slot's loads at entry, in the same memory round trip as its workgroup's
@@ -700,15 +716,15 @@ struct SlotLoad {
 template <int NSH>
 __device__ __forceinline__ SlotLoad<NSH> load_slot(const ShadeArgs& S, uint32_t p) {
   SlotLoad<NSH> L;
-  L.s0 = S.ps0[p];
-  L.s1 = S.ps1[p];
+  L.s0 = S.ps0_in[p];
+  L.s1 = S.ps1_in[p];
   L.r0 = S.ray[RSTRIDE * p];
   L.r1 = S.ray[RSTRIDE * p + 1];
   L.h0 = S.ray[RSTRIDE * (S.N + p) + 1];
-  L.c0 = S.ps2[p];
+  L.c0 = S.ps2_in[p];
   if (NSH > 1) {
     L.h1 = S.ray[RSTRIDE * (2 * S.N + p) + 1];
-    L.c1 = S.ps3[p];
+    L.c1 = S.ps3_in[p];
   } else {
     L.h1 = L.c1 = make_float4(0.f, 0.f, 0.f, 0.f);
   }
@@ -739,16 +755,16 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
       cs[s] = s ? pre.c1 : pre.c0;
     }
   } else {
-    s0 = S.ps0[p];
+    s0 = S.ps0_in[p];
   }
   auto load_rest = [&]() {
-    s1 = S.ps1[p];
+    s1 = S.ps1_in[p];
     r0 = S.ray[RSTRIDE * p];
     r1 = S.ray[RSTRIDE * p + 1];
 #pragma unroll
     for (int s = 0; s < NSH; ++s) {
       hs[s] = S.ray[RSTRIDE * ((1 + s) * S.N + p) + 1];
-      cs[s] = (s ? S.ps3 : S.ps2)[p];
+      cs[s] = (s ? S.ps3_in : S.ps2_in)[p];
     }
   };
   if (use_pre) {
@@ -813,14 +829,32 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
     ended = !(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || ((st.flags >> 8) & 0xffu) - 1u >= (uint32_t)S.passes;
   }
   if constexpr (PT_SORT_WAVE == 3) {  // (every lane of the wave: uniform control flow here)
-    uint32_t key = HIST_BINS - 1;
-    if (live && !ended && new_ext && ext_hit) {
+    // continuing paths first (those whose new ray hit something in key
+    // order, then the rest), ended paths and free slots last
+    const bool cont = live && !ended;
+    uint32_t key = cont ? HIST_BINS - 2 : HIST_BINS - 1;
+    if (cont && new_ext && ext_hit) {
       key = PT_SORT_KMAP ? S.kmap[prim >> S.kmshift] : min(prim >> S.kshift, SORT_KEYS - 1u);
       if (PT_SORT_DIR)
         key = (key << 3) | (ext.d.x < 0.0f ? 1u : 0u) | (ext.d.y < 0.0f ? 2u : 0u) | (ext.d.z < 0.0f ? 4u : 0u);
     }
     const uint32_t r = wave_hist_rank(key, act, bins);
     if (act) q = (q & ~63u) + r;
+    if (S.compact) {
+      // compaction pass (uniform; every thread of the workgroup is here): the
+      // workgroup's continuing paths take consecutive slots of the output
+      // buffers from one atomic, wave by wave, each wave's in key order
+      // (ranks 0 .. its count - 1)
+      const unsigned long long mc = __ballot(act && cont);
+      const uint32_t wv = threadIdx.x >> 6;
+      if ((threadIdx.x & 63) == 0) kc[0][wv] = (uint32_t)__popcll(mc);
+      __syncthreads();
+      if (threadIdx.x == 0) kc[1][0] = atomicAdd(S.compact, kc[0][0] + kc[0][1] + kc[0][2] + kc[0][3]);
+      __syncthreads();
+      uint32_t base = kc[1][0];
+      for (uint32_t w = 0; w < wv; ++w) base += kc[0][w];
+      if (act && cont) q = base + r;
+    }
     if (!live) return SLOT_FREE;
   }
   if (ended) {
@@ -955,6 +989,8 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   SlotLoad<NSH> pre{z4, z4, z4, z4, z4, z4, z4, z4};
   if (S.dense) pre = load_slot<NSH>(S, blockIdx.x * TPB + tid < S.N ? blockIdx.x * TPB + tid : 0u);
+  // slots [0, nin) hold paths (after a compaction fewer than N)
+  const uint32_t nin = S.nact ? *S.nact : S.N;
   if (tid == 0) {
     const uint4 ws = S.wstate[blockIdx.x];
     s_next = ws.x;
@@ -988,14 +1024,14 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t s_kc[SORT_KEYS + 1][4];
   __shared__ uint32_t s_bins[PT_SORT_WAVE == 3 ? 4 * HIST_BINS : 1];
   uint32_t q = p;  // where this lane's path state and new rays go
-  int state = shade_slot<NSH, REFA>(S, p, p < S.N, q, new_ext, ext, new_sh, shr, s_kc,
+  int state = shade_slot<NSH, REFA>(S, p, p < nin, q, new_ext, ext, new_sh, shr, s_kc,
                                     s_bins + (PT_SORT_WAVE == 3 ? wave * HIST_BINS : 0), s_sparse != 0,
                                     S.dense != 0, pre);
   // ---- regeneration: free slots take the next paths in rank order, from the
   // current block and then from a newly claimed one
-  const bool fr = p < S.N && state != SLOT_LIVE;
-  const unsigned long long mf = __ballot(fr), ml = __ballot(p < S.N && state == SLOT_LIVE),
-                           mb = __ballot(p < S.N && state != SLOT_FREE);
+  const bool fr = p < nin && state != SLOT_LIVE;
+  const unsigned long long mf = __ballot(fr), ml = __ballot(p < nin && state == SLOT_LIVE),
+                           mb = __ballot(p < nin && state != SLOT_FREE);
   if ((tid & 63) == 0) {
     s_free[wave] = (uint32_t)__popcll(mf);
     s_live[wave] = (uint32_t)__popcll(ml);
@@ -1005,11 +1041,14 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   const uint32_t nf = s_free[0] + s_free[1] + s_free[2] + s_free[3];
   const uint32_t next = s_next, end = s_end;
   const uint32_t avail = end > next ? end - next : 0u;
-  const uint32_t t1 = min(nf, avail);
+  // (compaction pass: the block's paths start in the extra round below, not in
+  // the free slots, whose positions mean nothing in the compacted layout)
+  const uint32_t t1 = S.compact ? 0u : min(nf, avail);
   if (wave == 0) {
     // (nf <= 256 = POOL_BLOCK: one new block always covers the rest)
     int c = -1;
-    if (nf > t1) c = claim_block(S, nblocks);
+    // (no new paths once the tail is compacted: every block is handed out)
+    if (nf > t1 && !S.compact && !S.nact) c = claim_block(S, nblocks);
     if (tid == 0) {
       uint32_t nb = 0, nbn = 0, nnext = next + t1, nend = end;
       if (c >= 0) {
@@ -1021,6 +1060,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
       }
       s_nb = nb;
       s_nbn = nbn;
+      if (S.compact) nnext = nend;  // (all of them start below)
       S.wstate[blockIdx.x] = make_uint4(nnext, nend, s_live[0] + s_live[1] + s_live[2] + s_live[3] + t1 + nbn,
                                         s_shaded + s_busy[0] + s_busy[1] + s_busy[2] + s_busy[3]);
     }
@@ -1049,7 +1089,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
       S.ps1[q] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
       ext = RayV{ld3(S.cam.origin), mk(s_dir[0][rank], s_dir[1][rank], s_dir[2][rank]), __builtin_inff()};
       new_ext = true;
-    } else if (state == SLOT_ENDED || (PT_SORT_WAVE && q != p)) {
+    } else if (!S.compact && (state == SLOT_ENDED || (PT_SORT_WAVE && q != p))) {
       // the slot stays free (with PT_SORT_WAVE slot q may have held another
       // lane's path until now)
       S.ps0[q] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
@@ -1078,19 +1118,42 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   }
   root_pass<1 + NSH, REFA>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh);
   count_rays(S.rcount, n, sh + MAX_ROOT_TARGETS * 8);
+  if (S.compact && avail) {
+    // compaction pass, extra round (uniform): every unstarted path of the
+    // workgroup's block starts here, in consecutive slots of the compacted
+    // layout (the dispensers are dry: after this no workgroup holds any)
+    if (tid == 0) s_nb = atomicAdd(S.compact, avail);
+    __syncthreads();
+    const bool st0 = (uint32_t)tid < avail;
+    uint32_t id1[1] = {s_nb + (uint32_t)tid};
+    f3 o1[1] = {ld3(S.cam.origin)}, d1[1] = {mk(0.f, 0.f, 1.f)};
+    float tm1[1] = {__builtin_inff()};
+    bool valid1[1] = {st0}, anyhit1[1] = {false};
+    if (st0) {
+      const uint32_t P = next + (uint32_t)tid;
+      uint32_t g;
+      d1[0] = camera_dir<PT_SHADE_MAD64, REFA>(S, P, g);
+      S.ps0[id1[0]] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
+      S.ps1[id1[0]] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
+    }
+    root_pass<1, REFA>(S.A, S.T, blockIdx.x & (NLANE - 1), id1, o1, d1, tm1, valid1, anyhit1, sh);
+    count_rays(S.rcount, st0 ? 1u : 0u, sh + MAX_ROOT_TARGETS * 8);
+  }
 }
 
-// Work left in paths (the host polls it: 0 = the chunk is done): live slots
-// over all workgroups, the unstarted rest of each workgroup's current block,
-// and POOL_BLOCK paths for every block no dispenser has handed out yet (the
-// chunk's last block may hold fewer: an upper bound); with stats, also the
-// chunk's shaded vertices (stats[STAT_SHADED]).  A grid of LIVE_SUM_BLOCKS
-// workgroups, one atomic each into the zeroed *live.
+// Work left in paths (the host polls it: live[0] = 0 means the chunk is
+// done): live slots over all workgroups, the unstarted rest of each
+// workgroup's current block, and POOL_BLOCK paths for every block no
+// dispenser has handed out yet (the chunk's last block may hold fewer: an
+// upper bound); live[1] = the paths of the unclaimed blocks alone (0: the
+// dispensers are dry, the tail may be compacted); with stats, also the chunk's shaded
+// vertices (stats[STAT_SHADED]).  A grid of LIVE_SUM_BLOCKS workgroups, one
+// atomic each into the zeroed live[0..1].
 constexpr int LIVE_SUM_BLOCKS = 64;
 __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wstate, uint32_t G, const uint32_t* pool,
                                                    uint32_t nblocks, uint32_t* live, unsigned long long* shaded) {
-  __shared__ unsigned long long part[2][16];
-  unsigned long long v = 0, sh = 0;
+  __shared__ unsigned long long part[3][16];
+  unsigned long long v = 0, un = 0, sh = 0;
   for (uint32_t b = blockIdx.x * 1024 + threadIdx.x; b < G; b += gridDim.x * 1024) {
     const uint4 w = wstate[b];
     v += w.z + (w.y > w.x ? w.y - w.x : 0u);
@@ -1098,23 +1161,49 @@ __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wst
   }
   if (blockIdx.x == 0 && threadIdx.x < POOLS) {
     const uint32_t lim = pool_limit(nblocks, threadIdx.x), c = pool[(size_t)threadIdx.x * CSTRIDE];
-    v += c < lim ? (unsigned long long)(lim - c) * POOL_BLOCK : 0ull;
+    un += c < lim ? (unsigned long long)(lim - c) * POOL_BLOCK : 0ull;
   }
-  v = wave_sum64(v);
+  v = wave_sum64(v + un);
+  un = wave_sum64(un);
   sh = wave_sum64(sh);
   if ((threadIdx.x & 63) == 0) {
     part[0][threadIdx.x >> 6] = v;
     part[1][threadIdx.x >> 6] = sh;
+    part[2][threadIdx.x >> 6] = un;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long t = 0, u = 0;
+    unsigned long long t = 0, u = 0, n = 0;
     for (int w = 0; w < 16; ++w) {
       t += part[0][w];
       u += part[1][w];
+      n += part[2][w];
     }
     if (t) atomicAdd(live, (uint32_t)min(t, 0xFFFFFFFFull));
+    if (n) atomicAdd(live + 1, (uint32_t)min(n, 0xFFFFFFFFull));
     if (shaded && u) atomicAdd(shaded, u);
+  }
+}
+
+// After a compaction pass: the shade workgroups' states for the compacted
+// layout (Gnew workgroups over slots [0, *nact), nothing left to start), the
+// old layout's shaded-vertex counts added to *shaded first (stats; may be
+// null).  One thread per workgroup state, max(Gold, Gnew) of them.
+__global__ __launch_bounds__(TPB) void k_compact_wstate(uint4* wstate, uint32_t Gold, uint32_t Gnew,
+                                                        const uint32_t* nact, unsigned long long* shaded) {
+  const uint32_t b = blockIdx.x * TPB + threadIdx.x;
+  unsigned long long w = 0;
+  if (b < Gold) w = wstate[b].w;
+  if (shaded) {
+    w = wave_sum64(w);
+    if ((threadIdx.x & 63) == 0 && w) atomicAdd(shaded, w);
+  }
+  const uint32_t n = *nact;
+  if (b < Gnew) {
+    const uint32_t lo = b * TPB;
+    wstate[b] = make_uint4(0u, 0u, n > lo ? min((uint32_t)TPB, n - lo) : 0u, 0u);
+  } else if (b < Gold) {
+    wstate[b] = make_uint4(0u, 0u, 0u, 0u);
   }
 }
 

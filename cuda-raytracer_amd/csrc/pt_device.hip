@@ -89,6 +89,14 @@ struct pt_ctx {
   size_t cap_qfactor = 0;
   float4* d_ray = nullptr;  // 2N ray records (trace.h), RSTRIDE float4 each
   float4 *d_ps0 = nullptr, *d_ps1 = nullptr, *d_ps2 = nullptr, *d_ps3 = nullptr;
+  // the second buffer set of the tail compaction (ShadeArgs::compact), and
+  // the record buffer the traversal currently reads (null: d_ray)
+  float4* d_ray_b = nullptr;
+  float4 *d_ps0_b = nullptr, *d_ps1_b = nullptr, *d_ps2_b = nullptr, *d_ps3_b = nullptr;
+  float4* ray_cur = nullptr;
+  uint32_t* d_compact = nullptr;  // MAX_COMPACTIONS slot counters
+  bool compaction = true;         // PT_COMPACT=0: off
+  int compact_div = 2;            // compact when live slots <= layout / compact_div (PT_COMPACT=k)
   uint32_t* d_q = nullptr;   // ray-id queues (QREGIONS regions): the root's targets and the levels above entry_level
   size_t qcap = 0;           // ids per region
   int entry_level = 0;       // first level whose queues hold ray entries (build_root_table)
@@ -197,7 +205,8 @@ static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_kmap, c->d_res, c->d_wstate, c->d_live, c->d_pool,
-                  c->d_pix_of, c->d_accum, c->d_frame, c->d_tmin};
+                  c->d_pix_of, c->d_accum, c->d_frame, c->d_tmin, c->d_ray_b, c->d_ps0_b, c->d_ps1_b, c->d_ps2_b,
+                  c->d_ps3_b, c->d_compact};
   for (void* p : ptrs)
     if (p) hipFree(p);
 }
@@ -213,6 +222,7 @@ static void free_all(pt_ctx* c) {
 // records of a path, and its state arrays, a power of two apart and runs 7 %
 // slower on CBbunny (HBM channel aliasing); 28-42 Mi all measure within 1.5 %.
 static constexpr uint32_t DEFAULT_BATCH_PATHS = 36u << 20;
+static constexpr int MAX_COMPACTIONS = 8;  // tail compactions per chunk (slot counters, pt_ctx::d_compact)
 // paths per chunk (per-path radiance buffer: 16 B each); POLL_GROUP passes
 // are queued between two reads of the finished-path count
 static constexpr uint32_t CHUNK_PATHS = 1u << 28;
@@ -280,6 +290,13 @@ static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
   if ((rc = dalloc(c, &c->d_ps1, N))) return rc;
   if ((rc = dalloc(c, &c->d_ps2, N))) return rc;
   if (spp > 2 && (rc = dalloc(c, &c->d_ps3, N))) return rc;
+  if (c->compaction) {
+    if ((rc = dalloc(c, &c->d_ray_b, slots * RSTRIDE))) return rc;
+    if ((rc = dalloc(c, &c->d_ps0_b, N))) return rc;
+    if ((rc = dalloc(c, &c->d_ps1_b, N))) return rc;
+    if ((rc = dalloc(c, &c->d_ps2_b, N))) return rc;
+    if (spp > 2 && (rc = dalloc(c, &c->d_ps3_b, N))) return rc;
+  }
   // every root target needs root_per_lane ids per lane (see
   // set_root_child_offsets); the levels below get ray entries: a level needs at
   // most 4x the visits of the level above (the scan's allocation), which
@@ -444,7 +461,7 @@ static TraceArgs trace_args(pt_ctx* c) {
   TraceArgs A;
   A.nodes = c->d_nodes;
   A.prims = c->refa ? c->d_prims_ref : c->d_prims;
-  A.ray = c->d_ray;
+  A.ray = c->ray_cur ? c->ray_cur : c->d_ray;
   A.cnt = c->d_cnt;
   A.qoff = c->d_qoff;
   A.q = c->d_q;
@@ -762,6 +779,12 @@ int pt_create(pt_ctx** out, int device) {
   if (const char* q = getenv("PT_PATH_GUIDE")) c->path_guide = std::max(0, atoi(q));
   if (const char* q = getenv("PT_PATH_REGIONS")) c->path_regions = std::max(1, atoi(q));
   if (const char* q = getenv("PT_PATH_GUIDED_BELOW")) c->path_guided_below = std::max(0, atoi(q));
+  // tail compaction needs the wave record order's continuing-first ranks
+  if (const char* q = getenv("PT_COMPACT")) {
+    c->compaction = atoi(q) != 0;
+    if (atoi(q) > 1) c->compact_div = atoi(q);
+  }
+  c->compaction = c->compaction && PT_SORT_WAVE == 3;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return PT_E_HIP;
@@ -772,9 +795,10 @@ int pt_create(pt_ctx** out, int device) {
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, PATH_REGIONS_MAX * PATH_CTR_STRIDE * 4) != hipSuccess ||
       hipMalloc((void**)&c->d_kmap, KMAP_SIZE * 4) != hipSuccess ||
-      hipMalloc((void**)&c->d_live, 4) != hipSuccess ||
+      hipMalloc((void**)&c->d_live, 8) != hipSuccess ||
+      hipMalloc((void**)&c->d_compact, MAX_COMPACTIONS * 4) != hipSuccess ||
       hipMalloc((void**)&c->d_pool, POOLS * CSTRIDE * 4) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_poll, 16, hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void**)&c->h_poll, 32, hipHostMallocDefault) != hipSuccess) {
     delete c;
     return PT_E_HIP;
   }
@@ -1015,6 +1039,7 @@ int pt_get_stats(pt_ctx* c, pt_stats* out) {
 
 int pt_render(pt_ctx* c, const pt_render_params* P) {
   if (!c || !P) return PT_E_INVALID;
+  c->ray_cur = nullptr;
   if (!c->have_scene) return fail(c, PT_E_NOSCENE, "no scene loaded");
   if (P->width <= 0 || P->height <= 0 || P->spp <= 0 || P->max_bounces < 0 || P->max_bounces > 250)
     return fail(c, PT_E_INVALID, "bad render parameters");
@@ -1143,18 +1168,39 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       if (realloc && (rc = set_root_child_offsets(c))) return rc;
       if (first) c->stats.batch_paths = (int32_t)N;
       // (device buffers as (re)allocated by ensure_paths)
-      S.ray = c->d_ray;
-      S.ps0 = c->d_ps0;
-      S.ps1 = c->d_ps1;
-      S.ps2 = c->d_ps2;
-      S.ps3 = c->d_ps3;
       S.N = N;
       c->shadow_base = N;  // slots >= N hold shadow rays
-      S.A = trace_args(c);
+      // slot buffers: set a until the tail's first compaction, then the two
+      // sets alternate (ShadeArgs::compact); in: what the shade kernel reads,
+      // out: what it writes and the traversal then reads
+      float4* const RAY[2] = {c->d_ray, c->d_ray_b};
+      float4* const PS[4][2] = {{c->d_ps0, c->d_ps0_b}, {c->d_ps1, c->d_ps1_b}, {c->d_ps2, c->d_ps2_b},
+                                {c->d_ps3, c->d_ps3_b}};
+      auto bind = [&](int in, int out) {
+        S.ray = RAY[in];
+        S.ps0_in = PS[0][in];
+        S.ps1_in = PS[1][in];
+        S.ps2_in = PS[2][in];
+        S.ps3_in = PS[3][in];
+        S.ps0 = PS[0][out];
+        S.ps1 = PS[1][out];
+        S.ps2 = PS[2][out];
+        S.ps3 = PS[3][out];
+        c->ray_cur = RAY[out];
+        S.A = trace_args(c);
+      };
+      int cur = 0;
+      bind(0, 0);
+      S.compact = nullptr;
+      S.nact = nullptr;
       S.T = c->rt;
       const dim3 grid((N + TPB - 1) / TPB);
       // workgroup b of the shade grid runs its slots' share of the chunk
       const uint32_t G = (N + TPB - 1) / TPB;
+      uint32_t Gc = G;        // shade workgroups of the current slot layout
+      uint32_t nbound = N;    // slots of the current layout that may hold paths
+      int ncomp = 0;          // compactions so far in this chunk
+      bool compact_next = false;  // the next group starts with a compaction pass
       if (G > c->wstate_cap) {
         if ((rc = dalloc(c, &c->d_wstate, G))) return rc;
         c->wstate_cap = G;
@@ -1182,22 +1228,47 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       const char* de = getenv("PT_DENSE");
       const bool dense_ok = !(de && atoi(de) == 0);
       S.dense = dense_ok ? 1u : 0u;
-      auto enqueue_group = [&](int g, int np) -> int {
+      auto enqueue_group = [&](int g, int np, uint32_t nlive) -> int {
         for (int k = 0; k < np; ++k) {
-          int r = trace_levels(c);
+          int r = trace_levels(c);  // (the rays in c->ray_cur)
           if (r) return r;
+          const bool comp = k == 0 && compact_next;
+          uint32_t Gnew = Gc;
+          if (comp) {
+            // this pass writes the continuing paths densely into the other
+            // set; the live slots are at most the last poll's count
+            HIPCHK(c, hipMemsetAsync(c->d_compact + ncomp, 0, 4, c->stream));
+            S.compact = c->d_compact + ncomp;
+            bind(cur, 1 - cur);
+            Gnew = std::max(1u, (nlive + TPB - 1) / TPB);
+          }
           if (c->timing) {
             const auto e = c->pair(pt_ctx::K_SHADE, 0);
-            HIPCHK(c, pt_launch_shade_push(nsh, c->refa, grid.x, c->stream, e.first, e.second, &S));
+            HIPCHK(c, pt_launch_shade_push(nsh, c->refa, Gc, c->stream, e.first, e.second, &S));
           } else {
-            HIPCHK(c, pt_launch_shade_push(nsh, c->refa, grid.x, c->stream, nullptr, nullptr, &S));
+            HIPCHK(c, pt_launch_shade_push(nsh, c->refa, Gc, c->stream, nullptr, nullptr, &S));
+          }
+          if (comp) {
+            const uint32_t gm = std::max(Gc, Gnew);
+            hipLaunchKernelGGL(k_compact_wstate, dim3((gm + TPB - 1) / TPB), dim3(TPB), 0, c->stream, S.wstate, Gc,
+                               Gnew, (const uint32_t*)(c->d_compact + ncomp),
+                               timed ? c->d_stats + STAT_SHADED : (unsigned long long*)nullptr);
+            HIPCHK(c, hipGetLastError());
+            S.nact = c->d_compact + ncomp;
+            S.compact = nullptr;
+            cur = 1 - cur;
+            bind(cur, cur);
+            Gc = Gnew;
+            nbound = nlive;
+            ++ncomp;
+            compact_next = false;
           }
         }
-        HIPCHK(c, hipMemsetAsync(c->d_live, 0, 4, c->stream));
-        hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G,
+        HIPCHK(c, hipMemsetAsync(c->d_live, 0, 8, c->stream));
+        hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, Gc,
                            (const uint32_t*)c->d_pool, nblocks, c->d_live, (unsigned long long*)nullptr);
-        HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1), c->d_live, 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_poll + 2 * (g & 1) + 1, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_poll + 4 * (g & 1), c->d_live, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_poll + 4 * (g & 1) + 2, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->ev_poll[g & 1], c->stream));
         return PT_OK;
       };
@@ -1207,10 +1278,11 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       const uint64_t max_passes = (uint64_t)(M / N + 2) * passes + 2 * POLL_GROUP;
       uint64_t queued = 2 * POLL_GROUP;
       bool overflow = false, finished = false;
-      if ((rc = enqueue_group(0, POLL_GROUP)) || (rc = enqueue_group(1, POLL_GROUP))) return rc;
+      if ((rc = enqueue_group(0, POLL_GROUP, N)) || (rc = enqueue_group(1, POLL_GROUP, N))) return rc;
       for (int g = 0; queued <= max_passes + 2 * POLL_GROUP; ++g) {
         HIPCHK(c, hipEventSynchronize(c->ev_poll[g & 1]));
-        const uint32_t nlive = c->h_poll[2 * (g & 1)], err = c->h_poll[2 * (g & 1) + 1];
+        const uint32_t nlive = c->h_poll[4 * (g & 1)], unclaimed = c->h_poll[4 * (g & 1) + 1],
+                       err = c->h_poll[4 * (g & 1) + 2];
         if (err) {
           overflow = true;
           break;
@@ -1221,9 +1293,16 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         }
         // paths left (live slots + unstarted paths, k_live_sum) below 1/16
         // of the pool: the chunk's tail, one pass per poll
-        const int np = (uint64_t)nlive * 16 < N ? 1 : POLL_GROUP;
-        S.dense = dense_ok && (uint64_t)nlive > 2ull * N ? 1u : 0u;
-        if ((rc = enqueue_group(g + 2, np))) return rc;
+        // (once the dispensers are dry with compaction on, one pass per poll
+        // too: the compaction decision is then at most two passes old)
+        const int np = (uint64_t)nlive * 16 < N || (c->compaction && unclaimed == 0) ? 1 : POLL_GROUP;
+        // the dispensers are dry and at most a quarter of the current layout's
+        // slots are live or unstarted: compact them (the next group's first
+        // pass; it also starts every path still left in a workgroup's block)
+        compact_next = c->compaction && c->d_ray_b && unclaimed == 0 && ncomp < MAX_COMPACTIONS &&
+                       (uint64_t)nlive * c->compact_div <= (uint64_t)nbound * (c->compact_div == 3 ? 2 : 1);
+        S.dense = dense_ok && ((uint64_t)nlive > 2ull * N || (ncomp > 0 && (uint64_t)nlive * 2 > nbound)) ? 1u : 0u;
+        if ((rc = enqueue_group(g + 2, np, nlive))) return rc;
         queued += (uint64_t)np;
       }
       if (overflow) {
@@ -1237,8 +1316,9 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         continue;
       }
       if (!finished) return fail(c, PT_E_HIP, "paths did not finish within the pass bound");
+      c->ray_cur = nullptr;
       if (timed)  // shaded vertices of the chunk (stats only)
-        hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, G,
+        hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, Gc,
                            (const uint32_t*)c->d_pool, nblocks, c->d_live, c->d_stats + STAT_SHADED);
     }
     c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_res,
@@ -1354,6 +1434,7 @@ int pt_owned_pixels(pt_ctx* c, int32_t* n_pixels, int32_t* pixel_index, size_t m
 int pt_intersect(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits) { return pt_intersect_ex(c, rays, n, hits, 0); }
 
 int pt_intersect_ex(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits, uint32_t flags) {
+  if (c) c->ray_cur = nullptr;  // (a failed render may have left the compaction's second set bound)
   if (!c || (!rays && n > 0) || (!hits && n > 0) || n < 0) return PT_E_INVALID;
   if (!c->have_scene) return fail(c, PT_E_NOSCENE, "no scene loaded");
   c->refa = (flags & PT_FLAG_REF_ARITH) != 0;
