@@ -162,3 +162,29 @@ def test_rays_in_a_triangle_plane_miss_it(gpu_ctx):
     assert np.array_equal(gpu_ctx.intersect(rays), o)
     t = ptrace.hit_t(o)
     assert not np.isinf(t[o != ptrace.PT_HIT_NONE]).any()
+
+
+@pytest.mark.parametrize("batch", [None, 700])
+def test_tail_compaction_matches_oracle(batch, monkeypatch):
+    """Tail compaction (k_shade_push with ShadeArgs::compact, then passes over
+    the compacted slots): a context with it (the default) and one without
+    (PT_COMPACT=0, read at pt_create) give the oracle's image and ray count,
+    with the default schedule and the reference schedule (two shadow-ray slots
+    per path), in one chunk and in many small ones (batch_paths=700)."""
+    sc = load_fixture("CBbunny")
+    d = sc.desc()
+    W, H, SPP = 48, 40, 3
+    kw = {} if batch is None else {"batch_paths": batch}
+    for flags in (0, ptrace.PT_FLAG_REF_SCHEDULE):
+        o, orays = pyoracle.image(d, W, H, SPP, max_bounces=8, seed=15618, flags=flags)
+        for comp in ("2", "0"):
+            monkeypatch.setenv("PT_COMPACT", comp)
+            ctx = ptrace.Context(0)
+            try:
+                ctx.load_scene(sc)
+                ctx.reset_stats()
+                ctx.render(W, H, SPP, max_bounces=8, seed=15618, flags=flags, **kw)
+                assert np.array_equal(ctx.get_image(), o), (flags, comp)
+                assert ctx.stats().rays == orays, (flags, comp)
+            finally:
+                ctx.close()
