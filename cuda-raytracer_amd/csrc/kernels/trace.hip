@@ -692,34 +692,20 @@ __global__ __launch_bounds__(TPB) void k_trace_root(TraceArgs A, RootTable T, ui
 // one atomic round trip.  A grandchild's box is tested only for rays that
 // entered its parent's box.  Ray ids only (the queues hold ids).
 __device__ __forceinline__ float f4c(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
-__device__ __forceinline__ float rdl(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-// crow: the node's four children's records, prefetched by process_wave one
-// row per lane (lane 8c + r holds float4 row r of child c: rows 0-5 its
-// grandchild boxes, row 6 its links, row 7 {prim_start, prim_count, ..}), so
-// the children's data arrives in the same round trip as the rays instead of
-// one scalar round trip per interior child after them
 __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, const CPTR(pt_node) nd, int lane,
                                                const uint32_t (&id)[RPTW], const f3 (&inv)[RPTW],
                                                const f3 (&oi)[RPTW], const float (&tmax)[RPTW],
-                                               const bool (&valid)[RPTW], int nj, const float4 crow) {
+                                               const bool (&valid)[RPTW], int nj) {
   const uint32_t lid = lane_id();
   // the targets (node data only): lane t = 4c + g holds the node of target
   // t -- leaf child c (g = 0) or child g of interior child c -- or -1
-  const int c0 = nd->child[0], c1 = nd->child[1], c2 = nd->child[2], c3 = nd->child[3];
-  const int tc = (int)(lid >> 2) & 3, tg = (int)(lid & 3);
-  // (every lane runs the shuffles: the source lanes must be active)
-  const int pcc = __shfl(__float_as_int(crow.y), 8 * tc + 7, 64);
-  const int l0 = __shfl(__float_as_int(crow.x), 8 * tc + 6, 64), l1 = __shfl(__float_as_int(crow.y), 8 * tc + 6, 64),
-            l2 = __shfl(__float_as_int(crow.z), 8 * tc + 6, 64), l3 = __shfl(__float_as_int(crow.w), 8 * tc + 6, 64);
   int tnode = -1;
   bool tleaf = false;
   if (lid < 16) {
-    const int ch = tc == 0 ? c0 : tc == 1 ? c1 : tc == 2 ? c2 : c3;
+    const int ch = A.nodes[node].child[lid >> 2];
     if (ch >= 0) {
-      tleaf = pcc > 0;
-      tnode = tleaf ? (tg == 0 ? ch : -1) : (tg == 0 ? l0 : tg == 1 ? l1 : tg == 2 ? l2 : l3);
+      tleaf = A.nodes[ch].prim_count > 0;
+      tnode = tleaf ? ((lid & 3) == 0 ? ch : -1) : A.nodes[ch].child[lid & 3];
     }
   }
   const uint32_t tmask = (uint32_t)__ballot(tnode >= 0);           // (uniform)
@@ -750,14 +736,16 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
       for (int j = 0; j < RPTW; ++j) bits[j] |= ((hc >> j) & 1u) << (4 * c);
       continue;
     }
-    // the four grandchild boxes (SoA rows 0-5 of the child node), from the
-    // prefetched rows: lane 8c + r
+    // the four grandchild boxes (SoA rows of the child node) in one round trip
+    const CPTR(f4v) cn = (const CPTR(f4v))(A.nodes + nd->child[c]);
+    const float4 gx0 = f4(cn[0]), gx1 = f4(cn[1]), gy0 = f4(cn[2]), gy1 = f4(cn[3]), gz0 = f4(cn[4]),
+                 gz1 = f4(cn[5]);
+    asm volatile("" ::"s"(gx0.x), "s"(gx1.x), "s"(gy0.x), "s"(gy1.x), "s"(gz0.x), "s"(gz1.x));
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       if (!((cm >> g) & 1u)) continue;
-      const int L = 8 * c;
-      const float b0 = rdl(f4c(crow, g), L), b1 = rdl(f4c(crow, g), L + 1), b2 = rdl(f4c(crow, g), L + 2),
-                  b3 = rdl(f4c(crow, g), L + 3), b4 = rdl(f4c(crow, g), L + 4), b5 = rdl(f4c(crow, g), L + 5);
+      const float b0 = f4c(gx0, g), b1 = f4c(gx1, g), b2 = f4c(gy0, g), b3 = f4c(gy1, g), b4 = f4c(gz0, g),
+                  b5 = f4c(gz1, g);
 #pragma unroll
       for (int j = 0; j < RPTW; ++j) {
         if (j >= nj) break;
@@ -828,15 +816,6 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     if (valid[j]) load_ray(A, ids, base + (uint32_t)i, id[j], o[j], d[j], tmax[j]);
   }
   const int nj = (n + 63) >> 6;  // ray groups with at least one valid lane (uniform)
-  // an interior node of a two-level pass: its children's records, one row per
-  // lane, loaded behind the rays (push_two_level)
-  float4 crow = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (!LEAF && two_level && nd->prim_count == 0) {
-    const int c = (int)(lid >> 3) & 3;
-    const int c0 = nd->child[0], c1 = nd->child[1], c2 = nd->child[2], c3 = nd->child[3];
-    const int ch = c == 0 ? c0 : c == 1 ? c1 : c == 2 ? c2 : c3;
-    if (lid < 32 && ch >= 0) crow = reinterpret_cast<const float4*>(A.nodes + ch)[lid & 7];
-  }
   float tlo[RPTW];  // the rays' t_min (pt_intersect; TMIN only)
 #pragma unroll
   for (int j = 0; j < RPTW; ++j) tlo[j] = (TMIN && valid[j]) ? A.tmin[id[j]] : 0.0f;
@@ -893,7 +872,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
                   __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
       oi[j] = mk(o[j].x * inv[j].x, o[j].y * inv[j].y, o[j].z * inv[j].z);
     }
-    push_two_level(A, node, nd, lane, id, inv, oi, tmax, valid, nj, crow);
+    push_two_level(A, node, nd, lane, id, inv, oi, tmax, valid, nj);
     return;
   }
   uint32_t bits[RPTW];
