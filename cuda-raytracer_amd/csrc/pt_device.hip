@@ -96,7 +96,8 @@ struct pt_ctx {
   float4* ray_cur = nullptr;
   uint32_t* d_compact = nullptr;  // MAX_COMPACTIONS slot counters
   bool compaction = true;         // PT_COMPACT=0: off
-  int compact_div = 2;            // compact when live slots <= layout / compact_div (PT_COMPACT=k)
+  int compact_pct = 50;           // compact when live slots <= this % of the layout (PT_COMPACT=pct)
+  int compact_first = 50;         // the same for the chunk's first compaction (PT_COMPACT_FIRST=pct)
   uint32_t* d_q = nullptr;   // ray-id queues (QREGIONS regions): the root's targets and the levels above entry_level
   size_t qcap = 0;           // ids per region
   int entry_level = 0;       // first level whose queues hold ray entries (build_root_table)
@@ -782,7 +783,10 @@ int pt_create(pt_ctx** out, int device) {
   // tail compaction needs the wave record order's continuing-first ranks
   if (const char* q = getenv("PT_COMPACT")) {
     c->compaction = atoi(q) != 0;
-    if (atoi(q) > 1) c->compact_div = atoi(q);
+    if (atoi(q) > 1) c->compact_pct = std::min(100, atoi(q));
+  }
+  if (const char* q = getenv("PT_COMPACT_FIRST")) {
+    c->compact_first = std::min(100, std::max(1, atoi(q)));
   }
   c->compaction = c->compaction && PT_SORT_WAVE == 3;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1300,7 +1304,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         // slots are live or unstarted: compact them (the next group's first
         // pass; it also starts every path still left in a workgroup's block)
         compact_next = c->compaction && c->d_ray_b && unclaimed == 0 && ncomp < MAX_COMPACTIONS &&
-                       (uint64_t)nlive * c->compact_div <= (uint64_t)nbound * (c->compact_div == 3 ? 2 : 1);
+                       (uint64_t)nlive * 100 <= (uint64_t)nbound * (ncomp ? c->compact_pct : c->compact_first);
         S.dense = dense_ok && ((uint64_t)nlive > 2ull * N || (ncomp > 0 && (uint64_t)nlive * 2 > nbound)) ? 1u : 0u;
         if ((rc = enqueue_group(g + 2, np, nlive))) return rc;
         queued += (uint64_t)np;
