@@ -105,7 +105,10 @@ __device__ __forceinline__ f3 xyz(float4 a) { return mk(a.x, a.y, a.z); }
 // REFA: cu:347-354 literally -- k / length(k) as k * (1 / length(k))
 // (cuda_util.h operator/), dir = k.x left + k.y up + k.z lookAt as an FMA chain,
 // not normalised.
-template <bool M64 = false, bool REFA = false>
+template <bool KR>
+__device__ __forceinline__ pt_camera cam_of(const ShadeArgs& S);
+// KR: the camera re-read from the kernel-argument segment (cam_of)
+template <bool M64 = false, bool REFA = false, bool KR = false>
 __device__ __forceinline__ f3 camera_dir(const ShadeArgs& S, uint32_t p, uint32_t& g) {
   const uint32_t j = udiv_q(p, S.div_npix), q = p - j * S.npix;
   g = S.pix_of[q];
@@ -118,7 +121,8 @@ __device__ __forceinline__ f3 camera_dir(const ShadeArgs& S, uint32_t p, uint32_
   float kx = ssy / (float)S.width - 0.5f;
   float ky = -(ssx / (float)S.height - 0.5f);
   float kz = 1.0f;
-  const f3 L = ld3(S.cam.left), U = ld3(S.cam.up), K = ld3(S.cam.look_at);
+  const pt_camera cam = cam_of<KR>(S);
+  const f3 L = ld3(cam.left), U = ld3(cam.up), K = ld3(cam.look_at);
   if constexpr (REFA) {
     const float inv = 1.0f / length(mk(kx, ky, kz));
     const f3 k = mk(kx, ky, kz) * inv;
@@ -167,6 +171,25 @@ __device__ __forceinline__ pt_light light_of(const ShadeArgs& S) {
     return L;
   }
   return S.light;
+}
+// The camera likewise (k_path_leaf: its 12 floats are not held in SGPRs --
+// and spilled to VGPR lanes -- across the path loop; the launch check covers
+// it too)
+template <bool KR>
+__device__ __forceinline__ pt_camera cam_of(const ShadeArgs& S) {
+  if (KR) {
+    const CPTR(char) kp = (const CPTR(char))__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));  // not loop-invariant for the compiler
+    constexpr int NW = sizeof(pt_camera) / 4;
+    const CPTR(uint32_t) q = (const CPTR(uint32_t))(kp + offsetof(ShadeArgs, cam));
+    uint32_t w[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) w[i] = q[i];
+    pt_camera c;
+    __builtin_memcpy(&c, w, sizeof(c));
+    return c;
+  }
+  return S.cam;
 }
 // Shadow-ray tmax of the reference (cu:446, 1279): the light counts when the
 // closest hit t satisfies t > maxT - 1e-3 in double precision (1e-3 is a
@@ -1295,6 +1318,10 @@ constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 #ifndef PT_PATH_WAVES
 #define PT_PATH_WAVES 8
 #endif
+// the camera re-read from the kernel arguments at each path start (cam_of)
+#ifndef PT_PATH_CAM_RELOAD
+#define PT_PATH_CAM_RELOAD true
+#endif
 #ifndef PT_PATH_LDS_SH
 #define PT_PATH_LDS_SH 1
 #endif
@@ -1371,14 +1398,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
   // kernel-argument segment, so S must stay this kernel's FIRST parameter:
   // checked at every launch (wave-uniform, a few cached scalar loads); a
   // mismatch sets ERR_KERNARG and the kernel does nothing (pt_render fails)
-  if (PT_PATH_LIGHT_RELOAD) {
+  if (PT_PATH_LIGHT_RELOAD || PT_PATH_CAM_RELOAD) {
     const pt_light a = light_of<true>(S), b = S.light;
-    uint32_t wa[sizeof a / 4], wb[sizeof b / 4];
+    const pt_camera ca = cam_of<true>(S), cb = S.cam;
+    uint32_t wa[sizeof a / 4], wb[sizeof b / 4], wc[sizeof ca / 4], wd[sizeof cb / 4];
     __builtin_memcpy(wa, &a, sizeof a);
     __builtin_memcpy(wb, &b, sizeof b);
+    __builtin_memcpy(wc, &ca, sizeof ca);
+    __builtin_memcpy(wd, &cb, sizeof cb);
     bool same = true;
 #pragma unroll
     for (uint32_t i = 0; i < sizeof a / 4; ++i) same = same && wa[i] == wb[i];
+#pragma unroll
+    for (uint32_t i = 0; i < sizeof ca / 4; ++i) same = same && wc[i] == wd[i];
     if (!same) {
       if (threadIdx.x == 0) atomicOr(err, ERR_KERNARG);
       return;
@@ -1461,7 +1493,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
         const uint32_t p = next + r;
         sh_p[threadIdx.x] = p;
         active = true;
-        const f3 dir = camera_dir<PT_PATH_MAD64, REFA>(S, p, st.g);
+        const f3 dir = camera_dir<PT_PATH_MAD64, REFA, PT_PATH_CAM_RELOAD>(S, p, st.g);
         st.T = mk(1.0f, 1.0f, 1.0f);
         st.L = mk(0.0f, 0.0f, 0.0f);
         if constexpr (PT_PATH_LDS_SH) {
@@ -1473,7 +1505,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
           Lq[5 * TPB] = 1.0f;
         }
         st.flags = F_EXT | (1u << 8);
-        ext = RayV{ld3(S.cam.origin), dir, __builtin_inff()};
+        ext = RayV{ld3(cam_of<PT_PATH_CAM_RELOAD>(S).origin), dir, __builtin_inff()};
       }
       next += min((uint32_t)__popcll(idle), avail);
     }
