@@ -94,12 +94,43 @@ __device__ __forceinline__ bool prim_sphere(const Prim& q) {
 // plane hit (a wave skips the inside test when no lane has t in [tlo, tbest]),
 // the inside test predicated.  A ray parallel to the plane has t = +-inf or
 // NaN and misses.
+// t = num / den of the Baldwin-Weber test.  PT_FAST_DIV: the compiler's IEEE
+// division sequence (reciprocal, one refinement, quotient, two residual
+// corrections) without its range scaling (v_div_scale x 2) and special-case
+// fixup (v_div_fixup): 8 instead of 11 instructions and the same bits wherever
+// the scaling is the identity -- both operands and the quotient in the normal
+// range, away from the extremes.  Outside it (|den| denormal or zero, an
+// overflowing quotient: a ray parallel to the plane) the result is NaN, an
+// infinity or a huge t, and the test misses as it does for the IEEE quotient
+// (|u| or |v| huge, or unordered); only a hit at t below ~2^-100 (an origin
+// on the plane to 30 decimal places) could differ in t's last bits.  The
+// oracle divides with IEEE `/`; the GPU parity tests check the two agree.
+#ifndef PT_FAST_DIV
+#define PT_FAST_DIV 1
+#endif
+__device__ __forceinline__ float div_rn(float a, float b) {
+  if constexpr (!PT_FAST_DIV) return a / b;
+  const float y0 = __builtin_amdgcn_rcpf(b);
+  const float e = __builtin_fmaf(-b, y0, 1.0f);
+  const float y1 = __builtin_fmaf(e, y0, y0);
+  const float q0 = a * y1;
+  const float r0 = __builtin_fmaf(-b, q0, a);
+  const float q1 = __builtin_fmaf(r0, y1, q0);
+  const float r1 = __builtin_fmaf(-b, q1, a);
+  return __builtin_fmaf(r1, y1, q1);
+}
+// pt_check_division: div_rn over host-given pairs
+__global__ __launch_bounds__(TPB) void k_check_division(const float* __restrict__ a, const float* __restrict__ b,
+                                                        float* __restrict__ q, uint32_t n) {
+  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+  if (i < n) q[i] = div_rn(a[i], b[i]);
+}
 __device__ __forceinline__ float bw_plane(const f3 o, const float4 W) {
   return __builtin_fmaf(W.z, o.z, __builtin_fmaf(W.y, o.y, __builtin_fmaf(W.x, o.x, W.w)));
 }
 __device__ __forceinline__ float bw_test(const f3 o, const f3 d, const float4 U, const float4 V, const float4 W,
                                          float tbest, float tlo = 0.0f) {
-  const float t = -bw_plane(o, W) / fdot(W.x, W.y, W.z, d.x, d.y, d.z);
+  const float t = div_rn(-bw_plane(o, W), fdot(W.x, W.y, W.z, d.x, d.y, d.z));
   if (!(t >= tlo) | (t > tbest)) return -1.0f;
   const float u = __builtin_fmaf(t, fdot(U.x, U.y, U.z, d.x, d.y, d.z), bw_plane(o, U));
   const float v = __builtin_fmaf(t, fdot(V.x, V.y, V.z, d.x, d.y, d.z), bw_plane(o, V));
@@ -229,7 +260,8 @@ __device__ __forceinline__ f2v bw_plane2(const f3x2& o, const float4 R) {
 }
 __device__ __forceinline__ f2v bw_test2(const f3x2& o, const f3x2& d, const float4 U, const float4 V, const float4 W,
                                         f2v tbest, f2v tlo) {
-  const f2v t = -bw_plane2(o, W) / fdot2(sp3(W.x, W.y, W.z), d);
+  const f2v nm = -bw_plane2(o, W), dn = fdot2(sp3(W.x, W.y, W.z), d);
+  const f2v t = f2v{div_rn(nm[0], dn[0]), div_rn(nm[1], dn[1])};
   const f2v u = fma2(t, fdot2(sp3(U.x, U.y, U.z), d), bw_plane2(o, U));
   const f2v v = fma2(t, fdot2(sp3(V.x, V.y, V.z), d), bw_plane2(o, V));
   const f2v uv = u + v;

@@ -756,6 +756,26 @@ int pt_dbg_path_timing(unsigned long long* out, int nwaves) {
 }
 #endif
 
+int pt_check_division(pt_ctx* c, const float* num, const float* den, float* q, int32_t n) {
+  if (!c || !num || !den || !q || n < 0) return PT_E_INVALID;
+  if (n == 0) return PT_OK;
+  float* d = nullptr;
+  HIPCHK(c, hipMalloc((void**)&d, (size_t)n * 12));
+  int rc = PT_OK;
+  if (hipMemcpy(d, num, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d + n, den, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess)
+    rc = fail(c, PT_E_HIP, "pt_check_division: copy in");
+  if (rc == PT_OK) {
+    hipLaunchKernelGGL(k_check_division, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, (const float*)d,
+                       (const float*)(d + n), d + 2 * (size_t)n, (uint32_t)n);
+    if (hipStreamSynchronize(c->stream) != hipSuccess ||
+        hipMemcpy(q, d + 2 * (size_t)n, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = fail(c, PT_E_HIP, "pt_check_division: kernel");
+  }
+  hipFree(d);
+  return rc;
+}
+
 int pt_device_count(int* n) {
   if (!n) return PT_E_INVALID;
   hipError_t e = hipGetDeviceCount(n);

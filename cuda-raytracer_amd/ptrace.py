@@ -118,7 +118,7 @@ API_SYMBOLS = [
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
     "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex", "pt_copy_owned_sums",
     "pt_get_stats", "pt_reset_stats", "pt_median_filter", "pt_get_display_image", "pt_tonemap",
-    "pt_write_png", "pt_write_pfm",
+    "pt_write_png", "pt_write_pfm", "pt_check_division",
 ]
 
 
@@ -171,6 +171,7 @@ def _load():
         "pt_intersect_ex": (C.c_int, [P, C.POINTER(C.c_float), I32, C.POINTER(C.c_uint64), U32]),
         "pt_get_stats": (C.c_int, [P, C.POINTER(pt_stats)]),
         "pt_reset_stats": (C.c_int, [P]),
+        "pt_check_division": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float), I32]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -389,6 +390,15 @@ class Context:
     def _chk(self, rc):
         if rc != PT_OK:
             raise PTError(rc, LIB.pt_last_error(self.h).decode(errors="replace"))
+
+    def check_division(self, num, den):
+        """num / den as the device's triangle test divides (pt_check_division)."""
+        num = np.ascontiguousarray(num, dtype=np.float32)
+        den = np.ascontiguousarray(den, dtype=np.float32)
+        q = np.empty_like(num)
+        self._chk(LIB.pt_check_division(self.h, _ptr(num, C.c_float), _ptr(den, C.c_float), _ptr(q, C.c_float),
+                                        len(num)))
+        return q
 
     def load_scene(self, scene: Scene):
         self._desc = scene.desc()

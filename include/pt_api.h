@@ -382,6 +382,12 @@ typedef struct pt_stats {
 int pt_get_stats(pt_ctx* ctx, pt_stats* out);
 int pt_reset_stats(pt_ctx* ctx);
 
+/* Self-check of the triangle test's division on the device (no reference
+ * counterpart): q[i] = num[i] / den[i] as the Baldwin-Weber test computes it
+ * (trace.hip div_rn), for n host pairs.  Tests compare it with IEEE
+ * division. */
+int pt_check_division(pt_ctx* ctx, const float* num, const float* den, float* q, int32_t n);
+
 #ifdef __cplusplus
 }
 #endif
