@@ -1294,7 +1294,8 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
 #define PT_PATH_MAD64 true  // Philox products as v_mad_u64_u32 (CBempty +1.4 %; k_shade_push would lose its 7th wave)
 #endif
 // paths a wave takes from the global counter at a time (CBempty: 128: -1.3 %,
-// 512: +1.6 %, 1024: +1.4 %, 2048: +0.1 % against 256)
+// 512: +1.6 %, 1024: +1.4 %, 2048: +0.1 % against 256; re-measured in round
+// 3: 1024 -0.3 %, 256 -1.2 % against 512)
 #ifndef PT_PATH_CHUNK
 #define PT_PATH_CHUNK 512
 #endif
