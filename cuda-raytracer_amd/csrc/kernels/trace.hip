@@ -967,8 +967,10 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 // LEAF: a level whose queued nodes are all leaves (the levels between two
 // real levels hold only the leaf rays of the real level above them): the
 // leaf-only code needs fewer registers and runs PT_LEAF_WAVES waves per SIMD
+// (8, round 3: 64 VGPRs, 4 spilled, against 68 at 7 waves: the leaf levels'
+// share of the dragon proxy's levels ~1 % faster)
 #ifndef PT_LEAF_WAVES
-#define PT_LEAF_WAVES 6
+#define PT_LEAF_WAVES 8
 #endif
 // TMIN: the rays carry a t_min (pt_intersect with t_min > 0 somewhere in the
 // batch): hits before it do not count (TraceArgs::tmin)
@@ -982,9 +984,11 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
 // push exists for wave items only): without the workgroup-item code the
 // kernel needs 22 SGPR spills instead of 51, and runs 6 waves per SIMD (80
 // VGPRs, 5 spilled): dragon proxy level 6 30.1 -> 28.4 ms, frame +0.9 %
-// (at 5 waves it measured the same as k_trace_level)
+// (at 5 waves it measured the same as k_trace_level); round 3: 7 waves (72
+// VGPRs, 6 spilled) with the leaf kernel at 8: levels -1.5 to -3 % on the
+// dragon proxy trees and bunny.dae
 #ifndef PT_REAL_WAVES
-#define PT_REAL_WAVES 6
+#define PT_REAL_WAVES 7
 #endif
 #define PT_REAL_ATTR __attribute__((amdgpu_waves_per_eu(PT_REAL_WAVES, 8)))
 template <bool REFA, bool TMIN = false>
