@@ -48,7 +48,10 @@ instrumented frame (the headline frames run without events):
     also counts an FMA as 2); PMC VALU activity beside it when profiled.
 Each workload also reports "ms_1spp" (one 1-spp frame, outside the timed
 steps) and, under "trace", the traversal passes of a frame and ms per pass
-(SURVEY §8(d)).
+(SURVEY §8(d)).  The stdout line stays compact (< 12 KB, compact_line: the
+headline, its roofline and cpu_baseline, and per other workload its value,
+ms/frame and roofline fraction); every workload's full record -- per-level
+traces, notes, PMC sources -- goes to --detail-out, which the line names.
 "traffic" is HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x 2 +
 WRITE_SIZE, MI355X_MICROARCH.md) when a matching summary is committed under
 profiles/ (scripts/pmc.sh, scripts/pmc_summary.py), else null.
@@ -93,7 +96,7 @@ def parse():
     p.add_argument("--bounces", type=int, default=8)
     p.add_argument("--batch", type=int, default=0, help="paths in flight per batch (0 = auto)")
     p.add_argument("--tile", type=int, default=32)
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=20.0, help="target length of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--seed", type=int, default=15618)
     p.add_argument("--config5", choices=["auto", "on", "off"], default="auto",
@@ -106,7 +109,13 @@ def parse():
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="collective backend of the frame gather (nccl = RCCL over xGMI; gloo: tests only -- ranks "
                         "may share a GPU, device LOCAL_RANK %% device_count, the gather runs on host tensors)")
+    p.add_argument("--force-gather", action="store_true",
+                   help="tests: initialise the process group and gather the frame even at WORLD_SIZE=1 (runs "
+                        "the nccl path -- local_sums_tensor on the device, dist.gather, index_copy_ -- on one GPU)")
     p.add_argument("--save-frame", default=None, help="rank 0 saves the last headline frame (.npy; tests)")
+    p.add_argument("--detail-out", default="gpurun_out/bench_detail.json",
+                   help="rank 0 writes every workload's full record (per-level traces, notes, PMC sources) here; "
+                        "the stdout line stays compact and names this file ('' = none)")
     p.add_argument("--ref-arith", default="CBbunny",
                    help="workloads also measured with PT_FLAG_REF_ARITH, the reference kernels' literal "
                         "arithmetic ('' = none)")
@@ -122,14 +131,35 @@ def _free_port():
     return port
 
 
+def visible_gpus(topology="/sys/class/kfd/kfd/topology/nodes", env=None):
+    """GPUs this process may use, counted without touching the HIP runtime:
+    KFD topology nodes with SIMDs (CPU nodes have simd_count 0), narrowed by
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES."""
+    env = os.environ if env is None else env
+    n = 0
+    for props in sorted(Path(topology).glob("*/properties")):
+        try:
+            kv = dict(l.split()[:2] for l in props.read_text().splitlines() if len(l.split()) >= 2)
+        except OSError:
+            continue
+        if int(kv.get("simd_count", "0")) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            ids = [s for s in v.split(",") if s.strip() != ""]
+            n = min(n, len(ids))
+    return n
+
+
 def launch_ranks(args):
     """--gpus N > 1 without a torch.distributed launcher around us: start the
     N ranks as a child torch.distributed.run (one process per GPU) and return
-    its exit status.  Nothing here touches the GPU (torch.cuda.device_count
-    does not initialise it), so the ranks own their devices."""
+    its exit status.  Nothing here touches the GPU or the HIP runtime (the
+    GPUs are counted from the KFD topology in sysfs), so the ranks own their
+    devices."""
     import subprocess
-    import torch
-    n = torch.cuda.device_count()
+    n = visible_gpus()
     if n < args.gpus and args.backend == "nccl":
         print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {n}", file=sys.stderr, flush=True)
         return 2
@@ -180,9 +210,8 @@ def cpu_baseline(desc, args):
     _, rays, dt, thr = pyoracle.scotty_render(desc, args.width, args.height, 4, args.bounces, seed=args.seed,
                                               tile_stride=cal, threads=ncpu)
     full_s = dt * cal * args.spp / 4  # estimated seconds for the whole frame
-    stride = 1
-    while full_s / stride > args.cpu_seconds and stride < ntiles:
-        stride *= 2
+    # the smallest tile stride whose share fits --cpu-seconds (a 10-30 s sample)
+    stride = min(ntiles, max(1, int(-(-full_s // args.cpu_seconds))))
     _, rays, dt, thr = pyoracle.scotty_render(desc, args.width, args.height, args.spp, args.bounces,
                                               seed=args.seed, tile_stride=stride, threads=ncpu)
     nt = len(range(0, ntiles, stride))
@@ -285,7 +314,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
         ctx.render(args.width, args.height, args.spp, max_bounces=args.bounces, seed=args.seed,
                    batch_paths=args.batch, tile_size=args.tile, rank=t_rank, nranks=t_world,
                    flags=flags | (ptrace.PT_FLAG_STATS if stats else 0))
-        if world > 1:
+        if world > 1 or args.force_gather:
             # RCCL gathers device tensors; gloo (tests) host tensors
             sdev = dev if args.backend == "nccl" else "cpu"
             sums[0] = ptdist.local_sums_tensor(ctx, sdev, out=sums[0])
@@ -441,6 +470,79 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
     return out, scene
 
 
+LINE_MAX = 12000  # the driver parses the stdout line; keep it well under its limit
+_ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "launches", "avg_launch_us",
+              "flop_per_launch", "bytes_per_launch", "valu_busy", "traffic_gbs", "line_frac")
+
+
+def _short_roof(r, keys=_ROOF_KEYS):
+    return {k: r[k] for k in keys if k in r and r[k] is not None} if r else None
+
+
+def detail_record(head, others, cpu, args, world):
+    """Everything a workload measured (per-level traces, notes, PMC sources):
+    written to --detail-out, referenced from the stdout line."""
+    return {"argv": sys.argv[1:], "n_gpus": world, "headline": head, "configs": others, "cpu_baseline": cpu}
+
+
+def compact_line(head, others, cpu, args, world, detail_path=None):
+    """The one JSON line rank 0 prints (the driver's contract): the headline
+    fields, its roofline and cpu_baseline, and each other workload as
+    {scene, value, ms_per_frame, roofline: {kernel, frac, achieved, traffic}}.
+    Everything else goes to the detail file.  Bounded by LINE_MAX."""
+    configs = []
+    for o in others:
+        r = o.get("roofline") or {}
+        c = {"scene": o["scene"], "value": o["value"], "ms_per_frame": o["ms_per_frame"],
+             "roofline": {k: r.get(k) for k in ("kernel", "frac", "achieved", "traffic")}}
+        if o.get("config"):
+            c["config"] = o["config"]
+        ro = (o.get("roofline_other") or [None])[0]
+        if ro:
+            c["roofline_other"] = {k: ro.get(k) for k in ("kernel", "frac", "achieved", "traffic")}
+        configs.append(c)
+    tr = head.get("trace") or {}
+    out = {
+        "metric": f"Mrays/sec at {args.width}x{args.height}, {args.spp} spp, {args.bounces} bounces",
+        "value": head["value"],
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": head["ms_per_frame"],
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic rays (Philox seed {args.seed}) on scene {args.scene} (reference media, flattened fixture)",
+        "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.spp}spp {args.bounces} bounces",
+                   "scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
+                   "max_bounces": args.bounces, "batch_paths": head["batch_paths"],
+                   "parallelism": f"tiles{args.tile}x{world}"},
+        "ms_per_frame": head["ms_per_frame"],
+        "ms_1spp": head.get("ms_1spp"),
+        "rays_per_frame": head["rays_per_frame"],
+        "roofline": _short_roof(head["roofline"]),
+        "roofline_other": [_short_roof(r) for r in head.get("roofline_other") or []],
+        "trace": {k: tr.get(k) for k in ("visits_per_ray", "passes", "ms_per_pass", "ms_path", "ms_levels",
+                                         "ms_shade_push") if k in tr},
+        "configs": configs,
+    }
+    if cpu is not None:
+        out["cpu_baseline"] = {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample") if k in cpu}
+    if detail_path:
+        out["detail"] = str(detail_path)
+    line = json.dumps(out, separators=(",", ":"))
+    if len(line) > LINE_MAX:  # never print a line the driver cannot take: drop the extras first
+        for k in ("trace", "roofline_other", "ms_1spp"):
+            out.pop(k, None)
+        for c in out["configs"]:
+            c.pop("roofline_other", None)
+            c.pop("config", None)
+        line = json.dumps(out, separators=(",", ":"))
+    return line
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -456,7 +558,7 @@ def main():
     # one GPU per rank (gloo test runs may put several ranks on one GPU)
     gpu = local if args.backend == "nccl" else local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(gpu)
-    if world > 1:
+    if world > 1 or args.force_gather:
         import torch.distributed as dist
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
@@ -504,35 +606,14 @@ def main():
         o["config"] = "config 5 workload, single GPU: the whole 2048x2048 1024spp 8-bounce frame on one MI355X"
         others.append(o)
     if rank == 0:
-        out = {
-            "metric": f"Mrays/sec at {args.width}x{args.height}, {args.spp} spp, {args.bounces} bounces",
-            "value": head["value"],
-            "unit": "Mrays/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": head["ms_per_frame"],
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": f"scene {args.scene} (reference media, flattened fixture); rays sampled with Philox seed {args.seed}",
-            "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.spp}spp {args.bounces} bounces",
-                       "scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
-                       "max_bounces": args.bounces, "batch_paths": head["batch_paths"],
-                       "parallelism": f"tiles{args.tile}x{world}"},
-            "ms_per_frame": head["ms_per_frame"],
-            "ms_1spp": head["ms_1spp"],
-            "rays_per_frame": head["rays_per_frame"],
-            "roofline": head["roofline"],
-            "scene_build_ms": head["scene_build_ms"],
-            "bvh": head["bvh"],
-            "trace": head["trace"],
-            "configs": others,
-        }
-        if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(head_scene.desc(), args)
-        print(json.dumps(out), flush=True)
+        cpu = cpu_baseline(head_scene.desc(), args) if world == 1 and not args.no_cpu else None
+        detail = detail_record(head, others, cpu, args, world)
+        line = compact_line(head, others, cpu, args, world, detail_path=args.detail_out)
+        if args.detail_out:
+            p = Path(args.detail_out)
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_text(json.dumps(detail, indent=1) + "\n")
+        print(line, flush=True)
     ctx.close()
     if dist:
         dist.destroy_process_group()

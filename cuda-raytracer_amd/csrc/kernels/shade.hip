@@ -412,6 +412,18 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           emitter = rad.x != 0.0f || rad.y != 0.0f || rad.z != 0.0f;  // cu:436
         }
         if (B.type == PT_BSDF_EMISSION) B.type = PT_BSDF_DIFFUSE;  // albedo = radiance (cu:1705-1711)
+        // a delta BSDF is read through a MirrorBSDF reinterpret_cast
+        // (cu:1713-1719): over a GlassBSDF its reflectance is (roughness,
+        // reflectance.r, reflectance.g), over a RefractionBSDF (roughness,
+        // transmittance.r, transmittance.g) (bsdf.h:138-139, 180-182, 206-210)
+        if (B.type == PT_BSDF_GLASS || B.type == PT_BSDF_REFRACTION) {
+          const float c1 = B.type == PT_BSDF_GLASS ? B.albedo[0] : B.transmittance[0];
+          const float c2 = B.type == PT_BSDF_GLASS ? B.albedo[1] : B.transmittance[1];
+          B.albedo[0] = B.roughness;
+          B.albedo[1] = c1;
+          B.albedo[2] = c2;
+          B.type = PT_BSDF_MIRROR;
+        }
       }
       if (!REFA && B.type == PT_BSDF_EMISSION) {
         if (!(S.flags & PT_FLAG_NO_EMISSION) && (vtx == 1u || spec)) {
@@ -522,7 +534,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           }
           Tset(mulv(Tv(), ld3(B.albedo)));
           spec = F_SPEC;
-        } else {  // PT_BSDF_GLASS (Fresnel-weighted reflect / refract, bsdf.h:187-212)
+        } else {  // PT_BSDF_GLASS / _REFRACTION (Fresnel-weighted reflect / refract, bsdf.h:167-212)
           const float ior = B.ior;
           const float eta = front ? (1.0f / ior) : ior;
           const float cosi = -dot(d, n);

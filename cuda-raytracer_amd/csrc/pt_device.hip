@@ -65,10 +65,11 @@ struct pt_ctx {
   std::vector<pt_node> nodes_host;
   pt_light light{};
   pt_camera camera{};
-  // The stored BVH boxes carry a guard band G = 2^-17 M (scene_internal.h
+  // The stored BVH boxes carry a guard band G = 2^-14 M (scene_internal.h
   // box_guard) that keeps the fp32 slab test conservative for ray origins
-  // with |coordinates| up to ~22 M (M: the scene's largest coordinate
-  // magnitude); camera and query-ray origins beyond origin_bound = 16 M are
+  // with |coordinates| up to ~180 M (M: the scene's largest coordinate
+  // magnitude); camera and query-ray origins beyond origin_bound = 64 M
+  // (beyond Scotty3D's farthest camera, ~52 x the scene's half-extent) are
   // refused (PT_E_UNSUPPORTED) rather than risking a culled grazing hit.
   double origin_bound = INFINITY;
   pt_node* d_nodes = nullptr;
@@ -93,6 +94,7 @@ struct pt_ctx {
   // the record buffer the traversal currently reads (null: d_ray)
   float4* d_ray_b = nullptr;
   float4 *d_ps0_b = nullptr, *d_ps1_b = nullptr, *d_ps2_b = nullptr, *d_ps3_b = nullptr;
+  uint32_t b_paths = 0, b_spp = 0;  // shape of the second set (allocated at a chunk's first compaction)
   float4* ray_cur = nullptr;
   uint32_t* d_compact = nullptr;  // MAX_COMPACTIONS slot counters
   bool compaction = true;         // PT_COMPACT=0: off
@@ -130,6 +132,7 @@ struct pt_ctx {
   int path_guide = 4;               // k_path_leaf grab schedule (path_grab; PT_PATH_GUIDE)
   int path_regions = 8;             // k_path_leaf path regions / counters (PT_PATH_REGIONS)
   int path_guided_below = 128;      // guided grabs below this many paths per resident lane (PT_PATH_GUIDED_BELOW)
+  uint32_t chunk_paths = 1u << 28;  // paths per chunk (PT_CHUNK_PATHS; tests force multi-chunk frames)
 
   // framebuffer
   int fb_w = 0, fb_h = 0, fb_tile = 0, fb_rank = 0, fb_nranks = 0;
@@ -224,9 +227,8 @@ static void free_all(pt_ctx* c) {
 // slower on CBbunny (HBM channel aliasing); 28-42 Mi all measure within 1.5 %.
 static constexpr uint32_t DEFAULT_BATCH_PATHS = 36u << 20;
 static constexpr int MAX_COMPACTIONS = 8;  // tail compactions per chunk (slot counters, pt_ctx::d_compact)
-// paths per chunk (per-path radiance buffer: 16 B each); POLL_GROUP passes
-// are queued between two reads of the finished-path count
-static constexpr uint32_t CHUNK_PATHS = 1u << 28;
+// paths per chunk: pt_ctx::chunk_paths (per-path radiance buffer: 12 B each);
+// POLL_GROUP passes are queued between two reads of the finished-path count
 #ifndef PT_POLL_GROUP
 #define PT_POLL_GROUP 4
 #endif
@@ -291,12 +293,15 @@ static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
   if ((rc = dalloc(c, &c->d_ps1, N))) return rc;
   if ((rc = dalloc(c, &c->d_ps2, N))) return rc;
   if (spp > 2 && (rc = dalloc(c, &c->d_ps3, N))) return rc;
-  if (c->compaction) {
-    if ((rc = dalloc(c, &c->d_ray_b, slots * RSTRIDE))) return rc;
-    if ((rc = dalloc(c, &c->d_ps0_b, N))) return rc;
-    if ((rc = dalloc(c, &c->d_ps1_b, N))) return rc;
-    if ((rc = dalloc(c, &c->d_ps2_b, N))) return rc;
-    if (spp > 2 && (rc = dalloc(c, &c->d_ps3_b, N))) return rc;
+  // the tail compaction's second set follows lazily (ensure_compact_set):
+  // pt_intersect and single-leaf scenes never compact
+  if (c->b_paths) {
+    for (float4** p : {&c->d_ray_b, &c->d_ps0_b, &c->d_ps1_b, &c->d_ps2_b, &c->d_ps3_b})
+      if (*p) {
+        hipFree(*p);
+        *p = nullptr;
+      }
+    c->b_paths = c->b_spp = 0;
   }
   // every root target needs root_per_lane ids per lane (see
   // set_root_child_offsets); the levels below get ray entries: a level needs at
@@ -317,6 +322,24 @@ static int ensure_paths(pt_ctx* c, uint32_t N, uint32_t spp) {
   c->cap_paths = N;
   c->cap_spp = spp;
   c->cap_qfactor = c->qfactor;
+  return PT_OK;
+}
+
+// The tail compaction's second slot-buffer set (ray records + path state
+// again), in the shape of the first: allocated at the first compaction a
+// render decides on.
+static int ensure_compact_set(pt_ctx* c) {
+  if (c->b_paths == c->cap_paths && c->b_spp == c->cap_spp) return PT_OK;
+  const size_t N = c->cap_paths, slots = (size_t)c->cap_spp * N;
+  int rc;
+  c->b_paths = c->b_spp = 0;
+  if ((rc = dalloc(c, &c->d_ray_b, slots * RSTRIDE))) return rc;
+  if ((rc = dalloc(c, &c->d_ps0_b, N))) return rc;
+  if ((rc = dalloc(c, &c->d_ps1_b, N))) return rc;
+  if ((rc = dalloc(c, &c->d_ps2_b, N))) return rc;
+  if (c->cap_spp > 2 && (rc = dalloc(c, &c->d_ps3_b, N))) return rc;
+  c->b_paths = c->cap_paths;
+  c->b_spp = c->cap_spp;
   return PT_OK;
 }
 
@@ -800,6 +823,9 @@ int pt_create(pt_ctx** out, int device) {
   if (const char* q = getenv("PT_PATH_GUIDE")) c->path_guide = std::max(0, atoi(q));
   if (const char* q = getenv("PT_PATH_REGIONS")) c->path_regions = std::max(1, atoi(q));
   if (const char* q = getenv("PT_PATH_GUIDED_BELOW")) c->path_guided_below = std::max(0, atoi(q));
+  // paths per chunk (a frame of npix x spp paths runs in ceil(spp / (chunk / npix))
+  // chunks, summed per pixel in sample order across them): tests set it small
+  if (const char* q = getenv("PT_CHUNK_PATHS")) c->chunk_paths = (uint32_t)std::min<long long>(1ll << 28, std::max(1ll, atoll(q)));
   // tail compaction needs the wave record order's continuing-first ranks
   if (const char* q = getenv("PT_COMPACT")) {
     c->compaction = atoi(q) != 0;
@@ -895,7 +921,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     if ((meta >> 28) == PT_PRIM_SPHERE) c->has_sphere = true;
   }
   for (int i = 0; i < s->n_bsdfs; ++i)
-    if (s->bsdfs[i].type == PT_BSDF_GLASS) c->has_glass = true;
+    if (s->bsdfs[i].type == PT_BSDF_GLASS || s->bsdfs[i].type == PT_BSDF_REFRACTION) c->has_glass = true;
   build_root_table(c);
   {  // record-order key map: the root target whose subtree holds primitive i << kmap_shift
     uint32_t b = 0;
@@ -994,7 +1020,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   HIPCHK(c, hipMemset(c->d_qoff, 0, (size_t)s->n_nodes * NLANE * 4));
   c->light = s->light;
   c->camera = s->camera;
-  {  // origin_bound: 16 x the largest magnitude of the scene's vertices, sphere extents, camera, light
+  {  // origin_bound: 64 x the largest magnitude of the scene's vertices, sphere extents, camera, light
     double m = 0.0;
     auto upd = [&](double v) { m = std::max(m, std::fabs(v)); };
     for (int i = 0; i < s->n_prims; ++i) {
@@ -1015,7 +1041,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
       upd(s->camera.origin[k]);
       upd(s->light.position[k]);
     }
-    c->origin_bound = 16.0 * m;
+    c->origin_bound = 64.0 * m;
   }
   c->have_scene = true;
   c->cap_paths = 0;  // force re-derivation of root queue offsets
@@ -1027,7 +1053,7 @@ int pt_set_camera(pt_ctx* c, const pt_camera* cam) {
   if (!c || !cam) return PT_E_INVALID;
   for (int k = 0; k < 3; ++k)
     if (!(std::fabs((double)cam->origin[k]) <= c->origin_bound))
-      return fail(c, PT_E_UNSUPPORTED, "pt_set_camera: origin beyond 16x the scene's extent (conservative box guard)");
+      return fail(c, PT_E_UNSUPPORTED, "pt_set_camera: origin beyond 64x the scene's extent (conservative box guard)");
   c->camera = *cam;
   return pt_clear(c);
 }
@@ -1101,8 +1127,10 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   const uint32_t nsh = ref_sched ? 2u : 1u;
   c->refa = (P->flags & PT_FLAG_REF_ARITH) != 0;
   c->tmin = false;
-  if (c->refa && (c->has_sphere || c->has_glass))
-    return fail(c, PT_E_UNSUPPORTED, "PT_FLAG_REF_ARITH: the reference renders triangles with diffuse/mirror BSDFs only");
+  // (glass is read as the reference reads it, a mirror: shade.hip; spheres
+  // the reference cannot render at all: cu:1765 casts every primitive to Triangle)
+  if (c->refa && c->has_sphere)
+    return fail(c, PT_E_UNSUPPORTED, "PT_FLAG_REF_ARITH: the reference renders triangles only");
   const int max_bounces = ref_sched ? 2 : P->max_bounces;
   const int passes = max_bounces + 2;  // vertices per path at most
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
@@ -1115,7 +1143,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   // chunks of spp_c samples of every owned pixel: M = npix * spp_c paths, each
   // path's radiance lands in res[j * npix + q] and is summed in sample order
   for (int done = 0; done < P->spp;) {
-    const uint32_t spp_c = std::min<uint32_t>(std::max<uint32_t>(1, CHUNK_PATHS / npix), (uint32_t)(P->spp - done));
+    const uint32_t spp_c = std::min<uint32_t>(std::max<uint32_t>(1, c->chunk_paths / npix), (uint32_t)(P->spp - done));
     const uint32_t M = npix * spp_c;
     if ((size_t)M > c->res_cap) {
       if ((rc = dalloc(c, &c->d_res, M))) return rc;
@@ -1197,9 +1225,10 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       // slot buffers: set a until the tail's first compaction, then the two
       // sets alternate (ShadeArgs::compact); in: what the shade kernel reads,
       // out: what it writes and the traversal then reads
-      float4* const RAY[2] = {c->d_ray, c->d_ray_b};
-      float4* const PS[4][2] = {{c->d_ps0, c->d_ps0_b}, {c->d_ps1, c->d_ps1_b}, {c->d_ps2, c->d_ps2_b},
-                                {c->d_ps3, c->d_ps3_b}};
+      // (the second set is allocated at the first compaction: refreshed below)
+      float4* RAY[2] = {c->d_ray, c->d_ray_b};
+      float4* PS[4][2] = {{c->d_ps0, c->d_ps0_b}, {c->d_ps1, c->d_ps1_b}, {c->d_ps2, c->d_ps2_b},
+                          {c->d_ps3, c->d_ps3_b}};
       auto bind = [&](int in, int out) {
         S.ray = RAY[in];
         S.ps0_in = PS[0][in];
@@ -1323,8 +1352,16 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         // the dispensers are dry and at most a quarter of the current layout's
         // slots are live or unstarted: compact them (the next group's first
         // pass; it also starts every path still left in a workgroup's block)
-        compact_next = c->compaction && c->d_ray_b && unclaimed == 0 && ncomp < MAX_COMPACTIONS &&
+        compact_next = c->compaction && unclaimed == 0 && ncomp < MAX_COMPACTIONS &&
                        (uint64_t)nlive * 100 <= (uint64_t)nbound * (ncomp ? c->compact_pct : c->compact_first);
+        if (compact_next) {
+          if ((rc = ensure_compact_set(c))) return rc;
+          RAY[1] = c->d_ray_b;
+          PS[0][1] = c->d_ps0_b;
+          PS[1][1] = c->d_ps1_b;
+          PS[2][1] = c->d_ps2_b;
+          PS[3][1] = c->d_ps3_b;
+        }
         S.dense = dense_ok && ((uint64_t)nlive > 2ull * N || (ncomp > 0 && (uint64_t)nlive * 2 > nbound)) ? 1u : 0u;
         if ((rc = enqueue_group(g + 2, np, nlive))) return rc;
         queued += (uint64_t)np;
@@ -1476,9 +1513,14 @@ int pt_intersect_ex(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits, uin
     const float* r = rays + (size_t)8 * i;
     if (!(std::fabs((double)r[0]) <= c->origin_bound && std::fabs((double)r[1]) <= c->origin_bound &&
           std::fabs((double)r[2]) <= c->origin_bound))
-      return fail(c, PT_E_UNSUPPORTED, "pt_intersect: ray origin beyond 16x the scene's extent (conservative box guard)");
+      return fail(c, PT_E_UNSUPPORTED, "pt_intersect: ray origin beyond 64x the scene's extent (conservative box guard)");
     const float t = r[7];
     if (t != t) return fail(c, PT_E_INVALID, "pt_intersect: t_min is NaN");
+    if (c->has_sphere) {  // the sphere test assumes a unit direction (trace.hip sphere_test)
+      const double l2 = (double)r[4] * r[4] + (double)r[5] * r[5] + (double)r[6] * r[6];
+      if (!(std::fabs(l2 - 1.0) <= 1e-5))
+        return fail(c, PT_E_INVALID, "pt_intersect: a scene with spheres needs unit ray directions");
+    }
     if (t > 0.0f) {
       if (tmin.empty()) tmin.assign((size_t)n, 0.0f);
       tmin[i] = t;

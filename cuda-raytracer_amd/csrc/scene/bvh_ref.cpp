@@ -292,7 +292,7 @@ double box_guard(const Scene& S) {
   // PT_BOX_GUARD=0 turns the band off (diagnostics: scripts/dev/guard_off.py)
   const char* e = getenv("PT_BOX_GUARD");
   if (e && atoi(e) == 0) return 0.0;
-  return std::ldexp(m, -17);
+  return std::ldexp(m, -14);
 }
 
 // BSDF table: one entry per scene object (cu:1694-1723)
@@ -306,6 +306,7 @@ void flatten_bsdfs(Scene& S) {
       b.transmittance[k] = m.trans[k];
     }
     b.ior = m.ior;
+    b.roughness = m.roughness;
     S.dbsdfs.push_back(b);
   }
 }

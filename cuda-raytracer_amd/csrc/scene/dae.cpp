@@ -221,13 +221,14 @@ struct Loader {
           spectrum_from(get_element(b.get(), "reflectance"), m.albedo);
         } else if (t == "glass" || t == "refraction") {
           m = Material();
-          m.type = PT_BSDF_GLASS;
+          m.type = t == "glass" ? PT_BSDF_GLASS : PT_BSDF_REFRACTION;
           if (t == "glass")
             spectrum_from(get_element(b.get(), "reflectance"), m.albedo);
           else
             m.albedo[0] = m.albedo[1] = m.albedo[2] = 0.f;
           spectrum_from(get_element(b.get(), "transmittance"), m.trans);
           if (XNode* ior = get_element(b.get(), "ior")) m.ior = (float)atof(ior->text.c_str());
+          if (XNode* r = get_element(b.get(), "roughness")) m.roughness = (float)atof(r->text.c_str());
         }
       }
     } else if (com) {

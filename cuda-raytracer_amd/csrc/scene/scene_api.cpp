@@ -71,6 +71,7 @@ int scene_from_mesh(const pt_mesh_desc* md, Scene& S) {
       mat.trans[k] = md->bsdfs[b].transmittance[k];
     }
     mat.ior = md->bsdfs[b].ior;
+    mat.roughness = md->bsdfs[b].roughness;
     S.materials.push_back(mat);
   }
   if (md->light) S.light = *md->light;
@@ -148,6 +149,7 @@ int pt_scene_from_triangles(const float* positions, int32_t n_tris, const pt_bsd
       mat.trans[k] = bsdf0->transmittance[k];
     }
     mat.ior = bsdf0->ior;
+    mat.roughness = bsdf0->roughness;
   } else {
     mat.albedo[0] = mat.albedo[1] = mat.albedo[2] = 0.5f;
   }

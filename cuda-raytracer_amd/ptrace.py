@@ -35,7 +35,7 @@ PT_FLAG_REF_DROP_ON_MISS = 0x8   # reference quirk (i)
 PT_FLAG_REF_GUIDE = 0x10         # reference quirk (ii)
 PT_FLAG_REF_SCHEDULE = 0x20      # reference quirk (vi): 2 bounces, NEE 2/2/1 weighted 0.5/0.5/1
 PT_FLAG_REF_ARITH = 0x40         # the reference kernels' literal arithmetic (pt_api.h)
-PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION = 0, 1, 2, 3
+PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION, PT_BSDF_REFRACTION = 0, 1, 2, 3, 4
 PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT = 0, 1, 2
 PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1
 PT_GPU_BVH_PLOC, PT_GPU_BVH_LBVH = 0, 1
@@ -60,7 +60,7 @@ class pt_node(C.Structure):
 
 class pt_bsdf(C.Structure):
     _fields_ = [("type", C.c_int32), ("albedo", C.c_float * 3),
-                ("transmittance", C.c_float * 3), ("ior", C.c_float)]
+                ("transmittance", C.c_float * 3), ("ior", C.c_float), ("roughness", C.c_float)]
 
 
 class pt_light(C.Structure):
@@ -325,9 +325,29 @@ def scene_to_arrays(scene: "Scene") -> dict:
         "nodes": nodes,
         "level_start": np.ctypeslib.as_array(d.level_start, shape=(d.n_levels + 1,)).copy(),
         "bsdfs": bsdfs,
+        "bsdf_size": np.array([C.sizeof(pt_bsdf)], np.int32),
         "light": np.frombuffer(bytes(d.light), dtype=np.uint8).copy(),
         "camera": np.frombuffer(bytes(d.camera), dtype=np.uint8).copy(),
     }
+
+
+BSDF_V1_SIZE = 32  # pt_bsdf before its roughness field (rounds 1-3 fixtures)
+
+
+def _upgrade_bsdfs(a: dict) -> dict:
+    """Fixtures written before pt_bsdf grew `roughness` hold 32-byte records
+    (no "bsdf_size" key): append roughness 0 -- every <roughness> in the
+    reference's media is 0."""
+    size = int(np.asarray(a["bsdf_size"]).reshape(-1)[0]) if "bsdf_size" in a else BSDF_V1_SIZE
+    if size == C.sizeof(pt_bsdf):
+        return a
+    old = a["bsdfs"].reshape(-1, size)
+    new = np.zeros((len(old), C.sizeof(pt_bsdf)), np.uint8)
+    new[:, :size] = old
+    a = dict(a)
+    a["bsdfs"] = new.reshape(-1)
+    a["bsdf_size"] = np.array([C.sizeof(pt_bsdf)], np.int32)
+    return a
 
 
 class ArrayScene:
@@ -340,7 +360,8 @@ class ArrayScene:
     @classmethod
     def load(cls, path):
         with np.load(path, allow_pickle=False) as z:
-            return cls({k: z[k] for k in z.files})
+            a = {k: z[k] for k in z.files}
+        return cls(_upgrade_bsdfs(a))
 
     def desc(self) -> pt_scene_desc:
         a = self.a

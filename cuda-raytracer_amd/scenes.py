@@ -65,6 +65,7 @@ def fixture_arrays(name):
     normals (n, 9), tri_bsdf, spheres (m, 4), sphere_bsdf, bsdfs, light,
     camera (the inputs of pt_scene_from_mesh / pt_scene_build_gpu)."""
     with np.load(FIXTURES / f"{name}.npz", allow_pickle=False) as z:
+        z = ptrace._upgrade_bsdfs({k: z[k] for k in z.files})
         q = z["prims"]
         sh = z["shading"]
         order = np.argsort(z["sorted_to_input"], kind="stable")
@@ -108,6 +109,7 @@ def bunny_lit():
 def dragon_proxy_arrays():
     """positions (n, 9), normals (n, 9), tri_bsdf (n,), bsdfs, light, camera."""
     with np.load(FIXTURES / "CBbunny.npz", allow_pickle=False) as z:
+        z = ptrace._upgrade_bsdfs({k: z[k] for k in z.files})
         q = z["prims"]
         sh = z["shading"]
         order = np.argsort(z["sorted_to_input"], kind="stable")  # back to mesh input order

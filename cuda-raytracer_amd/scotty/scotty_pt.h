@@ -79,7 +79,9 @@ class BSDF {
  public:
   virtual ~BSDF() = default;
   const pt_bsdf& params() const { return b_; }
-  bool is_delta() const { return b_.type == PT_BSDF_MIRROR || b_.type == PT_BSDF_GLASS; }
+  bool is_delta() const {
+    return b_.type == PT_BSDF_MIRROR || b_.type == PT_BSDF_GLASS || b_.type == PT_BSDF_REFRACTION;
+  }
 
  protected:
   BSDF(int type, const Spectrum& a) {
@@ -96,13 +98,24 @@ struct DiffuseBSDF : BSDF {  // bsdf.h:108
 struct MirrorBSDF : BSDF {  // bsdf.h:126
   explicit MirrorBSDF(const Spectrum& reflectance) : BSDF(PT_BSDF_MIRROR, reflectance) {}
 };
-struct GlassBSDF : BSDF {  // bsdf.h:190 (roughness is not modelled, as in the reference)
-  GlassBSDF(const Spectrum& transmittance, const Spectrum& reflectance, float /*roughness*/, float ior)
+struct GlassBSDF : BSDF {  // bsdf.h:190 (roughness: read only by PT_FLAG_REF_ARITH, pt_api.h pt_bsdf)
+  GlassBSDF(const Spectrum& transmittance, const Spectrum& reflectance, float roughness, float ior)
       : BSDF(PT_BSDF_GLASS, reflectance) {
     b_.transmittance[0] = transmittance.r;
     b_.transmittance[1] = transmittance.g;
     b_.transmittance[2] = transmittance.b;
     b_.ior = ior;
+    b_.roughness = roughness;
+  }
+};
+struct RefractionBSDF : BSDF {  // bsdf.h:167: glass without reflectance
+  RefractionBSDF(const Spectrum& transmittance, float roughness, float ior)
+      : BSDF(PT_BSDF_REFRACTION, Spectrum(0.f, 0.f, 0.f)) {
+    b_.transmittance[0] = transmittance.r;
+    b_.transmittance[1] = transmittance.g;
+    b_.transmittance[2] = transmittance.b;
+    b_.ior = ior;
+    b_.roughness = roughness;
   }
 };
 struct EmissionBSDF : BSDF {  // bsdf.h:217
@@ -447,6 +460,7 @@ class BVHAccel {
         throw Error(PT_E_UNSUPPORTED, "BVHAccel: primitives must be Triangles or Spheres");
     }
     if (tris.empty() && sphs.empty()) throw Error(PT_E_INVALID, "BVHAccel: no primitives");
+    has_spheres_ = !sphs.empty();
     std::vector<float> pos, nrm, sph;
     std::vector<int32_t> tb, sb;
     std::vector<pt_bsdf> bsdfs;
@@ -516,18 +530,38 @@ class BVHAccel {
   }
   // a batch of closest-hit queries (one traversal pass on the GPU): out[i]
   // is rays[i]'s Intersection, primitive == nullptr for a miss
+  //
+  // Directions need not be unit length (Scotty3D's shadow rays run o + t (light
+  // - o) over [eps, 1]).  The triangle test's t is the parametric t for any |d|,
+  // so triangle-only scenes pass the ray as given; the kernels' sphere test
+  // assumes a unit d (trace.hip sphere_test), so with spheres in the scene a
+  // non-unit ray is traced as (o, d / |d|) over [min_t |d|, max_t |d|] and its
+  // t scaled back by 1 / |d|.
   std::vector<Intersection> intersect(const std::vector<Ray>& rays) const {
     std::vector<float> r(rays.size() * 8);
+    std::vector<double> scale(rays.size(), 1.0);
     for (size_t i = 0; i < rays.size(); ++i) {
       float* p = &r[i * 8];
+      Vector3D d = rays[i].d;
+      double lo = rays[i].min_t, hi = rays[i].max_t;
+      if (has_spheres_) {
+        const double l2 = dot(d, d);
+        if (std::fabs(l2 - 1.0) > 1e-6 && l2 > 0.0) {
+          const double len = std::sqrt(l2);
+          d = d * (1.0 / len);
+          lo *= len;
+          hi *= len;
+          scale[i] = len;
+        }
+      }
       p[0] = (float)rays[i].o.x;
       p[1] = (float)rays[i].o.y;
       p[2] = (float)rays[i].o.z;
-      p[3] = round_down(rays[i].max_t);
-      p[4] = (float)rays[i].d.x;
-      p[5] = (float)rays[i].d.y;
-      p[6] = (float)rays[i].d.z;
-      p[7] = round_up(rays[i].min_t);
+      p[3] = round_down(hi);
+      p[4] = (float)d.x;
+      p[5] = (float)d.y;
+      p[6] = (float)d.z;
+      p[7] = round_up(lo);
     }
     std::vector<uint64_t> h(rays.size());
     dev_.check(pt_intersect(dev_.get(), r.data(), (int32_t)rays.size(), h.data()), "pt_intersect");
@@ -540,7 +574,7 @@ class BVHAccel {
       Intersection& is = out[i];
       is.index = (int)(uint32_t)h[i];
       is.primitive = sorted_[(size_t)is.index];
-      is.t = t;
+      is.t = scale[i] == 1.0 ? (double)t : (double)t / scale[i];
       is.bsdf = is.primitive->get_bsdf();
       if (auto* tri = dynamic_cast<const Triangle*>(is.primitive))
         is.n = tri->shading_normal(rays[i]);
@@ -560,6 +594,7 @@ class BVHAccel {
   Device& device() { return dev_; }
 
  private:
+  bool has_spheres_ = false;
   // the fp32 interval [round_up(min_t), round_down(max_t)] holds exactly the
   // fp32 values of the double interval [min_t, max_t]
   static float round_down(double x) {

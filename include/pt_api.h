@@ -113,13 +113,22 @@ typedef struct pt_node {
 #define PT_BSDF_MIRROR 1
 #define PT_BSDF_GLASS 2
 #define PT_BSDF_EMISSION 3
+#define PT_BSDF_REFRACTION 4 /* RefractionBSDF (bsdf.h:167-185): glass without reflectance */
 
-/* 32 bytes; CuBSDF (cudaRenderer.h:135-140) extended with glass and emission. */
+/* 36 bytes; CuBSDF (cudaRenderer.h:135-140) extended with glass and emission.
+ * roughness: the COLLADA <roughness> of glass / refraction (collada.cpp:910-933).
+ * The kernels' default arithmetic does not model it (a smooth dielectric);
+ * PT_FLAG_REF_ARITH reads a glass BSDF as the reference's CUDA path does: a
+ * MirrorBSDF reinterpret_cast over the GlassBSDF object (cu:1713-1719), whose
+ * reflectance is then (roughness, reflectance.r, reflectance.g) (bsdf.h:138-139
+ * against bsdf.h:206-210), and (roughness, transmittance.r, transmittance.g)
+ * over a RefractionBSDF (bsdf.h:180-182). */
 typedef struct pt_bsdf {
   int32_t type;
   float albedo[3];        /* diffuse albedo / mirror+glass reflectance / emitted radiance */
-  float transmittance[3]; /* glass */
-  float ior;              /* glass */
+  float transmittance[3]; /* glass, refraction */
+  float ior;              /* glass, refraction */
+  float roughness;        /* glass, refraction (PT_FLAG_REF_ARITH only) */
 } pt_bsdf;
 
 /* Light kinds */
@@ -237,7 +246,7 @@ const char* pt_last_error(const pt_ctx* ctx);
 int pt_device_count(int* n);
 
 int pt_load_scene(pt_ctx* ctx, const pt_scene_desc* scene);
-/* PT_E_UNSUPPORTED when the origin lies beyond 16 x the scene's largest
+/* PT_E_UNSUPPORTED when the origin lies beyond 64 x the scene's largest
  * coordinate magnitude M (vertices, sphere extents, the scene's camera and
  * light): the stored boxes' guard band keeps the fp32 box test conservative
  * only for origins within ~22 M.  pt_intersect applies the same bound to its
@@ -342,7 +351,10 @@ int pt_write_pfm(const char* path, const float* rgba, int32_t width, int32_t hei
  * both ends inclusive (Ray::min_t / max_t as Triangle::intersect tests them,
  * triangle.cpp:189; a tmin <= 0 means 0, a NaN tmin is PT_E_INVALID).  hits:
  * n records of (uint64) ((float bits of t) << 32 | sorted prim index), the
- * closest such hit (ties to the lowest index), or PT_HIT_NONE. */
+ * closest such hit (ties to the lowest index), or PT_HIT_NONE.  Directions may
+ * have any length for triangle-only scenes (t is the parametric t); a scene
+ * with spheres needs unit directions (|d|^2 within 1e-5 of 1, else
+ * PT_E_INVALID) -- scotty::BVHAccel::intersect normalises for its callers. */
 #define PT_HIT_NONE 0xFFFFFFFFFFFFFFFFull
 int pt_intersect(pt_ctx* ctx, const float* rays, int32_t n, uint64_t* hits);
 /* The same with render flags: PT_FLAG_REF_ARITH selects the reference's

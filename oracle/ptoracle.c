@@ -592,6 +592,18 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
         emitter = rad.x != 0.0f || rad.y != 0.0f || rad.z != 0.0f; /* cu:436 */
       }
       if (Bv.type == PT_BSDF_EMISSION) Bv.type = PT_BSDF_DIFFUSE;
+      /* cu:1713-1719: a delta BSDF read through MirrorBSDF -- over a GlassBSDF
+       * reflectance = (roughness, reflectance.r, reflectance.g), over a
+       * RefractionBSDF (roughness, transmittance.r, transmittance.g)
+       * (bsdf.h:138-139 against 180-182 and 206-210) */
+      if (Bv.type == PT_BSDF_GLASS || Bv.type == PT_BSDF_REFRACTION) {
+        float c1 = Bv.type == PT_BSDF_GLASS ? Bv.albedo[0] : Bv.transmittance[0];
+        float c2 = Bv.type == PT_BSDF_GLASS ? Bv.albedo[1] : Bv.transmittance[1];
+        Bv.albedo[0] = Bv.roughness;
+        Bv.albedo[1] = c1;
+        Bv.albedo[2] = c2;
+        Bv.type = PT_BSDF_MIRROR;
+      }
     }
     if (!refa && Bs->type == PT_BSDF_EMISSION) {
       if (!(J->flags & PT_FLAG_NO_EMISSION) && (vtx == 1 || spec)) L = add(L, mulv(T, ld3(Bs->albedo)));
@@ -676,7 +688,7 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
       }
       T = mulv(T, ld3(Bs->albedo));
       spec = 1;
-    } else { /* glass */
+    } else { /* glass, refraction */
       float ior = Bs->ior;
       float eta = front ? (1.0f / ior) : ior;
       float cosi = -dot(d, n);

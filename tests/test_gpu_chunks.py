@@ -1,0 +1,135 @@
+"""Multi-chunk frames.  pt_render splits a frame of
+npix x spp paths into chunks of floor(chunk_paths / npix) samples; each
+chunk's per-path radiance is summed into the owned pixels' accumulators in
+sample order, so the image cannot depend on the chunking -- the property the
+reference's renderAccumulate gives across frames (cudaRenderer.cu:2419-2457:
+accumulate one frame's samples after the previous frame's).  PT_CHUNK_PATHS
+(read at pt_create) shrinks the chunk so the oracle-sized renders here cross
+chunks, on the single-leaf path (CBempty) and the wavefront path (CBbunny,
+the dragon proxy), including a ragged last chunk; and config 5's own size
+(2048x2048, 1024 spp: 16 chunks of 2^28 paths) is checked against the oracle
+on every 512th tile, with its eight 1/8 tile shares (the per-GPU work at 8
+GPUs) against the whole frame."""
+import os
+
+import numpy as np
+import pytest
+
+import ptrace
+import pyoracle
+
+pytestmark = pytest.mark.gpu
+SEED = 15618
+
+
+def _scene(name):
+    import scenes
+    return scenes.load(name)
+
+
+def _ctx_with_chunk(chunk):
+    old = os.environ.get("PT_CHUNK_PATHS")
+    os.environ["PT_CHUNK_PATHS"] = str(chunk)
+    try:
+        return ptrace.Context(0)
+    finally:
+        if old is None:
+            del os.environ["PT_CHUNK_PATHS"]
+        else:
+            os.environ["PT_CHUNK_PATHS"] = old
+
+
+@pytest.fixture(scope="module")
+def chunk_ctxs(gpu_ctx):
+    # W x H = 96 x 80 = 7680 pixels: chunks of 4 samples (4 chunks at 16 spp),
+    # of 5 samples (5, 5, 5, 1: a ragged last chunk) and of one sample with a
+    # chunk smaller than the frame (16 chunks)
+    npix = 96 * 80
+    ctxs = {k: _ctx_with_chunk(c) for k, c in (("4", 4 * npix), ("5", 5 * npix + 17), ("1", npix // 3))}
+    yield ctxs
+    for c in ctxs.values():
+        c.close()
+
+
+@pytest.mark.parametrize("name", ["CBempty", "CBbunny", "dragon_proxy"])
+def test_multi_chunk_frame_bit_exact(gpu_ctx, chunk_ctxs, name):
+    W, H, SPP, B = 96, 80, 16, 8
+    sc = _scene(name)
+    d = sc.desc()
+    o, orays = pyoracle.image(d, W, H, SPP, max_bounces=B, seed=SEED, threads=16)
+    gpu_ctx.load_scene(sc)
+    gpu_ctx.clear()
+    gpu_ctx.render(W, H, SPP, max_bounces=B, seed=SEED)
+    one = gpu_ctx.get_image()
+    assert np.array_equal(one[..., :3], o[..., :3])
+    for key, ctx in chunk_ctxs.items():
+        ctx.load_scene(sc)
+        ctx.reset_stats()
+        ctx.clear()
+        ctx.render(W, H, SPP, max_bounces=B, seed=SEED)
+        g = ctx.get_image()
+        bad = np.argwhere(g[..., :3] != o[..., :3])
+        assert len(bad) == 0, f"{name} chunk {key}: {len(bad)} values differ, max {np.abs(g - o).max()}"
+        assert ctx.stats().rays == orays
+        assert np.isfinite(g).all() and o[..., :3].mean() > 1e-3
+
+
+def test_multi_chunk_wavefront_with_batches(chunk_ctxs):
+    """A small path pool (several shade workgroups' regeneration plus the tail
+    compaction in every chunk) across chunks: same pixels as the oracle."""
+    W, H, SPP, B = 96, 80, 12, 8
+    sc = _scene("CBbunny")
+    o, _ = pyoracle.image(sc.desc(), W, H, SPP, max_bounces=B, seed=SEED, threads=16)
+    ctx = chunk_ctxs["5"]
+    ctx.load_scene(sc)
+    ctx.clear()
+    ctx.render(W, H, SPP, max_bounces=B, seed=SEED, batch_paths=8192)
+    assert np.array_equal(ctx.get_image()[..., :3], o[..., :3])
+
+
+def _owned_mask(W, H, tile, k):
+    ntx = (W + tile - 1) // tile
+    r = np.arange(H)[:, None] // tile
+    c = np.arange(W)[None, :] // tile
+    return ((r * ntx + c) % k) == 0
+
+
+def test_config5_fullsize_frame(gpu_ctx):
+    """BASELINE config 5 at its own size on one GPU: the dragon proxy at
+    2048x2048, 1024 spp, 8 bounces (2^32 paths = 16 chunks of 2^28).  The
+    oracle renders every 512th 32x32 tile (8 tiles, 8 M paths); those pixels
+    agree bit for bit, and the same tiles alone on the GPU cast the oracle's
+    rays.  Each of the eight 1/8 tile shares (what one rank renders at 8 GPUs)
+    gives the whole frame's pixels on its tiles, and their ray counts add up
+    to the whole frame's."""
+    W = H = 2048
+    SPP, B, TILE, K = 1024, 8, 32, 512
+    sc = _scene("dragon_proxy")
+    d = sc.desc()
+    gpu_ctx.load_scene(sc)
+    gpu_ctx.reset_stats()
+    gpu_ctx.clear()
+    gpu_ctx.render(W, H, SPP, max_bounces=B, seed=SEED)
+    whole_rays = gpu_ctx.stats().rays
+    g = gpu_ctx.get_image()
+    assert np.isfinite(g).all() and g[..., :3].mean() > 1e-3
+    o, orays = pyoracle.image(d, W, H, SPP, max_bounces=B, seed=SEED, tile=TILE, rank=0, nranks=K, threads=16)
+    m = _owned_mask(W, H, TILE, K)
+    assert m.sum() == 8 * TILE * TILE
+    bad = np.argwhere(g[m][:, :3] != o[m][:, :3])
+    assert len(bad) == 0, f"{len(bad)} values differ, max {np.abs(g[m] - o[m]).max()}"
+    gpu_ctx.reset_stats()
+    gpu_ctx.clear()
+    gpu_ctx.render(W, H, SPP, max_bounces=B, seed=SEED, tile_size=TILE, rank=0, nranks=K)
+    assert gpu_ctx.stats().rays == orays
+    share_rays = 0
+    for r in range(8):
+        gpu_ctx.reset_stats()
+        gpu_ctx.clear()
+        gpu_ctx.render(W, H, SPP, max_bounces=B, seed=SEED, tile_size=TILE, rank=r, nranks=8)
+        share_rays += gpu_ctx.stats().rays
+        ntx = W // TILE
+        t = (np.arange(H)[:, None] // TILE) * ntx + np.arange(W)[None, :] // TILE
+        ms = (t % 8) == r
+        assert np.array_equal(gpu_ctx.get_image()[ms], g[ms]), f"share {r}"
+    assert share_rays == whole_rays

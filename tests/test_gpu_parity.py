@@ -186,7 +186,9 @@ REF_FULL = REF | ptrace.PT_FLAG_REF_ARITH | ptrace.PT_FLAG_NO_EMISSION
                                         # every other reference switch
                                         ("CBbunny", ptrace.PT_FLAG_REF_ARITH), ("CBcoil", ptrace.PT_FLAG_REF_ARITH),
                                         ("CBempty", ptrace.PT_FLAG_REF_ARITH), ("CBbunny", REF_FULL),
-                                        ("CBcoil", REF_FULL | ptrace.PT_FLAG_REF_GUIDE), ("CBempty", REF_FULL)])
+                                        ("CBcoil", REF_FULL | ptrace.PT_FLAG_REF_GUIDE), ("CBempty", REF_FULL),
+                                        # glass read as the reference reads it: a MirrorBSDF cast (cu:1713-1719)
+                                        ("CBgems", ptrace.PT_FLAG_REF_ARITH), ("CBgems", REF_FULL)])
 def test_render_bit_exact(gpu_ctx, name, flags):
     sc = load_fixture(name)
     d = sc.desc()
@@ -224,12 +226,32 @@ def test_closest_hit_ref_arith_bit_exact(gpu_ctx, name):
     assert np.array_equal(dflt, pyoracle.intersect(d, rays, use_bvh=True))
 
 
-def test_ref_arith_refuses_spheres_and_glass(gpu_ctx):
-    for name in ["CBspheres", "CBgems"]:
-        gpu_ctx.load_scene(load_fixture(name))
-        with pytest.raises(ptrace.PTError) as e:
-            gpu_ctx.render(16, 16, 1, flags=ptrace.PT_FLAG_REF_ARITH)
-        assert e.value.code == ptrace.PT_E_UNSUPPORTED
+def test_ref_arith_refuses_spheres(gpu_ctx):
+    """The reference renders triangles only (cu:1765 casts every primitive to
+    a Triangle): spheres are refused under PT_FLAG_REF_ARITH."""
+    gpu_ctx.load_scene(load_fixture("CBspheres"))
+    with pytest.raises(ptrace.PTError) as e:
+        gpu_ctx.render(16, 16, 1, flags=ptrace.PT_FLAG_REF_ARITH)
+    assert e.value.code == ptrace.PT_E_UNSUPPORTED
+
+
+def test_ref_arith_glass_is_the_reference_mirror(gpu_ctx):
+    """Under PT_FLAG_REF_ARITH a glass BSDF is the reference's MirrorBSDF
+    reinterpret_cast (cu:1713-1719): the CBgems frame equals, bit for bit, the
+    frame of the same scene with each glass BSDF replaced by a mirror of
+    reflectance (roughness, reflectance.r, reflectance.g) (bsdf.h:138-139 over
+    bsdf.h:206-210) -- and differs from the default glass frame."""
+    from test_oracle import gems_glass_as_mirror
+    sc, mir = gems_glass_as_mirror()
+    W = H = 40
+    imgs = []
+    for s, fl in ((sc, ptrace.PT_FLAG_REF_ARITH), (mir, ptrace.PT_FLAG_REF_ARITH), (sc, 0)):
+        gpu_ctx.load_scene(s)
+        gpu_ctx.clear()
+        gpu_ctx.render(W, H, 2, max_bounces=8, seed=15618, flags=fl)
+        imgs.append(gpu_ctx.get_image())
+    assert np.array_equal(imgs[0], imgs[1])
+    assert not np.array_equal(imgs[0], imgs[2])
 
 
 def test_dragon_proxy_parity(gpu_ctx):

@@ -86,11 +86,37 @@ def _bench(tmp_path, gpus, tag):
     cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(gpus), "--backend", "gloo", "--steps", "1",
            "--warmup", "0", "--configs", "none", "--config5", "off", "--ref-arith", "none", "--no-cpu",
            "--no-1spp", "--width", "96", "--height", "64", "--spp", "4", "--bounces", "4", "--batch", "8192",
-           "--save-frame", str(out)]
+           "--save-frame", str(out), "--detail-out", str(tmp_path / f"detail{tag}.json")]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     return line, np.load(out)
+
+
+def test_rccl_gather_on_one_gpu(tmp_path):
+    """The nccl (RCCL) gather path on one GPU:
+    torch.distributed.run with one rank and --force-gather runs
+    ptdist.local_sums_tensor into a device tensor, dist.gather over RCCL and
+    the device index_copy_ into the frame; the gathered frame equals
+    pt_get_image's bit for bit."""
+    import socket
+    one, f1 = _bench(tmp_path, 1, "1")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = tmp_path / "frame_rccl.npy"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", "1", "--force-gather",
+           "--backend", "nccl", "--steps", "1", "--warmup", "0", "--configs", "none", "--config5", "off",
+           "--ref-arith", "none", "--no-cpu", "--no-1spp", "--width", "96", "--height", "64", "--spp", "4",
+           "--bounces", "4", "--batch", "8192", "--save-frame", str(out), "--detail-out", str(tmp_path / "d.json")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["rays_per_frame"] == one["rays_per_frame"]
+    f2 = np.load(out)
+    assert np.array_equal(f1, f2) and f1[..., :3].mean() > 0
 
 
 def test_bench_launches_ranks_itself(tmp_path):
@@ -106,9 +132,9 @@ def test_bench_launches_ranks_itself(tmp_path):
 
 
 def test_origin_bound(gpu_ctx):
-    """Camera and query-ray origins beyond 16x the scene's extent are refused
-    (the boxes' guard band keeps the fp32 box test conservative only within
-    ~22x); origins inside still work."""
+    """Camera and query-ray origins beyond 64x the scene's largest coordinate
+    magnitude are refused (the boxes' guard band G = 2^-14 M keeps the fp32
+    box test conservative to ~180x); origins inside still work."""
     sc = load_fixture("CBbunny")
     d = sc.desc()
     gpu_ctx.load_scene(sc)
@@ -122,8 +148,32 @@ def test_origin_bound(gpu_ctx):
     with pytest.raises(ptrace.PTError) as e:
         gpu_ctx.intersect(rays)
     assert e.value.code == ptrace.PT_E_UNSUPPORTED
-    rays[7, 0] = 20.0  # CBbunny's extent is ~1.5: 16 x is 24
+    rays[7, 0] = 60.0  # CBbunny's largest coordinate magnitude is ~1.5: 64 x is ~96
     assert np.array_equal(gpu_ctx.intersect(rays), pyoracle.intersect(d, rays, use_bvh=True))
+
+
+@pytest.mark.parametrize("name", ["CBbunny", "CBgems"])
+def test_scotty_farthest_camera(gpu_ctx, name):
+    """Scotty3D's framing zooms out to max_view_distance = 20 canonical view
+    distances = 15 |bbox extent| from the bbox centroid (application.cpp:
+    395-408); a camera placed there is accepted by pt_set_camera
+    and its frame is bit-exact against the oracle."""
+    sc = load_fixture(name)
+    d = sc.desc()
+    q = sc.a["prims"]
+    tri = (q[:, 3].view(np.uint32) >> 28) == 0
+    v = q[tri][:, [0, 1, 2, 4, 5, 6, 8, 9, 10]].reshape(-1, 3).astype(np.float64)
+    lo, hi = v.min(0), v.max(0)
+    canonical = np.linalg.norm(hi - lo) / 2 * 1.5
+    cam, _, _ = ptrace.scotty_camera_place(50.0, 35.0, 64, 48, (lo + hi) / 2, 0.9, 0.4, 20 * canonical,
+                                           0.0, 20 * canonical, [[0.5, 0.5]])
+    gpu_ctx.load_scene(sc)
+    gpu_ctx.set_camera(cam)
+    gpu_ctx.render(64, 48, 2, max_bounces=4, seed=15618)
+    g = gpu_ctx.get_image()
+    d.camera = cam
+    o, _ = pyoracle.image(d, 64, 48, 2, max_bounces=4, seed=15618)
+    assert np.array_equal(g[..., :3], o[..., :3])
 
 
 def _in_plane_scene():

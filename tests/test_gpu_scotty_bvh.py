@@ -206,3 +206,50 @@ def test_pt_intersect_tmin_matches_oracle(gpu_ctx, name):
     assert np.array_equal(g, pyoracle.intersect(d, rays, use_bvh=True))
     t = ptrace.hit_t(g)
     assert (t[np.isfinite(t)] >= np.maximum(rays[np.isfinite(t), 7], 0)).all()
+
+
+def test_bvhaccel_non_unit_directions(gpu_ctx):
+    """Scotty3D callers may pass non-unit directions (a shadow ray o + t (light
+    - o) over [eps, 1]).  With spheres in the scene BVHAccel traces (o, d/|d|)
+    over [min_t |d|, max_t |d|] and scales t back (the sphere test assumes a
+    unit d): the same primitives as the unit rays over the same
+    segments, t within fp32 rounding.  The C ABI refuses non-unit directions
+    on sphere scenes, and takes them as given on triangle-only scenes (the
+    triangle test's t is parametric: bit-exact against the oracle's brute
+    force on the same non-unit rays)."""
+    P, N, S = _scene("CBgems", "CBspheres")
+    bvh = ptrace.ScottyBVH(P.reshape(-1, 3), N.reshape(-1, 3), np.arange(3 * len(P)).reshape(-1, 3), S)
+    rays = _rays(P, S, 6000, seed=21)
+    rays[:, 6] = 1e-3
+    h0, t0, p0, _ = bvh.intersect(rays)
+    s = np.exp(np.random.default_rng(4).uniform(np.log(0.05), np.log(20.0), len(rays)))
+    r2 = rays.copy()
+    r2[:, 3:6] *= s[:, None]
+    r2[:, 6] /= s
+    h1, t1, p1, _ = bvh.intersect(r2)
+    assert h0.mean() > 0.5 and (p0[h0] >= len(P)).sum() > 50  # sphere hits among them
+    same = (p0 == p1)
+    assert same.mean() > 0.999, same.mean()
+    both = h0 & h1 & same
+    assert np.all(np.abs(t1[both] * s[both] - t0[both]) <= 1e-5 * np.maximum(1.0, t0[both]))
+    bvh.close()
+    # the C ABI on a sphere scene: unit directions only
+    sph = load_fixture("CBspheres")
+    gpu_ctx.load_scene(sph)
+    from rays import camera_rays
+    cr = camera_rays(sph.desc(), 64, seed=1)
+    gpu_ctx.intersect(cr)
+    bad = cr.copy()
+    bad[:, 4:7] *= 2.0
+    with pytest.raises(ptrace.PTError) as e:
+        gpu_ctx.intersect(bad)
+    assert e.value.code == ptrace.PT_E_INVALID
+    # triangle-only: non-unit directions as given, bit-exact
+    sc = load_fixture("CBbunny")
+    d = sc.desc()
+    gpu_ctx.load_scene(sc)
+    cr = camera_rays(d, 4000, seed=2)
+    cr[:, 4:7] *= np.float32(3.0)
+    g = gpu_ctx.intersect(cr)
+    assert (g != ptrace.PT_HIT_NONE).sum() > 1000
+    assert np.array_equal(g, pyoracle.intersect(d, cr, use_bvh=False))

@@ -70,6 +70,57 @@ def test_golden_render_regression():
     assert np.array_equal(g["sums"], sums)
 
 
+def gems_glass_as_mirror():
+    """(CBgems, CBgems with every glass BSDF replaced by the MirrorBSDF the
+    reference's reinterpret_cast reads: reflectance (roughness, refl.r,
+    refl.g), bsdf.h:138-139 against bsdf.h:206-210)."""
+    sc = load_fixture("CBgems")
+    mir = ptrace.ArrayScene(dict(sc.a))
+    sz = ptrace.C.sizeof(ptrace.pt_bsdf)
+    raw = bytearray(sc.a["bsdfs"].tobytes())
+    nglass = 0
+    for i in range(len(raw) // sz):
+        b = ptrace.pt_bsdf.from_buffer(raw, i * sz)
+        if b.type == ptrace.PT_BSDF_GLASS:
+            r, g = b.albedo[0], b.albedo[1]
+            b.albedo[0], b.albedo[1], b.albedo[2] = b.roughness, r, g
+            b.type = ptrace.PT_BSDF_MIRROR
+            nglass += 1
+    assert nglass == 3
+    mir.a["bsdfs"] = np.frombuffer(bytes(raw), dtype=np.uint8).copy()
+    return sc, mir
+
+
+def test_oracle_ref_arith_glass_reads_as_mirror():
+    """PT_FLAG_REF_ARITH (cu:1713-1719): the oracle renders CBgems' glass as
+    the reference's mirror cast -- the same frame as a scene whose glass
+    BSDFs are those mirrors; with roughness 0 (every media file) the red
+    channel of a glass bounce is 0."""
+    sc, mir = gems_glass_as_mirror()
+    a, ra = pyoracle.render(sc.desc(), 24, 20, 2, max_bounces=8, flags=ptrace.PT_FLAG_REF_ARITH, threads=4)
+    b, rb = pyoracle.render(mir.desc(), 24, 20, 2, max_bounces=8, flags=ptrace.PT_FLAG_REF_ARITH, threads=4)
+    assert np.array_equal(a, b) and ra == rb
+    c, _ = pyoracle.render(sc.desc(), 24, 20, 2, max_bounces=8, threads=4)
+    assert not np.array_equal(a, c)
+
+
+def test_fixture_bsdf_roughness():
+    """Fixtures carry the COLLADA <roughness> of glass (pt_bsdf.roughness):
+    0 in every reference media file; pre-roughness (32-byte) records load
+    with roughness 0."""
+    sc = load_fixture("CBgems")
+    d = sc.desc()
+    kinds = [d.bsdfs[i].type for i in range(d.n_bsdfs)]
+    assert kinds.count(ptrace.PT_BSDF_GLASS) == 3
+    assert all(d.bsdfs[i].roughness == 0.0 for i in range(d.n_bsdfs))
+    old = dict(sc.a)
+    n = d.n_bsdfs
+    old["bsdfs"] = sc.a["bsdfs"].reshape(n, -1)[:, :32].reshape(-1).copy()
+    del old["bsdf_size"]
+    up = ptrace._upgrade_bsdfs(old)
+    assert np.array_equal(up["bsdfs"], sc.a["bsdfs"])
+
+
 def test_oracle_quirk_modes():
     """Reference-quirk modes of the oracle (SURVEY §8(a) parity decisions)."""
     d = load_fixture("CBempty").desc()
