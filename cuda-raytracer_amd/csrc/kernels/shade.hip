@@ -34,6 +34,11 @@ constexpr float REF_DIFFUSE_MULT = 0.3183f;  // BSDF_DIFFUSE_MULTIPLIER, cu:272
 constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
 constexpr int SHADE_REC = 5;  // float4 per hit-shading record (ShadeArgs::shade)
 constexpr uint32_t SHADE_SMOOTH = 1u << 27;  // shading-record meta bit: a triangle with distinct vertex normals
+// a flat triangle's shading record holds its normalised normal in the first
+// 16 B (host-computed, bit-identical to the device's normalize)
+#ifndef PT_FLAT_NS
+#define PT_FLAT_NS 1
+#endif
 constexpr uint32_t ERR_KERNARG = 2u;  // pt_ctx::d_err bit: k_path_leaf's kernel-argument layout check failed
 
 struct ShadeArgs {
@@ -367,14 +372,17 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
       if ((meta >> 28) == PT_PRIM_SPHERE) {
         ns = normalize(mk(P.x - q0.x, P.y - q0.y, P.z - q0.z));
       } else {
-        const f3 n0 = xyz(q0);
-        if (!REFA && !(__float_as_uint(q0.w) & SHADE_SMOOTH)) {
+        const bool flat = !(__float_as_uint(q0.w) & SHADE_SMOOTH);
+        if (!REFA && flat) {
           // flat triangle (n0 == n1 == n2): the barycentric blend is a
           // positive multiple of n0, so its normalisation is normalize(n0)
-          ns = normalize(n0);
+          // (PT_FLAT_NS: computed on the host, pt_load_scene)
+          ns = PT_FLAT_NS ? xyz(q0) : normalize(xyz(q0));
         } else {
           const float4 q1 = Q[1], q2 = Q[2], q3 = Q[3], q4 = Q[4];
           const f3 n1 = mk(q1.w, q2.w, q3.w), n2 = xyz(q4);
+          // (a flat triangle's first 16 B hold normalize(n0): its raw n0 is n2)
+          const f3 n0 = (PT_FLAT_NS && flat) ? n2 : xyz(q0);
           // barycentric shading normal (cu:1213-1221)
           const f3 A = xyz(q1), B = xyz(q2), Cv = xyz(q3);
           float total = length(cross(A - B, B - Cv));
@@ -1250,6 +1258,15 @@ __global__ __launch_bounds__(TPB) void k_compact_wstate(uint4* wstate, uint32_t 
 // use the same primitive tests and tie rule as the leaf code of
 // process_item (trace.hip); results are bit-identical to the wavefront path.
 // SPH: the leaf may hold spheres (else the sphere branch is not compiled in)
+// PT_PATH_STRICT (extension rays, tmax = +inf): the triangle test admits only
+// t < the best so far, so a hit is a new best and the update is two selects
+// (no exec-mask branches: fewer SALU per primitive).  The same hits as
+// take_hit: a tie keeps the lower index either way, and the inclusive tmax
+// of take_hit matters only for a first hit at t = tmax = +inf, which no test
+// returns (an infinite t fails the barycentric test).
+#ifndef PT_PATH_STRICT
+#define PT_PATH_STRICT 1
+#endif
 template <bool REFA, bool SPH = true>
 __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, int pcount, const RayV& r,
                                              uint32_t& prim, float& t) {
@@ -1262,8 +1279,16 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
     const Prim q = load_prim<REFA>(P);
     // (a tri_outside pre-test does not pay here: extension rays of one wave
     // rarely all miss a plane, measured -7 % on CBempty)
-    const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1) : tri_test<REFA>(r.o, r.d, q, bt);
-    take_hit(tt, pstart + k, bt, bp);
+    if constexpr (PT_PATH_STRICT) {
+      const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1)
+                                                     : tri_test<REFA, true>(r.o, r.d, q, bt);
+      const bool take = (tt >= 0.0f) & (tt < bt);
+      bt = take ? tt : bt;
+      bp = take ? pstart + k : bp;
+    } else {
+      const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1) : tri_test<REFA>(r.o, r.d, q, bt);
+      take_hit(tt, pstart + k, bt, bp);
+    }
   }
   prim = bp < 0 ? PT_PRIM_NONE : (uint32_t)bp;
   t = bt;

@@ -102,9 +102,13 @@ __device__ __forceinline__ bool prim_sphere(const Prim& q) {
 // range, away from the extremes.  Outside it (|den| denormal or zero, an
 // overflowing quotient: a ray parallel to the plane) the result is NaN, an
 // infinity or a huge t, and the test misses as it does for the IEEE quotient
-// (|u| or |v| huge, or unordered); only a hit at t below ~2^-100 (an origin
-// on the plane to 30 decimal places) could differ in t's last bits.  The
-// oracle divides with IEEE `/`; the GPU parity tests check the two agree.
+// (|u| or |v| huge, or unordered).  The residuals r0, r1 are ~2^-24 |num|:
+// for |num| below ~2^-101 they are subnormal and the quotient may differ
+// from IEEE's by one ulp -- a t below ~2^-96 at a unit ray (an origin on the
+// plane to 29 decimal places).  The oracle divides with IEEE `/`; the GPU
+// parity tests check the two agree, tests/test_gpu_regress.py checks the
+// division itself down to |num| = 2^-100 bit for bit and to 2^-126 within
+// one ulp.
 #ifndef PT_FAST_DIV
 #define PT_FAST_DIV 1
 #endif
@@ -128,10 +132,13 @@ __global__ __launch_bounds__(TPB) void k_check_division(const float* __restrict_
 __device__ __forceinline__ float bw_plane(const f3 o, const float4 W) {
   return __builtin_fmaf(W.z, o.z, __builtin_fmaf(W.y, o.y, __builtin_fmaf(W.x, o.x, W.w)));
 }
+// STRICT: a hit needs t < tbest (the caller's best so far, no hit yet at
+// tbest = +inf, which no hit reaches): then every hit returned is a new best
+template <bool STRICT = false>
 __device__ __forceinline__ float bw_test(const f3 o, const f3 d, const float4 U, const float4 V, const float4 W,
                                          float tbest, float tlo = 0.0f) {
   const float t = div_rn(-bw_plane(o, W), fdot(W.x, W.y, W.z, d.x, d.y, d.z));
-  if (!(t >= tlo) | (t > tbest)) return -1.0f;
+  if (!(t >= tlo) | (STRICT ? !(t < tbest) : (t > tbest))) return -1.0f;
   const float u = __builtin_fmaf(t, fdot(U.x, U.y, U.z, d.x, d.y, d.z), bw_plane(o, U));
   const float v = __builtin_fmaf(t, fdot(V.x, V.y, V.z, d.x, d.y, d.z), bw_plane(o, V));
   // (unordered compares: a NaN u or v -- a ray parallel to the plane, t =
@@ -153,6 +160,7 @@ __device__ __forceinline__ float edge_ref(const float4 N, float ex, float ey, fl
 }
 // The reference's literal test (REFA records): plane hit, then the three edge
 // tests dot(N, cross(e_k, P - v_k)) < 0 (cu:223-267).
+template <bool STRICT = false>
 __device__ __forceinline__ float tri_test_ref(const f3 o, const f3 d, const float4 q0, const float4 q1,
                                               const float4 q2, const float4 q3, const float4 q4, const float4 q5,
                                               const float tbest, const float tlo = 0.0f) {
@@ -161,7 +169,7 @@ __device__ __forceinline__ float tri_test_ref(const f3 o, const f3 d, const floa
   float t = (q1.w - fdot(q3.x, q3.y, q3.z, o.x, o.y, o.z)) / ndd;
   // t > tbest cannot win (ties need t == tbest): skip the edge tests; hits
   // before the ray's t_min (tlo >= 0, pt_intersect) do not count
-  if (t < tlo || t > tbest) return -1.0f;
+  if (t < tlo || (STRICT ? !(t < tbest) : (t > tbest))) return -1.0f;
   f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
   if (edge_ref(q3, q2.w, q3.w, q4.w, P, q0) < 0.0f) return -1.0f;
   if (edge_ref(q3, q4.x, q4.y, q4.z, P, q1) < 0.0f) return -1.0f;
@@ -169,10 +177,10 @@ __device__ __forceinline__ float tri_test_ref(const f3 o, const f3 d, const floa
   return t == 0.0f ? 0.0f : t;
 }
 // A triangle's closest-hit test in the record's arithmetic.
-template <bool REFA>
+template <bool REFA, bool STRICT = false>
 __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const Prim& q, float tbest, float tlo = 0.0f) {
-  if constexpr (REFA) return tri_test_ref(o, d, q.q0, q.q1, q.q2, q.q3, q.q4, q.q5, tbest, tlo);
-  else return bw_test(o, d, q.q0, q.q1, q.q2, tbest, tlo);
+  if constexpr (REFA) return tri_test_ref<STRICT>(o, d, q.q0, q.q1, q.q2, q.q3, q.q4, q.q5, tbest, tlo);
+  else return bw_test<STRICT>(o, d, q.q0, q.q1, q.q2, tbest, tlo);
 }
 // The plane hit as t = num / ndd, for the division-free pre-test.
 template <bool REFA>

@@ -1006,7 +1006,17 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
       const uint32_t m2 = meta | (flat ? 0u : SHADE_SMOOTH);
       float mf;
       memcpy(&mf, &m2, 4);
-      r[0] = make_float4(n0[0], n0[1], n0[2], mf);
+      if (flat && PT_FLAT_NS) {
+        // a flat triangle's shading normal normalize(n0) (ptmath.h normalize:
+        // n0 * (1 / sqrt(fma-chain dot)), correctly rounded fp32 here as on
+        // the device), so the kernels read it instead of computing it; the
+        // raw n0 stays in r[4] (= n2) for the reference arithmetic's blend
+        const float dd = std::fmaf(n0[2], n0[2], std::fmaf(n0[1], n0[1], n0[0] * n0[0]));
+        const float inv = 1.0f / std::sqrt(dd);
+        r[0] = make_float4(n0[0] * inv, n0[1] * inv, n0[2] * inv, mf);
+      } else {
+        r[0] = make_float4(n0[0], n0[1], n0[2], mf);
+      }
       r[1] = make_float4(q[0], q[1], q[2], n1[0]);
       r[2] = make_float4(q[4], q[5], q[6], n1[1]);
       r[3] = make_float4(q[8], q[9], q[10], n1[2]);

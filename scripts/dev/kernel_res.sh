@@ -5,7 +5,7 @@ set -e
 SRC=$1; shift
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 OUT=/tmp/kres_$$.s
-/opt/rocm/bin/hipcc -std=c++17 -O3 -ffp-contract=off --offload-arch=gfx950 --cuda-device-only -S \
+/opt/rocm/bin/hipcc -std=c++17 -O3 -ffp-contract=off --offload-arch=${ARCH:-gfx950} --cuda-device-only -S \
   -I"$ROOT/include" -I"$ROOT/cuda-raytracer_amd/csrc" "$@" "$SRC" -o $OUT 2>/dev/null
 awk '/^\t\.globl\t/ {k=$2} /; TotalNumSgprs:/ {s=$3} /; NumVgprs:/ {v=$3} /; ScratchSize:/ {sc=$3}
      /; Occupancy:/ {print k, "vgpr", v, "sgpr", s, "scratch", sc, "occ", $3}' $OUT | c++filt |

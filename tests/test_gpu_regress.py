@@ -263,3 +263,20 @@ def test_triangle_test_division_is_ieee(gpu_ctx):
     assert np.all(q[~nz] == 0.0)
     z = gpu_ctx.check_division(np.array([1.0, -1.0, 0.0], np.float32), np.zeros(3, np.float32))
     assert np.all(np.isnan(z) | np.isinf(z))
+    # small numerators: down to |num| = 2^-100 the residuals stay
+    # normal and every quotient is IEEE's; below that (|num| in [2^-126,
+    # 2^-101]: the fma residuals are subnormal) a quotient may differ from
+    # IEEE's -- by at most one ulp.  That band is a t below ~2^-96 at a unit
+    # ray (an origin on the plane to 29 decimal places): not pinned.
+    m = 4_000_000
+    num = (rng.uniform(1, 2, m) * np.exp2(rng.integers(-100, -59, m)) * rng.choice([-1, 1], m)).astype(np.float32)
+    den = (rng.uniform(1, 2, m) * np.exp2(rng.integers(-60, 5, m)) * rng.choice([-1, 1], m)).astype(np.float32)
+    q = gpu_ctx.check_division(num, den)
+    assert np.array_equal(q.view(np.uint32), (num / den).view(np.uint32))
+    num = (rng.uniform(1, 2, m) * np.exp2(rng.integers(-126, -100, m)) * rng.choice([-1, 1], m)).astype(np.float32)
+    den = (rng.uniform(1, 2, m) * np.exp2(rng.integers(-4, 5, m)) * rng.choice([-1, 1], m)).astype(np.float32)
+    q = gpu_ctx.check_division(num, den)
+    with np.errstate(all="ignore"):
+        ref = num / den
+    ulps = np.abs(q.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+    assert ulps.max() <= 1, ulps.max()
