@@ -33,6 +33,47 @@ __device__ __forceinline__ f3 normalize(f3 a) {
   return a * inv;
 }
 
+// ---- correctly rounded sqrt / reciprocal in a bounded range ----------------------
+// PT_FAST_SQRT: the compiler's IEEE sqrtf is 16 instructions -- v_sqrt_f32
+// (within one ulp), the choice among s - ulp, s, s + ulp by the signs of two
+// fma residuals, plus a 2^32 pre-scaling of inputs below 2^-96 (where
+// v_sqrt_f32 loses accuracy) and a special-case select.  sqrt_rn keeps the
+// residual choice only: the same bits for x = 0, +inf, NaN and every x >=
+// 2^-96.  It is used only where the argument is provably 0 or >= 2^-96 (a
+// squared length of a near-unit vector, 1 - z^2 of a 24-bit uniform), or
+// where a tiny argument's result is discarded (a light sample closer than
+// 1e-2); the oracle takes IEEE sqrtf everywhere.
+#ifndef PT_FAST_SQRT
+#define PT_FAST_SQRT 1
+#endif
+__device__ __forceinline__ float sqrt_rn(float x) {
+  if constexpr (!PT_FAST_SQRT) return sqrtf(x);
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
+  const float r = rm <= 0.0f ? sm : s;
+  return rp > 0.0f ? sp : r;
+}
+// 1 / b for a normal b in [2^-100, 2^100] (a length): the IEEE quotient's
+// reciprocal-and-correction sequence without its range scaling and fixup
+// (trace.hip div_rn, the same 8-instruction form)
+__device__ __forceinline__ float rcp_rn(float b) {
+  if constexpr (!PT_FAST_SQRT) return 1.0f / b;
+  const float y0 = __builtin_amdgcn_rcpf(b);
+  const float e = __builtin_fmaf(-b, y0, 1.0f);
+  const float y1 = __builtin_fmaf(e, y0, y0);
+  const float r0 = __builtin_fmaf(-b, y1, 1.0f);
+  const float q1 = __builtin_fmaf(r0, y1, y1);
+  const float r1 = __builtin_fmaf(-b, q1, 1.0f);
+  return __builtin_fmaf(r1, y1, q1);
+}
+// normalize for |a|^2 in [2^-96, 2^126] (directions, unit-normal blends):
+// bit-identical to normalize
+__device__ __forceinline__ f3 normalize_u(f3 a) {
+  const float inv = rcp_rn(sqrt_rn(dot(a, a)));
+  return a * inv;
+}
+
 // ---- division by a run-time constant -------------------------------------------
 // floor(n / d) = (n * m) >> s for every n < 2^30 (m, s from udiv_make): with
 // s = 30 + ceil(log2 d) and m = ceil(2^s / d), e = m d - 2^s < d, so n e < 2^s.

@@ -133,12 +133,14 @@ __device__ __forceinline__ f3 camera_dir(const ShadeArgs& S, uint32_t p, uint32_
     const f3 k = mk(kx, ky, kz) * inv;
     return mk(dot(k, mk(L.x, U.x, K.x)), dot(k, mk(L.y, U.y, K.y)), dot(k, mk(L.z, U.z, K.z)));
   }
-  float len = sqrtf(kx * kx + ky * ky + kz * kz);
-  kx = kx / len;
-  ky = ky / len;
-  kz = kz / len;
+  // (sqrt_rn / div_rn / normalize_u give IEEE's bits here: len^2 >= 1, the
+  // numerators are 0 or >= 2^-25 in magnitude, |dir| ~ 1)
+  float len = sqrt_rn(kx * kx + ky * ky + kz * kz);
+  kx = div_rn(kx, len);
+  ky = div_rn(ky, len);
+  kz = div_rn(kz, len);
   f3 dir = mk(kx * L.x + ky * U.x + kz * K.x, kx * L.y + ky * U.y + kz * K.y, kx * L.z + ky * U.z + kz * K.z);
-  return normalize(dir);
+  return normalize_u(dir);
 }
 
 // Path state between vertices (ps0/ps1/ps2 in memory, registers in k_path_leaf).
@@ -254,8 +256,10 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
     const f3 lpt = mk(pos.x + sx * dx.x + sy * dy.x, pos.y + sx * dx.y + sy * dy.y, pos.z + sx * dx.z + sy * dy.z);
     const f3 dv = lpt - pt;
     const float sq = dot(dv, dv);
-    const float dist = sqrtf(sq);
-    const float inv = 1.0f / dist;
+    // (sqrt_rn / rcp_rn: IEEE's bits for sq >= 2^-96; a smaller sq fails
+    // dist > 1e-2 either way and its w is never used)
+    const float dist = sqrt_rn(sq);
+    const float inv = rcp_rn(dist);
     const f3 w = mk(dv.x * inv, dv.y * inv, dv.z * inv);
     const float cosl = dot(w, ld3(L.direction));
     const float cosn = dot(n, w);
@@ -273,8 +277,8 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
   } else if (L.type == PT_LIGHT_POINT) {
     const f3 dv = ld3(L.position) - pt;
     const float sq = dot(dv, dv);
-    const float dist = sqrtf(sq);
-    const float inv = 1.0f / dist;
+    const float dist = sqrt_rn(sq);  // (as above)
+    const float inv = rcp_rn(dist);
     const f3 w = mk(dv.x * inv, dv.y * inv, dv.z * inv);
     const float cosn = dot(n, w);
     if (dist > 1e-2f && cosn > 0.0f) {
@@ -455,7 +459,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           dpdv = normalize(cross(dpdu, n));
         } else {
           const f3 guide = (fabsf(n.x) < 0.9f) ? mk(1.0f, 0.0f, 0.0f) : mk(0.0f, 1.0f, 0.0f);
-          dpdu = normalize(cross(guide, n));
+          dpdu = normalize_u(cross(guide, n));  // (|cross|^2 >= 0.19)
           dpdv = cross(n, dpdu);
         }
         if (B.type == PT_BSDF_DIFFUSE) {
@@ -494,14 +498,15 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           sincos2pi(u01(u.w), &sn, &cs);
           if (S.flags & PT_FLAG_COSINE_DIFFUSE) {
             const float u2 = u01(u.z);
-            const float r = sqrtf(u2);
+            // (u2 and 1 - u2 are 0 or >= 2^-24: sqrt_rn is IEEE's sqrt)
+            const float r = sqrt_rn(u2);
             x = r * cs;
             y = r * sn;
-            z = sqrtf(fmaxf(0.0f, 1.0f - u2));
+            z = sqrt_rn(fmaxf(0.0f, 1.0f - u2));
           } else {
             // uniform hemisphere: the reference's folded uniform sphere (cu:619-622)
             z = fabsf(2.0f * u01(u.z) - 1.0f);
-            const float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+            const float r = sqrt_rn(fmaxf(0.0f, 1.0f - z * z));  // (0 or >= 2^-24)
             x = r * cs;
             y = r * sn;
           }
@@ -510,7 +515,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
                        __builtin_fmaf(y, dpdv.y, __builtin_fmaf(x, dpdu.y, n.y * z)),
                        __builtin_fmaf(y, dpdv.z, __builtin_fmaf(x, dpdu.z, n.z * z)));
           } else {
-            d_new = normalize(mk(n.x * z + x * dpdu.x + y * dpdv.x, n.y * z + x * dpdu.y + y * dpdv.y,
+            d_new = normalize_u(mk(n.x * z + x * dpdu.x + y * dpdv.x, n.y * z + x * dpdu.y + y * dpdv.y,
                                  n.z * z + x * dpdu.z + y * dpdv.z));
           }
           if (S.flags & PT_FLAG_COSINE_DIFFUSE) {
@@ -537,7 +542,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
             o_new = mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y), __builtin_fmaf(n.z, EPS, pt.z));
           } else {
             const float dn = dot(d, n);
-            d_new = normalize(d - n * (2.0f * dn));
+            d_new = normalize_u(d - n * (2.0f * dn));  // (unit d, n: |d_new| ~ 1)
             o_new = pt + n * EPS;
           }
           Tset(mulv(Tv(), ld3(B.albedo)));
@@ -550,7 +555,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           bool refl = true;
           float cost = 0.0f;
           if (sin2t < 1.0f) {
-            cost = sqrtf(1.0f - sin2t);
+            cost = sqrt_rn(1.0f - sin2t);  // (sin2t < 1: 1 - sin2t >= 2^-24)
             float r0 = (1.0f - ior) / (1.0f + ior);
             r0 = r0 * r0;
             const float c = front ? cosi : cost;
@@ -562,11 +567,11 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           }
           if (refl) {
             const float dn = dot(d, n);
-            d_new = normalize(d - n * (2.0f * dn));
+            d_new = normalize_u(d - n * (2.0f * dn));
             Tset(mulv(Tv(), ld3(B.albedo)));
             o_new = pt + n * EPS;
           } else {
-            d_new = normalize(d * eta + n * (eta * cosi - cost));
+            d_new = normalize_u(d * eta + n * (eta * cosi - cost));  // (|.| ~ 1: Snell's refracted direction)
             Tset(mulv(Tv(), ld3(B.transmittance)));
             o_new = P - n * EPS;
           }
