@@ -1302,6 +1302,9 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
 // any primitive at t in [0, tmax]; triangles whose plane hit is certainly
 // outside [0, tmax] for every lane (tri_outside: shadow rays toward the light
 // mostly point away from the walls or end before them) cost no division
+#ifndef PT_OCC_BITWISE
+#define PT_OCC_BITWISE 1
+#endif
 template <bool REFA, bool SPH = true>
 __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, int pcount, const RayV& r) {
   constexpr int PS = prim_stride<REFA>();
@@ -1317,8 +1320,14 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
       plane_nd<REFA>(r.o, r.d, q, ndd, num);
       if (!tri_outside<REFA>(ndd, num, r.tmax)) tt = tri_test<REFA>(r.o, r.d, q, r.tmax);
     }
-    hit = hit || (tt >= 0.0f && tt <= r.tmax);
-    if (!__any(!hit)) break;  // every active lane is occluded
+    if constexpr (PT_OCC_BITWISE) {
+      // (no short-circuit: one mask update, no exec-mask branch per primitive)
+      hit = hit | ((tt >= 0.0f) & (tt <= r.tmax));
+      if (__ballot(!hit) == 0ull) break;  // every active lane is occluded
+    } else {
+      hit = hit || (tt >= 0.0f && tt <= r.tmax);
+      if (!__any(!hit)) break;  // every active lane is occluded
+    }
   }
   return hit;
 }

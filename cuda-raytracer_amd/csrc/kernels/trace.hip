@@ -177,10 +177,32 @@ __device__ __forceinline__ float tri_test_ref(const f3 o, const f3 d, const floa
   return t == 0.0f ? 0.0f : t;
 }
 // A triangle's closest-hit test in the record's arithmetic.
+// The U and V rows of a Baldwin-Weber record.  PT_UV_PAIRS: the record holds
+// them interleaved, {Ux, Vx, Uy, Vy}{Uz, Vz, Uw, Vw}{W} (bw_prim_records), so
+// the packed u / v evaluation (v_pk_fma_f32 with an SGPR pair operand) reads
+// each (U_k, V_k) pair straight from the record's SGPRs instead of copying
+// them into place (6 s_mov per primitive)
+#ifndef PT_UV_PAIRS
+#define PT_UV_PAIRS 1
+#endif
+__device__ __forceinline__ void bw_uv(const Prim& q, float4& U, float4& V) {
+  if constexpr (PT_UV_PAIRS) {
+    U = make_float4(q.q0.x, q.q0.z, q.q1.x, q.q1.z);
+    V = make_float4(q.q0.y, q.q0.w, q.q1.y, q.q1.w);
+  } else {
+    U = q.q0;
+    V = q.q1;
+  }
+}
 template <bool REFA, bool STRICT = false>
 __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const Prim& q, float tbest, float tlo = 0.0f) {
-  if constexpr (REFA) return tri_test_ref<STRICT>(o, d, q.q0, q.q1, q.q2, q.q3, q.q4, q.q5, tbest, tlo);
-  else return bw_test<STRICT>(o, d, q.q0, q.q1, q.q2, tbest, tlo);
+  if constexpr (REFA) {
+    return tri_test_ref<STRICT>(o, d, q.q0, q.q1, q.q2, q.q3, q.q4, q.q5, tbest, tlo);
+  } else {
+    float4 U, V;
+    bw_uv(q, U, V);
+    return bw_test<STRICT>(o, d, U, V, q.q2, tbest, tlo);
+  }
 }
 // The plane hit as t = num / ndd, for the division-free pre-test.
 template <bool REFA>
@@ -291,7 +313,9 @@ __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const Pri
                          sp3(q2.x, q2.y, q2.z), sp3(q2.w, q3.w, q4.w), sp3(q4.x, q4.y, q4.z),
                          sp3(q5.x, q5.y, q5.z), tbest, tlo);
   } else {
-    return bw_test2(o, d, q.q0, q.q1, q.q2, tbest, tlo);
+    float4 U, V;
+    bw_uv(q, U, V);
+    return bw_test2(o, d, U, V, q.q2, tbest, tlo);
   }
 }
 

@@ -748,8 +748,13 @@ static std::vector<float4> bw_prim_records(const pt_scene_desc* s) {
     } else {
       double r[12];
       bw_rows(q, r);
-      o[0] = make_float4((float)r[0], (float)r[1], (float)r[2], (float)r[3]);
-      o[1] = make_float4((float)r[4], (float)r[5], (float)r[6], (float)r[7]);
+      if (PT_UV_PAIRS) {  // U and V interleaved (trace.hip bw_uv)
+        o[0] = make_float4((float)r[0], (float)r[4], (float)r[1], (float)r[5]);
+        o[1] = make_float4((float)r[2], (float)r[6], (float)r[3], (float)r[7]);
+      } else {
+        o[0] = make_float4((float)r[0], (float)r[1], (float)r[2], (float)r[3]);
+        o[1] = make_float4((float)r[4], (float)r[5], (float)r[6], (float)r[7]);
+      }
       o[2] = make_float4((float)r[8], (float)r[9], (float)r[10], (float)r[11]);
     }
     o[3] = make_float4(q[3], 0.f, 0.f, 0.f);
