@@ -94,6 +94,13 @@ __device__ __forceinline__ uint32_t udiv_q(uint32_t n, udiv d) {
 struct u4 {
   uint32_t x, y, z, w;
 };
+// PT_PHILOX_KEYS_INLINE: the seed-dependent round keys k0 + r 0x9E3779B9 are
+// recomputed (one s_add each) at every call instead of being hoisted out of
+// the path loop as ten loop-invariant SGPRs, which the register allocator
+// then spills to VGPR lanes (a v_readlane per round)
+#ifndef PT_PHILOX_KEYS_INLINE
+#define PT_PHILOX_KEYS_INLINE 1
+#endif
 // M64: each 32x32 -> 64-bit product as one v_mad_u64_u32 instead of
 // v_mul_hi_u32 + v_mul_lo_u32 (same bits; faster, but 4 more VGPRs live)
 template <bool M64 = false>
@@ -111,6 +118,7 @@ __device__ __forceinline__ u4 philox(u4 c, uint32_t k0, uint32_t k1) {
     }
     c = u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
+    if constexpr (PT_PHILOX_KEYS_INLINE) asm volatile("" : "+s"(k0));
     k1 += 0xBB67AE85u;
   }
   return c;
@@ -148,20 +156,21 @@ __device__ __forceinline__ void sincos2pi(float u, float* s, float* c) {
   float f = x4 - q;
   float th = f * 1.57079637f;
   float t2 = th * th;
+  // Horner steps as FMAs (one instruction each)
   float sp = -2.50521084e-08f;
-  sp = sp * t2 + 2.75573192e-06f;
-  sp = sp * t2 + -1.98412698e-04f;
-  sp = sp * t2 + 8.33333333e-03f;
-  sp = sp * t2 + -1.66666667e-01f;
-  sp = sp * t2 + 1.0f;
+  sp = __builtin_fmaf(sp, t2, 2.75573192e-06f);
+  sp = __builtin_fmaf(sp, t2, -1.98412698e-04f);
+  sp = __builtin_fmaf(sp, t2, 8.33333333e-03f);
+  sp = __builtin_fmaf(sp, t2, -1.66666667e-01f);
+  sp = __builtin_fmaf(sp, t2, 1.0f);
   float sn = sp * th;
   float cp = 2.08767570e-09f;
-  cp = cp * t2 + -2.75573192e-07f;
-  cp = cp * t2 + 2.48015873e-05f;
-  cp = cp * t2 + -1.38888889e-03f;
-  cp = cp * t2 + 4.16666667e-02f;
-  cp = cp * t2 + -0.5f;
-  cp = cp * t2 + 1.0f;
+  cp = __builtin_fmaf(cp, t2, -2.75573192e-07f);
+  cp = __builtin_fmaf(cp, t2, 2.48015873e-05f);
+  cp = __builtin_fmaf(cp, t2, -1.38888889e-03f);
+  cp = __builtin_fmaf(cp, t2, 4.16666667e-02f);
+  cp = __builtin_fmaf(cp, t2, -0.5f);
+  cp = __builtin_fmaf(cp, t2, 1.0f);
   int iq = ((int)q) & 3;
   float rs = sn, rc = cp;
   if (iq == 1) {

@@ -123,8 +123,9 @@ __device__ __forceinline__ f3 camera_dir(const ShadeArgs& S, uint32_t p, uint32_
   // cu:338-354: ss = (x + u, y + v); k = ((ss.y/W)-.5, -((ss.x/H)-.5), 1) / |k|
   float ssx = (float)row + u01(u.x);
   float ssy = (float)col + u01(u.y);
-  float kx = ssy / (float)S.width - 0.5f;
-  float ky = -(ssx / (float)S.height - 0.5f);
+  // (div_rn: IEEE's quotient for ssx, ssy = 0 or >= 2^-24 over W, H >= 1)
+  float kx = div_rn(ssy, (float)S.width) - 0.5f;
+  float ky = -(div_rn(ssx, (float)S.height) - 0.5f);
   float kz = 1.0f;
   const pt_camera cam = cam_of<KR>(S);
   const f3 L = ld3(cam.left), U = ld3(cam.up), K = ld3(cam.look_at);
@@ -549,14 +550,14 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           spec = F_SPEC;
         } else {  // PT_BSDF_GLASS / _REFRACTION (Fresnel-weighted reflect / refract, bsdf.h:167-212)
           const float ior = B.ior;
-          const float eta = front ? (1.0f / ior) : ior;
+          const float eta = front ? rcp_rn(ior) : ior;  // (an index of refraction: normal range)
           const float cosi = -dot(d, n);
           const float sin2t = (eta * eta) * (1.0f - cosi * cosi);
           bool refl = true;
           float cost = 0.0f;
           if (sin2t < 1.0f) {
             cost = sqrt_rn(1.0f - sin2t);  // (sin2t < 1: 1 - sin2t >= 2^-24)
-            float r0 = (1.0f - ior) / (1.0f + ior);
+            float r0 = div_rn(1.0f - ior, 1.0f + ior);  // (1 - ior: 0 or >= 2^-24 in magnitude)
             r0 = r0 * r0;
             const float c = front ? cosi : cost;
             const float m = 1.0f - c;

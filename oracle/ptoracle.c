@@ -107,20 +107,21 @@ static void sincos2pi(float u, float* s, float* c) {
   float f = x4 - q;
   float th = f * 1.57079637f;
   float t2 = th * th;
+  /* Horner steps as FMAs (ptmath.h sincos2pi) */
   float sp = -2.50521084e-08f;
-  sp = sp * t2 + 2.75573192e-06f;
-  sp = sp * t2 + -1.98412698e-04f;
-  sp = sp * t2 + 8.33333333e-03f;
-  sp = sp * t2 + -1.66666667e-01f;
-  sp = sp * t2 + 1.0f;
+  sp = fmaf(sp, t2, 2.75573192e-06f);
+  sp = fmaf(sp, t2, -1.98412698e-04f);
+  sp = fmaf(sp, t2, 8.33333333e-03f);
+  sp = fmaf(sp, t2, -1.66666667e-01f);
+  sp = fmaf(sp, t2, 1.0f);
   float sn = sp * th;
   float cp = 2.08767570e-09f;
-  cp = cp * t2 + -2.75573192e-07f;
-  cp = cp * t2 + 2.48015873e-05f;
-  cp = cp * t2 + -1.38888889e-03f;
-  cp = cp * t2 + 4.16666667e-02f;
-  cp = cp * t2 + -0.5f;
-  cp = cp * t2 + 1.0f;
+  cp = fmaf(cp, t2, -2.75573192e-07f);
+  cp = fmaf(cp, t2, 2.48015873e-05f);
+  cp = fmaf(cp, t2, -1.38888889e-03f);
+  cp = fmaf(cp, t2, 4.16666667e-02f);
+  cp = fmaf(cp, t2, -0.5f);
+  cp = fmaf(cp, t2, 1.0f);
   int iq = ((int)q) & 3;
   float rs = sn, rc = cp;
   if (iq == 1) {

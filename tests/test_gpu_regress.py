@@ -280,3 +280,10 @@ def test_triangle_test_division_is_ieee(gpu_ctx):
         ref = num / den
     ulps = np.abs(q.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
     assert ulps.max() <= 1, ulps.max()
+    # the camera's pixel coordinate over the image size (shade.hip camera_dir):
+    # num in {0} U [2^-24, 2^15], den an image size in [1, 2^15]
+    num = (rng.uniform(1, 2, m) * np.exp2(rng.integers(-24, 15, m))).astype(np.float32)
+    num[:1000] = 0.0
+    den = rng.integers(1, 1 << 15, m).astype(np.float32)
+    q = gpu_ctx.check_division(num, den)
+    assert np.array_equal(q.view(np.uint32), (num / den).view(np.uint32))
