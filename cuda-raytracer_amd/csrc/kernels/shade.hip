@@ -1638,21 +1638,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
 #endif
 }
 
-// Sum each owned pixel's samples of this batch into the accumulation buffer,
-// in sample order (deterministic; replaces kernelUpdateSSImage +
+// Sum each active pixel's samples of this batch into the accumulation buffer
+// (slot[q]: its owned slot; culled pixels add exact zeros, so they are not
+// touched), in sample order (deterministic; replaces kernelUpdateSSImage +
 // kernelReconstructImage + kernelAccumulate, cu:666-742).
-__global__ __launch_bounds__(TPB) void k_accum(const float4* __restrict__ ps1, float4* accum, uint32_t npix,
-                                               uint32_t spp_b) {
+__global__ __launch_bounds__(TPB) void k_accum(const float4* __restrict__ ps1, float4* accum,
+                                               const uint32_t* __restrict__ slot, uint32_t npix, uint32_t spp_b) {
   const uint32_t q = blockIdx.x * TPB + threadIdx.x;
   if (q >= npix) return;
-  float4 a = accum[q];
+  const uint32_t o = slot[q];
+  float4 a = accum[o];
   for (uint32_t j = 0; j < spp_b; ++j) {
     const f3 l = get_res(ps1, (size_t)j * npix + q);
     a.x = a.x + l.x;
     a.y = a.y + l.y;
     a.z = a.z + l.z;
   }
-  accum[q] = a;
+  accum[o] = a;
 }
 
 // Repack pt_intersect's 8-float rays {o, tmax, d, 0} into ray records.

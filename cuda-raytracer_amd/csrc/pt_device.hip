@@ -138,6 +138,17 @@ struct pt_ctx {
   int fb_w = 0, fb_h = 0, fb_tile = 0, fb_rank = 0, fb_nranks = 0;
   std::vector<uint32_t> pix_of;  // owned pixel slot -> global pixel
   uint32_t* d_pix_of = nullptr;
+  // camera-ray culling (cull_pixels): the owned pixels whose camera rays may
+  // reach the scene (global pixel index, owned slot), valid for cull_cam and
+  // the current framebuffer / scene; the others' camera rays provably miss
+  // the root box: radiance 0, counted as cast (host_rays)
+  bool cull = true;  // PT_CULL=0: trace every camera ray
+  bool cull_valid = false;
+  pt_camera cull_cam{};
+  std::vector<uint32_t> act_pix, act_slot;
+  uint32_t* d_act_pix = nullptr;
+  uint32_t* d_act_slot = nullptr;
+  uint64_t host_rays = 0;
   float4* d_accum = nullptr;
   float4* d_frame = nullptr;  // row-major frame staged for pt_get_image (k_frame)
   size_t frame_cap = 0;
@@ -210,7 +221,7 @@ static void free_all(pt_ctx* c) {
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_kmap, c->d_res, c->d_wstate, c->d_live, c->d_pool,
                   c->d_pix_of, c->d_accum, c->d_frame, c->d_tmin, c->d_ray_b, c->d_ps0_b, c->d_ps1_b, c->d_ps2_b,
-                  c->d_ps3_b, c->d_compact};
+                  c->d_ps3_b, c->d_compact, c->d_act_pix, c->d_act_slot};
   for (void* p : ptrs)
     if (p) hipFree(p);
 }
@@ -638,7 +649,8 @@ static int read_device_stats(pt_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   unsigned long long R = 0;
   for (int s = 0; s < RCOUNT_SLOTS; ++s) R += rl[s * 16];
-  c->stats.rays = R;
+  c->stats.rays = R + c->host_rays;
+  c->stats.culled_rays = c->host_rays;
   c->stats.visits = st[STAT_V] + R;
   st[STAT_LV0] += R;
   c->stats.peak_queue_entries = st[STAT_PEAKQ];
@@ -762,6 +774,105 @@ static std::vector<float4> bw_prim_records(const pt_scene_desc* s) {
   return out;
 }
 
+// Camera-ray culling.  A camera ray of pixel (row, col) is
+//   dir ~ kx left + ky up + look_at,  kx = (col + v) / W - 1/2,
+//   ky = -((row + u) / H - 1/2),  u, v in [0, 1)          (camera_dir, cu:338-354)
+// from the camera origin.  Each corner X of the root node's box (the union
+// of its children's boxes, guard band included) is solved for the (kx, ky, s)
+// with X - origin = s (kx left + ky up + look_at), in double; when every corner
+// lies in front (s > 0), the box's projection -- the convex hull of the
+// corners' (kx, ky) -- lies in their bounding rectangle.  A pixel whose whole
+// footprint lies outside that rectangle, widened by 4 pixels (the device's
+// fp32 directions deviate by ~1e-7 from the exact ones; a pixel is ~1e-3),
+// has camera rays that miss the root box, hence every primitive: its paths
+// end at the camera vertex with radiance 0, exactly what tracing them gives
+// (no emission from a miss, no shadow or extension ray), so it is left out of
+// the path space and its camera rays are counted as cast.  Returns false (no
+// culling) for a single-leaf tree, a box that reaches behind the camera, or a
+// degenerate camera basis.
+static bool cull_rect(const pt_ctx* c, int W, int H, double& x0, double& x1, double& y0, double& y1) {
+  if (c->root_leaf || c->nodes_host.empty()) return false;
+  const pt_node& r = c->nodes_host[0];
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int k = 0; k < 4; ++k) {
+    if (r.child[k] < 0) continue;
+    lo[0] = std::min(lo[0], (double)r.bmin_x[k]);
+    hi[0] = std::max(hi[0], (double)r.bmax_x[k]);
+    lo[1] = std::min(lo[1], (double)r.bmin_y[k]);
+    hi[1] = std::max(hi[1], (double)r.bmax_y[k]);
+    lo[2] = std::min(lo[2], (double)r.bmin_z[k]);
+    hi[2] = std::max(hi[2], (double)r.bmax_z[k]);
+  }
+  if (!(lo[0] <= hi[0])) return false;
+  const pt_camera& cam = c->camera;
+  // columns left, up, look_at; solve A y = X - origin by Cramer's rule
+  const double A[3][3] = {{cam.left[0], cam.up[0], cam.look_at[0]},
+                          {cam.left[1], cam.up[1], cam.look_at[1]},
+                          {cam.left[2], cam.up[2], cam.look_at[2]}};
+  auto det3 = [](const double m[3][3]) {
+    return m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) - m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+           m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+  };
+  const double D = det3(A);
+  if (!(std::fabs(D) > 1e-12)) return false;
+  x0 = y0 = INFINITY;
+  x1 = y1 = -INFINITY;
+  for (int k = 0; k < 8; ++k) {
+    const double X[3] = {((k & 1) ? hi[0] : lo[0]) - cam.origin[0], ((k & 2) ? hi[1] : lo[1]) - cam.origin[1],
+                         ((k & 4) ? hi[2] : lo[2]) - cam.origin[2]};
+    double y[3];
+    for (int j = 0; j < 3; ++j) {
+      double M[3][3];
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) M[a][b] = b == j ? X[a] : A[a][b];
+      y[j] = det3(M) / D;
+    }
+    const double s = y[2];
+    if (!(s > 1e-9 * (std::fabs(X[0]) + std::fabs(X[1]) + std::fabs(X[2]) + 1e-30))) return false;
+    x0 = std::min(x0, y[0] / s);
+    x1 = std::max(x1, y[0] / s);
+    y0 = std::min(y0, y[1] / s);
+    y1 = std::max(y1, y[1] / s);
+  }
+  const double mx = 4.0 / W + 1e-6 * (std::fabs(x0) + std::fabs(x1)), my = 4.0 / H + 1e-6 * (std::fabs(y0) + std::fabs(y1));
+  x0 -= mx;
+  x1 += mx;
+  y0 -= my;
+  y1 += my;
+  return true;
+}
+
+// The active (not culled) owned pixels for the current camera and frame
+// (cached until either changes); act_slot[i] is pixel act_pix[i]'s owned slot.
+static int cull_pixels(pt_ctx* c, int W, int H) {
+  if (c->cull_valid && !memcmp(&c->cull_cam, &c->camera, sizeof(pt_camera))) return PT_OK;
+  c->act_pix.clear();
+  c->act_slot.clear();
+  double x0, x1, y0, y1;
+  const bool on = c->cull && cull_rect(c, W, H, x0, x1, y0, y1);
+  for (size_t i = 0; i < c->pix_of.size(); ++i) {
+    const uint32_t g = c->pix_of[i];
+    if (on) {
+      const int row = (int)(g / (uint32_t)W), col = (int)(g % (uint32_t)W);
+      const double kx0 = (double)col / W - 0.5, kx1 = (double)(col + 1) / W - 0.5;
+      const double ky0 = -((double)(row + 1) / H - 0.5), ky1 = -((double)row / H - 0.5);
+      if (kx1 < x0 || kx0 > x1 || ky1 < y0 || ky0 > y1) continue;  // the whole footprint misses
+    }
+    c->act_pix.push_back(g);
+    c->act_slot.push_back((uint32_t)i);
+  }
+  int rc;
+  if ((rc = dalloc(c, &c->d_act_pix, std::max<size_t>(1, c->act_pix.size())))) return rc;
+  if ((rc = dalloc(c, &c->d_act_slot, std::max<size_t>(1, c->act_slot.size())))) return rc;
+  if (!c->act_pix.empty()) {
+    HIPCHK(c, hipMemcpy(c->d_act_pix, c->act_pix.data(), c->act_pix.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_act_slot, c->act_slot.data(), c->act_slot.size() * 4, hipMemcpyHostToDevice));
+  }
+  c->cull_cam = c->camera;
+  c->cull_valid = true;
+  return PT_OK;
+}
+
 static void build_owned_pixels(pt_ctx* c, int W, int H, int T, int rank, int nranks) {
   c->pix_of.clear();
   const int ntx = (W + T - 1) / T, nty = (H + T - 1) / T;
@@ -830,6 +941,7 @@ int pt_create(pt_ctx** out, int device) {
   if (const char* q = getenv("PT_PATH_GUIDED_BELOW")) c->path_guided_below = std::max(0, atoi(q));
   // paths per chunk (a frame of npix x spp paths runs in ceil(spp / (chunk / npix))
   // chunks, summed per pixel in sample order across them): tests set it small
+  if (const char* q = getenv("PT_CULL")) c->cull = atoi(q) != 0;
   if (const char* q = getenv("PT_CHUNK_PATHS")) c->chunk_paths = (uint32_t)std::min<long long>(1ll << 28, std::max(1ll, atoll(q)));
   // tail compaction needs the wave record order's continuing-first ranks
   if (const char* q = getenv("PT_COMPACT")) {
@@ -1059,6 +1171,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     c->origin_bound = 64.0 * m;
   }
   c->have_scene = true;
+  c->cull_valid = false;
   c->cap_paths = 0;  // force re-derivation of root queue offsets
   c->cap_spp = 0;
   return PT_OK;
@@ -1070,6 +1183,7 @@ int pt_set_camera(pt_ctx* c, const pt_camera* cam) {
     if (!(std::fabs((double)cam->origin[k]) <= c->origin_bound))
       return fail(c, PT_E_UNSUPPORTED, "pt_set_camera: origin beyond 64x the scene's extent (conservative box guard)");
   c->camera = *cam;
+  c->cull_valid = false;
   return pt_clear(c);
 }
 
@@ -1089,6 +1203,7 @@ int pt_reset_stats(pt_ctx* c) {
   HIPCHK(c, hipMemset(c->d_stats, 0, STAT_COUNT * 8));
   HIPCHK(c, hipMemset(c->d_rcount, 0, RCOUNT_SLOTS * 16 * 8));
   memset(&c->stats, 0, sizeof(c->stats));
+  c->host_rays = 0;
   return PT_OK;
 }
 
@@ -1120,6 +1235,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   if (P->width != c->fb_w || P->height != c->fb_h || tile != c->fb_tile || rank != c->fb_rank ||
       nranks != c->fb_nranks) {
     build_owned_pixels(c, P->width, P->height, tile, rank, nranks);
+    c->cull_valid = false;
     c->fb_w = P->width;
     c->fb_h = P->height;
     c->fb_tile = tile;
@@ -1132,7 +1248,15 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     HIPCHK(c, hipMemset(c->d_accum, 0, std::max<size_t>(1, c->pix_of.size()) * sizeof(float4)));
     c->samples = 0;
   }
-  const uint32_t npix = (uint32_t)c->pix_of.size();
+  if (c->pix_of.empty()) {
+    c->samples += P->spp;
+    return PT_OK;
+  }
+  // the owned pixels whose camera rays may reach the scene (cull_pixels); the
+  // rest end at their camera vertex with radiance 0: counted, not traced
+  if ((rc = cull_pixels(c, P->width, P->height))) return rc;
+  c->host_rays += (uint64_t)(c->pix_of.size() - c->act_pix.size()) * (uint64_t)P->spp;
+  const uint32_t npix = (uint32_t)c->act_pix.size();
   if (npix == 0) {
     c->samples += P->spp;
     return PT_OK;
@@ -1168,7 +1292,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.prims = c->refa ? c->d_prims_ref : c->d_prims;
     S.shade = c->d_shade;
     S.bsdfs = c->d_bsdfs;
-    S.pix_of = c->d_pix_of;
+    S.pix_of = c->d_act_pix;
     S.light = c->light;
     S.cam = c->camera;
     S.npix = npix;
@@ -1398,7 +1522,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
                            (const uint32_t*)c->d_pool, nblocks, c->d_live, c->d_stats + STAT_SHADED);
     }
     c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_res,
-              c->d_accum, npix, spp_c);
+              c->d_accum, (const uint32_t*)c->d_act_slot, npix, spp_c);
     HIPCHK(c, hipGetLastError());
     done += (int)spp_c;
     first = false;

@@ -101,7 +101,7 @@ class pt_stats(C.Structure):
                 ("ms_path", C.c_double), ("path_launches", C.c_uint64),
                 ("shaded", C.c_uint64), ("ms_shade_push", C.c_double), ("shade_launches", C.c_uint64),
                 ("queue_factor", C.c_int32), ("pad_", C.c_int32),
-                ("ms_scan_level", C.c_double * 16)]
+                ("ms_scan_level", C.c_double * 16), ("culled_rays", C.c_uint64)]
 
 
 class pt_mesh_desc(C.Structure):

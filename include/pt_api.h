@@ -390,6 +390,10 @@ typedef struct pt_stats {
   int32_t queue_factor;   /* current queue factor (grows when a level overflows) */
   int32_t pad_;
   double ms_scan_level[16]; /* k_scan_level per BVH level (part of ms_scan)  */
+  uint64_t culled_rays;     /* camera rays of pixels whose whole footprint
+                               provably misses the scene's root box: resolved
+                               by pt_render's pixel test (radiance 0, no
+                               further ray) and counted in `rays` as cast */
 } pt_stats;
 int pt_get_stats(pt_ctx* ctx, pt_stats* out);
 int pt_reset_stats(pt_ctx* ctx);

@@ -133,3 +133,42 @@ def test_config5_fullsize_frame(gpu_ctx):
         ms = (t % 8) == r
         assert np.array_equal(gpu_ctx.get_image()[ms], g[ms]), f"share {r}"
     assert share_rays == whole_rays
+
+
+@pytest.mark.parametrize("name", ["bunny", "CBbunny"])
+def test_camera_ray_culling(gpu_ctx, name):
+    """pt_render leaves out of the path space the pixels whose camera rays
+    provably miss the root box (pt_device.hip cull_rect: the box's projection
+    widened by 4 pixels) and counts their rays as cast: the frame and the ray
+    count equal an unculled render (PT_CULL=0) and the oracle's bit for bit.
+    bunny.dae (an open scene) culls most of its frame; the Cornell box, whose
+    walls fill the view, nothing."""
+    W, H, SPP, B = 160, 120, 4, 8
+    sc = _scene(name)
+    o, orays = pyoracle.image(sc.desc(), W, H, SPP, max_bounces=B, seed=SEED, threads=16)
+    old = os.environ.get("PT_CULL")
+    os.environ["PT_CULL"] = "0"
+    try:
+        nc = ptrace.Context(0)
+    finally:
+        if old is None:
+            del os.environ["PT_CULL"]
+        else:
+            os.environ["PT_CULL"] = old
+    try:
+        out = []
+        for ctx in (gpu_ctx, nc):
+            ctx.load_scene(sc)
+            ctx.reset_stats()
+            ctx.clear()
+            ctx.render(W, H, SPP, max_bounces=B, seed=SEED)
+            out.append((ctx.get_image(), ctx.stats()))
+    finally:
+        nc.close()
+    (g, st), (g0, st0) = out
+    assert np.array_equal(g[..., :3], o[..., :3]) and np.array_equal(g0[..., :3], o[..., :3])
+    assert st.rays == orays and st0.rays == orays and st0.culled_rays == 0
+    if name == "bunny":
+        assert st.culled_rays > W * H * SPP // 4, st.culled_rays
+    else:
+        assert st.culled_rays == 0
