@@ -529,6 +529,9 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 #ifndef PT_ROOT_EXT_PRETEST
 #define PT_ROOT_EXT_PRETEST 0
 #endif
+#ifndef PT_ROOT_SELECT
+#define PT_ROOT_SELECT 1
+#endif
 template <int R, bool REFA = false, bool TMIN = false>
 __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T, int lane, const uint32_t (&id)[R],
                                           const f3 (&o)[R], const f3 (&d)[R], const float (&tmax)[R],
@@ -569,7 +572,13 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
           }
           // ties go to the lowest primitive across the inline leaves too
           // (their primitive ranges are not in increasing order)
-          if (tt >= 0.0f && (tt < bt || (tt == bt && (bp < 0 || pstart + kk < bp)))) {
+          if constexpr (PT_ROOT_SELECT) {
+            // (as selects: no exec-mask branch per primitive; bp < 0 is the
+            // largest unsigned value)
+            const bool take = (tt >= 0.0f) & ((tt < bt) | ((tt == bt) & ((uint32_t)(pstart + kk) < (uint32_t)bp)));
+            bt = take ? tt : bt;
+            bp = take ? pstart + kk : bp;
+          } else if (tt >= 0.0f && (tt < bt || (tt == bt && (bp < 0 || pstart + kk < bp)))) {
             bt = tt;
             bp = pstart + kk;
           }
