@@ -1359,8 +1359,13 @@ constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 // instead of per path: fewer scattered result writes, and k_accum reads a
 // quarter of the bytes).  The wave pool hands out units, PATH_CHUNK paths'
 // worth per grab.  Off: one path per pool entry, one result per path.
+// Measured (round 4, CBempty / CBspheres): 69.5k / 48.9k Mrays/s on against
+// 71.0k / 50.0k off -- the block's partial sum takes the LDS to 20 KB per
+// workgroup, the whole 160 KB of a CU at 8 workgroups, and the lane logic
+// costs more than the 0.4 ms of k_accum reads and the scattered writes it
+// saves.  Off by default.
 #ifndef PT_PATH_BLOCKS
-#define PT_PATH_BLOCKS 1
+#define PT_PATH_BLOCKS 0
 #endif
 constexpr uint32_t PATH_UNIT = PT_PATH_BLOCKS ? PT_SAMPLE_BLOCK : 1u;
 static_assert((PT_SAMPLE_BLOCK & (PT_SAMPLE_BLOCK - 1)) == 0, "PT_SAMPLE_BLOCK must be a power of two");

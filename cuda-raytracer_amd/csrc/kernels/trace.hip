@@ -529,8 +529,9 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 #ifndef PT_ROOT_EXT_PRETEST
 #define PT_ROOT_EXT_PRETEST 0
 #endif
+// (selects measured slower: CBbunny -2.4 %, dragon proxy -0.6 %, round 4)
 #ifndef PT_ROOT_SELECT
-#define PT_ROOT_SELECT 1
+#define PT_ROOT_SELECT 0
 #endif
 template <int R, bool REFA = false, bool TMIN = false>
 __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T, int lane, const uint32_t (&id)[R],

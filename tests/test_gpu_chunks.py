@@ -141,8 +141,8 @@ def test_camera_ray_culling(gpu_ctx, name):
     provably miss the root box (pt_device.hip cull_rect: the box's projection
     widened by 4 pixels) and counts their rays as cast: the frame and the ray
     count equal an unculled render (PT_CULL=0) and the oracle's bit for bit.
-    bunny.dae (an open scene) culls most of its frame; the Cornell box, whose
-    walls fill the view, nothing."""
+    bunny.dae (an open scene) culls most of its frame, the Cornell box the
+    margins around its open front."""
     W, H, SPP, B = 160, 120, 4, 8
     sc = _scene(name)
     o, orays = pyoracle.image(sc.desc(), W, H, SPP, max_bounces=B, seed=SEED, threads=16)
@@ -168,7 +168,6 @@ def test_camera_ray_culling(gpu_ctx, name):
     (g, st), (g0, st0) = out
     assert np.array_equal(g[..., :3], o[..., :3]) and np.array_equal(g0[..., :3], o[..., :3])
     assert st.rays == orays and st0.rays == orays and st0.culled_rays == 0
+    assert 0 < st.culled_rays < W * H * SPP
     if name == "bunny":
         assert st.culled_rays > W * H * SPP // 4, st.culled_rays
-    else:
-        assert st.culled_rays == 0
