@@ -68,7 +68,6 @@ struct ShadeArgs {
   // writes res[P] and starts the next unstarted path
   float4* res;        // per-path radiance of the chunk
   uint32_t M;         // paths in the chunk
-  uint32_t spp_c;     // samples in the chunk (k_path_leaf: a block's samples stay below it)
   // paths are handed out in blocks of POOL_BLOCK consecutive paths (one sample
   // of 256 owned pixels): block c comes from dispenser c % POOLS
   uint4* wstate;      // per workgroup: {next, end} of its current block, live slots after its last pass,
@@ -1353,24 +1352,6 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
 #define PT_PATH_CHUNK 512
 #endif
 constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
-// PT_PATH_BLOCKS: a lane runs the PT_SAMPLE_BLOCK samples of one pixel's
-// block one after another (a unit), sums their radiance in LDS in sample
-// order and writes one partial sum per block (12 B per PT_SAMPLE_BLOCK paths
-// instead of per path: fewer scattered result writes, and k_accum reads a
-// quarter of the bytes).  The wave pool hands out units, PATH_CHUNK paths'
-// worth per grab.  Off: one path per pool entry, one result per path.
-// Measured (round 4, CBempty / CBspheres): 69.5k / 48.9k Mrays/s on against
-// 71.0k / 50.0k off -- the block's partial sum takes the LDS to 20 KB per
-// workgroup, the whole 160 KB of a CU at 8 workgroups, and the lane logic
-// costs more than the 0.4 ms of k_accum reads and the scattered writes it
-// saves.  Off by default.
-#ifndef PT_PATH_BLOCKS
-#define PT_PATH_BLOCKS 0
-#endif
-constexpr uint32_t PATH_UNIT = PT_PATH_BLOCKS ? PT_SAMPLE_BLOCK : 1u;
-static_assert((PT_SAMPLE_BLOCK & (PT_SAMPLE_BLOCK - 1)) == 0, "PT_SAMPLE_BLOCK must be a power of two");
-constexpr uint32_t UNIT_CHUNK = PATH_CHUNK / PATH_UNIT > 0 ? PATH_CHUNK / PATH_UNIT : 1u;
-constexpr uint32_t CONT_BIT = 0x80000000u;  // sh_p: the lane's next path is its block's next sample
 
 // With all path state in registers: 6 waves per SIMD (80 VGPRs, no spills);
 // 7 waves (72 VGPRs) ran within 0.6 % of it but spilled ~20 VGPRs around the
@@ -1422,14 +1403,14 @@ constexpr uint32_t PATH_CTR_STRIDE = 32;  // u32s between region counters (128 B
 // hi (tail_unit = the region's waves x the guide factor; 0: one phase).
 // Returns false once the region's paths are all handed out.
 __device__ __forceinline__ bool path_grab(uint32_t lo, uint32_t hi, uint32_t tail_unit, uint32_t k, uint32_t& b,
-                                          uint32_t& e, uint32_t chunk = PATH_CHUNK) {
+                                          uint32_t& e) {
   uint32_t s0 = lo, g = 0;
 #pragma unroll
   for (int j = 0; j < PATH_PHASES; ++j) {
-    const uint32_t c = max(1u, chunk >> j);
+    const uint32_t c = PATH_CHUNK >> j;
     uint32_t s1 = hi;
     if (j + 1 < PATH_PHASES) {
-      const uint64_t rem = (uint64_t)tail_unit * c;
+      const uint64_t rem = (uint64_t)tail_unit * (PATH_CHUNK >> j);
       s1 = rem >= (uint64_t)(hi - s0) ? s0 : hi - (uint32_t)rem;
     }
     const uint32_t n = (s1 - s0 + c - 1) / c;
@@ -1506,7 +1487,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
   // the lane's path index lives in LDS between its uses (camera ray, sample
   // index, result): one VGPR less across the vertex loop
   __shared__ uint32_t sh_p[TPB];
-  sh_p[threadIdx.x] = 0u;  // (no CONT_BIT: the lane takes its first unit from the pool)
   PathState st{mk(0, 0, 0), 0u, mk(0, 0, 0), 0u};
   RayV ext{mk(0, 0, 0), mk(0, 0, 1), -1.0f}, shr[NSH];
   f3 C[NSH];
@@ -1516,36 +1496,29 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
     C[s] = mk(0, 0, 0);
   }
   // PT_PATH_LDS_SH: the pending shadow rays live in LDS between vertices
-  // (PT_PATH_BLOCKS: three more rows, the block's partial sum)
-  __shared__ float sh_lds[PT_PATH_LDS_SH ? (NSH * 10 + 6 + (PT_PATH_BLOCKS ? 3 : 0)) * TPB : 1];
-  __shared__ float sh_blk[PT_PATH_LDS_SH || !PT_PATH_BLOCKS ? 1 : 3 * TPB];
+  __shared__ float sh_lds[PT_PATH_LDS_SH ? (NSH * 10 + 6) * TPB : 1];
   float* const Lq = sh_lds + (size_t)10 * NSH * TPB + threadIdx.x;  // (PT_PATH_LDS_SH: the radiance)
-  float* const Aq = PT_PATH_LDS_SH ? Lq + 6 * TPB : sh_blk + threadIdx.x;  // the block's partial sum
   for (;;) {
-    // ---- refill idle lanes: a lane whose path ended inside its block starts
-    // the block's next sample; the others take units from the pool (new paths
-    // start at their camera ray)
-    bool cont = false;
-    if constexpr (PT_PATH_BLOCKS) cont = !active && (sh_p[threadIdx.x] & CONT_BIT);
-    unsigned long long idle = __ballot(!active && !cont);
+    // ---- refill idle lanes from the pool (new paths start at their camera ray)
+    unsigned long long idle = __ballot(!active);
     if (idle && next == end && !drained) {
 #if PT_PATH_TIMING
       const unsigned long long tg = wall_clock64();
 #endif
       uint32_t b = 0, e = 0;
       if constexpr (!GUIDED) {
-        if (lid == 0) b = atomicAdd(work, UNIT_CHUNK);
+        if (lid == 0) b = atomicAdd(work, PATH_CHUNK);
         b = __builtin_amdgcn_readfirstlane(b);
         drained = b >= S.N;
         next = drained ? 0u : b;
-        end = drained ? 0u : min(b + UNIT_CHUNK, S.N);
+        end = drained ? 0u : min(b + PATH_CHUNK, S.N);
       } else {
       if (lid == 0) {
         while (tried < nreg) {
           const uint32_t k = atomicAdd(work + reg * PATH_CTR_STRIDE, 1u);
           const uint32_t lo = (uint32_t)((uint64_t)S.N * reg / nreg);
           const uint32_t hi = (uint32_t)((uint64_t)S.N * (reg + 1) / nreg);
-          if (path_grab(lo, hi, tail_unit, k, b, e, UNIT_CHUNK)) break;
+          if (path_grab(lo, hi, tail_unit, k, b, e)) break;
           reg = reg + 1 == nreg ? 0u : reg + 1;
           ++tried;
         }
@@ -1566,23 +1539,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       else ++nchunks;
 #endif
     }
-    bool start = cont;
-    uint32_t pnew = cont ? (sh_p[threadIdx.x] & ~CONT_BIT) + S.npix : 0u;
     if (idle && next < end) {
       const uint32_t r = mbcnt64(idle);
       const uint32_t avail = end - next;
-      if (!active && !cont && r < avail) {
-        // unit u: pixel q, samples [b B, b B + B) of the chunk (path index j npix + q)
-        const uint32_t u = next + r;
-        const uint32_t bb = PT_PATH_BLOCKS ? udiv_q(u, S.div_npix) : 0u;
-        pnew = PT_PATH_BLOCKS ? bb * (PATH_UNIT * S.npix) + (u - bb * S.npix) : u;
-        start = true;
-      }
-      next += min((uint32_t)__popcll(idle), avail);
-    }
-    {
-      if (start) {
-        const uint32_t p = pnew;
+      if (!active && r < avail) {
+        const uint32_t p = next + r;
         sh_p[threadIdx.x] = p;
         active = true;
         const f3 dir = camera_dir<PT_PATH_MAD64, REFA, PT_PATH_CAM_RELOAD>(S, p, st.g);
@@ -1599,6 +1560,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
         st.flags = F_EXT | (1u << 8);
         ext = RayV{ld3(cam_of<PT_PATH_CAM_RELOAD>(S).origin), dir, __builtin_inff()};
       }
+      next += min((uint32_t)__popcll(idle), avail);
     }
     if (!__any(active)) {
       if (drained) break;
@@ -1652,25 +1614,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       const uint32_t done = ((st.flags >> 8) & 0xffu) - 1u;
       if (!(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || done >= (uint32_t)passes) {
         if constexpr (PT_PATH_LDS_SH) st.L = mk(Lq[0], Lq[TPB], Lq[2 * TPB]);
-        const uint32_t P = sh_p[threadIdx.x];
-        if constexpr (PT_PATH_BLOCKS) {
-          // the block's sum, left to right (pt_api.h PT_SAMPLE_BLOCK)
-          const uint32_t j = udiv_q(P, S.div_npix);
-          const uint32_t k = j & (PATH_UNIT - 1u);
-          f3 a = st.L;
-          if (k) a = mk(Aq[0] + st.L.x, Aq[TPB] + st.L.y, Aq[2 * TPB] + st.L.z);
-          if (k + 1u < PATH_UNIT && j + 1u < S.spp_c) {
-            Aq[0] = a.x;
-            Aq[TPB] = a.y;
-            Aq[2 * TPB] = a.z;
-            sh_p[threadIdx.x] = P | CONT_BIT;
-          } else {
-            // partial sum of block j / B of pixel q = P - j npix
-            put_res(S.ps1, (j / PATH_UNIT) * S.npix + (P - j * S.npix), a);
-          }
-        } else {
-          put_res(S.ps1, P, st.L);
-        }
+        put_res(S.ps1, sh_p[threadIdx.x], st.L);
         active = false;
       }
     }
@@ -1696,33 +1640,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
 
 // Sum each active pixel's samples of this batch into the accumulation buffer
 // (slot[q]: its owned slot; culled pixels add exact zeros, so they are not
-// touched), in blocks of PT_SAMPLE_BLOCK samples, the block sums in sample
-// order (pt_api.h; deterministic; replaces kernelUpdateSSImage +
-// kernelReconstructImage + kernelAccumulate, cu:666-742).  res holds one
-// radiance per path (P = j npix + q), or with `partial` one sum per block
-// (b npix + q, k_path_leaf).
+// touched), in sample order (deterministic; replaces kernelUpdateSSImage +
+// kernelReconstructImage + kernelAccumulate, cu:666-742).
 __global__ __launch_bounds__(TPB) void k_accum(const float4* __restrict__ ps1, float4* accum,
-                                               const uint32_t* __restrict__ slot, uint32_t npix, uint32_t spp_b,
-                                               uint32_t partial) {
+                                               const uint32_t* __restrict__ slot, uint32_t npix, uint32_t spp_b) {
   const uint32_t q = blockIdx.x * TPB + threadIdx.x;
   if (q >= npix) return;
   const uint32_t o = slot[q];
   float4 a = accum[o];
-  for (uint32_t j0 = 0, b = 0; j0 < spp_b; j0 += PT_SAMPLE_BLOCK, ++b) {
-    f3 p;
-    if (partial) {
-      p = get_res(ps1, (size_t)b * npix + q);
-    } else {
-      p = get_res(ps1, (size_t)j0 * npix + q);
-      const uint32_t j1 = min(spp_b, j0 + PT_SAMPLE_BLOCK);
-      for (uint32_t j = j0 + 1; j < j1; ++j) {
-        const f3 l = get_res(ps1, (size_t)j * npix + q);
-        p = mk(p.x + l.x, p.y + l.y, p.z + l.z);
-      }
-    }
-    a.x = a.x + p.x;
-    a.y = a.y + p.y;
-    a.z = a.z + p.z;
+  for (uint32_t j = 0; j < spp_b; ++j) {
+    const f3 l = get_res(ps1, (size_t)j * npix + q);
+    a.x = a.x + l.x;
+    a.y = a.y + l.y;
+    a.z = a.z + l.z;
   }
   accum[o] = a;
 }

@@ -1282,12 +1282,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   // chunks of spp_c samples of every owned pixel: M = npix * spp_c paths, each
   // path's radiance lands in res[j * npix + q] and is summed in sample order
   for (int done = 0; done < P->spp;) {
-    // (chunks hold whole PT_SAMPLE_BLOCK blocks: the block sums must not
-    // depend on where a frame's chunks end)
-    const uint32_t left = (uint32_t)(P->spp - done);
-    uint32_t spp_c = std::min<uint32_t>(std::max<uint32_t>(1, c->chunk_paths / npix), left);
-    if (spp_c < left) spp_c = std::max<uint32_t>(spp_c / PT_SAMPLE_BLOCK, 1u) * PT_SAMPLE_BLOCK;
-    spp_c = std::min(spp_c, left);
+    const uint32_t spp_c = std::min<uint32_t>(std::max<uint32_t>(1, c->chunk_paths / npix), (uint32_t)(P->spp - done));
     const uint32_t M = npix * spp_c;
     if ((size_t)M > c->res_cap) {
       if ((rc = dalloc(c, &c->d_res, M))) return rc;
@@ -1312,7 +1307,6 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.sample_base = (uint32_t)(P->sample_offset + done);
     S.res = c->d_res;
     S.M = M;
-    S.spp_c = spp_c;
     S.passes = passes;
     {  // record-order keys: SORT_KEYS equal primitive ranges (BVH order, so ~subtrees)
       uint32_t b = 0;
@@ -1328,8 +1322,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       S.ray = nullptr;
       S.ps0 = S.ps2 = S.ps3 = nullptr;
       S.ps1 = c->d_res;
-      // the pool hands out units: one pixel's block of PATH_UNIT samples
-      S.N = npix * ((spp_c + PATH_UNIT - 1) / PATH_UNIT);
+      S.N = M;
       const uint32_t want = (M + 4 * PATH_CHUNK - 1) / (4 * PATH_CHUNK);
       const int kv = (nsh == 2 ? 1 : 0) + (c->refa ? 2 : 0);
       const uint32_t blocks = std::min<uint32_t>(want, c->path_grid[kv]);
@@ -1528,10 +1521,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, Gc,
                            (const uint32_t*)c->d_pool, nblocks, c->d_live, c->d_stats + STAT_SHADED);
     }
-    // (k_path_leaf left one partial sum per block, the wavefront one radiance per path)
     c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_res,
-              c->d_accum, (const uint32_t*)c->d_act_slot, npix, spp_c,
-              (uint32_t)(c->root_leaf && PT_PATH_BLOCKS ? 1 : 0));
+              c->d_accum, (const uint32_t*)c->d_act_slot, npix, spp_c);
     HIPCHK(c, hipGetLastError());
     done += (int)spp_c;
     first = false;

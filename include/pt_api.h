@@ -288,17 +288,6 @@ int pt_set_camera(pt_ctx* ctx, const pt_camera* camera);
                                          emission BSDFs only (PT_E_UNSUPPORTED
                                          for spheres and glass)              */
 
-/* Summation order of a pixel's samples (part of the result's definition, so
- * that every path through the kernels and the CPU oracle give the same bits):
- * the samples of one pt_render call are summed in blocks of PT_SAMPLE_BLOCK
- * consecutive samples (the last block of a call may be shorter), each block
- * left to right, and the block sums are added to the pixel's running sum in
- * sample order -- ((acc + ((s0 + s1) + s2) + s3) + ((s4 + s5) + s6) + s7) ...
- * (cu:2419-2457 accumulates frame after frame likewise).  The blocks let the
- * single-leaf kernel sum a block in place and write one partial sum per
- * block instead of one radiance per path. */
-#define PT_SAMPLE_BLOCK 4
-
 typedef struct pt_render_params {
   int32_t width, height;
   int32_t spp;         /* samples per pixel rendered by this call             */

@@ -737,20 +737,12 @@ static void* worker(void* arg) {
     for (int r = ty * T; r < (ty + 1) * T && r < J->H; ++r)
       for (int c = tx * T; c < (tx + 1) * T && c < J->W; ++c) {
         uint32_t g = (uint32_t)(r * J->W + c);
-        /* blocks of PT_SAMPLE_BLOCK samples (pt_api.h): each block summed
-         * left to right, the block sums added in order */
         float ax = 0.0f, ay = 0.0f, az = 0.0f;
-        for (int b = 0; b < J->spp; b += PT_SAMPLE_BLOCK) {
-          v3 p = path_radiance(J, g, (uint32_t)(J->sample_offset + b), &nrays);
-          for (int s = b + 1; s < b + PT_SAMPLE_BLOCK && s < J->spp; ++s) {
-            v3 l = path_radiance(J, g, (uint32_t)(J->sample_offset + s), &nrays);
-            p.x = p.x + l.x;
-            p.y = p.y + l.y;
-            p.z = p.z + l.z;
-          }
-          ax = ax + p.x;
-          ay = ay + p.y;
-          az = az + p.z;
+        for (int s = 0; s < J->spp; ++s) {
+          v3 l = path_radiance(J, g, (uint32_t)(J->sample_offset + s), &nrays);
+          ax = ax + l.x;
+          ay = ay + l.y;
+          az = az + l.z;
         }
         float* px = J->img + (size_t)g * 4;
         px[0] = ax;
