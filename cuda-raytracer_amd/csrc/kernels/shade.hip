@@ -34,6 +34,12 @@ constexpr float REF_DIFFUSE_MULT = 0.3183f;  // BSDF_DIFFUSE_MULTIPLIER, cu:272
 constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
 constexpr int SHADE_REC = 5;  // float4 per hit-shading record (ShadeArgs::shade)
 constexpr uint32_t SHADE_SMOOTH = 1u << 27;  // shading-record meta bit: a triangle with distinct vertex normals
+// the diffuse sampling frame: Duff et al.'s branchless orthonormal basis and
+// the sampled direction left unnormalised (default arithmetic; 0: the
+// guide-vector frame and a normalised direction, rounds 1-3)
+#ifndef PT_ONB_DUFF
+#define PT_ONB_DUFF 1
+#endif
 // a flat triangle's shading record holds its normalised normal in the first
 // 16 B (host-computed, bit-identical to the device's normalize)
 #ifndef PT_FLAT_NS
@@ -458,6 +464,16 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           const f3 guide = (n.y <= 1e-4f) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
           dpdu = normalize(cross(guide, n));
           dpdv = normalize(cross(dpdu, n));
+        } else if (!REFA && PT_ONB_DUFF) {
+          // branchless orthonormal basis (Duff et al., JCGT 6(1), 2017):
+          // dpdu x dpdv = n; one reciprocal of sign(n.z) + n.z in [1, 2]
+          // instead of a cross product, a normalisation and a second cross
+          const float sg = __builtin_copysignf(1.0f, n.z);
+          const float a = -rcp_rn(sg + n.z);
+          const float b = (n.x * n.y) * a;
+          const float sx = sg * n.x;
+          dpdu = mk(__builtin_fmaf(sx * n.x, a, 1.0f), sg * b, -sx);
+          dpdv = mk(b, __builtin_fmaf(n.y * n.y, a, sg), -n.y);
         } else {
           const f3 guide = (fabsf(n.x) < 0.9f) ? mk(1.0f, 0.0f, 0.0f) : mk(0.0f, 1.0f, 0.0f);
           dpdu = normalize_u(cross(guide, n));  // (|cross|^2 >= 0.19)
@@ -511,7 +527,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
             x = r * cs;
             y = r * sn;
           }
-          if constexpr (REFA) {  // cu:631-637: not normalised
+          if (REFA || PT_ONB_DUFF) {  // cu:631-637: not normalised (the basis is orthonormal: |d_new| = 1 + O(ulp))
             d_new = mk(__builtin_fmaf(y, dpdv.x, __builtin_fmaf(x, dpdu.x, n.x * z)),
                        __builtin_fmaf(y, dpdv.y, __builtin_fmaf(x, dpdu.y, n.y * z)),
                        __builtin_fmaf(y, dpdv.z, __builtin_fmaf(x, dpdu.z, n.z * z)));

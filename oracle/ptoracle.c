@@ -616,6 +616,15 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
       v3 guide = ((double)n.y < 1e-4) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
       dpdu = nrm(cross(guide, n));
       dpdv = nrm(cross(dpdu, n));
+    } else if (!refa) {
+      /* branchless orthonormal basis (Duff et al., JCGT 6(1), 2017), shade.hip
+       * PT_ONB_DUFF */
+      float sg = copysignf(1.0f, n.z);
+      float a = -(1.0f / (sg + n.z));
+      float b = (n.x * n.y) * a;
+      float sx = sg * n.x;
+      dpdu = mk(fmaf(sx * n.x, a, 1.0f), sg * b, -sx);
+      dpdv = mk(b, fmaf(n.y * n.y, a, sg), -n.y);
     } else {
       v3 guide = (fabsf(n.x) < 0.9f) ? mk(1.0f, 0.0f, 0.0f) : mk(0.0f, 1.0f, 0.0f);
       dpdu = nrm(cross(guide, n));
@@ -654,11 +663,9 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
         x = rr * cs;
         y = rr * sn;
       }
-      if (refa) /* cu:631-637, not normalised */
-        dn = mk(fmaf(y, dpdv.x, fmaf(x, dpdu.x, n.x * z)), fmaf(y, dpdv.y, fmaf(x, dpdu.y, n.y * z)),
-                fmaf(y, dpdv.z, fmaf(x, dpdu.z, n.z * z)));
-      else
-        dn = nrm(mk(n.x * z + x * dpdu.x + y * dpdv.x, n.y * z + x * dpdu.y + y * dpdv.y, n.z * z + x * dpdu.z + y * dpdv.z));
+      /* cu:631-637, not normalised (the default basis is orthonormal) */
+      dn = mk(fmaf(y, dpdv.x, fmaf(x, dpdu.x, n.x * z)), fmaf(y, dpdv.y, fmaf(x, dpdu.y, n.y * z)),
+              fmaf(y, dpdv.z, fmaf(x, dpdu.z, n.z * z)));
       if (J->flags & PT_FLAG_COSINE_DIFFUSE) {
         T = mulv(T, alb);
       } else {
