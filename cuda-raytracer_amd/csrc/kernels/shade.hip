@@ -1289,6 +1289,11 @@ __global__ __launch_bounds__(TPB) void k_compact_wstate(uint4* wstate, uint32_t 
 #ifndef PT_PATH_STRICT
 #define PT_PATH_STRICT 1
 #endif
+// PT_PATH_PAIR: two primitive records per scalar round trip in the
+// single-leaf loops (default arithmetic; one wait and one loop step per pair)
+#ifndef PT_PATH_PAIR
+#define PT_PATH_PAIR 1
+#endif
 template <bool REFA, bool SPH = true>
 __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, int pcount, const RayV& r,
                                              uint32_t& prim, float& t) {
@@ -1296,7 +1301,23 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
   int bp = -1;
   constexpr int PS = prim_stride<REFA>();
   const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * PS);
-  for (int k = 0; k < pcount; ++k, P += PS) {
+  int k0 = 0;
+  if constexpr (PT_PATH_PAIR && PT_PATH_STRICT && !REFA) {
+    auto step = [&](const Prim& q, int k) {
+      const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1)
+                                                     : tri_test<REFA, true>(r.o, r.d, q, bt);
+      const bool take = (tt >= 0.0f) & (tt < bt);
+      bt = take ? tt : bt;
+      bp = take ? pstart + k : bp;
+    };
+    for (; k0 + 1 < pcount; k0 += 2, P += 2 * PS) {
+      Prim qa, qb;
+      load_prim_pair(P, qa, qb);
+      step(qa, k0);
+      step(qb, k0 + 1);
+    }
+  }
+  for (int k = k0; k < pcount; ++k, P += PS) {
     // the whole record in one scalar round trip (load_prim)
     const Prim q = load_prim<REFA>(P);
     // (a tri_outside pre-test does not pay here: extension rays of one wave
@@ -1327,7 +1348,28 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
   constexpr int PS = prim_stride<REFA>();
   const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * PS);
   bool hit = false;
-  for (int k = 0; k < pcount; ++k, P += PS) {
+  int k0 = 0;
+  if constexpr (PT_PATH_PAIR && PT_OCC_BITWISE && !REFA) {
+    auto test = [&](const Prim& q) {
+      float tt = -1.0f;
+      if (SPH && prim_sphere<REFA>(q)) {
+        tt = sphere_test(r.o, r.d, q.q0, q.q1);
+      } else {
+        float ndd, num;
+        plane_nd<REFA>(r.o, r.d, q, ndd, num);
+        if (!tri_outside<REFA>(ndd, num, r.tmax)) tt = tri_test<REFA>(r.o, r.d, q, r.tmax);
+      }
+      return (tt >= 0.0f) & (tt <= r.tmax);
+    };
+    for (; k0 + 1 < pcount; k0 += 2, P += 2 * PS) {
+      Prim qa, qb;
+      load_prim_pair(P, qa, qb);
+      hit = hit | test(qa);
+      hit = hit | test(qb);
+      if (__ballot(!hit) == 0ull) return hit;  // every active lane is occluded
+    }
+  }
+  for (int k = k0; k < pcount; ++k, P += PS) {
     const Prim q = load_prim<REFA>(P);
     float tt = -1.0f;
     if (SPH && prim_sphere<REFA>(q)) {

@@ -86,6 +86,20 @@ __device__ __forceinline__ Prim load_prim(const CPTR(f4v) P) {
   }
   return r;
 }
+// two consecutive records (default arithmetic) in one scalar round trip
+__device__ __forceinline__ void load_prim_pair(const CPTR(f4v) P, Prim& a, Prim& b) {
+  a.q0 = f4(P[0]);
+  a.q1 = f4(P[1]);
+  a.q2 = f4(P[2]);
+  a.q3 = f4(P[3]);
+  b.q0 = f4(P[4]);
+  b.q1 = f4(P[5]);
+  b.q2 = f4(P[6]);
+  b.q3 = f4(P[7]);
+  a.q4 = a.q5 = b.q4 = b.q5 = make_float4(0.f, 0.f, 0.f, 0.f);
+  asm volatile("" ::"s"(a.q0.x), "s"(a.q1.x), "s"(a.q2.x), "s"(a.q3.x), "s"(b.q0.x), "s"(b.q1.x), "s"(b.q2.x),
+               "s"(b.q3.x));
+}
 template <bool REFA>
 __device__ __forceinline__ bool prim_sphere(const Prim& q) {
   return !REFA && (__float_as_uint(q.q3.x) >> 28) == PT_PRIM_SPHERE;
