@@ -142,11 +142,12 @@ __device__ __forceinline__ f3 camera_dir(const ShadeArgs& S, uint32_t p, uint32_
   }
   // (sqrt_rn / div_rn / normalize_u give IEEE's bits here: len^2 >= 1, the
   // numerators are 0 or >= 2^-25 in magnitude, |dir| ~ 1)
-  float len = sqrt_rn(kx * kx + ky * ky + kz * kz);
+  float len = sqrt_rn(dot(mk(kx, ky, kz), mk(kx, ky, kz)));
   kx = div_rn(kx, len);
   ky = div_rn(ky, len);
   kz = div_rn(kz, len);
-  f3 dir = mk(kx * L.x + ky * U.x + kz * K.x, kx * L.y + ky * U.y + kz * K.y, kx * L.z + ky * U.z + kz * K.z);
+  const f3 k = mk(kx, ky, kz);
+  f3 dir = mk(dot(k, mk(L.x, U.x, K.x)), dot(k, mk(L.y, U.y, K.y)), dot(k, mk(L.z, U.z, K.z)));
   return normalize_u(dir);
 }
 
@@ -260,7 +261,9 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
   if (L.type == PT_LIGHT_AREA) {
     const float sx = ux - 0.5f, sy = uy - 0.5f;
     const f3 pos = ld3(L.position), dx = ld3(L.dim_x), dy = ld3(L.dim_y);
-    const f3 lpt = mk(pos.x + sx * dx.x + sy * dy.x, pos.y + sx * dx.y + sy * dy.y, pos.z + sx * dx.z + sy * dy.z);
+    const f3 lpt = mk(__builtin_fmaf(sy, dy.x, __builtin_fmaf(sx, dx.x, pos.x)),
+                      __builtin_fmaf(sy, dy.y, __builtin_fmaf(sx, dx.y, pos.y)),
+                      __builtin_fmaf(sy, dy.z, __builtin_fmaf(sx, dx.z, pos.z)));
     const f3 dv = lpt - pt;
     const float sq = dot(dv, dv);
     // (sqrt_rn / rcp_rn: IEEE's bits for sq >= 2^-96; a smaller sq fails
@@ -371,8 +374,8 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
   // 2. shade the hit of the extension ray
   if (flags & F_EXT) {
     if (prim != PT_PRIM_NONE) {
-      const f3 P = REFA ? mk(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z))
-                        : mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+      // (hit point and the offsets below as FMAs in both arithmetics)
+      const f3 P = mk(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z));
       // the record's first 16 B answer spheres ({centre, meta}) and flat
       // triangles ({n0, meta}); the rest is read only for a triangle with
       // distinct vertex normals (or the reference arithmetic's blend)
@@ -401,18 +404,15 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           float bA = length(cross(B - P, Cv - P)) / total;
           float bB = length(cross(Cv - P, A - P)) / total;
           const f3 bw = mk(bA, bB, bC);
-          ns = REFA ? normalize(mk(dot(bw, mk(n0.x, n1.x, n2.x)), dot(bw, mk(n0.y, n1.y, n2.y)),
-                                   dot(bw, mk(n0.z, n1.z, n2.z))))
-                    : normalize(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y,
-                                   bA * n0.z + bB * n1.z + bC * n2.z));
+          // (FMA chains in both arithmetics)
+          ns = normalize(mk(dot(bw, mk(n0.x, n1.x, n2.x)), dot(bw, mk(n0.y, n1.y, n2.y)),
+                            dot(bw, mk(n0.z, n1.z, n2.z))));
         }
       }
       const bool front = dot(ns, d) < 0.0f;
       const f3 n = front ? ns : mk(-ns.x, -ns.y, -ns.z);  // faces the incoming ray (cu:1222)
       // cu:1224 (its.pt += -r->d * 1e-3)
-      const f3 pt = REFA ? mk(__builtin_fmaf(-d.x, EPS, P.x), __builtin_fmaf(-d.y, EPS, P.y),
-                              __builtin_fmaf(-d.z, EPS, P.z))
-                         : P - d * EPS;
+      const f3 pt = mk(__builtin_fmaf(-d.x, EPS, P.x), __builtin_fmaf(-d.y, EPS, P.y), __builtin_fmaf(-d.z, EPS, P.z));
       pt_bsdf B = S.bsdfs[meta & 0x0FFFFFFFu];
       bool emitter = false;
       if (REFA) {
@@ -542,9 +542,8 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
             const f3 T0 = Tv();
             Tset(mk(((T0.x * c) * alb.x) * 2.0f, ((T0.y * c) * alb.y) * 2.0f, ((T0.z * c) * alb.z) * 2.0f));
           }
-          o_new = REFA ? mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y),
-                            __builtin_fmaf(n.z, EPS, pt.z))
-                       : pt + n * EPS;  // cu:593
+          o_new = mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y),
+                     __builtin_fmaf(n.z, EPS, pt.z));  // cu:593
           spec = 0;
         } else if (B.type == PT_BSDF_MIRROR) {
           if constexpr (REFA) {
@@ -560,7 +559,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           } else {
             const float dn = dot(d, n);
             d_new = normalize_u(d - n * (2.0f * dn));  // (unit d, n: |d_new| ~ 1)
-            o_new = pt + n * EPS;
+            o_new = mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y), __builtin_fmaf(n.z, EPS, pt.z));
           }
           Tset(mulv(Tv(), ld3(B.albedo)));
           spec = F_SPEC;
@@ -577,7 +576,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
             r0 = r0 * r0;
             const float c = front ? cosi : cost;
             const float m = 1.0f - c;
-            const float F = r0 + (1.0f - r0) * (((m * m) * (m * m)) * m);
+            const float F = __builtin_fmaf(1.0f - r0, ((m * m) * (m * m)) * m, r0);
             // u.x: a glass vertex takes no NEE sample, so the vertex's first
             // Philox word is free (no second Philox call in a divergent branch)
             refl = u01(u.x) < F;
@@ -586,11 +585,11 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
             const float dn = dot(d, n);
             d_new = normalize_u(d - n * (2.0f * dn));
             Tset(mulv(Tv(), ld3(B.albedo)));
-            o_new = pt + n * EPS;
+            o_new = mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y), __builtin_fmaf(n.z, EPS, pt.z));
           } else {
             d_new = normalize_u(d * eta + n * (eta * cosi - cost));  // (|.| ~ 1: Snell's refracted direction)
             Tset(mulv(Tv(), ld3(B.transmittance)));
-            o_new = P - n * EPS;
+            o_new = mk(__builtin_fmaf(-n.x, EPS, P.x), __builtin_fmaf(-n.y, EPS, P.y), __builtin_fmaf(-n.z, EPS, P.z));
           }
           spec = F_SPEC;
         }

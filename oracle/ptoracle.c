@@ -405,7 +405,8 @@ static int nee_sample(const pt_scene_desc* S, v3 T, v3 alb, v3 n, v3 pt, float u
   if (S->light.type == PT_LIGHT_AREA) {
     float sx = ux - 0.5f, sy = uy - 0.5f;
     v3 pos = ld3(S->light.position), dx = ld3(S->light.dim_x), dy = ld3(S->light.dim_y);
-    v3 lpt = mk(pos.x + sx * dx.x + sy * dy.x, pos.y + sx * dx.y + sy * dy.y, pos.z + sx * dx.z + sy * dy.z);
+    v3 lpt = mk(fmaf(sy, dy.x, fmaf(sx, dx.x, pos.x)), fmaf(sy, dy.y, fmaf(sx, dx.y, pos.y)),
+                fmaf(sy, dy.z, fmaf(sx, dx.z, pos.z)));
     v3 dv = sub(lpt, pt);
     float sq = dot(dv, dv);
     float dist = sqrtf(sq);
@@ -497,7 +498,7 @@ static v3 camera_dir(const pt_camera* cam, int W, int H, float ssx, float ssy, i
   float kx = ssy / (float)W - 0.5f;
   float ky = -(ssx / (float)H - 0.5f);
   float kz = 1.0f;
-  float len = sqrtf(kx * kx + ky * ky + kz * kz);
+  float len = sqrtf(fmaf(kz, kz, fmaf(ky, ky, kx * kx)));
   kx = kx / len;
   ky = ky / len;
   kz = kz / len;
@@ -507,7 +508,8 @@ static v3 camera_dir(const pt_camera* cam, int W, int H, float ssx, float ssy, i
     k = scl(k, 1.0f / len3(k));
     return mk(dot(k, mk(Lf.x, Up.x, K.x)), dot(k, mk(Lf.y, Up.y, K.y)), dot(k, mk(Lf.z, Up.z, K.z)));
   }
-  return nrm(mk(kx * Lf.x + ky * Up.x + kz * K.x, kx * Lf.y + ky * Up.y + kz * K.y, kx * Lf.z + ky * Up.z + kz * K.z));
+  v3 k = mk(kx, ky, kz);
+  return nrm(mk(dot(k, mk(Lf.x, Up.x, K.x)), dot(k, mk(Lf.y, Up.y, K.y)), dot(k, mk(Lf.z, Up.z, K.z))));
 }
 /* The camera ray of sensor point (ssx, ssy) as out[6] = o.xyz, d.xyz. */
 void pto_camera_ray(const pt_camera* cam, int W, int H, float ssx, float ssy, uint32_t flags, float* out) {
@@ -548,8 +550,8 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
     float t;
     memcpy(&t, &tb, 4);
     /* cu:1205 its.pt = r->o + r->d * t */
-    v3 P = refa ? mk(fmaf(d.x, t, o.x), fmaf(d.y, t, o.y), fmaf(d.z, t, o.z))
-                : mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+    /* hit point and offsets as FMAs in both arithmetics (shade.hip) */
+    v3 P = mk(fmaf(d.x, t, o.x), fmaf(d.y, t, o.y), fmaf(d.z, t, o.z));
     const float* q = S->prims[prim].q;
     uint32_t meta;
     memcpy(&meta, &q[3], 4);
@@ -568,19 +570,16 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
         float bC = len3(cross(sub(A, P), sub(B, P))) / total;
         float bA = len3(cross(sub(B, P), sub(Cv, P))) / total;
         float bB = len3(cross(sub(Cv, P), sub(A, P))) / total;
-        if (refa) { /* cu:1221 normalize(bA * n0 + bB * n1 + bC * n2) */
+        { /* cu:1221 normalize(bA * n0 + bB * n1 + bC * n2), FMA chains in both arithmetics */
           v3 bw = mk(bA, bB, bC);
           ns = nrm(mk(dot(bw, mk(n0.x, n1.x, n2.x)), dot(bw, mk(n0.y, n1.y, n2.y)), dot(bw, mk(n0.z, n1.z, n2.z))));
-        } else {
-          ns = nrm(mk(bA * n0.x + bB * n1.x + bC * n2.x, bA * n0.y + bB * n1.y + bC * n2.y,
-                      bA * n0.z + bB * n1.z + bC * n2.z));
         }
       }
     }
     int front = dot(ns, d) < 0.0f;
     v3 n = front ? ns : mk(-ns.x, -ns.y, -ns.z);
     /* cu:1224 its.pt += -r->d * 1e-3 */
-    v3 pt = refa ? mk(fmaf(-d.x, EPS, P.x), fmaf(-d.y, EPS, P.y), fmaf(-d.z, EPS, P.z)) : sub(P, scl(d, EPS));
+    v3 pt = mk(fmaf(-d.x, EPS, P.x), fmaf(-d.y, EPS, P.y), fmaf(-d.z, EPS, P.z));
     pt_bsdf Bv = S->bsdfs[meta & 0x0FFFFFFFu];
     const pt_bsdf* Bs = &Bv;
     int emitter = 0;
@@ -672,7 +671,7 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
         float c = fabsf(dot(dn, n));
         T = mk(((T.x * c) * alb.x) * 2.0f, ((T.y * c) * alb.y) * 2.0f, ((T.z * c) * alb.z) * 2.0f);
       }
-      on = refa ? mk(fmaf(n.x, EPS, pt.x), fmaf(n.y, EPS, pt.y), fmaf(n.z, EPS, pt.z)) : add(pt, scl(n, EPS)); /* cu:593 */
+      on = mk(fmaf(n.x, EPS, pt.x), fmaf(n.y, EPS, pt.y), fmaf(n.z, EPS, pt.z)); /* cu:593 */
       spec = 0;
       for (int k = 0; k < nee; ++k) {
         if (!have_sh[k]) continue;
@@ -692,7 +691,7 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
       } else {
         float dd = dot(d, n);
         dn = nrm(sub(d, scl(n, 2.0f * dd)));
-        on = add(pt, scl(n, EPS));
+        on = mk(fmaf(n.x, EPS, pt.x), fmaf(n.y, EPS, pt.y), fmaf(n.z, EPS, pt.z));
       }
       T = mulv(T, ld3(Bs->albedo));
       spec = 1;
@@ -709,18 +708,18 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
         r0 = r0 * r0;
         float c = front ? cosi : cost;
         float m = 1.0f - c;
-        float F = r0 + (1.0f - r0) * (((m * m) * (m * m)) * m);
+        float F = fmaf(1.0f - r0, ((m * m) * (m * m)) * m, r0);
         refl = u01(r.v[0]) < F; /* the vertex's first word: no NEE at glass */
       }
       if (refl) {
         float dd = dot(d, n);
         dn = nrm(sub(d, scl(n, 2.0f * dd)));
         T = mulv(T, ld3(Bs->albedo));
-        on = add(pt, scl(n, EPS));
+        on = mk(fmaf(n.x, EPS, pt.x), fmaf(n.y, EPS, pt.y), fmaf(n.z, EPS, pt.z));
       } else {
         dn = nrm(add(scl(d, eta), scl(n, eta * cosi - cost)));
         T = mulv(T, ld3(Bs->transmittance));
-        on = sub(P, scl(n, EPS));
+        on = mk(fmaf(-n.x, EPS, P.x), fmaf(-n.y, EPS, P.y), fmaf(-n.z, EPS, P.z));
       }
       spec = 1;
     }
