@@ -275,7 +275,7 @@ __device__ __forceinline__ f2v edge_ref2(const f3x2& N, const f3x2& P, const f3x
 
 // REFA: N normal, pd plane offset, v0..v2 vertices, e0..e2 edges (the
 // reference's operands, tri_test_ref); element i is tri_test_ref of ray i
-template <bool REFA = true>
+template <bool STRICT = false>
 __device__ __forceinline__ f2v tri_test2_ref(const f3x2& o, const f3x2& d, const f3x2& N, f2v pd, const f3x2& v0,
                                              const f3x2& v1, const f3x2& v2, const f3x2& m0, const f3x2& m1,
                                              const f3x2& m2, f2v tbest, f2v tlo = f2v{0.0f, 0.0f}) {
@@ -293,7 +293,8 @@ __device__ __forceinline__ f2v tri_test2_ref(const f3x2& o, const f3x2& d, const
   for (int i = 0; i < 2; ++i) {
     // non-short-circuit: every comparison is one v_cmp, combined on the SALU
     const bool flat = fabsf(ndd[i]) <= 1e-6f;
-    const bool miss = flat | (t[i] < tlo[i]) | (t[i] > tbest[i]) | (s0[i] < 0.0f) | (s1[i] < 0.0f) | (s2[i] < 0.0f);
+    const bool beyond = STRICT ? !(t[i] < tbest[i]) : (t[i] > tbest[i]);
+    const bool miss = flat | (t[i] < tlo[i]) | beyond | (s0[i] < 0.0f) | (s1[i] < 0.0f) | (s2[i] < 0.0f);
     r[i] = miss ? -1.0f : tz[i];
   }
   return r;
@@ -302,6 +303,7 @@ __device__ __forceinline__ f2v tri_test2_ref(const f3x2& o, const f3x2& d, const
 __device__ __forceinline__ f2v bw_plane2(const f3x2& o, const float4 R) {
   return fma2(sp(R.z), o.z, fma2(sp(R.y), o.y, fma2(sp(R.x), o.x, sp(R.w))));
 }
+template <bool STRICT = false>
 __device__ __forceinline__ f2v bw_test2(const f3x2& o, const f3x2& d, const float4 U, const float4 V, const float4 W,
                                         f2v tbest, f2v tlo) {
   const f2v nm = -bw_plane2(o, W), dn = fdot2(sp3(W.x, W.y, W.z), d);
@@ -313,23 +315,24 @@ __device__ __forceinline__ f2v bw_test2(const f3x2& o, const f3x2& d, const floa
   f2v r;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const bool miss = !(t[i] >= tlo[i]) | (t[i] > tbest[i]) | !(u[i] >= 0.0f) | !(v[i] >= 0.0f) | !(uv[i] <= 1.0f);
+    const bool beyond = STRICT ? !(t[i] < tbest[i]) : (t[i] > tbest[i]);
+    const bool miss = !(t[i] >= tlo[i]) | beyond | !(u[i] >= 0.0f) | !(v[i] >= 0.0f) | !(uv[i] <= 1.0f);
     r[i] = miss ? -1.0f : tz[i];
   }
   return r;
 }
 // Two rays (pair j, j + 1) against triangle q in the record's arithmetic.
-template <bool REFA>
+template <bool REFA, bool STRICT = false>
 __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const Prim& q, f2v tbest, f2v tlo) {
   if constexpr (REFA) {
     const float4 q0 = q.q0, q1 = q.q1, q2 = q.q2, q3 = q.q3, q4 = q.q4, q5 = q.q5;
-    return tri_test2_ref(o, d, sp3(q3.x, q3.y, q3.z), sp(q1.w), sp3(q0.x, q0.y, q0.z), sp3(q1.x, q1.y, q1.z),
+    return tri_test2_ref<STRICT>(o, d, sp3(q3.x, q3.y, q3.z), sp(q1.w), sp3(q0.x, q0.y, q0.z), sp3(q1.x, q1.y, q1.z),
                          sp3(q2.x, q2.y, q2.z), sp3(q2.w, q3.w, q4.w), sp3(q4.x, q4.y, q4.z),
                          sp3(q5.x, q5.y, q5.z), tbest, tlo);
   } else {
     float4 U, V;
     bw_uv(q, U, V);
-    return bw_test2(o, d, U, V, q.q2, tbest, tlo);
+    return bw_test2<STRICT>(o, d, U, V, q.q2, tbest, tlo);
   }
 }
 
@@ -352,6 +355,25 @@ __device__ __forceinline__ void take_hit(float t, int k, float& bt, int& bp) {
     bp = k;
   }
 #endif
+}
+
+// PT_LEVEL_STRICT (the level kernels' leaf loops): the running best starts one
+// ulp above the ray's tmax (the key's t from the leaves already visited) and
+// the triangle tests admit only t below it, so "t <= tmax, and a first hit at
+// t == tmax counts" becomes "t < best", every hit the test returns is a new
+// best, and the update is a compare and two selects.  The same hits as
+// take_hit: equal t within a leaf keeps the lower index (tested first), a
+// hit at the incoming tmax still reaches the key's atomicMin.
+#ifndef PT_LEVEL_STRICT
+#define PT_LEVEL_STRICT 1
+#endif
+__device__ __forceinline__ float next_up(float x) {  // (x >= 0, or negative for an empty lane: unchanged)
+  return x >= 0.0f && x < __builtin_inff() ? __uint_as_float(__float_as_uint(x) + 1u) : x;
+}
+__device__ __forceinline__ void take_strict(float t, int k, float& bt, int& bp) {
+  const bool take = (t >= 0.0f) & (t < bt);
+  bt = take ? t : bt;
+  bp = take ? k : bp;
 }
 
 // Ray-sphere (the reference has none: spheres are reinterpret_cast to
@@ -669,7 +691,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
     int bp[RPT];
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
-      bt[j] = tmax[j];
+      bt[j] = PT_LEVEL_STRICT ? next_up(tmax[j]) : tmax[j];
       bp[j] = -1;
     }
     constexpr int PS = prim_stride<REFA>();
@@ -680,16 +702,20 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {
           if (j >= nj) break;
-          take_hit(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
+          if constexpr (PT_LEVEL_STRICT) take_strict(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
+          else take_hit(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
         }
       } else {
 #pragma unroll
         for (int j = 0; j < RPT; j += 2) {
           if (j >= nj) break;
-          const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{bt[j], bt[j + 1]},
-                                         f2v{tlo[j], tlo[j + 1]});
+          const f2v t2 = tri_test2<REFA, PT_LEVEL_STRICT>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q,
+                                                          f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
-          for (int i = 0; i < 2; ++i) take_hit(t2[i], pstart + k, bt[j + i], bp[j + i]);
+          for (int i = 0; i < 2; ++i) {
+            if constexpr (PT_LEVEL_STRICT) take_strict(t2[i], pstart + k, bt[j + i], bp[j + i]);
+            else take_hit(t2[i], pstart + k, bt[j + i], bp[j + i]);
+          }
         }
       }
     }
@@ -914,7 +940,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     int bp[RPTW];
 #pragma unroll
     for (int j = 0; j < RPTW; ++j) {
-      bt[j] = tmax[j];
+      bt[j] = PT_LEVEL_STRICT ? next_up(tmax[j]) : tmax[j];
       bp[j] = -1;
     }
     constexpr int PS = prim_stride<REFA>();
@@ -927,16 +953,20 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 #pragma unroll
         for (int j = 0; j < RPTW; ++j) {
           if (j >= nj) break;
-          take_hit(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
+          if constexpr (PT_LEVEL_STRICT) take_strict(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
+          else take_hit(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
         }
       } else {
 #pragma unroll
         for (int j = 0; j < RPTW; j += 2) {
           if (j >= nj) break;
-          const f2v t2 = tri_test2<REFA>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{bt[j], bt[j + 1]},
-                                         f2v{tlo[j], tlo[j + 1]});
+          const f2v t2 = tri_test2<REFA, PT_LEVEL_STRICT>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q,
+                                                          f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
-          for (int i = 0; i < 2; ++i) take_hit(t2[i], pstart + k, bt[j + i], bp[j + i]);
+          for (int i = 0; i < 2; ++i) {
+            if constexpr (PT_LEVEL_STRICT) take_strict(t2[i], pstart + k, bt[j + i], bp[j + i]);
+            else take_hit(t2[i], pstart + k, bt[j + i], bp[j + i]);
+          }
         }
       }
     }
