@@ -47,6 +47,9 @@ constexpr uint32_t SHADE_SMOOTH = 1u << 27;  // shading-record meta bit: a trian
 #endif
 constexpr uint32_t ERR_KERNARG = 2u;  // pt_ctx::d_err bit: k_path_leaf's kernel-argument layout check failed
 
+// slot regions of the tail compaction (ShadeArgs::compact)
+constexpr uint32_t CREGIONS = 64;
+
 struct ShadeArgs {
   float4* ray;  // ray records (trace.h): ext ray of path p in slot p, shadow ray s in slot (1+s)N + p
   float4* ps0;  // T.xyz, flags | vertex << 8
@@ -88,9 +91,15 @@ struct ShadeArgs {
   uint32_t kmshift;
   // Tail compaction (pt_render): once every path of the chunk has started and
   // few slots are still live, one shade pass writes the continuing paths'
-  // state and new rays densely into a second set of buffers (slot from the
-  // counter *compact), and the passes after it launch ceil(n / 256)
-  // workgroups over slots [0, *nact) of that set.  A shade workgroup's time is
+  // state and new rays densely into a second set of buffers, and the passes
+  // after it launch ceil(n / 256) workgroups over slots [0, *nact) of that
+  // set.  The output slots come from CREGIONS counters, not one: workgroup b
+  // takes them from region b % CREGIONS, whose slots start at the sum of the
+  // lower regions' bounds creg[] (each region's live + unstarted paths after
+  // the last pass, k_live_sum: an upper bound on what it writes); one counter
+  // bumped by every workgroup cost a 73k-workgroup compaction pass 1.3 ms of
+  // serialised atomics.  What a region leaves of its bound is a hole of free
+  // slots (k_compact_slots).  A shade workgroup's time is
   // mostly a chain of dependent memory round trips, nearly the same for 20
   // live slots as for 256, so without this the tail's passes cost almost as
   // much as full ones.  The slots are read from the *_in buffers (and S.ray)
@@ -100,8 +109,9 @@ struct ShadeArgs {
   const float4* ps1_in;
   const float4* ps2_in;
   const float4* ps3_in;
-  uint32_t* compact;     // compaction pass: the output buffers' slot counter (zeroed); else null
-  const uint32_t* nact;  // after a compaction: the live slots are [0, *nact); else null ([0, N))
+  uint32_t* compact;     // compaction pass: the regions' slot counters (CREGIONS, zeroed); else null
+  const uint32_t* creg;  // compaction pass: the regions' slot bounds (k_live_sum)
+  const uint32_t* nact;  // after a compaction: paths are in slots [0, *nact); else null ([0, N))
   // dense pass (set by the host while the chunk has more than 2 N paths of
   // work left, i.e. nearly every slot is live): k_shade_push issues every
   // slot's loads at entry, in the same memory round trip as its workgroup's
@@ -912,8 +922,15 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
       const unsigned long long mc = __ballot(act && cont);
       const uint32_t wv = threadIdx.x >> 6;
       if ((threadIdx.x & 63) == 0) kc[0][wv] = (uint32_t)__popcll(mc);
+      if (wv == 0) {  // the region's first slot: the bounds of the regions below it
+        const uint32_t j = threadIdx.x & 63;
+        const uint32_t lo = wave_sum(j < (blockIdx.x & (CREGIONS - 1)) ? S.creg[j] : 0u);
+        if (j == 0) kc[1][1] = lo;
+      }
       __syncthreads();
-      if (threadIdx.x == 0) kc[1][0] = atomicAdd(S.compact, kc[0][0] + kc[0][1] + kc[0][2] + kc[0][3]);
+      if (threadIdx.x == 0)
+        kc[1][0] = kc[1][1] + atomicAdd(S.compact + (blockIdx.x & (CREGIONS - 1)),
+                                        kc[0][0] + kc[0][1] + kc[0][2] + kc[0][3]);
       __syncthreads();
       uint32_t base = kc[1][0];
       for (uint32_t w = 0; w < wv; ++w) base += kc[0][w];
@@ -1186,7 +1203,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     // compaction pass, extra round (uniform): every unstarted path of the
     // workgroup's block starts here, in consecutive slots of the compacted
     // layout (the dispensers are dry: after this no workgroup holds any)
-    if (tid == 0) s_nb = atomicAdd(S.compact, avail);
+    if (tid == 0) s_nb = s_kc[1][1] + atomicAdd(S.compact + (blockIdx.x & (CREGIONS - 1)), avail);
     __syncthreads();
     const bool st0 = (uint32_t)tid < avail;
     uint32_t id1[1] = {s_nb + (uint32_t)tid};
@@ -1210,19 +1227,27 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
 // workgroup's current block, and POOL_BLOCK paths for every block no
 // dispenser has handed out yet (the chunk's last block may hold fewer: an
 // upper bound); live[1] = the paths of the unclaimed blocks alone (0: the
-// dispensers are dry, the tail may be compacted); with stats, also the chunk's shaded
-// vertices (stats[STAT_SHADED]).  A grid of LIVE_SUM_BLOCKS workgroups, one
-// atomic each into the zeroed live[0..1].
+// dispensers are dry, the tail may be compacted); live[2 + k] = the live
+// slots and unstarted paths of the workgroups b with b % CREGIONS = k (the
+// compaction regions' bounds); with stats, also the chunk's shaded
+// vertices (stats[STAT_SHADED]).  A grid of LIVE_SUM_BLOCKS workgroups, a few
+// atomics each into the zeroed live[0 .. 2 + CREGIONS).
 constexpr int LIVE_SUM_BLOCKS = 64;
+static_assert(LIVE_SUM_BLOCKS * 1024 % CREGIONS == 0 && CREGIONS == 64, "k_live_sum: thread t sums region t % 64");
 __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wstate, uint32_t G, const uint32_t* pool,
                                                    uint32_t nblocks, uint32_t* live, unsigned long long* shaded) {
   __shared__ unsigned long long part[3][16];
+  __shared__ uint32_t reg[16][CREGIONS];
   unsigned long long v = 0, un = 0, sh = 0;
+  uint32_t vr = 0;  // (every b this thread visits has b % CREGIONS = threadIdx.x % CREGIONS)
   for (uint32_t b = blockIdx.x * 1024 + threadIdx.x; b < G; b += gridDim.x * 1024) {
     const uint4 w = wstate[b];
-    v += w.z + (w.y > w.x ? w.y - w.x : 0u);
+    const uint32_t n = w.z + (w.y > w.x ? w.y - w.x : 0u);
+    v += n;
+    vr += n;
     sh += w.w;
   }
+  reg[threadIdx.x >> 6][threadIdx.x & 63] = vr;
   if (blockIdx.x == 0 && threadIdx.x < POOLS) {
     const uint32_t lim = pool_limit(nblocks, threadIdx.x), c = pool[(size_t)threadIdx.x * CSTRIDE];
     un += c < lim ? (unsigned long long)(lim - c) * POOL_BLOCK : 0ull;
@@ -1247,14 +1272,18 @@ __global__ __launch_bounds__(1024) void k_live_sum(const uint4* __restrict__ wst
     if (n) atomicAdd(live + 1, (uint32_t)min(n, 0xFFFFFFFFull));
     if (shaded && u) atomicAdd(shaded, u);
   }
+  if (threadIdx.x < CREGIONS) {
+    uint32_t r = 0;
+    for (int w = 0; w < 16; ++w) r += reg[w][threadIdx.x];
+    if (r) atomicAdd(live + 2 + threadIdx.x, r);
+  }
 }
 
-// After a compaction pass: the shade workgroups' states for the compacted
-// layout (Gnew workgroups over slots [0, *nact), nothing left to start), the
-// old layout's shaded-vertex counts added to *shaded first (stats; may be
-// null).  One thread per workgroup state, max(Gold, Gnew) of them.
+// After a compaction pass, first: the old layout's shaded-vertex counts
+// added to *shaded (stats; may be null), and the states of its workgroups
+// beyond the new layout's Gnew cleared.  One thread per workgroup state.
 __global__ __launch_bounds__(TPB) void k_compact_wstate(uint4* wstate, uint32_t Gold, uint32_t Gnew,
-                                                        const uint32_t* nact, unsigned long long* shaded) {
+                                                        unsigned long long* shaded) {
   const uint32_t b = blockIdx.x * TPB + threadIdx.x;
   unsigned long long w = 0;
   if (b < Gold) w = wstate[b].w;
@@ -1262,13 +1291,39 @@ __global__ __launch_bounds__(TPB) void k_compact_wstate(uint4* wstate, uint32_t 
     w = wave_sum64(w);
     if ((threadIdx.x & 63) == 0 && w) atomicAdd(shaded, w);
   }
-  const uint32_t n = *nact;
-  if (b < Gnew) {
-    const uint32_t lo = b * TPB;
-    wstate[b] = make_uint4(0u, 0u, n > lo ? min((uint32_t)TPB, n - lo) : 0u, 0u);
-  } else if (b < Gold) {
-    wstate[b] = make_uint4(0u, 0u, 0u, 0u);
+  if (b >= Gnew && b < Gold) wstate[b] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// Then, one workgroup per workgroup of the compacted layout: region k holds
+// slots [lo_k, lo_k + creg[k]) (lo_k = the sum of the lower bounds), of which
+// the pass filled the first cnt[k]; the rest is a hole whose slots are marked
+// free (ps0 flags 0: the shade kernel reads nothing else of a free slot), and
+// the workgroup's state = nothing to start, its live slots.  Workgroup 0 also
+// writes the layout's extent (*nact = the sum of the bounds).
+__global__ __launch_bounds__(TPB) void k_compact_slots(float4* ps0, uint4* wstate, const uint32_t* cnt,
+                                                       const uint32_t* creg, uint32_t* nact) {
+  __shared__ uint32_t s_r[CREGIONS], s_lo[CREGIONS], s_n[TPB / 64];
+  if (threadIdx.x < CREGIONS) s_r[threadIdx.x] = creg[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x < CREGIONS) {
+    uint32_t lo = 0;
+    for (uint32_t j = 0; j < threadIdx.x; ++j) lo += s_r[j];
+    s_lo[threadIdx.x] = lo;
+    if (threadIdx.x == CREGIONS - 1 && blockIdx.x == 0) *nact = lo + s_r[threadIdx.x];
   }
+  __syncthreads();
+  const uint32_t q = blockIdx.x * TPB + threadIdx.x;
+  // the region of q: the last k with lo_k <= q (empty regions share their lo)
+  uint32_t k = 0;
+#pragma unroll
+  for (uint32_t st = CREGIONS / 2; st; st >>= 1) k = s_lo[k + st] <= q ? k + st : k;
+  const bool in = q < s_lo[k] + s_r[k];
+  const bool live = in && q < s_lo[k] + cnt[k];
+  if (in && !live) ps0[q] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+  const unsigned long long m = __ballot(live);
+  if ((threadIdx.x & 63) == 0) s_n[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) wstate[blockIdx.x] = make_uint4(0u, 0u, s_n[0] + s_n[1] + s_n[2] + s_n[3], 0u);
 }
 
 // ---- scenes whose BVH root is a leaf -----------------------------------------
