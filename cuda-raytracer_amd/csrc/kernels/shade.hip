@@ -117,7 +117,22 @@ struct ShadeArgs {
   // slot's loads at entry, in the same memory round trip as its workgroup's
   // wstate word, instead of after the barrier that shares the wstate
   uint32_t dense;
+  // diagnostic build only (PT_SHADE_TIMING=1, env PT_SHADE_TIMING): per-phase
+  // cycle sums of k_shade_push, 64 x 16 counters; else null
+  unsigned long long* tprof;
 };
+
+#ifndef PT_SHADE_TIMING
+#define PT_SHADE_TIMING 0
+#endif
+// k_shade_push phase stamps (PT_SHADE_TIMING): thread 0's s_memtime right
+// after the workgroup barriers that close each phase
+#if PT_SHADE_TIMING
+#define SHADE_STAMP(k) \
+  if (tid == 0) t_[k] = __builtin_amdgcn_s_memtime()
+#else
+#define SHADE_STAMP(k)
+#endif
 
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 __device__ __forceinline__ f3 xyz(float4 a) { return mk(a.x, a.y, a.z); }
@@ -1066,6 +1081,10 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   __shared__ float s_dir[3][TPB];
   __shared__ int s_skip, s_sparse;
   const int tid = threadIdx.x, wave = tid >> 6;
+#if PT_SHADE_TIMING
+  unsigned long long t_[8];
+#endif
+  SHADE_STAMP(0);
   const uint32_t nblocks = (S.M + POOL_BLOCK - 1) / POOL_BLOCK;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   SlotLoad<NSH> pre{z4, z4, z4, z4, z4, z4, z4, z4};
@@ -1082,6 +1101,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     s_sparse = ws.z < (uint32_t)PT_SPARSE_LIVE;
   }
   __syncthreads();
+  SHADE_STAMP(1);
   if (s_skip) {  // (uniform: every thread has read it before the barrier below)
     __syncthreads();
     if (wave == 0) {
@@ -1119,6 +1139,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     s_busy[wave] = (uint32_t)__popcll(mb);
   }
   __syncthreads();
+  SHADE_STAMP(2);
   const uint32_t nf = s_free[0] + s_free[1] + s_free[2] + s_free[3];
   const uint32_t next = s_next, end = s_end;
   const uint32_t avail = end > next ? end - next : 0u;
@@ -1147,6 +1168,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     }
   }
   __syncthreads();
+  SHADE_STAMP(3);
   // camera rays of the paths that start here, computed by the first ns threads
   // of the workgroup (whole waves, not one lane in four of every wave: the
   // camera code then runs in ceil(ns / 64) waves instead of all four), handed
@@ -1161,6 +1183,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     s_dir[2][tid] = dir.z;
   }
   __syncthreads();
+  SHADE_STAMP(4);
   if (fr) {
     uint32_t rank = mbcnt64(mf);
     for (int w = 0; w < wave; ++w) rank += s_free[w];
@@ -1199,6 +1222,19 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   }
   root_pass<1 + NSH, REFA>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh);
   count_rays(S.rcount, n, sh + MAX_ROOT_TARGETS * 8);
+#if PT_SHADE_TIMING
+  __syncthreads();
+  SHADE_STAMP(5);
+  if (tid == 0 && S.tprof) {
+    unsigned long long* tp = S.tprof + (blockIdx.x & 63) * 16;
+    for (int k = 1; k <= 5; ++k) atomicAdd(tp + k, t_[k] - t_[k - 1]);
+    atomicAdd(tp, 1ull);
+    atomicAdd(tp + 6, (unsigned long long)(s_live[0] + s_live[1] + s_live[2] + s_live[3]));
+    for (int k = 1; k <= 3; ++k) atomicAdd(tp + 6 + k, g_rp_t[k] - g_rp_t[k - 1]);
+    atomicAdd(tp + 10, g_rp_t[5] - g_rp_t[3]);
+    atomicAdd(tp + 11, t_[5] - g_rp_t[5]);
+  }
+#endif
   if (S.compact && avail) {
     // compaction pass, extra round (uniform): every unstarted path of the
     // workgroup's block starts here, in consecutive slots of the compacted

@@ -480,6 +480,24 @@ struct TableTargets {
   __device__ __forceinline__ int node(const TraceArgs&, int c) const { return T.tnode[c]; }
 };
 
+#ifndef PT_SHADE_TIMING
+#define PT_SHADE_TIMING 0
+#endif
+#if PT_SHADE_TIMING
+// diagnostic: thread 0's s_memtime after the root pass's stages (barriers
+// without a memory fence added in this build only, so stores in flight do not
+// count): inline leaves and record writes issued, target counts, reservations,
+// pushes
+static __shared__ unsigned long long g_rp_t[6];
+#define RP_STAMP(k)              \
+  __builtin_amdgcn_s_barrier();  \
+  if (threadIdx.x == 0) g_rp_t[k] = __builtin_amdgcn_s_memtime()
+__device__ __forceinline__ void g_rp_t_set(int k) { g_rp_t[k] = __builtin_amdgcn_s_memtime(); }
+#else
+#define RP_STAMP(k)
+__device__ __forceinline__ void g_rp_t_set(int) {}
+#endif
+
 // Block-wide push of R rays per thread into the queues of up to NC targets in
 // queue lane `lane`: slab tests, wave64 ballot compaction, one atomic slot
 // reservation per target for the whole workgroup, cross-wave offsets through
@@ -525,25 +543,29 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
     if ((tid & 63) == 0) sh[c * 4 + wave] = wc;
   }
   __syncthreads();
+  if (threadIdx.x == 0 && PT_SHADE_TIMING) g_rp_t_set(2);
   if (tid < nt) {
     const int c = tid;
     const int child = tg.node(A, c);
     uint32_t w0 = sh[c * 4 + 0], w1 = sh[c * 4 + 1], w2 = sh[c * 4 + 2], w3 = sh[c * 4 + 3];
     uint32_t tot = w0 + w1 + w2 + w3;
     uint32_t b = 0;
-    if (child >= 0 && tot) b = atomicAdd(A.cnt + cnt_idx(child, lane), tot);
+    // the queue's absolute offset is read here, in the round trip of the
+    // reservation, and folded into the bases (not after the barrier below)
+    if (child >= 0 && tot) b = atomicAdd(A.cnt + cnt_idx(child, lane), tot) + A.qoff[(size_t)child * NLANE + lane];
     sh[NC * 4 + c * 4 + 0] = b;
     sh[NC * 4 + c * 4 + 1] = b + w0;
     sh[NC * 4 + c * 4 + 2] = b + w0 + w1;
     sh[NC * 4 + c * 4 + 3] = b + w0 + w1 + w2;
   }
   __syncthreads();
+  if (threadIdx.x == 0 && PT_SHADE_TIMING) g_rp_t_set(3);
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     if (c >= nt) break;
     const int child = tg.node(A, c);
     if (child < 0) continue;
-    uint32_t off = sh[NC * 4 + c * 4 + wave] + A.qoff[(size_t)child * NLANE + lane];
+    uint32_t off = sh[NC * 4 + c * 4 + wave];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const bool h = (bits[j] >> c) & 1u;
@@ -575,6 +597,7 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
                                           const bool (&valid)[R], const bool (&anyhit)[R], uint32_t* sh) {
   float tm[R];
   bool pv[R];
+  RP_STAMP(0);
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     float bt = tmax[j];
@@ -631,7 +654,9 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
     tm[j] = bt;
     pv[j] = valid[j] && !(anyhit[j] && bp >= 0);
   }
+  RP_STAMP(1);
   push_children<R, MAX_ROOT_TARGETS>(A, TableTargets{T}, lane, id, o, d, tm, pv, R, sh, false);
+  RP_STAMP(5);
 }
 
 // LEAF: the node is known to be a leaf (the leaf-only level kernel): the

@@ -1390,6 +1390,14 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       S.compact = nullptr;
       S.creg = nullptr;
       S.nact = nullptr;
+      S.tprof = nullptr;
+#if PT_SHADE_TIMING
+      unsigned long long* d_tprof = nullptr;
+      if (getenv("PT_SHADE_TIMING") && hipMalloc((void**)&d_tprof, 1024 * 8) == hipSuccess) {
+        HIPCHK(c, hipMemset(d_tprof, 0, 1024 * 8));
+        S.tprof = d_tprof;
+      }
+#endif
       S.T = c->rt;
       const dim3 grid((N + TPB - 1) / TPB);
       // workgroup b of the shade grid runs its slots' share of the chunk
@@ -1525,6 +1533,21 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         continue;
       }
       if (!finished) return fail(c, PT_E_HIP, "paths did not finish within the pass bound");
+#if PT_SHADE_TIMING
+      if (d_tprof) {
+        unsigned long long h[1024], a[16] = {};
+        HIPCHK(c, hipMemcpy(h, d_tprof, sizeof(h), hipMemcpyDeviceToHost));
+        for (int i = 0; i < 1024; ++i) a[i % 16] += h[i];
+        const double n = a[0] ? (double)a[0] : 1.0;
+        fprintf(stderr,
+                "PT_SHADE_TIMING workgroup-passes %llu  cycles per workgroup-pass: wstate %.0f  shade %.0f  claim %.0f  "
+                "camera %.0f  root %.0f  (live slots per workgroup-pass %.1f); root: inline leaves + records %.0f  "
+                "target tests + counts %.0f  reservations %.0f  pushes %.0f  tail %.0f\n",
+                a[0], a[1] / n, a[2] / n, a[3] / n, a[4] / n, a[5] / n, a[6] / n, a[7] / n, a[8] / n, a[9] / n,
+                a[10] / n, a[11] / n);
+        hipFree(d_tprof);
+      }
+#endif
       c->ray_cur = nullptr;
       if (timed)  // shaded vertices of the chunk (stats only)
         hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, Gc,
