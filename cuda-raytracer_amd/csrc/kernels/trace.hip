@@ -587,6 +587,12 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 #ifndef PT_ROOT_EXT_PRETEST
 #define PT_ROOT_EXT_PRETEST 0
 #endif
+#ifndef PT_ROOT_PAIR
+#define PT_ROOT_PAIR 1
+#endif
+#ifndef PT_ROOT_RANGE_EARLY
+#define PT_ROOT_RANGE_EARLY 1
+#endif
 // (selects measured slower: CBbunny -2.4 %, dragon proxy -0.6 %, round 4)
 #ifndef PT_ROOT_SELECT
 #define PT_ROOT_SELECT 0
@@ -609,14 +615,15 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
                         __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
       const f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
       for (int i = 0; i < T.ni; ++i) {
-        if (!valid[j] || !box_hit(T.ib[0][i], T.ib[1][i], T.ib[2][i], T.ib[3][i], T.ib[4][i], T.ib[5][i], oi, inv,
-                                  bt))
-          continue;
-        const int pstart = T.istart[i];
+        // the leaf's primitive range in the round trip of its box (the
+        // compiler would read it behind the box test: two more round trips)
+        const int pstart = T.istart[i], pcount = T.icount[i];
+        const float b0 = T.ib[0][i], b1 = T.ib[1][i], b2 = T.ib[2][i], b3 = T.ib[3][i], b4 = T.ib[4][i], b5 = T.ib[5][i];
+        if constexpr (PT_ROOT_RANGE_EARLY) asm volatile("" ::"s"(pstart), "s"(pcount));
+        if (!valid[j] || !box_hit(b0, b1, b2, b3, b4, b5, oi, inv, bt)) continue;
         constexpr int PS = prim_stride<REFA>();
         const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * PS);
-        for (int kk = 0; kk < T.icount[i]; ++kk, P += PS) {
-          const Prim q = load_prim<REFA>(P);
+        auto test = [&](const Prim& q, int k) {
           float tt;
           if (prim_sphere<REFA>(q)) {
             tt = sphere_test(o[j], d[j], q.q0, q.q1, tlo);
@@ -635,14 +642,25 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
           if constexpr (PT_ROOT_SELECT) {
             // (as selects: no exec-mask branch per primitive; bp < 0 is the
             // largest unsigned value)
-            const bool take = (tt >= 0.0f) & ((tt < bt) | ((tt == bt) & ((uint32_t)(pstart + kk) < (uint32_t)bp)));
+            const bool take = (tt >= 0.0f) & ((tt < bt) | ((tt == bt) & ((uint32_t)(pstart + k) < (uint32_t)bp)));
             bt = take ? tt : bt;
-            bp = take ? pstart + kk : bp;
-          } else if (tt >= 0.0f && (tt < bt || (tt == bt && (bp < 0 || pstart + kk < bp)))) {
+            bp = take ? pstart + k : bp;
+          } else if (tt >= 0.0f && (tt < bt || (tt == bt && (bp < 0 || pstart + k < bp)))) {
             bt = tt;
-            bp = pstart + kk;
+            bp = pstart + k;
+          }
+        };
+        int kk = 0;
+        if constexpr (!REFA && PT_ROOT_PAIR) {
+          // two records per scalar round trip
+          for (; kk + 1 < pcount; kk += 2, P += 2 * PS) {
+            Prim qa, qb;
+            load_prim_pair(P, qa, qb);
+            test(qa, kk);
+            test(qb, kk + 1);
           }
         }
+        for (; kk < pcount; ++kk, P += PS) test(load_prim<REFA>(P), kk);
       }
     }
     if (valid[j]) {  // the whole 32-B record at once (one full half line per ray)
