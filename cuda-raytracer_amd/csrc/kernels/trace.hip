@@ -138,6 +138,27 @@ __device__ __forceinline__ float div_rn(float a, float b) {
   return __builtin_fmaf(r1, y1, q1);
 }
 // pt_check_division: div_rn over host-given pairs
+// pt_check_fast_math: every fp32 bit pattern x in [lo, hi) through sqrt_rn
+// (which = 0) or rcp_rn (which = 1) against the compiler's IEEE sqrtf / 1 / x;
+// out[0] += mismatches, out[1] = min mismatching pattern (zeroed / 0xFFFFFFFF by
+// the host)
+__global__ __launch_bounds__(TPB) void k_check_fast_math(int which, uint32_t lo, uint32_t hi, unsigned int* out) {
+  uint32_t bad = 0, first = 0xFFFFFFFFu;
+  for (uint64_t b = (uint64_t)lo + (uint64_t)blockIdx.x * TPB + threadIdx.x; b < hi; b += (uint64_t)gridDim.x * TPB) {
+    const float x = __uint_as_float((uint32_t)b);
+    const float f = which == 0 ? sqrt_rn(x) : rcp_rn(x);
+    const float r = which == 0 ? sqrtf(x) : 1.0f / x;
+    if (__float_as_uint(f) != __float_as_uint(r)) {
+      ++bad;
+      first = min(first, (uint32_t)b);
+    }
+  }
+  if (bad) {
+    atomicAdd(out, bad);
+    atomicMin(out + 1, first);
+  }
+}
+
 __global__ __launch_bounds__(TPB) void k_check_division(const float* __restrict__ a, const float* __restrict__ b,
                                                         float* __restrict__ q, uint32_t n) {
   const uint32_t i = blockIdx.x * TPB + threadIdx.x;

@@ -919,6 +919,26 @@ int pt_check_division(pt_ctx* c, const float* num, const float* den, float* q, i
   return rc;
 }
 
+int pt_check_fast_math(pt_ctx* c, int32_t which, uint32_t lo, uint32_t hi, uint64_t* mismatches,
+                       uint32_t* first_bad) {
+  if (!c || (which != 0 && which != 1) || hi < lo || !mismatches || !first_bad) return PT_E_INVALID;
+  unsigned int* d = nullptr;
+  HIPCHK(c, hipMalloc((void**)&d, 8));
+  const unsigned int init[2] = {0u, 0xFFFFFFFFu};
+  unsigned int h[2] = {0u, 0xFFFFFFFFu};
+  int rc = PT_OK;
+  if (hipMemcpy(d, init, 8, hipMemcpyHostToDevice) != hipSuccess) rc = fail(c, PT_E_HIP, "pt_check_fast_math: init");
+  if (rc == PT_OK && hi > lo) {
+    hipLaunchKernelGGL(k_check_fast_math, dim3(16384), dim3(TPB), 0, c->stream, (int)which, lo, hi, d);
+    if (hipStreamSynchronize(c->stream) != hipSuccess || hipMemcpy(h, d, 8, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = fail(c, PT_E_HIP, "pt_check_fast_math: kernel");
+  }
+  hipFree(d);
+  *mismatches = h[0];
+  *first_bad = h[1];
+  return rc;
+}
+
 int pt_device_count(int* n) {
   if (!n) return PT_E_INVALID;
   hipError_t e = hipGetDeviceCount(n);

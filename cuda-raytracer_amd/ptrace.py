@@ -118,7 +118,7 @@ API_SYMBOLS = [
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
     "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex", "pt_copy_owned_sums",
     "pt_get_stats", "pt_reset_stats", "pt_median_filter", "pt_get_display_image", "pt_tonemap",
-    "pt_write_png", "pt_write_pfm", "pt_check_division",
+    "pt_write_png", "pt_write_pfm", "pt_check_division", "pt_check_fast_math",
 ]
 
 
@@ -172,6 +172,7 @@ def _load():
         "pt_get_stats": (C.c_int, [P, C.POINTER(pt_stats)]),
         "pt_reset_stats": (C.c_int, [P]),
         "pt_check_division": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float), I32]),
+        "pt_check_fast_math": (C.c_int, [P, I32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -420,6 +421,14 @@ class Context:
         self._chk(LIB.pt_check_division(self.h, _ptr(num, C.c_float), _ptr(den, C.c_float), _ptr(q, C.c_float),
                                         len(num)))
         return q
+
+    def check_fast_math(self, which, lo, hi):
+        """(mismatches, first mismatching bit pattern or None) of sqrt_rn
+        (which 0) or rcp_rn (which 1) against IEEE over the fp32 bit patterns
+        [lo, hi), on the device (pt_check_fast_math)."""
+        n, first = C.c_uint64(0), C.c_uint32(0)
+        self._chk(LIB.pt_check_fast_math(self.h, int(which), int(lo), int(hi), C.byref(n), C.byref(first)))
+        return n.value, (None if first.value == 0xFFFFFFFF else first.value)
 
     def load_scene(self, scene: Scene):
         self._desc = scene.desc()

@@ -404,6 +404,14 @@ int pt_reset_stats(pt_ctx* ctx);
  * division. */
 int pt_check_division(pt_ctx* ctx, const float* num, const float* den, float* q, int32_t n);
 
+/* Self-check of the shading code's fast square root and reciprocal (no
+ * reference counterpart): every fp32 bit pattern x in [lo, hi) through
+ * sqrt_rn (which = 0) or rcp_rn (which = 1; ptmath.h), compared on the device
+ * with the IEEE sqrtf(x) / 1.0f / x; *mismatches = how many differ,
+ * *first_bad = the smallest such pattern (0xFFFFFFFF: none). */
+int pt_check_fast_math(pt_ctx* ctx, int32_t which, uint32_t lo, uint32_t hi, uint64_t* mismatches,
+                       uint32_t* first_bad);
+
 #ifdef __cplusplus
 }
 #endif

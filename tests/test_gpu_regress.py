@@ -240,6 +240,23 @@ def test_tail_compaction_matches_oracle(batch, monkeypatch):
                 ctx.close()
 
 
+def test_fast_sqrt_rcp_are_ieee(gpu_ctx):
+    """sqrt_rn and rcp_rn (ptmath.h: the hardware approximations plus one
+    correction, without the IEEE sequences' range scaling) give the IEEE
+    results bit for bit on every fp32 input of the ranges their call sites
+    are restricted to: sqrt_rn for 0 and every x >= 2^-96 up to +inf, rcp_rn
+    for |b| in [2^-100, 2^100] (exhaustive, ~1.9 G patterns each, on the
+    device against the compiler's correctly rounded sqrtf and 1/b).  Below
+    2^-96 sqrt_rn does differ (which is why the IEEE sequence pre-scales)."""
+    ok = [(0, 0x00000000, 0x00000001), (0, 0x0F800000, 0x7F800001),
+          (1, 0x0D800000, 0x71800001), (1, 0x8D800000, 0xF1800001)]
+    for which, lo, hi in ok:
+        n, first = gpu_ctx.check_fast_math(which, lo, hi)
+        assert n == 0, (which, hex(lo), hex(hi), n, hex(first))
+    n, _ = gpu_ctx.check_fast_math(0, 0x00800000, 0x0F800000)  # (normal inputs below 2^-96)
+    assert n > 0
+
+
 def test_triangle_test_division_is_ieee(gpu_ctx):
     """The Baldwin-Weber test divides without the IEEE sequence's range
     scaling and fixup (trace.hip div_rn): over 20 M operand pairs spanning the
