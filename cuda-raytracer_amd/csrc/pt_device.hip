@@ -390,6 +390,7 @@ static void build_root_table(pt_ctx* c) {
     box_row(T.ib, T.ni, nd[parent], k);
     T.istart[T.ni] = leaf.prim_start;
     T.icount[T.ni] = leaf.prim_count;
+    T.ninl += leaf.prim_count;
     T.ni++;
     budget -= leaf.prim_count;
     return true;
@@ -1562,9 +1563,10 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         fprintf(stderr,
                 "PT_SHADE_TIMING workgroup-passes %llu  cycles per workgroup-pass: wstate %.0f  shade %.0f  claim %.0f  "
                 "camera %.0f  root %.0f  (live slots per workgroup-pass %.1f); root: inline leaves + records %.0f  "
-                "target tests + counts %.0f  reservations %.0f  pushes %.0f  tail %.0f\n",
+                "target tests + counts %.0f  reservations %.0f  pushes %.0f  tail %.0f  (first ray's inline leaves "
+                "%.0f)\n",
                 a[0], a[1] / n, a[2] / n, a[3] / n, a[4] / n, a[5] / n, a[6] / n, a[7] / n, a[8] / n, a[9] / n,
-                a[10] / n, a[11] / n);
+                a[10] / n, a[11] / n, a[12] / n);
         hipFree(d_tprof);
       }
 #endif

@@ -18,7 +18,10 @@ files = {}
 for l in lines:
     m = re.match(r'\s*\.file\s+(\d+)\s+"([^"]*)"\s+"([^"]*)"', l)
     if m:
-        files[int(m.group(1))] = str(Path(m.group(2)) / m.group(3))
+        d = Path(m.group(2))
+        if not d.is_absolute() and 0 in files:  # (relative to the compilation directory, file 0's)
+            d = Path(files[0]).parent.parent.parent / d if files[0].endswith(".hip") else d
+        files[int(m.group(1))] = str(d / m.group(3))
 
 # function line ranges of the kernel sources
 FUNC_RE = re.compile(r'^(?:template\s*<[^>]*>\s*)?(?:__device__|__global__|static|inline|constexpr)[^;{(]*?\b([A-Za-z_]\w*)\s*\(')
