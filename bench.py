@@ -82,6 +82,12 @@ PMC_DIR = max((d for d in (ROOT / "profiles").glob("r[0-9][0-9]") if any(d.glob(
               default=ROOT / "profiles" / "r02")
 
 
+
+def _ordinal(n):
+    """2 -> '2nd', 11 -> '11th', 23 -> '23rd' (the CPU sample's tile stride)."""
+    suf = "th" if 10 <= n % 100 <= 20 else {1: "st", 2: "nd", 3: "rd"}.get(n % 10, "th")
+    return f"{n}{suf}"
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -216,7 +222,7 @@ def cpu_baseline(desc, args):
                                               seed=args.seed, tile_stride=stride, threads=ncpu)
     nt = len(range(0, ntiles, stride))
     out = {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": thr, "kind": "port",
-           "sample": f"{args.scene} {args.width}x{args.height}: {nt} of {ntiles} 32x32 tiles (every {stride}th), "
+           "sample": f"{args.scene} {args.width}x{args.height}: {nt} of {ntiles} 32x32 tiles (every {_ordinal(stride)}), "
                      f"{args.spp} spp, {args.bounces} bounces, through the Scotty3D PathTracer surface "
                      f"({thr} worker threads = the usable CPUs); {rays} rays in {dt:.1f} s",
            "hardware_concurrency": os.cpu_count()}

@@ -1027,6 +1027,11 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
   }
 }
 
+// PT_LEAF_PREFETCH: the wave-item leaf loop loads primitive k + 1's record
+// while it tests primitive k
+#ifndef PT_LEAF_PREFETCH
+#define PT_LEAF_PREFETCH 0
+#endif
 template <bool REFA = false, bool LEAF = false, bool TMIN = false>
 __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane, bool ids,
                                              bool out_ids, bool two_level) {
@@ -1064,8 +1069,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * PS);
     // one primitive's tests against the wave's rays (its record in SGPRs,
     // loaded in one scalar round trip)
-    for (int k = 0; k < pcount; ++k, P += PS) {
-      const Prim q = load_prim<REFA>(P);
+    auto leaf_test = [&](const Prim& q, int k) {
       if (prim_sphere<REFA>(q)) {
 #pragma unroll
         for (int j = 0; j < RPTW; ++j) {
@@ -1086,6 +1090,24 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
           }
         }
       }
+    };
+    if constexpr (PT_LEAF_PREFETCH && !REFA) {
+      // software-pipelined: the next record's scalar loads are issued before
+      // this one's tests, so they complete under them
+      Prim q = load_prim<REFA>(P);
+      for (int k = 0; k < pcount; ++k, P += PS) {
+        Prim qn = q;
+        if (k + 1 < pcount) {
+          qn.q0 = f4(P[PS]);
+          qn.q1 = f4(P[PS + 1]);
+          qn.q2 = f4(P[PS + 2]);
+          qn.q3 = f4(P[PS + 3]);
+        }
+        leaf_test(q, k);
+        q = qn;
+      }
+    } else {
+      for (int k = 0; k < pcount; ++k, P += PS) leaf_test(load_prim<REFA>(P), k);
     }
 #pragma unroll
     for (int j = 0; j < RPTW; ++j) {
