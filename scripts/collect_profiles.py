@@ -5,6 +5,7 @@ after scripts/profile_round.sh came back in gpurun_out/):
   python scripts/collect_profiles.py r02
 
 * bench_default.json                      the bench line (gpurun_out/bench.log)
+* bench_detail.json                       its detail side file (gpurun_out/bench_detail.json)
 * rocprof_kernel_stats_<scene>.csv        rocprofv3 --stats of one frame per workload
 * pmc_<scene>.json                        per-kernel PMC totals (scripts/pmc_summary.py)
 """
@@ -27,7 +28,12 @@ def main():
     if log.exists():
         line = [x for x in log.read_text().splitlines() if x.startswith("{")]
         if line:
-            (dst / "bench_default.json").write_text(json.dumps(json.loads(line[-1]), indent=1) + "\n")
+            rec = json.loads(line[-1])
+            det = OUT / "bench_detail.json"
+            if det.exists():  # the line's side file travels with it
+                shutil.copy(det, dst / "bench_detail.json")
+                rec["detail"] = f"profiles/{rnd}/bench_detail.json"
+            (dst / "bench_default.json").write_text(json.dumps(rec, indent=1) + "\n")
     for d in sorted(OUT.glob("prof_*")):
         if not d.is_dir():
             continue
