@@ -3,11 +3,12 @@ scotty/scotty_capi.cpp): CMU462::PathTracer's tile queue and worker threads
 over the GPU estimator (pathtracer.cpp:183-213, 499-558), and the progressive
 viewer loop of display.cpp:99-190 with CudaRenderer::renderAccumulate /
 setViewpoint (cu:1845-1870, 2419-2457).  Both must give exactly the frames the
-C ABI gives for the same work."""
+C ABI gives for the same work, and those equal the CPU oracle's frames."""
 import numpy as np
 import pytest
 
 import ptrace
+import pyoracle
 from conftest import load_fixture
 
 pytestmark = pytest.mark.gpu
@@ -24,6 +25,9 @@ def test_pathtracer_surface_matches_c_abi(gpu_ctx, threads):
     ref = gpu_ctx.get_image()
     assert np.array_equal(img, ref)
     assert img[..., :3].mean() > 0
+    # and the frame is the oracle's (not only the C ABI's)
+    o, _ = pyoracle.image(scene.desc(), W, H, 4, max_bounces=4)
+    assert np.array_equal(img, o)
 
 
 def _moved(cam, dx, dz):
@@ -52,6 +56,12 @@ def test_viewer_loop_matches_progressive_render(gpu_ctx, keys, frames_after_move
         gpu_ctx.render(W, H, spf, max_bounces=2, sample_offset=f * spf)
     ref = gpu_ctx.get_display_image()  # median filtered below 32 samples, like getImage
     assert np.array_equal(img, ref)
+    # the oracle's frame from the moved camera: the progressive frames sum the
+    # samples in order, as one render of all of them does
+    d = scene.desc()
+    d.camera = _moved(d.camera, dx, dz)
+    o, _ = pyoracle.image(d, W, H, spf * frames_after_move, max_bounces=2)
+    assert np.array_equal(img, pyoracle.median(o))
 
 
 def test_viewer_pause():
