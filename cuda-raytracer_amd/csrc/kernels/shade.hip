@@ -1091,10 +1091,6 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   if (S.dense) pre = load_slot<NSH>(S, blockIdx.x * TPB + tid < S.N ? blockIdx.x * TPB + tid : 0u);
   // slots [0, nin) hold paths (after a compaction fewer than N)
   const uint32_t nin = S.nact ? *S.nact : S.N;
-  // the root pass's inline primitives in LDS (read after the barrier below)
-  __shared__ float4 s_inl[INL_LDS_MAX * prim_stride<REFA>()];
-  stage_inline<REFA>(S.A, S.T, s_inl);
-  const float4* inl = inline_in_lds<REFA>(S.T) ? s_inl : nullptr;
   if (tid == 0) {
     const uint4 ws = S.wstate[blockIdx.x];
     s_next = ws.x;
@@ -1224,7 +1220,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     anyhit[1 + s] = true;
     n += new_sh[s] ? 1u : 0u;
   }
-  root_pass<1 + NSH, REFA>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh, inl);
+  root_pass<1 + NSH, REFA>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh);
   count_rays(S.rcount, n, sh + MAX_ROOT_TARGETS * 8);
 #if PT_SHADE_TIMING
   __syncthreads();
@@ -1258,7 +1254,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
       S.ps0[id1[0]] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
       S.ps1[id1[0]] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
     }
-    root_pass<1, REFA>(S.A, S.T, blockIdx.x & (NLANE - 1), id1, o1, d1, tm1, valid1, anyhit1, sh, inl);
+    root_pass<1, REFA>(S.A, S.T, blockIdx.x & (NLANE - 1), id1, o1, d1, tm1, valid1, anyhit1, sh);
     count_rays(S.rcount, st0 ? 1u : 0u, sh + MAX_ROOT_TARGETS * 8);
   }
 }

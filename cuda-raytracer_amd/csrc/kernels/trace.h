@@ -128,7 +128,6 @@ struct RootTable {
   int ibox[MAX_INLINE_LEAVES];     // parent * 4 + slot of the leaf's box
   int istart[MAX_INLINE_LEAVES];   // its primitives
   int icount[MAX_INLINE_LEAVES];
-  int ninl;                        // inline primitives in all (sum of icount)
   // the boxes themselves ({bmin_x, bmax_x, bmin_y, bmax_y, bmin_z, bmax_z}
   // rows), so the root pass reads them from the kernel arguments in a few wide
   // scalar loads instead of six dword loads per box from the node array

@@ -100,24 +100,6 @@ __device__ __forceinline__ void load_prim_pair(const CPTR(f4v) P, Prim& a, Prim&
   asm volatile("" ::"s"(a.q0.x), "s"(a.q1.x), "s"(a.q2.x), "s"(a.q3.x), "s"(b.q0.x), "s"(b.q1.x), "s"(b.q2.x),
                "s"(b.q3.x));
 }
-// a primitive's record from an LDS copy (uniform address: broadcast reads;
-// the meta word made wave-uniform for the sphere/triangle branch)
-template <bool REFA>
-__device__ __forceinline__ Prim load_prim_lds(const float4* P) {
-  Prim r;
-  r.q0 = P[0];
-  r.q1 = P[1];
-  r.q2 = P[2];
-  r.q3 = P[3];
-  r.q3.x = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(r.q3.x)));
-  if constexpr (REFA) {
-    r.q4 = P[4];
-    r.q5 = P[5];
-  } else {
-    r.q4 = r.q5 = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  return r;
-}
 template <bool REFA>
 __device__ __forceinline__ bool prim_sphere(const Prim& q) {
   return !REFA && (__float_as_uint(q.q3.x) >> 28) == PT_PRIM_SPHERE;
@@ -636,35 +618,10 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 #ifndef PT_ROOT_SELECT
 #define PT_ROOT_SELECT 0
 #endif
-// PT_ROOT_LDS: the ray producer has staged the inline primitives in LDS
-// (inl: their records in leaf order, stage_inline), read there instead of one
-// scalar round trip per primitive
-#ifndef PT_ROOT_LDS
-#define PT_ROOT_LDS 0
-#endif
-constexpr int INL_LDS_MAX = 32;  // inline primitives an LDS copy holds
-template <bool REFA>
-__device__ __forceinline__ bool inline_in_lds(const RootTable& T) {
-  return PT_ROOT_LDS && T.ni > 0 && T.ninl <= INL_LDS_MAX;
-}
-// Every thread of the workgroup: copy the inline primitives' records into
-// inl[INL_LDS_MAX * prim_stride] (a barrier must follow before root_pass)
-template <bool REFA>
-__device__ __forceinline__ void stage_inline(const TraceArgs& A, const RootTable& T, float4* inl) {
-  if (!inline_in_lds<REFA>(T)) return;
-  constexpr int PS = prim_stride<REFA>();
-  for (int w = threadIdx.x; w < T.ninl * PS; w += TPB) {
-    const int k = w / PS, r = w - k * PS;
-    int i = 0, cum = 0;
-    while (i + 1 < T.ni && k >= cum + T.icount[i]) cum += T.icount[i++];
-    inl[w] = A.prims[(size_t)(T.istart[i] + k - cum) * PS + r];
-  }
-}
 template <int R, bool REFA = false, bool TMIN = false>
 __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T, int lane, const uint32_t (&id)[R],
                                           const f3 (&o)[R], const f3 (&d)[R], const float (&tmax)[R],
-                                          const bool (&valid)[R], const bool (&anyhit)[R], uint32_t* sh,
-                                          const float4* inl = nullptr) {
+                                          const bool (&valid)[R], const bool (&anyhit)[R], uint32_t* sh) {
   float tm[R];
   bool pv[R];
   RP_STAMP(0);
@@ -678,15 +635,12 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
       const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
                         __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
       const f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
-      int cum = 0;  // (inline primitives of the leaves before leaf i)
       for (int i = 0; i < T.ni; ++i) {
         // the leaf's primitive range in the round trip of its box (the
         // compiler would read it behind the box test: two more round trips)
         const int pstart = T.istart[i], pcount = T.icount[i];
         const float b0 = T.ib[0][i], b1 = T.ib[1][i], b2 = T.ib[2][i], b3 = T.ib[3][i], b4 = T.ib[4][i], b5 = T.ib[5][i];
         if constexpr (PT_ROOT_RANGE_EARLY) asm volatile("" ::"s"(pstart), "s"(pcount));
-        const int cum_i = cum;
-        cum += pcount;
         if (!valid[j] || !box_hit(b0, b1, b2, b3, b4, b5, oi, inv, bt)) continue;
         constexpr int PS = prim_stride<REFA>();
         const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * PS);
@@ -718,10 +672,6 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
           }
         };
         int kk = 0;
-        if (inl) {  // (uniform)
-          for (; kk < pcount; ++kk) test(load_prim_lds<REFA>(inl + (size_t)(cum_i + kk) * PS), kk);
-          continue;
-        }
         if constexpr (!REFA && PT_ROOT_PAIR) {
           // two records per scalar round trip
           for (; kk + 1 < pcount; kk += 2, P += 2 * PS) {
@@ -1027,11 +977,6 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
   }
 }
 
-// PT_LEAF_PREFETCH: the wave-item leaf loop loads primitive k + 1's record
-// while it tests primitive k
-#ifndef PT_LEAF_PREFETCH
-#define PT_LEAF_PREFETCH 0
-#endif
 template <bool REFA = false, bool LEAF = false, bool TMIN = false>
 __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane, bool ids,
                                              bool out_ids, bool two_level) {
@@ -1091,24 +1036,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
         }
       }
     };
-    if constexpr (PT_LEAF_PREFETCH && !REFA) {
-      // software-pipelined: the next record's scalar loads are issued before
-      // this one's tests, so they complete under them
-      Prim q = load_prim<REFA>(P);
-      for (int k = 0; k < pcount; ++k, P += PS) {
-        Prim qn = q;
-        if (k + 1 < pcount) {
-          qn.q0 = f4(P[PS]);
-          qn.q1 = f4(P[PS + 1]);
-          qn.q2 = f4(P[PS + 2]);
-          qn.q3 = f4(P[PS + 3]);
-        }
-        leaf_test(q, k);
-        q = qn;
-      }
-    } else {
-      for (int k = 0; k < pcount; ++k, P += PS) leaf_test(load_prim<REFA>(P), k);
-    }
+    for (int k = 0; k < pcount; ++k, P += PS) leaf_test(load_prim<REFA>(P), k);
 #pragma unroll
     for (int j = 0; j < RPTW; ++j) {
 #ifdef PT_DBG_BOUNDS

@@ -390,7 +390,6 @@ static void build_root_table(pt_ctx* c) {
     box_row(T.ib, T.ni, nd[parent], k);
     T.istart[T.ni] = leaf.prim_start;
     T.icount[T.ni] = leaf.prim_count;
-    T.ninl += leaf.prim_count;
     T.ni++;
     budget -= leaf.prim_count;
     return true;
