@@ -169,13 +169,26 @@ __device__ __forceinline__ float bw_plane(const f3 o, const float4 W) {
 }
 // STRICT: a hit needs t < tbest (the caller's best so far, no hit yet at
 // tbest = +inf, which no hit reaches): then every hit returned is a new best
+// PT_BW_POINT (default; the oracle's form): u and v from the hit point
+#ifndef PT_BW_POINT
+#define PT_BW_POINT 1
+#endif
 template <bool STRICT = false>
 __device__ __forceinline__ float bw_test(const f3 o, const f3 d, const float4 U, const float4 V, const float4 W,
                                          float tbest, float tlo = 0.0f) {
   const float t = div_rn(-bw_plane(o, W), fdot(W.x, W.y, W.z, d.x, d.y, d.z));
   if (!(t >= tlo) | (STRICT ? !(t < tbest) : (t > tbest))) return -1.0f;
-  const float u = __builtin_fmaf(t, fdot(U.x, U.y, U.z, d.x, d.y, d.z), bw_plane(o, U));
-  const float v = __builtin_fmaf(t, fdot(V.x, V.y, V.z, d.x, d.y, d.z), bw_plane(o, V));
+  float u, v;
+  if constexpr (PT_BW_POINT) {
+    // barycentrics of the plane hit P = o + t d: U(P), V(P) (9 FMAs for
+    // both instead of 14 for U(o) + t U.d and V(o) + t V.d)
+    const f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
+    u = bw_plane(P, U);
+    v = bw_plane(P, V);
+  } else {
+    u = __builtin_fmaf(t, fdot(U.x, U.y, U.z, d.x, d.y, d.z), bw_plane(o, U));
+    v = __builtin_fmaf(t, fdot(V.x, V.y, V.z, d.x, d.y, d.z), bw_plane(o, V));
+  }
   // (unordered compares: a NaN u or v -- a ray parallel to the plane, t =
   // +-inf -- is a miss)
   const bool miss = !(u >= 0.0f) | !(v >= 0.0f) | !(u + v <= 1.0f);
@@ -329,8 +342,15 @@ __device__ __forceinline__ f2v bw_test2(const f3x2& o, const f3x2& d, const floa
                                         f2v tbest, f2v tlo) {
   const f2v nm = -bw_plane2(o, W), dn = fdot2(sp3(W.x, W.y, W.z), d);
   const f2v t = f2v{div_rn(nm[0], dn[0]), div_rn(nm[1], dn[1])};
-  const f2v u = fma2(t, fdot2(sp3(U.x, U.y, U.z), d), bw_plane2(o, U));
-  const f2v v = fma2(t, fdot2(sp3(V.x, V.y, V.z), d), bw_plane2(o, V));
+  f2v u, v;
+  if constexpr (PT_BW_POINT) {
+    const f3x2 P{fma2(t, d.x, o.x), fma2(t, d.y, o.y), fma2(t, d.z, o.z)};
+    u = bw_plane2(P, U);
+    v = bw_plane2(P, V);
+  } else {
+    u = fma2(t, fdot2(sp3(U.x, U.y, U.z), d), bw_plane2(o, U));
+    v = fma2(t, fdot2(sp3(V.x, V.y, V.z), d), bw_plane2(o, V));
+  }
   const f2v uv = u + v;
   const f2v tz = t + sp(0.0f);
   f2v r;

@@ -192,13 +192,15 @@ static float* bw_table(const pt_scene_desc* S) {
   return t;
 }
 static inline float bw_plane(const float* R, v3 o) { return fmaf(R[2], o.z, fmaf(R[1], o.y, fmaf(R[0], o.x, R[3]))); }
-/* t = -W(o) / W(d); a hit iff t >= tlo, u = U(o) + t U(d) >= 0, v >= 0, u + v <= 1
- * (trace.hip bw_test) */
+/* t = -W(o) / W(d); a hit iff t >= tlo and the plane hit P = o + t d (FMAs)
+ * has u = U(P) >= 0, v = V(P) >= 0, u + v <= 1 (trace.hip bw_test,
+ * PT_BW_POINT) */
 static float pto_tri(v3 o, v3 d, const float* M, float tlo) {
   const float t = -bw_plane(M + 8, o) / fdot(M[8], M[9], M[10], d.x, d.y, d.z);
   if (!(t >= tlo)) return -1.0f;
-  const float u = fmaf(t, fdot(M[0], M[1], M[2], d.x, d.y, d.z), bw_plane(M, o));
-  const float v = fmaf(t, fdot(M[4], M[5], M[6], d.x, d.y, d.z), bw_plane(M + 4, o));
+  const v3 P = mk(fmaf(t, d.x, o.x), fmaf(t, d.y, o.y), fmaf(t, d.z, o.z));
+  const float u = bw_plane(M, P);
+  const float v = bw_plane(M + 4, P);
   /* unordered compares: a NaN u or v (t = +-inf, a ray parallel to the plane) misses */
   if (!(u >= 0.0f) || !(v >= 0.0f) || !(u + v <= 1.0f)) return -1.0f;
   return t + 0.0f; /* (-0 -> +0) */
