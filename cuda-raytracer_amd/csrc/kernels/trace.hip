@@ -173,7 +173,9 @@ __device__ __forceinline__ float bw_plane(const f3 o, const float4 W) {
 #ifndef PT_BW_POINT
 #define PT_BW_POINT 1
 #endif
-template <bool STRICT = false>
+// ZFIX: a hit at t = -0 is returned as +0 (the {prim, t} keys order t by its
+// bits); false where t only feeds comparisons and the hit point
+template <bool STRICT = false, bool ZFIX = true>
 __device__ __forceinline__ float bw_test(const f3 o, const f3 d, const float4 U, const float4 V, const float4 W,
                                          float tbest, float tlo = 0.0f) {
   const float t = div_rn(-bw_plane(o, W), fdot(W.x, W.y, W.z, d.x, d.y, d.z));
@@ -192,7 +194,7 @@ __device__ __forceinline__ float bw_test(const f3 o, const f3 d, const float4 U,
   // (unordered compares: a NaN u or v -- a ray parallel to the plane, t =
   // +-inf -- is a miss)
   const bool miss = !(u >= 0.0f) | !(v >= 0.0f) | !(u + v <= 1.0f);
-  return miss ? -1.0f : t + 0.0f;  // (t + 0 maps -0 to +0)
+  return miss ? -1.0f : (ZFIX ? t + 0.0f : t);  // (t + 0 maps -0 to +0)
 }
 // PT_FLAG_REF_ARITH (REFA): the literal edge test of cu:251-267,
 // dot(N, cross(e_k, P - v_k)) < 0, on the reference-arithmetic primitive
@@ -242,14 +244,14 @@ __device__ __forceinline__ void bw_uv(const Prim& q, float4& U, float4& V) {
     V = q.q1;
   }
 }
-template <bool REFA, bool STRICT = false>
+template <bool REFA, bool STRICT = false, bool ZFIX = true>
 __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const Prim& q, float tbest, float tlo = 0.0f) {
   if constexpr (REFA) {
     return tri_test_ref<STRICT>(o, d, q.q0, q.q1, q.q2, q.q3, q.q4, q.q5, tbest, tlo);
   } else {
     float4 U, V;
     bw_uv(q, U, V);
-    return bw_test<STRICT>(o, d, U, V, q.q2, tbest, tlo);
+    return bw_test<STRICT, ZFIX>(o, d, U, V, q.q2, tbest, tlo);
   }
 }
 // The plane hit as t = num / ndd, for the division-free pre-test.
