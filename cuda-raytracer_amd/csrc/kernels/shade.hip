@@ -1445,6 +1445,11 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
 #ifndef PT_OCC_BITWISE
 #define PT_OCC_BITWISE 1
 #endif
+// PT_OCC_TRIM: the sphere-free kernel's occlusion loop takes its answer as a
+// bool from the test's own compares (bw_occludes), on the pre-test's num / ndd
+#ifndef PT_OCC_TRIM
+#define PT_OCC_TRIM 1
+#endif
 template <bool REFA, bool SPH = true>
 __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, int pcount, const RayV& r) {
   constexpr int PS = prim_stride<REFA>();
@@ -1452,7 +1457,14 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
   bool hit = false;
   int k0 = 0;
   if constexpr (PT_PATH_PAIR && PT_OCC_BITWISE && !REFA) {
-    auto test = [&](const Prim& q) {
+    auto test = [&](const Prim& q) -> bool {
+      if constexpr (PT_OCC_TRIM && !SPH && PT_BW_POINT) {
+        // (a bool straight from the test's compares, on the pre-test's
+        // num / ndd)
+        float ndd, num;
+        plane_nd<REFA>(r.o, r.d, q, ndd, num);
+        return !tri_outside<REFA>(ndd, num, r.tmax) && bw_occludes(r.o, r.d, q, num, ndd, r.tmax);
+      }
       float tt = -1.0f;
       if (SPH && prim_sphere<REFA>(q)) {
         tt = sphere_test(r.o, r.d, q.q0, q.q1);

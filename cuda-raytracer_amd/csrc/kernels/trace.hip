@@ -254,6 +254,18 @@ __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const Prim& q,
     return bw_test<STRICT, ZFIX>(o, d, U, V, q.q2, tbest, tlo);
   }
 }
+// Occlusion form of the Baldwin-Weber test (default arithmetic): true iff
+// tri_test(o, d, q, tmax) would return a t in [0, tmax], from the pre-test's
+// num and ndd (the same expressions bw_test evaluates, so the same bits)
+__device__ __forceinline__ bool bw_occludes(const f3 o, const f3 d, const Prim& q, float num, float ndd, float tmax) {
+  float4 U, V;
+  bw_uv(q, U, V);
+  const float t = div_rn(num, ndd);
+  if (!(t >= 0.0f) | (t > tmax)) return false;
+  const f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
+  const float u = bw_plane(P, U), v = bw_plane(P, V);
+  return (u >= 0.0f) & (v >= 0.0f) & (u + v <= 1.0f);
+}
 // The plane hit as t = num / ndd, for the division-free pre-test.
 template <bool REFA>
 __device__ __forceinline__ void plane_nd(const f3 o, const f3 d, const Prim& q, float& ndd, float& num) {
