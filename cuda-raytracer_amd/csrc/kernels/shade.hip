@@ -1391,6 +1391,11 @@ __global__ __launch_bounds__(TPB) void k_compact_slots(float4* ps0, uint4* wstat
 #ifndef PT_PATH_TRIM
 #define PT_PATH_TRIM 1
 #endif
+// PT_CLOSEST_DIRECT: with the trim, the hit update is made inside the test
+// (bw_closest_update) instead of through its -1 / t result
+#ifndef PT_CLOSEST_DIRECT
+#define PT_CLOSEST_DIRECT 1
+#endif
 template <bool REFA, bool SPH = true>
 __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, int pcount, const RayV& r,
                                              uint32_t& prim, float& t) {
@@ -1406,6 +1411,11 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
       // (the kernel with the sphere test compiled in keeps both: measured
       // -0.9 % on CBspheres with the trim)
       constexpr bool TRIM = PT_PATH_TRIM && !SPH;
+      if constexpr (TRIM && PT_BW_POINT && PT_CLOSEST_DIRECT) {
+        // the update straight from the test's compares (no -1 sentinel)
+        bw_closest_update(r.o, r.d, q, pstart + k, bt, bp);
+        return;
+      }
       const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1)
                                                      : tri_test<REFA, true, !TRIM>(r.o, r.d, q, bt);
       const bool take = TRIM ? (tt >= 0.0f) : ((tt >= 0.0f) & (tt < bt));

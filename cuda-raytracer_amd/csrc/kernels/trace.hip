@@ -254,6 +254,22 @@ __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const Prim& q,
     return bw_test<STRICT, ZFIX>(o, d, U, V, q.q2, tbest, tlo);
   }
 }
+// Closest-hit update form of the strict Baldwin-Weber test (default
+// arithmetic, tlo = 0): where tri_test<false, true>(o, d, q, bt) would return
+// t >= 0, bt = t and bp = idx (a -0 t is kept: for callers whose t only feeds
+// compares and the hit point)
+__device__ __forceinline__ void bw_closest_update(const f3 o, const f3 d, const Prim& q, int idx, float& bt, int& bp) {
+  float4 U, V;
+  bw_uv(q, U, V);
+  const float4 W = q.q2;
+  const float t = div_rn(-bw_plane(o, W), fdot(W.x, W.y, W.z, d.x, d.y, d.z));
+  if (!(t >= 0.0f) | !(t < bt)) return;
+  const f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
+  const float u = bw_plane(P, U), v = bw_plane(P, V);
+  const bool take = (u >= 0.0f) & (v >= 0.0f) & (u + v <= 1.0f);
+  bt = take ? t : bt;
+  bp = take ? idx : bp;
+}
 // Occlusion form of the Baldwin-Weber test (default arithmetic): true iff
 // tri_test(o, d, q, tmax) would return a t in [0, tmax], from the pre-test's
 // num and ndd (the same expressions bw_test evaluates, so the same bits)
