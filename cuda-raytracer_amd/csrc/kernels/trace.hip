@@ -392,6 +392,30 @@ __device__ __forceinline__ f2v bw_test2(const f3x2& o, const f3x2& d, const floa
   }
   return r;
 }
+// The strict two-ray test with the hit update inside (default arithmetic):
+// where tri_test2<false, true> would return t >= 0 for ray i, bt_i = t (-0 as
+// +0: the keys order t by its bits) and bp_i = idx
+#ifndef PT_LEVEL_DIRECT
+#define PT_LEVEL_DIRECT 1
+#endif
+__device__ __forceinline__ void bw_update2(const f3x2& o, const f3x2& d, const Prim& q, f2v tlo, int idx, float& bt0,
+                                           float& bt1, int& bp0, int& bp1) {
+  float4 U, V;
+  bw_uv(q, U, V);
+  const float4 W = q.q2;
+  const f2v nm = -bw_plane2(o, W), dn = fdot2(sp3(W.x, W.y, W.z), d);
+  const f2v t = f2v{div_rn(nm[0], dn[0]), div_rn(nm[1], dn[1])};
+  const f3x2 P{fma2(t, d.x, o.x), fma2(t, d.y, o.y), fma2(t, d.z, o.z)};
+  const f2v u = bw_plane2(P, U), v = bw_plane2(P, V);
+  const f2v uv = u + v;
+  const f2v tz = t + sp(0.0f);
+  const bool take0 = (t[0] >= tlo[0]) & (t[0] < bt0) & (u[0] >= 0.0f) & (v[0] >= 0.0f) & (uv[0] <= 1.0f);
+  const bool take1 = (t[1] >= tlo[1]) & (t[1] < bt1) & (u[1] >= 0.0f) & (v[1] >= 0.0f) & (uv[1] <= 1.0f);
+  bt0 = take0 ? tz[0] : bt0;
+  bp0 = take0 ? idx : bp0;
+  bt1 = take1 ? tz[1] : bt1;
+  bp1 = take1 ? idx : bp1;
+}
 // Two rays (pair j, j + 1) against triangle q in the record's arithmetic.
 template <bool REFA, bool STRICT = false>
 __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const Prim& q, f2v tbest, f2v tlo) {
@@ -826,6 +850,12 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 #pragma unroll
         for (int j = 0; j < RPT; j += 2) {
           if (j >= nj) break;
+          if constexpr (!REFA && PT_LEVEL_STRICT && PT_BW_POINT && PT_LEVEL_DIRECT) {
+            // (the update inside the test, no -1 sentinel)
+            bw_update2(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{tlo[j], tlo[j + 1]}, pstart + k, bt[j],
+                       bt[j + 1], bp[j], bp[j + 1]);
+            continue;
+          }
           const f2v t2 = tri_test2<REFA, PT_LEVEL_STRICT>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q,
                                                           f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
@@ -1076,6 +1106,12 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 #pragma unroll
         for (int j = 0; j < RPTW; j += 2) {
           if (j >= nj) break;
+          if constexpr (!REFA && PT_LEVEL_STRICT && PT_BW_POINT && PT_LEVEL_DIRECT) {
+            // (the update inside the test, no -1 sentinel)
+            bw_update2(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{tlo[j], tlo[j + 1]}, pstart + k, bt[j],
+                       bt[j + 1], bp[j], bp[j + 1]);
+            continue;
+          }
           const f2v t2 = tri_test2<REFA, PT_LEVEL_STRICT>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q,
                                                           f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
