@@ -1391,6 +1391,10 @@ __global__ __launch_bounds__(TPB) void k_compact_slots(float4* ps0, uint4* wstat
 #ifndef PT_PATH_TRIM
 #define PT_PATH_TRIM 1
 #endif
+// PT_CLOSEST_DIRECT_SPH: the same two for the triangles of the sphere kernel
+#ifndef PT_CLOSEST_DIRECT_SPH
+#define PT_CLOSEST_DIRECT_SPH 1
+#endif
 // PT_CLOSEST_DIRECT: with the trim, the hit update is made inside the test
 // (bw_closest_update) instead of through its -1 / t result
 #ifndef PT_CLOSEST_DIRECT
@@ -1415,6 +1419,13 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
         // the update straight from the test's compares (no -1 sentinel)
         bw_closest_update(r.o, r.d, q, pstart + k, bt, bp);
         return;
+      }
+      if constexpr (SPH && !REFA && PT_BW_POINT && PT_CLOSEST_DIRECT_SPH) {
+        // (the sphere kernel: triangles the same way, spheres as before)
+        if (!prim_sphere<REFA>(q)) {
+          bw_closest_update(r.o, r.d, q, pstart + k, bt, bp);
+          return;
+        }
       }
       const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1)
                                                      : tri_test<REFA, true, !TRIM>(r.o, r.d, q, bt);
@@ -1474,6 +1485,13 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
         float ndd, num;
         plane_nd<REFA>(r.o, r.d, q, ndd, num);
         return !tri_outside<REFA>(ndd, num, r.tmax) && bw_occludes(r.o, r.d, q, num, ndd, r.tmax);
+      }
+      if constexpr (SPH && !REFA && PT_BW_POINT && PT_CLOSEST_DIRECT_SPH) {
+        if (!prim_sphere<REFA>(q)) {
+          float ndd, num;
+          plane_nd<REFA>(r.o, r.d, q, ndd, num);
+          return !tri_outside<REFA>(ndd, num, r.tmax) && bw_occludes(r.o, r.d, q, num, ndd, r.tmax);
+        }
       }
       float tt = -1.0f;
       if (SPH && prim_sphere<REFA>(q)) {
