@@ -30,6 +30,9 @@ constexpr uint32_t F_SPEC = 4u;    // last scattering was specular
 constexpr uint32_t F_SHADOW2 = 8u; // second shadow ray pending in slot 2N + p (reference schedule)
 __device__ __forceinline__ uint32_t sh_bit(int s) { return s ? F_SHADOW2 : F_SHADOW; }
 constexpr float INV_PI = 0.318309886183790671f;
+#ifndef PT_INV_PI_SGPR
+#define PT_INV_PI_SGPR 1
+#endif
 constexpr float REF_DIFFUSE_MULT = 0.3183f;  // BSDF_DIFFUSE_MULTIPLIER, cu:272
 constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
 constexpr int SHADE_REC = 5;  // float4 per hit-shading record (ShadeArgs::shade)
@@ -301,7 +304,11 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
     if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
       // cosn / pdf with pdf = sq / (area * -cosl) (solid-angle pdf of the
       // light sample), as one division
-      float scale = ((cosn * (L.area * -cosl)) / sq) * INV_PI;
+      // (1/pi from an SGPR: as a literal the compiler paired it with another
+      // product in a v_pk_mul_f32 and spilled the VGPR pair holding it)
+      float inv_pi = INV_PI;
+      if constexpr (PT_INV_PI_SGPR) asm volatile("" : "+s"(inv_pi));
+      float scale = ((cosn * (L.area * -cosl)) / sq) * inv_pi;
       if (weight >= 0.0f) scale = scale * weight;
       C = mulv(mulv(T, alb), ld3(L.radiance)) * scale;
       r.o = pt;
