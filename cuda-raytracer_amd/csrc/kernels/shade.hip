@@ -30,6 +30,9 @@ constexpr uint32_t F_SPEC = 4u;    // last scattering was specular
 constexpr uint32_t F_SHADOW2 = 8u; // second shadow ray pending in slot 2N + p (reference schedule)
 __device__ __forceinline__ uint32_t sh_bit(int s) { return s ? F_SHADOW2 : F_SHADOW; }
 constexpr float INV_PI = 0.318309886183790671f;
+#ifndef PT_RNG_EARLY
+#define PT_RNG_EARLY 1
+#endif
 #ifndef PT_INV_PI_SGPR
 #define PT_INV_PI_SGPR 1
 #endif
@@ -413,6 +416,11 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
       // distinct vertex normals (or the reference arithmetic's blend)
       const float4* Q = S.shade + (size_t)prim * SHADE_REC;
       const float4 q0 = Q[0];
+      // PT_RNG_EARLY: the vertex's Philox words are computed while the
+      // shading record's first load is in flight (they depend on the path
+      // and vertex only)
+      u4 u_early{0u, 0u, 0u, 0u};
+      if constexpr (PT_RNG_EARLY) u_early = rng<M64>(S.seed, g, sidx, vtx, 0);
       const uint32_t meta = __float_as_uint(q0.w) & ~SHADE_SMOOTH;
       f3 ns;
       if ((meta >> 28) == PT_PRIM_SPHERE) {
@@ -488,7 +496,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           }
         }
       } else {
-        const u4 u = rng<M64>(S.seed, g, sidx, vtx, 0);
+        const u4 u = PT_RNG_EARLY ? u_early : rng<M64>(S.seed, g, sidx, vtx, 0);
         f3 dpdu, dpdv;
         if (S.flags & PT_FLAG_REF_GUIDE) {
           // reference quirk (ii): cu:572-574 (NaN when n is (0,-1,0)); n.y <
