@@ -12,8 +12,7 @@
 // accumulator (a miss keeps the light gathered so far); orthonormal frame with
 // a guide that cannot be parallel to n; counter-based Philox streams instead of
 // curand XORWOW; glass, spheres and point lights; parametric bounce count; and
-// in the default arithmetic: normalised camera / BSDF directions, the
-// normalised light cosine (cu:422 uses the unnormalised direction), a
+// in the default arithmetic: normalised camera / BSDF directions, a
 // one-sided emitter (cosl < -0.01: lights emit along their direction; cu:440
 // tests |cosTheta|), NEE only toward the front of the shading normal (cu:429
 // takes |n.w|), 1/pi = 0.3183099 (cu:272: 0.3183), the flat-triangle normal
@@ -302,16 +301,21 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
     const float dist = sqrt_rn(sq);
     const float inv = rcp_rn(dist);
     const f3 w = mk(dv.x * inv, dv.y * inv, dv.z * inv);
-    const float cosl = dot(w, ld3(L.direction));
+    // AreaLight::sample_L (light.cpp:81-92): cosTheta = dot(d, direction) of
+    // the UNnormalised d, pdf = sqDist / (area |cosTheta|), radiance only when
+    // cosTheta < 0 (one-sided); the pdf is the solid-angle pdf times dist.
+    // PT_FLAG_EXACT_LIGHT_PDF takes the normalised cosine instead.
+    const float cu = dot(dv, ld3(L.direction));
+    const float cosl = cu * inv;
     const float cosn = dot(n, w);
     if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
-      // cosn / pdf with pdf = sq / (area * -cosl) (solid-angle pdf of the
-      // light sample), as one division
+      // cosn / pdf with pdf = sq / (area * -cosTheta), as one division
       // (1/pi from an SGPR: as a literal the compiler paired it with another
       // product in a v_pk_mul_f32 and spilled the VGPR pair holding it)
       float inv_pi = INV_PI;
       if constexpr (PT_INV_PI_SGPR) asm volatile("" : "+s"(inv_pi));
-      float scale = ((cosn * (L.area * -cosl)) / sq) * inv_pi;
+      const float lc = (S.flags & PT_FLAG_EXACT_LIGHT_PDF) ? cosl : cu;
+      float scale = ((cosn * (L.area * -lc)) / sq) * inv_pi;
       if (weight >= 0.0f) scale = scale * weight;
       C = mulv(mulv(T, alb), ld3(L.radiance)) * scale;
       r.o = pt;

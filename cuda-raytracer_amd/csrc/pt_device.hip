@@ -939,6 +939,8 @@ int pt_check_fast_math(pt_ctx* c, int32_t which, uint32_t lo, uint32_t hi, uint6
   return rc;
 }
 
+int pt_api_version(void) { return PT_API_VERSION; }
+
 int pt_device_count(int* n) {
   if (!n) return PT_E_INVALID;
   hipError_t e = hipGetDeviceCount(n);

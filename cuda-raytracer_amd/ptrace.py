@@ -35,6 +35,8 @@ PT_FLAG_REF_DROP_ON_MISS = 0x8   # reference quirk (i)
 PT_FLAG_REF_GUIDE = 0x10         # reference quirk (ii)
 PT_FLAG_REF_SCHEDULE = 0x20      # reference quirk (vi): 2 bounces, NEE 2/2/1 weighted 0.5/0.5/1
 PT_FLAG_REF_ARITH = 0x40         # the reference kernels' literal arithmetic (pt_api.h)
+PT_FLAG_EXACT_LIGHT_PDF = 0x80   # area-light NEE with the normalised cosine (default: light.cpp:81-92)
+PT_API_VERSION = 2
 PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION, PT_BSDF_REFRACTION = 0, 1, 2, 3, 4
 PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT = 0, 1, 2
 PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1
@@ -113,7 +115,7 @@ class pt_mesh_desc(C.Structure):
 
 # every symbol include/pt_api.h declares (tests check the library exports them)
 API_SYMBOLS = [
-    "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_from_mesh_ex", "pt_scene_build_gpu", "pt_scene_build_gpu_ex", "pt_scene_camera_scotty", "pt_scene_free", "pt_scene_get_desc",
+    "pt_api_version", "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_from_mesh_ex", "pt_scene_build_gpu", "pt_scene_build_gpu_ex", "pt_scene_camera_scotty", "pt_scene_free", "pt_scene_get_desc",
     "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
     "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex", "pt_copy_owned_sums",
@@ -137,6 +139,7 @@ def _load():
     lib = C.CDLL(str(LIB_PATH))
     P, I32, U32, SZ = C.c_void_p, C.c_int32, C.c_uint32, C.c_size_t
     sigs = {
+        "pt_api_version": (C.c_int, []),
         "pt_scene_load_dae": (C.c_int, [C.c_char_p, C.POINTER(P), C.c_char_p, SZ]),
         "pt_scene_from_triangles": (C.c_int, [C.POINTER(C.c_float), I32, C.POINTER(pt_bsdf),
                                               C.POINTER(pt_light), C.POINTER(pt_camera), C.POINTER(P)]),
@@ -178,6 +181,8 @@ def _load():
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+    if lib.pt_api_version() != PT_API_VERSION:
+        raise ImportError(f"libptcore.so has API version {lib.pt_api_version()}, this binding {PT_API_VERSION}")
     return lib
 
 

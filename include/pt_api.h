@@ -48,7 +48,11 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 1
+/* 2: pt_bsdf grew `roughness` (36 B), pt_stats `culled_rays` (round 4);
+ * PT_FLAG_EXACT_LIGHT_PDF and the light.cpp pdf as the default (round 5).
+ * A client checks pt_api_version() == PT_API_VERSION before passing structs. */
+#define PT_API_VERSION 2
+int pt_api_version(void);
 
 /* ---- error codes ---------------------------------------------------------- */
 #define PT_OK 0
@@ -249,7 +253,7 @@ int pt_load_scene(pt_ctx* ctx, const pt_scene_desc* scene);
 /* PT_E_UNSUPPORTED when the origin lies beyond 64 x the scene's largest
  * coordinate magnitude M (vertices, sphere extents, the scene's camera and
  * light): the stored boxes' guard band keeps the fp32 box test conservative
- * only for origins within ~22 M.  pt_intersect applies the same bound to its
+ * for origins within ~180 M.  pt_intersect applies the same bound to its
  * ray origins. */
 int pt_set_camera(pt_ctx* ctx, const pt_camera* camera);
 
@@ -287,6 +291,14 @@ int pt_set_camera(pt_ctx* ctx, const pt_camera* camera);
                                          Triangles with diffuse / mirror /
                                          emission BSDFs only (PT_E_UNSUPPORTED
                                          for spheres and glass)              */
+/* The default NEE toward an area light uses the reference's light pdf,
+ * AreaLight::sample_L (light.cpp:81-92, also cu:422-430): pdf = sqDist /
+ * (area * |dot(d, direction)|) with d the UNnormalised vector to the light
+ * sample, i.e. the solid-angle pdf times the distance.  The reference's own
+ * renders (media/pathtracer/reference_results) follow it (tests/
+ * test_gpu_reference_renders.py).  This flag takes the normalised cosine,
+ * the unbiased estimator of the irradiance, instead.                         */
+#define PT_FLAG_EXACT_LIGHT_PDF 0x80u
 
 typedef struct pt_render_params {
   int32_t width, height;
@@ -414,5 +426,17 @@ int pt_check_fast_math(pt_ctx* ctx, int32_t which, uint32_t lo, uint32_t hi, uin
 
 #ifdef __cplusplus
 }
+#define PT_STATIC_ASSERT static_assert
+#else
+#define PT_STATIC_ASSERT _Static_assert
 #endif
+/* the record layouts of PT_API_VERSION 2 */
+PT_STATIC_ASSERT(sizeof(pt_prim) == 96, "pt_prim layout");
+PT_STATIC_ASSERT(sizeof(pt_node) == 128, "pt_node layout");
+PT_STATIC_ASSERT(sizeof(pt_bsdf) == 36, "pt_bsdf layout");
+PT_STATIC_ASSERT(sizeof(pt_light) == 76, "pt_light layout");
+PT_STATIC_ASSERT(sizeof(pt_camera) == 48, "pt_camera layout");
+PT_STATIC_ASSERT(sizeof(pt_render_params) == 44, "pt_render_params layout");
+PT_STATIC_ASSERT(sizeof(pt_stats) == 920, "pt_stats layout");
+#undef PT_STATIC_ASSERT
 #endif /* PT_API_H */

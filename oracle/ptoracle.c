@@ -401,8 +401,8 @@ static uint64_t trace(const job_t* J, v3 o, v3 d, float tmax) {
 /* One NEE sample toward the scene light, kernelDirectLightRays cu:380-481.
  * weight < 0: unweighted (default schedule); else the reference schedule's
  * per-sample weight (cu:2515-2533). */
-static int nee_sample(const pt_scene_desc* S, v3 T, v3 alb, v3 n, v3 pt, float ux, float uy, float weight, v3* C,
-                      v3* sw, float* stmax) {
+static int nee_sample(const pt_scene_desc* S, uint32_t flags, v3 T, v3 alb, v3 n, v3 pt, float ux, float uy,
+                      float weight, v3* C, v3* sw, float* stmax) {
   const float INV_PI = 0.318309886183790671f, EPS = 1e-3f;
   if (S->light.type == PT_LIGHT_AREA) {
     float sx = ux - 0.5f, sy = uy - 0.5f;
@@ -414,11 +414,16 @@ static int nee_sample(const pt_scene_desc* S, v3 T, v3 alb, v3 n, v3 pt, float u
     float dist = sqrtf(sq);
     float inv = 1.0f / dist;
     v3 w = mk(dv.x * inv, dv.y * inv, dv.z * inv);
-    float cosl = dot(w, ld3(S->light.direction));
+    /* AreaLight::sample_L, light.cpp:81-92: cosTheta = dot(d, direction) of
+     * the unnormalised d, pdf = sqDist / (area |cosTheta|), one-sided;
+     * PT_FLAG_EXACT_LIGHT_PDF: the normalised cosine (solid-angle pdf) */
+    float cu = dot(dv, ld3(S->light.direction));
+    float cosl = cu * inv;
     float cosn = dot(n, w);
     if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
-      /* cosn / pdf, pdf = sq / (area * -cosl), as one division */
-      float scale = ((cosn * (S->light.area * -cosl)) / sq) * INV_PI;
+      /* cosn / pdf, pdf = sq / (area * -cosTheta), as one division */
+      float lc = (flags & PT_FLAG_EXACT_LIGHT_PDF) ? cosl : cu;
+      float scale = ((cosn * (S->light.area * -lc)) / sq) * INV_PI;
       if (weight >= 0.0f) scale = scale * weight;
       *C = scl(mulv(mulv(T, alb), ld3(S->light.radiance)), scale);
       *sw = w;
@@ -648,7 +653,7 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
         }
         float weight = ref_sched ? (nee == 2 ? 0.5f : 1.0f) : -1.0f;
         have_sh[k] = refa ? nee_ref(S, T, alb, n, pt, ux, uy, weight, &C[k], &sw[k], &stmax[k])
-                          : nee_sample(S, T, alb, n, pt, ux, uy, weight, &C[k], &sw[k], &stmax[k]);
+                          : nee_sample(S, J->flags, T, alb, n, pt, ux, uy, weight, &C[k], &sw[k], &stmax[k]);
       }
       float x, y, z, sn, cs;
       sincos2pi(u01(r.v[3]), &sn, &cs);

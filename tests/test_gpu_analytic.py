@@ -16,10 +16,13 @@ answer from first principles, computed in the test with numpy / scipy:
   reads as a DiffuseBSDF of albedo Le (cu:1705-1711) and whose radiance it adds
   at every hit, light += radiance * importance (cu:1243): mean radiance
   Le * sum_{k=0}^{K} Le^k;
-* area light over a diffuse plane: a one-sided square light of radiance Le at
+* area light over a diffuse plane (default: the light pdf of light.cpp:81-92,
+  whose unnormalised cosine makes it the solid-angle pdf times the distance;
+  PT_FLAG_EXACT_LIGHT_PDF: the solid-angle pdf): a one-sided square light of radiance Le at
   height h over a plane of albedo rho.  The default estimator's expectation is
-  rho / pi * E with E = Le * integral cos cos / r^2 dA (the irradiance); the
-  reference formula (PT_FLAG_REF_ARITH: pdf from the unnormalised cosine,
+  rho / pi * Le * integral cos cos / r dA, PT_FLAG_EXACT_LIGHT_PDF's rho / pi * E
+  with E = Le * integral cos cos / r^2 dA (the irradiance); the reference
+  kernels' literal formula (PT_FLAG_REF_ARITH: pdf from the unnormalised cosine,
   cu:422-430, and BSDF_DIFFUSE_MULTIPLIER 0.3183) has expectation
   rho * 0.3183 * Le * integral cos cos / r dA.  Both integrals by scipy
   quadrature, at the point under the light's centre and under a corner.
@@ -211,8 +214,12 @@ def test_area_light_over_plane(gpu_ctx, split, where):
     rho, Le, K = 0.75, 3.0, 4
     tgt = (LIGHT_C[0], LIGHT_C[2]) if where == "centre" else (LIGHT_C[0] + A_SIDE / 2, LIGHT_C[2] - A_SIDE / 2)
     sc = _plane_scene(rho, Le, tgt, split)
-    # default: rho / pi * E, E = Le * int cos cos / r^2 dA
+    # default, the light pdf of AreaLight::sample_L (light.cpp:81-92: the
+    # unnormalised cosine, pdf x dist): rho / pi * Le * int cos cos / r dA
     img = _render(gpu_ctx, sc, K)
+    _assert_mean(img, rho / math.pi * Le * _light_integral(tgt[0], tgt[1], 1))
+    # PT_FLAG_EXACT_LIGHT_PDF: rho / pi * E, E = Le * int cos cos / r^2 dA (the irradiance)
+    img = _render(gpu_ctx, sc, K, flags=ptrace.PT_FLAG_EXACT_LIGHT_PDF)
     _assert_mean(img, rho / math.pi * Le * _light_integral(tgt[0], tgt[1], 2))
     # the reference's NEE formula (cu:416-446): rho * 0.3183 * Le * int cos cos / r dA
     img = _render(gpu_ctx, sc, K, flags=ptrace.PT_FLAG_REF_ARITH)
