@@ -1,0 +1,168 @@
+"""Fixture tests/golden/reference_renders.npz: what the reference's own renders
+(media/pathtracer/reference_results/sky/*.png, 640x480) say about each scene,
+reduced to the quantities the tests compare (tests/refrender.py):
+
+  <scene>/camera       the pt_camera of the reference's framing: Scotty3D's
+                       (pt_scene_camera_scotty, application.cpp:395-408,
+                       camera.cpp:15-46) moved along its view axis by `zoom`
+                       (the viewer's scroll, camera.cpp:61-72), zoom fitted
+                       here to the image's red / blue wall and light masks
+  <scene>/labels       region of every pixel (centre ray, closest hit, oracle)
+  <scene>/mask         region interiors where the reference is not saturated
+  <scene>/region_*     per region: id, role, reference mean radiance (linear)
+  <scene>/dist_bin     light-distance quintile of every wall pixel (255: none)
+  <scene>/bin_ref      reference mean radiance per (region, quintile)
+  <scene>/ref_blocks   8x8 block means of the reference's 8-bit RGB
+  <scene>/ref_masks    packed bit masks of the image: red, blue, light, black
+                       (background), for the framing check
+
+The PNGs are read here only; the tests read this file.  Run from the repo
+root on a machine holding /root/reference:
+
+  python tests/golden/make_reference_render_fixture.py
+"""
+import sys
+from pathlib import Path
+
+import numpy as np
+from PIL import Image
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path[:0] = [str(ROOT / "cuda-raytracer_amd"), str(ROOT / "oracle"), str(ROOT / "tests")]
+import ctypes as C  # noqa: E402
+
+import ptrace  # noqa: E402
+import pyoracle  # noqa: E402
+import refrender as rr  # noqa: E402
+
+MEDIA = Path("/root/reference/media/pathtracer")
+OUT = ROOT / "tests" / "golden" / "reference_renders.npz"
+
+
+def ref_image(rel):
+    a = np.asarray(Image.open(MEDIA / "reference_results" / rel).convert("RGB"))
+    assert a.shape == (rr.H, rr.W, 3), a.shape
+    return a[::-1].astype(np.float64)  # bottom-up rows, the ABI's frame order
+
+
+def ref_masks(ref):
+    red = ref[..., 0] > ref[..., 1] + 40
+    blue = ref[..., 2] > ref[..., 0] + 40
+    light = ref.min(-1) >= 254
+    black = ref.max(-1) == 0
+    return red, blue, light, black
+
+
+def zoomed(cam0, target, s):
+    cam = ptrace.pt_camera.from_buffer_copy(bytes(cam0))
+    o = np.array(list(cam0.origin), np.float64)
+    no = target + (o - target) * s
+    for i in range(3):
+        cam.origin[i] = no[i]
+    return cam
+
+
+def scene_bbox_centre(desc):
+    p = rr.prim_array(np.ctypeslib.as_array(C.cast(desc.prims, C.POINTER(C.c_float)),
+                                            shape=(desc.n_prims * 24,)))
+    sph = (p[:, 3].view(np.uint32) >> 28) == 1
+    pts = [p[~sph, 0:3], p[~sph, 4:7], p[~sph, 8:11]]
+    if sph.any():
+        pts += [p[sph, 0:3] - p[sph, 4:5], p[sph, 0:3] + p[sph, 4:5]]
+    a = np.concatenate(pts).astype(np.float64)
+    return (a.min(0) + a.max(0)) / 2
+
+
+def primary(desc, cam):
+    ray6 = ptrace.scotty_generate_rays(cam, rr.pixel_centres())
+    hits = pyoracle.intersect(desc, rr.pixel_rays(ray6))
+    return ray6, hits
+
+
+def agreement(desc, lab, masks, bsdf_alb, bsdf_type):
+    red_ids = [b for b, a in bsdf_alb.items() if bsdf_type[b] == 0 and a[0] > a[2] + 0.2]
+    blue_ids = [b for b, a in bsdf_alb.items() if bsdf_type[b] == 0 and a[2] > a[0] + 0.2]
+    light_ids = [b for b in bsdf_alb if bsdf_type[b] == 3]
+    b = np.where(lab >= 0, lab // 8, -1)
+    red, blue, light, black = masks
+    return float(np.mean([(np.isin(b, red_ids) == red).mean(), (np.isin(b, blue_ids) == blue).mean(),
+                          (np.isin(b, light_ids) == light).mean(), ((b < 0) == black).mean()]))
+
+
+def main():
+    out = {}
+    for name, (rel, settings) in rr.REFERENCE_IMAGES.items():
+        sc = ptrace.Scene.load_dae(MEDIA / "advanced" / f"{name}.dae")
+        d = sc.desc()
+        cam0 = sc.camera_scotty(rr.W, rr.H)
+        target = scene_bbox_centre(d)
+        prims = np.ctypeslib.as_array(C.cast(d.prims, C.POINTER(C.c_float)), shape=(d.n_prims * 24,))
+        bs = C.cast(d.bsdfs, C.POINTER(ptrace.pt_bsdf))
+        bsdf_type = np.array([bs[i].type for i in range(d.n_bsdfs)], np.int32)
+        bsdf_alb = {i: list(bs[i].albedo) for i in range(d.n_bsdfs)}
+        ref = ref_image(rel)
+        masks = ref_masks(ref)
+
+        def score(s):
+            cam = zoomed(cam0, target, s)
+            _, hits = primary(d, cam)
+            return agreement(d, rr.label_map(prims, ptrace.hit_prim(hits)), masks, bsdf_alb, bsdf_type)
+
+        # framing: the default placement, else a coarse-to-fine zoom search
+        best = (score(1.0), 1.0)
+        if best[0] < 0.995:
+            for s in np.arange(0.30, 1.0, 0.05):
+                best = max(best, (score(s), float(s)))
+            for s in best[1] + np.arange(-0.04, 0.0401, 0.002):
+                best = max(best, (score(s), float(s)))
+        agree, zoom = best
+        cam = zoomed(cam0, target, zoom)
+        ray6, hits = primary(d, cam)
+        lab = rr.label_map(prims, ptrace.hit_prim(hits))
+        role = rr.roles(prims, bsdf_type)
+        sat = ref.max(-1) >= 250
+        mask = rr.interior(lab) & ~sat & (lab >= 0)
+        lin = rr.linearize(ref)
+        reg = rr.region_means(lin, lab, mask)
+        rid = np.array(sorted(reg), np.int32)
+        # light-distance quintiles inside each wall region
+        t = ptrace.hit_t(hits).astype(np.float64).reshape(rr.H, rr.W)
+        P = ray6[:, 0:3].reshape(rr.H, rr.W, 3) + ray6[:, 3:6].reshape(rr.H, rr.W, 3) * t[..., None]
+        dist = np.linalg.norm(P - np.array(list(d.light.position), np.float64), axis=-1)
+        qb = np.full((rr.H, rr.W), 255, np.uint8)
+        bin_ref = np.zeros((len(rid), 5, 3))
+        for i, r in enumerate(rid):
+            if role[int(r)] not in rr.ROOM:
+                continue
+            m = mask & (lab == r)
+            edges = np.quantile(dist[m], [0.2, 0.4, 0.6, 0.8])
+            k = np.searchsorted(edges, dist[m])
+            qb[m] = k
+            for j in range(5):
+                bin_ref[i, j] = lin[m][k == j].mean(0)
+        pre = f"{name}/"
+        out.update({
+            pre + "camera": np.frombuffer(bytes(cam), np.uint8),
+            pre + "zoom": np.float64(zoom),
+            pre + "framing_agreement": np.float64(agree),
+            pre + "labels": lab.astype(np.int16),
+            pre + "mask": np.packbits(mask),
+            pre + "region_ids": rid,
+            pre + "region_roles": np.array([role[int(r)] for r in rid], np.int32),
+            pre + "region_pixels": np.array([reg[int(r)][0] for r in rid], np.int32),
+            pre + "region_ref": np.array([reg[int(r)][1] for r in rid]),
+            pre + "dist_bin": qb,
+            pre + "bin_ref": bin_ref,
+            pre + "ref_blocks": rr.block_means(ref).astype(np.float32),
+            pre + "ref_masks": np.packbits(np.stack(masks)),
+            pre + "settings": np.array(settings),
+            pre + "image": np.array(rel),
+        })
+        print(f"{name}: {rel} zoom {zoom:.3f} framing agreement {agree:.4f}, {len(rid)} regions "
+              f"({', '.join(f'{r}:{rr.ROLE_NAMES[role[int(r)]]}' for r in rid)})")
+    np.savez_compressed(OUT, **out)
+    print(f"wrote {OUT} ({OUT.stat().st_size} bytes)")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,92 @@
+"""The oracle's estimator against the renders the reference itself holds
+(media/pathtracer/reference_results/sky, 640x480, Scotty3D's completed CPU
+path tracer; tests/refrender.py says what a PNG is and how regions are
+formed; the numbers come from tests/golden/reference_renders.npz, made by
+tests/golden/make_reference_render_fixture.py).  No GPU: this pins the CPU
+oracle, which every GPU parity test then equals bit for bit.
+
+What the reference renders establish (stated tolerances below):
+  * the area-light estimator is AreaLight::sample_L's (light.cpp:81-92, the
+    unnormalised cosine): inside every wall the ratio reference / oracle is
+    flat in the distance to the light (max/min over distance quintiles
+    <= 1.03), while the solid-angle pdf (PT_FLAG_EXACT_LIGHT_PDF) is off by
+    the distance itself (>= 1.3 across the side walls);
+  * paths are not cut at the reference's "max depth 2": with 2 bounces the
+    colour bleed and the ceiling (lit only indirectly) fall short (ceiling /
+    floor ratio 1.14 at 2 bounces, 1.05 at 3, 1.02 at 4, 1.00 at 8), so the
+    comparison renders 8 bounces, the bench's count;
+  * one global factor remains: the reference's radiance is 0.67-0.68 x the
+    oracle's on every wall, floor and ceiling of both diffuse scenes (a
+    toColor exposure of 1 instead of sqrt(2) would give 0.707; the cause is
+    not in the reference's sources);
+  * residuals after that factor (documented, asserted as bands): the back
+    wall is 5-8 % brighter in the reference, the objects (bunny, spheres)
+    4-14 % darker.
+"""
+import numpy as np
+import pytest
+
+import ptrace
+import pyoracle
+import refrender as rr
+from conftest import ROOT
+
+FIXTURE = ROOT / "tests" / "golden" / "reference_renders.npz"
+DIFFUSE = ["CBbunny", "CBspheres_lambertian"]
+SPP_CPU = 16  # region means average >= 10^4 pixels: noise well under the bands
+
+
+@pytest.fixture(scope="module")
+def fixture():
+    return rr.load(FIXTURE)
+
+
+def oracle_frame(name, fx, spp, flags=0, max_bounces=8):
+    d = ptrace.ArrayScene.load(ROOT / "tests" / "golden" / "scenes" / f"{name}.npz").desc()
+    d.camera = ptrace.pt_camera.from_buffer_copy(fx["camera"].tobytes())
+    img, _ = pyoracle.image(d, rr.W, rr.H, spp, max_bounces=max_bounces, flags=flags)
+    return img
+
+
+def check_diffuse(c, block_frac):
+    """The bands every diffuse scene meets (module docstring)."""
+    assert 0.655 <= c["scale"] <= 0.695, c["scale"]
+    for r, v in c["rel"].items():
+        role = c["role"][r]
+        if role in (rr.SIDE, rr.FLOOR, rr.CEILING):
+            assert np.all(np.abs(v - 1.0) <= 0.03), (r, rr.ROLE_NAMES[role], v)
+        elif role == rr.BACK:
+            assert np.all((v >= 1.0) & (v <= 1.10)), (r, v)
+        elif role == rr.OBJECT:
+            assert np.all((v >= 0.80) & (v <= 1.0)), (r, v)
+    for r, (near_far, mx) in c["spread"].items():
+        lim = 1.03 if c["role"][r] == rr.SIDE else 1.08
+        assert mx <= lim, (r, rr.ROLE_NAMES[c["role"][r]], near_far, mx)
+    assert (c["block_diff"] <= 8).mean() >= block_frac, (c["block_diff"] <= 8).mean()
+
+
+def test_fixture_framing(fixture):
+    """The reference framing was recovered: its red / blue walls, light and
+    background coincide with the scene's regions under the stored camera."""
+    assert set(fixture) == set(rr.REFERENCE_IMAGES)
+    for name, fx in fixture.items():
+        assert fx["framing_agreement"] >= 0.985, (name, fx["framing_agreement"])
+        roles = set(fx["region_roles"].tolist())
+        assert {rr.SIDE, rr.FLOOR, rr.CEILING, rr.BACK} <= roles, name
+    assert float(fixture["CBbunny"]["zoom"]) == 1.0  # Scotty3D's own placement
+    assert 0.6 < float(fixture["CBspheres_lambertian"]["zoom"]) < 0.7
+
+
+@pytest.mark.parametrize("name", DIFFUSE)
+def test_oracle_matches_reference_render(fixture, name):
+    c = rr.compare(fixture[name], oracle_frame(name, fixture[name], SPP_CPU))
+    check_diffuse(c, block_frac=0.80)
+
+
+def test_exact_light_pdf_does_not_match(fixture):
+    """The discriminating check: the solid-angle pdf leaves the distance in
+    the ratio (the reference's pdf is light.cpp:81-92's)."""
+    c = rr.compare(fixture["CBbunny"], oracle_frame("CBbunny", fixture["CBbunny"], SPP_CPU,
+                                                    flags=ptrace.PT_FLAG_EXACT_LIGHT_PDF))
+    sides = [mx for r, (nf, mx) in c["spread"].items() if c["role"][r] == rr.SIDE]
+    assert len(sides) == 2 and min(sides) >= 1.3, sides
