@@ -36,7 +36,7 @@ PT_FLAG_REF_GUIDE = 0x10         # reference quirk (ii)
 PT_FLAG_REF_SCHEDULE = 0x20      # reference quirk (vi): 2 bounces, NEE 2/2/1 weighted 0.5/0.5/1
 PT_FLAG_REF_ARITH = 0x40         # the reference kernels' literal arithmetic (pt_api.h)
 PT_FLAG_EXACT_LIGHT_PDF = 0x80   # area-light NEE with the normalised cosine (default: light.cpp:81-92)
-PT_API_VERSION = 2
+PT_API_VERSION = 3
 PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION, PT_BSDF_REFRACTION = 0, 1, 2, 3, 4
 PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT = 0, 1, 2
 PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1
@@ -121,6 +121,9 @@ API_SYMBOLS = [
     "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex", "pt_copy_owned_sums",
     "pt_get_stats", "pt_reset_stats", "pt_median_filter", "pt_get_display_image", "pt_tonemap",
     "pt_write_png", "pt_write_pfm", "pt_check_division", "pt_check_fast_math",
+    "pt_group_create", "pt_group_destroy", "pt_group_last_error", "pt_group_gather_kind", "pt_group_size",
+    "pt_group_member", "pt_group_load_scene", "pt_group_set_camera", "pt_group_clear", "pt_group_render",
+    "pt_group_get_image", "pt_group_timing",
 ]
 
 
@@ -176,6 +179,18 @@ def _load():
         "pt_reset_stats": (C.c_int, [P]),
         "pt_check_division": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float), I32]),
         "pt_check_fast_math": (C.c_int, [P, I32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
+        "pt_group_create": (C.c_int, [C.POINTER(P), C.POINTER(I32), I32, I32]),
+        "pt_group_destroy": (None, [P]),
+        "pt_group_last_error": (C.c_char_p, [P]),
+        "pt_group_gather_kind": (C.c_int, [P, C.POINTER(I32)]),
+        "pt_group_size": (C.c_int, [P, C.POINTER(I32)]),
+        "pt_group_member": (P, [P, I32]),
+        "pt_group_load_scene": (C.c_int, [P, C.POINTER(pt_scene_desc)]),
+        "pt_group_set_camera": (C.c_int, [P, C.POINTER(pt_camera)]),
+        "pt_group_clear": (C.c_int, [P]),
+        "pt_group_render": (C.c_int, [P, C.POINTER(pt_render_params)]),
+        "pt_group_get_image": (C.c_int, [P, C.POINTER(C.c_float), SZ]),
+        "pt_group_timing": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -527,6 +542,72 @@ class Context:
         self._chk(LIB.pt_reset_stats(self.h))
 
 
+PT_GATHER_AUTO, PT_GATHER_RCCL, PT_GATHER_HOST = 0, 1, 2
+
+
+class Group:
+    """Several GPUs of one process rendering one frame (pt_group_*): member i
+    renders tiles t % n == i on its own host thread; the sums are gathered to
+    member 0 over RCCL (distinct devices) or through the host."""
+
+    def __init__(self, devices, gather=PT_GATHER_AUTO):
+        devs = (C.c_int32 * len(devices))(*devices)
+        self.h = C.c_void_p()
+        rc = LIB.pt_group_create(C.byref(self.h), devs, len(devices), gather)
+        if rc != PT_OK:
+            raise PTError(rc, f"pt_group_create({list(devices)}, gather={gather})")
+        self.width = self.height = 0
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value and LIB is not None:
+            LIB.pt_group_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+    def _chk(self, rc):
+        if rc != PT_OK:
+            raise PTError(rc, LIB.pt_group_last_error(self.h).decode(errors="replace"))
+
+    @property
+    def gather_kind(self):
+        k = C.c_int32()
+        self._chk(LIB.pt_group_gather_kind(self.h, C.byref(k)))
+        return k.value
+
+    @property
+    def note(self):
+        return LIB.pt_group_last_error(self.h).decode(errors="replace")
+
+    def load_scene(self, scene):
+        self._desc = scene.desc()
+        self._scene = scene
+        self._chk(LIB.pt_group_load_scene(self.h, C.byref(self._desc)))
+
+    def set_camera(self, cam):
+        self._chk(LIB.pt_group_set_camera(self.h, C.byref(cam)))
+
+    def clear(self):
+        self._chk(LIB.pt_group_clear(self.h))
+
+    def render(self, width, height, spp, max_bounces=8, seed=15618, sample_offset=0, batch_paths=0, tile_size=32,
+               flags=0):
+        p = pt_render_params(width, height, spp, max_bounces, seed, sample_offset, batch_paths, tile_size, 0, 1, flags)
+        self.width, self.height = width, height
+        self._chk(LIB.pt_group_render(self.h, C.byref(p)))
+
+    def get_image(self):
+        img = np.zeros((self.height, self.width, 4), dtype=np.float32)
+        self._chk(LIB.pt_group_get_image(self.h, _ptr(img, C.c_float), img.size))
+        return img
+
+    def timing(self):
+        g, r = C.c_double(), C.c_double()
+        self._chk(LIB.pt_group_timing(self.h, C.byref(g), C.byref(r)))
+        return g.value, r.value
+
+
 def device_count():
     n = C.c_int()
     LIB.pt_device_count(C.byref(n))
@@ -586,6 +667,9 @@ def _scotty():
         P, I32, U32, SZ, F = C.c_void_p, C.c_int32, C.c_uint32, C.c_size_t, C.POINTER(C.c_float)
         lib.scotty_render.restype = C.c_int
         lib.scotty_render.argtypes = [C.POINTER(pt_scene_desc), I32, I32, I32, I32, U32, I32, I32, F, C.c_char_p, SZ]
+        lib.scotty_render_multi.restype = C.c_int
+        lib.scotty_render_multi.argtypes = [C.POINTER(pt_scene_desc), I32, I32, I32, I32, U32, I32, C.POINTER(I32), I32,
+                                            I32, F, C.POINTER(I32), C.POINTER(C.c_double), C.c_char_p, SZ]
         lib.scotty_viewer.restype = C.c_int
         lib.scotty_viewer.argtypes = [C.POINTER(pt_scene_desc), I32, I32, I32, I32, U32, C.c_char_p, I32, F,
                                       C.POINTER(I32), C.c_char_p, SZ]
@@ -620,6 +704,21 @@ def scotty_render(scene, width, height, spp, max_depth, flags=0, threads=0, devi
     if rc:
         raise PTError(rc, err.value.decode(errors="replace"))
     return out
+
+
+def scotty_render_multi(scene, width, height, spp, max_depth, devices, gather=0, flags=0, threads=0):
+    """scotty::MultiGpuPathTracer: the same tile/worker loop over a pt_group
+    of `devices` (one process).  Returns (frame, gather kind, gather ms)."""
+    out = np.zeros((height, width, 4), dtype=np.float32)
+    err = C.create_string_buffer(512)
+    d = scene.desc()
+    devs = (C.c_int32 * len(devices))(*devices)
+    kind, gms = C.c_int32(), C.c_double()
+    rc = _scotty().scotty_render_multi(C.byref(d), width, height, spp, max_depth, flags, threads, devs, len(devices),
+                                       gather, _ptr(out, C.c_float), C.byref(kind), C.byref(gms), err, len(err))
+    if rc:
+        raise PTError(rc, err.value.decode(errors="replace"))
+    return out, kind.value, gms.value
 
 
 def scotty_viewer(scene, width, height, samples_per_frame, keys, max_bounces=2, flags=0, device=0):

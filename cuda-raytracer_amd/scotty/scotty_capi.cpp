@@ -54,6 +54,33 @@ int scotty_render(const pt_scene_desc* desc, int w, int h, int spp, int depth, u
   }
 }
 
+// The same PathTracer over several GPUs of one process (pt_group): tiles dealt
+// to devices[0..n), sums gathered into devices[0]; *gather_kind (optional):
+// PT_GATHER_RCCL or PT_GATHER_HOST, the gather used.
+int scotty_render_multi(const pt_scene_desc* desc, int w, int h, int spp, int depth, uint32_t flags, int threads,
+                        const int32_t* devices, int32_t n_devices, int32_t gather, float* out, int32_t* gather_kind,
+                        double* gather_ms, char* err, size_t errlen) {
+  if (!desc || !out || !devices || n_devices <= 0 || w <= 0 || h <= 0 || spp <= 0 || threads < 0)
+    return PT_E_INVALID;
+  try {
+    scotty::MultiGpuPathTracer pt(std::vector<int>(devices, devices + n_devices), (size_t)spp, (size_t)depth,
+                                  (size_t)threads, gather);
+    pt.set_scene(*desc);
+    pt.set_frame_size((size_t)w, (size_t)h);
+    pt.set_flags(flags);
+    pt.start_raytracing();
+    const std::vector<float>& f = pt.frame();
+    std::memcpy(out, f.data(), f.size() * sizeof(float));
+    if (gather_kind) *gather_kind = pt.gather_kind();
+    if (gather_ms) pt_group_timing(pt.group(), gather_ms, nullptr);
+    return PT_OK;
+  } catch (const scotty::Error& e) {
+    return fail(e, e.code, err, errlen);
+  } catch (const std::exception& e) {
+    return fail(e, PT_E_HIP, err, errlen);
+  }
+}
+
 // The viewer: one renderPicture per character of `keys`, after
 // handleKeyPress(c) unless c is '.'.  out: the last displayed frame;
 // *samples: the samples accumulated in it.

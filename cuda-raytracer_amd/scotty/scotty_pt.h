@@ -762,6 +762,66 @@ class GpuEstimator {
   const Image* img_ = nullptr;
 };
 
+// GPU estimator over several GPUs of one process (pt_group):
+// the frame's 32x32 tiles are dealt round-robin to the devices, each renders
+// its share on its own host thread, and the sums are gathered into
+// devices[0] (RCCL over xGMI when the devices are distinct, pt_api.h).  The
+// reference renders on one device only (cu:1874-1897).
+class GroupEstimator {
+ public:
+  explicit GroupEstimator(const std::vector<int>& devices, int gather = PT_GATHER_AUTO) {
+    std::vector<int32_t> d(devices.begin(), devices.end());
+    int rc = pt_group_create(&g_, d.data(), (int32_t)d.size(), gather);
+    if (rc) throw Error(rc, "pt_group_create");
+  }
+  ~GroupEstimator() { pt_group_destroy(g_); }
+  GroupEstimator(const GroupEstimator&) = delete;
+  GroupEstimator& operator=(const GroupEstimator&) = delete;
+  void set_scene(const std::string& dae_path) {
+    scene_ = std::make_unique<Scene>(dae_path);
+    check(pt_group_load_scene(g_, &scene_->desc()), "pt_group_load_scene");
+  }
+  void set_scene(const pt_scene_desc& desc) {
+    scene_ = std::make_unique<Scene>(desc);
+    check(pt_group_load_scene(g_, &scene_->desc()), "pt_group_load_scene");
+  }
+  void begin(size_t w, size_t h, size_t spp, size_t max_depth, uint32_t flags) {
+    check(pt_group_clear(g_), "pt_group_clear");
+    pt_render_params p{};
+    p.width = (int32_t)w;
+    p.height = (int32_t)h;
+    p.spp = (int32_t)spp;
+    p.max_bounces = (int32_t)max_depth;
+    p.seed = 15618;
+    p.tile_size = 32;
+    p.nranks = 1;
+    p.flags = flags;
+    check(pt_group_render(g_, &p), "pt_group_render");
+    img_.width = (int)w;
+    img_.height = (int)h;
+    img_.data.resize(w * h * 4);
+    check(pt_group_get_image(g_, img_.data.data(), img_.data.size()), "pt_group_get_image");
+  }
+  void pixel(size_t x, size_t y, float rgba[4]) const {
+    const float* p = &img_.data[((size_t)y * img_.width + x) * 4];
+    for (int k = 0; k < 4; ++k) rgba[k] = p[k];
+  }
+  pt_group* group() const { return g_; }
+  int gather_kind() const {
+    int32_t k = 0;
+    pt_group_gather_kind(g_, &k);
+    return k;
+  }
+
+ private:
+  void check(int rc, const char* what) const {
+    if (rc) throw Error(rc, std::string(what) + ": " + pt_group_last_error(g_));
+  }
+  pt_group* g_ = nullptr;
+  std::unique_ptr<Scene> scene_;
+  Image img_;
+};
+
 template <class Estimator>
 class PathTracerT {
  public:
@@ -878,6 +938,20 @@ class PathTracer : private GpuEstimator, public PathTracerT<GpuEstimator> {
   void set_scene(const pt_scene_desc& desc) { GpuEstimator::set_scene(desc); }
   void set_camera(const Camera&) {}  // the scene's camera is used (cu:1590-1607)
   CudaRenderer& renderer() { return GpuEstimator::renderer(); }
+};
+
+// The Scotty3D PathTracer over several GPUs of one process (pt_group).
+class MultiGpuPathTracer : private GroupEstimator, public PathTracerT<GroupEstimator> {
+ public:
+  MultiGpuPathTracer(const std::vector<int>& devices, size_t ns_aa = 1, size_t max_ray_depth = 4,
+                     size_t num_threads = 1, int gather = PT_GATHER_AUTO)
+      : GroupEstimator(devices, gather),
+        PathTracerT<GroupEstimator>(*static_cast<GroupEstimator*>(this), ns_aa, max_ray_depth, 1, 1, 1, 1,
+                                    num_threads) {}
+  void set_scene(const std::string& dae_path) { GroupEstimator::set_scene(dae_path); }
+  void set_scene(const pt_scene_desc& desc) { GroupEstimator::set_scene(desc); }
+  int gather_kind() const { return GroupEstimator::gather_kind(); }
+  pt_group* group() const { return GroupEstimator::group(); }
 };
 
 // ---- the progressive viewer (display.cpp:99-190 without the GLUT window) -----

@@ -50,8 +50,9 @@ extern "C" {
 
 /* 2: pt_bsdf grew `roughness` (36 B), pt_stats `culled_rays` (round 4);
  * PT_FLAG_EXACT_LIGHT_PDF and the light.cpp pdf as the default (round 5).
+ * 3: pt_group_* (several GPUs of one process, RCCL gather; round 5).
  * A client checks pt_api_version() == PT_API_VERSION before passing structs. */
-#define PT_API_VERSION 2
+#define PT_API_VERSION 3
 int pt_api_version(void);
 
 /* ---- error codes ---------------------------------------------------------- */
@@ -334,6 +335,43 @@ int pt_owned_pixels(pt_ctx* ctx, int32_t* n_pixels, int32_t* pixel_index, size_t
 int pt_copy_owned_sums(pt_ctx* ctx, void* dst, size_t n_bytes, int32_t dst_on_device);
 /* Samples per pixel accumulated so far. */
 int pt_samples(pt_ctx* ctx, int32_t* spp);
+
+/* ---- one frame over several GPUs of one process -------------
+ * For C/C++ callers (the Scotty3D surface, scotty::PathTracer with a device
+ * list): a group of contexts, member i on devices[i], renders the frame's
+ * tiles t with t % n == i (pt_render_params.rank / nranks are set per member,
+ * the caller's are ignored), each member on its own host thread; the members'
+ * owned-pixel sums are then gathered into member 0's device frame.  The
+ * gather is RCCL point-to-point over xGMI (ncclCommInitAll over the members'
+ * devices, one ncclGroupStart / ncclSend / ncclRecv / ncclGroupEnd round into
+ * member 0, librccl loaded at pt_group_create) when the devices are distinct
+ * and RCCL loads; otherwise (a device listed twice -- RCCL takes one rank per
+ * GPU -- or no librccl) a host-staged copy.  The reference has no multi-GPU
+ * path (cu:1874-1897 only enumerates devices); the Python bench gathers the
+ * same sums over torch.distributed (ptdist.py).  PT_GATHER_* select the
+ * gather; pt_group_gather_kind reports the one in use. */
+typedef struct pt_group pt_group;
+#define PT_GATHER_AUTO 0 /* RCCL when the devices are distinct and librccl loads */
+#define PT_GATHER_RCCL 1 /* RCCL or PT_E_UNSUPPORTED                             */
+#define PT_GATHER_HOST 2 /* host-staged copies                                   */
+int pt_group_create(pt_group** out, const int32_t* devices, int32_t n, int32_t gather);
+void pt_group_destroy(pt_group* g);
+const char* pt_group_last_error(const pt_group* g);
+int pt_group_gather_kind(const pt_group* g, int32_t* kind); /* PT_GATHER_RCCL / _HOST */
+int pt_group_size(const pt_group* g, int32_t* n);
+pt_ctx* pt_group_member(pt_group* g, int32_t i); /* borrowed; NULL if out of range */
+int pt_group_load_scene(pt_group* g, const pt_scene_desc* scene);
+int pt_group_set_camera(pt_group* g, const pt_camera* camera);
+int pt_group_clear(pt_group* g);
+/* Every member renders its tiles (and adds them to its accumulation), then
+ * the sums are gathered into member 0's frame: sums / accumulated samples,
+ * alpha 1, as pt_get_image of one context rendering the whole frame. */
+int pt_group_render(pt_group* g, const pt_render_params* params);
+/* The gathered frame, width*height*4 floats (host copy from member 0). */
+int pt_group_get_image(pt_group* g, float* rgba, size_t n_floats);
+/* Wall time (ms) of the last pt_group_render's gather (send + receive +
+ * assembly on member 0), and of the whole call. */
+int pt_group_timing(const pt_group* g, double* gather_ms, double* render_ms);
 
 /* ---- post-process and output --------------------------
  * 3x3 median filter of a width*height float RGBA frame on the device

@@ -35,6 +35,15 @@ extern "C" {
 int scotty_render(const pt_scene_desc* desc, int w, int h, int spp, int depth, uint32_t flags, int threads,
                   int device, float* out, char* err, size_t errlen);
 
+/* The same PathTracer over n_devices GPUs of one process (pt_group_*,
+ * pt_api.h): the tiles are dealt to devices[i] round-robin, each device
+ * renders on its own host thread, the sums are gathered into devices[0]
+ * (gather: PT_GATHER_AUTO / _RCCL / _HOST).  *gather_kind (optional): the
+ * gather used; *gather_ms (optional): its wall time. */
+int scotty_render_multi(const pt_scene_desc* desc, int w, int h, int spp, int depth, uint32_t flags, int threads,
+                        const int32_t* devices, int32_t n_devices, int32_t gather, float* out, int32_t* gather_kind,
+                        double* gather_ms, char* err, size_t errlen);
+
 /* The viewer: one renderPicture (samples_per_frame more samples, progressive)
  * per character of `keys`, after handleKeyPress(c) unless c is '.'
  * (w/a/s/d move the camera by 0.01 and restart the accumulation, p pauses).

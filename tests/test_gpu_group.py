@@ -1,0 +1,87 @@
+"""Several GPUs of one process through the C ABI (pt_group_*, pt_api.h;
+SURVEY §8(e)): each member renders its round-robin
+32x32-tile share on its own host thread and the sums are gathered into
+member 0's frame -- over RCCL (ncclCommInitAll + grouped ncclSend/ncclRecv)
+when the devices are distinct, through the host when a device is listed
+twice.  On this one-GPU box: RCCL at one member (the send/receive round runs,
+rank 0 to itself), the host path with 2-3 members on device 0; every
+gathered frame equals one context's whole frame (pt_get_image) bit for bit.
+More than one distinct device is unmeasured here (the driver's 8-GPU node
+runs the Python bench, ptdist.py)."""
+import numpy as np
+import pytest
+
+import ptrace
+from conftest import load_fixture
+
+pytestmark = pytest.mark.gpu
+
+W, H, SPP, BOUNCES = 200, 136, 3, 5  # tiles cut at the right and top edges
+
+
+def _single(gpu_ctx, sc, tile=32):
+    gpu_ctx.load_scene(sc)
+    gpu_ctx.clear()
+    gpu_ctx.render(W, H, SPP, max_bounces=BOUNCES, tile_size=tile)
+    return gpu_ctx.get_image()
+
+
+@pytest.mark.parametrize("devices,gather,kind", [
+    ([0], ptrace.PT_GATHER_AUTO, ptrace.PT_GATHER_RCCL),
+    ([0], ptrace.PT_GATHER_HOST, ptrace.PT_GATHER_HOST),
+    ([0, 0], ptrace.PT_GATHER_AUTO, ptrace.PT_GATHER_HOST),
+    ([0, 0, 0], ptrace.PT_GATHER_HOST, ptrace.PT_GATHER_HOST),
+])
+def test_group_frame_equals_single_context(gpu_ctx, devices, gather, kind):
+    sc = load_fixture("CBbunny")
+    ref = _single(gpu_ctx, sc)
+    g = ptrace.Group(devices, gather)
+    try:
+        assert g.gather_kind == kind, g.note
+        g.load_scene(sc)
+        for _ in range(2):  # the cached layout serves the second frame
+            g.clear()
+            g.render(W, H, SPP, max_bounces=BOUNCES)
+            img = g.get_image()
+            assert np.array_equal(img, ref)
+        gms, rms = g.timing()
+        assert 0 < gms <= rms
+    finally:
+        g.close()
+
+
+def test_group_rccl_refuses_a_shared_device():
+    with pytest.raises(ptrace.PTError) as e:
+        ptrace.Group([0, 0], ptrace.PT_GATHER_RCCL)
+    assert e.value.code == ptrace.PT_E_UNSUPPORTED
+
+
+def test_group_progressive_and_tile_size(gpu_ctx):
+    """Two renders accumulate (sample_offset continues) and a 16-pixel tile
+    deals a different share: still the single context's frame."""
+    sc = load_fixture("CBgems")
+    gpu_ctx.load_scene(sc)
+    gpu_ctx.clear()
+    gpu_ctx.render(W, H, 2, max_bounces=4, tile_size=16)
+    gpu_ctx.render(W, H, 2, max_bounces=4, tile_size=16, sample_offset=2)
+    ref = gpu_ctx.get_image()
+    g = ptrace.Group([0, 0, 0])
+    try:
+        g.load_scene(sc)
+        g.clear()
+        g.render(W, H, 2, max_bounces=4, tile_size=16)
+        g.render(W, H, 2, max_bounces=4, tile_size=16, sample_offset=2)
+        assert np.array_equal(g.get_image(), ref)
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_scotty_multi_gpu_path_tracer(devices):
+    """scotty::MultiGpuPathTracer (the Scotty3D tile/worker loop over a
+    pt_group) gives scotty::PathTracer's frame."""
+    sc = load_fixture("CBspheres")
+    one = ptrace.scotty_render(sc, W, H, SPP, BOUNCES, threads=4)
+    multi, kind, gms = ptrace.scotty_render_multi(sc, W, H, SPP, BOUNCES, devices, threads=4)
+    assert kind == (ptrace.PT_GATHER_RCCL if len(devices) == 1 else ptrace.PT_GATHER_HOST)
+    assert np.array_equal(multi, one) and multi[..., :3].mean() > 0
