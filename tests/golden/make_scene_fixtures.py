@@ -28,13 +28,23 @@ SCENES = {
     # 1,167 nodes, the level that overflows the reference's fixed per-level
     # buffers (BASELINE config 4)
     "bunny": "advanced/bunny.dae",
+    # basic/ scenes whose reference renders the tests compare against
+    # (tests/refrender.py): point lights, an area light, material-less meshes
+    "trigs1": "basic/trigs1.dae",
+    "trigs5": "basic/trigs5.dae",
+    "trigs10": "basic/trigs10.dae",
+    "plane4": "basic/plane4.dae",
+    "floating": "basic/floating.dae",
 }
 
 
 def main():
     out = Path(__file__).resolve().parent / "scenes"
     out.mkdir(exist_ok=True)
+    only = set(sys.argv[1:])
     for name, rel in SCENES.items():
+        if only and name not in only:
+            continue
         sc = ptrace.Scene.load_dae(MEDIA / rel)
         arr = ptrace.scene_to_arrays(sc)
         arr["level_counts"] = np.array(sc.level_counts(), dtype=np.int32)

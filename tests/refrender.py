@@ -27,18 +27,55 @@ GAMMA, LEVEL = 2.2, 1.0
 EXPOSURE = math.sqrt(2.0 ** LEVEL)
 
 # scene -> (reference image under media/pathtracer/reference_results, the
-# reference's max ray depth / spp per performance.txt)
+# reference's settings (performance.txt:36-69 for the sky/ renders; none
+# published for basic/), the .dae under media/pathtracer)
 REFERENCE_IMAGES = {
-    "CBbunny": ("sky/CBbunny.png", "max depth 2, 2500 spp, 2 area-light samples"),
-    "CBspheres_lambertian": ("sky/6400SPP_lambertian.png", "max depth 2, 5000 spp, 2 area-light samples"),
-    "CBcoil": ("sky/CBcoil.png", "max depth 2, 2500 spp, 2 area-light samples"),
-    "CBspheres": ("sky/6400SPP_classic.png", "max depth 4, 5000 spp, 2 area-light samples"),
+    "CBbunny": ("sky/CBbunny.png", "max depth 2, 2500 spp, 2 area-light samples", "advanced/CBbunny.dae"),
+    "CBspheres_lambertian": ("sky/6400SPP_lambertian.png", "max depth 2, 5000 spp, 2 area-light samples",
+                             "advanced/CBspheres_lambertian.dae"),
+    "CBcoil": ("sky/CBcoil.png", "max depth 2, 2500 spp, 2 area-light samples", "advanced/CBcoil.dae"),
+    "CBspheres": ("sky/6400SPP_classic.png", "max depth 4, 5000 spp, 2 area-light samples",
+                  "advanced/CBspheres.dae"),
+    # point light (light.cpp:50-57: radiance, pdf 1, no fall-off) over diffuse triangles
+    "trigs1": ("basic/trigs1.png", "point light", "basic/trigs1.dae"),
+    "trigs5": ("basic/trigs5.png", "point light", "basic/trigs5.dae"),
+    "trigs10": ("basic/trigs10.png", "point light", "basic/trigs10.dae"),
+    # material-less meshes (DEFAULT_ALBEDO below): a point light, an area light
+    "plane4": ("basic/plane.png", "point light, mesh without material", "basic/plane4.dae"),
+    "floating": ("basic/floating.png", "area light, meshes without material", "basic/floating.dae"),
 }
+# Scenes the reference renders reproduce with no free factor (scale 1).  The
+# Cornell boxes carry one constant per scene file (their renders are 0.67-0.68
+# of this build's radiance on every wall, floor and ceiling, whatever the
+# distance to the light): the course's copies of those .dae files evidently
+# differed from this repository's (e.g. the light's radiance), so their scale
+# is fitted and only the structure is compared.
+EXACT = ("trigs1", "trigs5", "trigs10", "plane4", "floating")
+# A mesh without a material is DiffuseBSDF(1, 1, 1) in this repository
+# (src/dynamic_scene/mesh.cpp:37, what pt_scene_load_dae restates) but was
+# DiffuseBSDF(0.5, 0.5, 0.5) in the course build that rendered
+# reference_results (the line left commented out at mesh.cpp:36): plane.png and
+# floating.png are exactly half of the albedo-1 radiance.  The tests render
+# those scenes with their default BSDFs at 0.5.
+DEFAULT_ALBEDO = {"plane4": 0.5, "floating": 0.5}
 
 ROLE_NAMES = ["side", "floor", "ceiling", "back", "object", "light", "mirror"]
 SIDE, FLOOR, CEILING, BACK, OBJECT, LIGHT, MIRROR = range(7)
 ROOM = (SIDE, FLOOR, CEILING, BACK)
 SPHERE_CODE = 6
+
+
+def course_bsdfs(name, bsdfs):
+    """The scene's pt_bsdf array (raw bytes, 36 B records) as the course build
+    had it: the material-less meshes' DiffuseBSDF(1) (diffuse, albedo 1)
+    at DEFAULT_ALBEDO (mesh.cpp:36-37)."""
+    b = np.array(np.frombuffer(np.asarray(bsdfs).tobytes(), np.uint8))
+    if name in DEFAULT_ALBEDO:
+        rec = b.view(np.float32).reshape(-1, 9)
+        typ = b.view(np.int32).reshape(-1, 9)[:, 0]
+        dflt = (typ == 0) & np.all(rec[:, 1:4] == 1.0, axis=1)
+        rec[dflt, 1:4] = DEFAULT_ALBEDO[name]
+    return b
 
 
 def linearize(v8):

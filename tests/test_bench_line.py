@@ -22,6 +22,11 @@ def _canned():
     head["scene"] = d["config"]["scene"]
     head["batch_paths"] = d["config"]["batch_paths"]
     head["roofline_other"] = []
+    # (round 5: traced rays only in value, host-culled camera rays beside it;
+    # the round-3 record predates the field)
+    head["culled_rays_per_frame"] = 0
+    for o in d["configs"]:
+        o.setdefault("culled_rays_per_frame", 0)
     return head, d["configs"], d["cpu_baseline"]
 
 
@@ -37,7 +42,7 @@ def test_line_is_bounded_and_complete():
     assert "\n" not in line and len(line) < 12000
     out = json.loads(line)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
-              "scaling", "vs_baseline", "dtype", "data", "config"):
+              "scaling", "vs_baseline", "dtype", "data", "config", "culled_rays_per_frame"):
         assert k in out, k
     assert out["value"] == head["value"] and out["ms_per_step"] == head["ms_per_frame"]
     r = out["roofline"]
@@ -50,6 +55,7 @@ def test_line_is_bounded_and_complete():
     assert len(out["configs"]) == len(others)
     for o, c in zip(others, out["configs"]):
         assert c["scene"] == o["scene"] and c["value"] == o["value"]
+        assert c["culled_rays_per_frame"] == o["culled_rays_per_frame"]
         assert set(c["roofline"]) == {"kernel", "frac", "achieved", "traffic"}
     assert out["detail"] == "gpurun_out/bench_detail.json"
 

@@ -21,6 +21,12 @@ there.  Bands (stated in that module's docstring, measured on the oracle):
     the mirror coil                                  0.05 .. 0.5 (the
       reference's coil reflects far less than a 0.9 mirror; unexplained)
 
+  exact scenes (trigs1/5/10, plane4, floating; no free factor)
+    every region's mean radiance                     within 1 %
+    light-distance profile inside a region           max/min <= 1.03
+    8x8 blocks of the 8-bit frames                   all within 4 levels,
+                                                     99 % within 2
+
 The pixel-centre closest hits (pt_intersect) must give the fixture's region
 map (made by the oracle), and the reference image's red / blue walls, light
 and background must coincide with it."""
@@ -30,7 +36,7 @@ import pytest
 import ptrace
 import refrender as rr
 from conftest import ROOT
-from test_reference_renders import check_diffuse
+from test_reference_renders import check_diffuse, check_exact, course_scene
 
 pytestmark = pytest.mark.gpu
 
@@ -48,7 +54,7 @@ class _Framed:
     PathTracer::set_camera hands the tracer)."""
 
     def __init__(self, name, fx):
-        self.scene = ptrace.ArrayScene.load(ROOT / "tests" / "golden" / "scenes" / f"{name}.npz")
+        self.scene = course_scene(name)
         self.camera = ptrace.pt_camera.from_buffer_copy(fx["camera"].tobytes())
 
     def desc(self):
@@ -112,3 +118,12 @@ def test_gpu_matches_reference_render_specular(fixture, name):
             assert np.all(np.abs(v - 1.0) <= 0.10), (r, v)
         elif role == rr.MIRROR:
             assert np.all((v >= 0.05) & (v <= 0.5)), (r, v)
+
+
+@pytest.mark.parametrize("name", rr.EXACT)
+def test_gpu_reproduces_reference_render(fixture, name):
+    """No free factor: the Scotty3D surface on the GPU gives the reference's
+    render (point lights, an area light with a shadow)."""
+    img = ptrace.scotty_render(_Framed(name, fixture[name]), rr.W, rr.H, 256, BOUNCES)
+    assert np.isfinite(img).all()
+    check_exact(rr.compare(fixture[name], img, scale=1.0))

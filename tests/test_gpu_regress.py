@@ -304,3 +304,37 @@ def test_triangle_test_division_is_ieee(gpu_ctx):
     den = rng.integers(1, 1 << 15, m).astype(np.float32)
     q = gpu_ctx.check_division(num, den)
     assert np.array_equal(q.view(np.uint32), (num / den).view(np.uint32))
+
+
+def _bench_c5(tmp_path, gpus, tag):
+    """bench.py with BASELINE config 5's branch at a small size (--config5-size)."""
+    out, out5 = tmp_path / f"h{tag}.npy", tmp_path / f"c5_{tag}.npy"
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(gpus), "--backend", "gloo", "--steps", "1",
+           "--warmup", "0", "--configs", "none", "--config5", "on", "--config5-size", "96x64x3", "--tile", "8",
+           "--ref-arith", "none", "--no-cpu", "--no-1spp", "--width", "64", "--height", "48", "--spp", "2",
+           "--bounces", "4", "--batch", "8192", "--save-frame", str(out), "--save-config5", str(out5),
+           "--detail-out", str(tmp_path / f"detail{tag}.json")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    return line, np.load(out), np.load(out5)
+
+
+def test_bench_eight_ranks_config5_branch(tmp_path):
+    """bench.py --gpus 8 runs BASELINE config 5's 8-rank branch (tiles over
+    all ranks + the gather), here over gloo with the eight
+    ranks sharing this box's GPU and config 5 shrunk to 96x64x3 on the
+    dragon proxy: the gathered config-5 frame equals one GPU's whole frame of
+    the same workload (the world-1 branch), and the headline frame the
+    world-1 headline, bit for bit."""
+    one, h1, c1 = _bench_c5(tmp_path, 1, "1")
+    eight, h8, c8 = _bench_c5(tmp_path, 8, "8")
+    assert one["n_gpus"] == 1 and eight["n_gpus"] == 8
+    cfg8 = [c for c in eight["configs"] if c["scene"] == "dragon_proxy"]
+    assert len(cfg8) == 1 and "tiles over all ranks + gloo gather" in cfg8[0]["config"]
+    whole1 = [c for c in one["configs"] if c["scene"] == "dragon_proxy" and "whole" in c["config"]]
+    assert len(whole1) == 1
+    assert cfg8[0]["value"] > 0 and one["rays_per_frame"] == eight["rays_per_frame"]
+    assert c1.shape == (64, 96, 4) and c1[..., :3].mean() > 0
+    assert np.array_equal(h1, h8)
+    assert np.array_equal(c1, c8)
