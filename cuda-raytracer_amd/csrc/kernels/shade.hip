@@ -71,6 +71,8 @@ struct ShadeArgs {
   const uint32_t* __restrict__ pix_of;
   pt_light light;
   pt_camera cam;
+  const pt_light* lights;  // pt_scene_desc.lights on the device when n_lights > 1
+  uint32_t n_lights;
   uint32_t N, npix, sample_base, seed;
   udiv div_npix, div_width;  // p / npix, pixel / width (N and width * height < 2^30)
   int width, height, max_bounces;
@@ -242,10 +244,24 @@ __device__ __forceinline__ pt_camera cam_of(const ShadeArgs& S) {
 // and for an fp32 t that is t <= D rounded down to fp32.
 __device__ __forceinline__ float ref_shadow_tmax(float dist) { return __double2float_rd((double)dist - 1e-3); }
 
-template <bool KR = false, bool REFA = false>
+// sel: the low byte of the sample's first Philox word (u01 uses the top 24
+// bits), which picks one of several lights (pt_scene_desc.lights): light k =
+// floor(sel n / 256) with probability cnt_k / 256, weighted by 256 / cnt_k.
+// XL: the extended light model (several lights, directional and hemisphere
+// lights; pt_scene_desc.lights) -- its own kernel variants, so the one-light
+// kernels keep their registers (the selection and the two light types cost
+// k_shade_push its 8th wave when compiled into it)
+template <bool KR = false, bool REFA = false, bool XL = false>
 __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const f3 alb, const f3 n, const f3 pt,
-                                           float ux, float uy, float weight, f3& C, RayV& r) {
-  const pt_light L = light_of<KR>(S);
+                                           float ux, float uy, float weight, f3& C, RayV& r, uint32_t sel = 0u) {
+  pt_light L = light_of<KR>(S);
+  float lw = 1.0f;
+  if (XL && S.n_lights > 1u) {
+    const uint32_t nl = S.n_lights, k = ((sel & 0xFFu) * nl) >> 8;
+    const uint32_t cnt = (256u * (k + 1u) + nl - 1u) / nl - (256u * k + nl - 1u) / nl;
+    lw = 256.0f / (float)cnt;
+    L = S.lights[k];
+  }
   if (REFA && L.type == PT_LIGHT_AREA) {
     // kernelDirectLightRays, cu:416-446, expression for expression
     const float sx = ux - 0.5f, sy = uy - 0.5f;
@@ -317,6 +333,7 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
       const float lc = (S.flags & PT_FLAG_EXACT_LIGHT_PDF) ? cosl : cu;
       float scale = ((cosn * (L.area * -lc)) / sq) * inv_pi;
       if (weight >= 0.0f) scale = scale * weight;
+      if (XL && lw != 1.0f) scale = scale * lw;
       C = mulv(mulv(T, alb), ld3(L.radiance)) * scale;
       r.o = pt;
       r.d = w;
@@ -333,10 +350,45 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
     if (dist > 1e-2f && cosn > 0.0f) {
       float scale = cosn * INV_PI;
       if (weight >= 0.0f) scale = scale * weight;
+      if (XL && lw != 1.0f) scale = scale * lw;
       C = mulv(mulv(T, alb), ld3(L.radiance)) * scale;
       r.o = pt;
       r.d = w;
       r.tmax = dist - EPS;
+      return true;
+    }
+  } else if (XL && L.type == PT_LIGHT_DIRECTIONAL) {
+    // DirectionalLight::sample_L (light.cpp:18-24): wi = dirToLight, pdf 1,
+    // distToLight infinite
+    const f3 w = ld3(L.direction);
+    const float cosn = dot(n, w);
+    if (cosn > 0.0f) {
+      float scale = cosn * INV_PI;
+      if (weight >= 0.0f) scale = scale * weight;
+      if (lw != 1.0f) scale = scale * lw;
+      C = mulv(mulv(T, alb), ld3(L.radiance)) * scale;
+      r.o = pt;
+      r.d = w;
+      r.tmax = __builtin_inff();
+      return true;
+    }
+  } else if (XL && L.type == PT_LIGHT_HEMISPHERE) {
+    // InfiniteHemisphereLight::sample_L (light.cpp:36-44): a uniform
+    // direction of the upper (+y) hemisphere (cos theta = ux, phi = 2 pi uy),
+    // pdf 1 / (2 pi): cos / pdf * albedo / pi = 2 cos albedo
+    float sn, cs;
+    sincos2pi(uy, &sn, &cs);
+    const float rr = sqrt_rn(fmaxf(0.0f, __builtin_fmaf(-ux, ux, 1.0f)));
+    const f3 w = mk(rr * cs, ux, rr * sn);
+    const float cosn = dot(n, w);
+    if (cosn > 0.0f) {
+      float scale = cosn * 2.0f;
+      if (weight >= 0.0f) scale = scale * weight;
+      if (lw != 1.0f) scale = scale * lw;
+      C = mulv(mulv(T, alb), ld3(L.radiance)) * scale;
+      r.o = pt;
+      r.d = w;
+      r.tmax = __builtin_inff();
       return true;
     }
   }
@@ -362,7 +414,7 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
 // thread's column of sh_lds ([NSH][10][TPB]: o, d, tmax, C) as soon as the NEE
 // sample has made them, instead of staying in registers through the BSDF
 // sample (k_path_leaf: fewer VGPRs live at its peak)
-template <int NSH, bool M64 = false, bool KR = false, bool REFA = false, bool LDSSH = false>
+template <int NSH, bool M64 = false, bool KR = false, bool REFA = false, bool LDSSH = false, bool XL = false>
 __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, PathState& st, const f3 o,
                                              const f3 d, uint32_t prim, float t, const bool (&clear)[NSH],
                                              f3 (&C)[NSH], bool& new_ext, RayV& ext, bool (&new_sh)[NSH],
@@ -532,13 +584,16 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           for (int s = 0; s < NSH; ++s) {
             if (s < nee) {
               float ux = u01(u.x), uy = u01(u.y);
+              uint32_t selw = u.x;
               if (s == 1) {
                 const u4 v = rng_nee2<M64>(S.seed, g, sidx, vtx);
                 ux = u01(v.x);
                 uy = u01(v.y);
+                selw = v.x;
               }
               const float weight = NSH == 2 ? (nee == 2 ? 0.5f : 1.0f) : -1.0f;
-              new_sh[s] = nee_sample<KR, REFA>(S, Tv(), alb, n, pt, ux, uy, weight, C[s], shr[s]);
+              new_sh[s] = nee_sample<KR, REFA, XL>(S, Tv(), alb, n, pt, ux, uy, weight, C[s], shr[s],
+                                               selw);
               if constexpr (LDSSH) {
                 float* q = sh_lds + (size_t)s * 10 * TPB + threadIdx.x;
                 q[0 * TPB] = shr[s].o.x;
@@ -838,7 +893,7 @@ __device__ __forceinline__ SlotLoad<NSH> load_slot(const ShadeArgs& S, uint32_t 
   }
   return L;
 }
-template <int NSH, bool REFA = false>
+template <int NSH, bool REFA = false, bool XL = false>
 __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool act, uint32_t& q, bool& new_ext,
                                           RayV& ext, bool (&new_sh)[NSH], RayV (&shr)[NSH], uint32_t (*kc)[4],
                                           uint32_t* bins, bool sparse, bool use_pre, const SlotLoad<NSH> pre) {
@@ -932,7 +987,8 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
     }
     const float t = ext_hit ? r1.w : 0.0f;
     const f3 o = ext_hit ? xyz(r0) : mk(0, 0, 0), d = ext_hit ? mk(r0.w, r1.x, r1.y) : mk(0, 0, 1);
-    shade_vertex<NSH, PT_SHADE_MAD64, false, REFA>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh, shr);
+    shade_vertex<NSH, PT_SHADE_MAD64, false, REFA, false, XL>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext,
+                                                              new_sh, shr);
     // (vertices done = vtx - 1: the last one resolves shadow rays only)
     ended = !(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || ((st.flags >> 8) & 0xffu) - 1u >= (uint32_t)S.passes;
   }
@@ -1089,7 +1145,7 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
 #ifndef PT_SHADE_ATTR
 #define PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(7, 8)))
 #endif
-template <int NSH, bool REFA>
+template <int NSH, bool REFA, bool XL = false>
 // a workgroup with fewer live slots than this reads its slots sparsely (shade_slot)
 #ifndef PT_SPARSE_LIVE
 #define PT_SPARSE_LIVE 128
@@ -1144,7 +1200,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t s_kc[SORT_KEYS + 1][4];
   __shared__ uint32_t s_bins[PT_SORT_WAVE == 3 ? 4 * HIST_BINS : 1];
   uint32_t q = p;  // where this lane's path state and new rays go
-  int state = shade_slot<NSH, REFA>(S, p, p < nin, q, new_ext, ext, new_sh, shr, s_kc,
+  int state = shade_slot<NSH, REFA, XL>(S, p, p < nin, q, new_ext, ext, new_sh, shr, s_kc,
                                     s_bins + (PT_SORT_WAVE == 3 ? wave * HIST_BINS : 0), s_sparse != 0,
                                     S.dense != 0, pre);
   // ---- regeneration: free slots take the next paths in rank order, from the
@@ -1597,6 +1653,12 @@ constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 #ifndef PT_PATH_LDS_SH
 #define PT_PATH_LDS_SH 1
 #endif
+// refill idle lanes only when at least this many are idle (the camera-ray code
+// then runs masked once per PT_REFILL_MIN path ends instead of at every
+// iteration with an idle lane; the idle lanes wait meanwhile)
+#ifndef PT_REFILL_MIN
+#define PT_REFILL_MIN 1
+#endif
 // (PT_PATH_LIGHT_RELOAD reads the light from the kernel-argument segment at
 // offsetof(ShadeArgs, light): S must stay this kernel's FIRST parameter; a
 // -DPT_DBG_BOUNDS build checks it at run time)
@@ -1661,7 +1723,7 @@ static __device__ unsigned long long g_path_timing[PT_TIMING_WAVES * 8];
 // resident lanes (PT_PATH_GUIDED_BELOW paths per lane, default 128).
 // SPH: the leaf holds spheres (false: the sphere test is not compiled in; the
 // host picks the variant, pt_ctx::has_sphere)
-template <int NSH, bool REFA, bool GUIDED, bool SPH = true>
+template <int NSH, bool REFA, bool GUIDED, bool SPH = true, bool XL = false>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
     uint32_t* __restrict__ work, uint32_t nreg, uint32_t tail_unit, uint32_t* __restrict__ err) {
@@ -1720,6 +1782,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
   for (;;) {
     // ---- refill idle lanes from the pool (new paths start at their camera ray)
     unsigned long long idle = __ballot(!active);
+    if (PT_REFILL_MIN > 1 && __popcll(idle) < PT_REFILL_MIN && idle != ~0ull) idle = 0;
     if (idle && next == end && !drained) {
 #if PT_PATH_TIMING
       const unsigned long long tg = wall_clock64();
@@ -1816,7 +1879,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       bool new_ext, new_sh[NSH];
       RayV e2, s2[NSH];
       // (the sample index is recomputed, not carried: one register less)
-      shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD, REFA, PT_PATH_LDS_SH>(
+      shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD, REFA, PT_PATH_LDS_SH, XL>(
           S, S.sample_base + udiv_q(sh_p[threadIdx.x], S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2, new_sh, s2,
           sh_lds);
       // (unconditional: without a new extension ray F_EXT is clear and ext is

@@ -30,7 +30,7 @@
 #include "kernels/post.hip"
 
 // k_shade_push lives in pt_shade.hip (its own compile flags)
-hipError_t pt_launch_shade_push(int nsh, bool refa, unsigned grid, hipStream_t stream, hipEvent_t e0,
+hipError_t pt_launch_shade_push(int nsh, bool refa, bool xl, unsigned grid, hipStream_t stream, hipEvent_t e0,
                                 hipEvent_t e1, const void* S);
 
 using namespace pt;
@@ -82,6 +82,8 @@ struct pt_ctx {
   size_t tmin_cap = 0;
   float4* d_shade = nullptr;  // hit-shading records (SHADE_REC float4 per primitive)
   pt_bsdf* d_bsdfs = nullptr;
+  pt_light* d_lights = nullptr;  // pt_scene_desc.lights (n_lights > 1)
+  uint32_t n_lights = 0;
 
   // wavefront buffers (sized for N paths = 2N ray slots)
   uint32_t cap_paths = 0;  // paths the buffers hold
@@ -217,7 +219,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 }
 
 static void free_all(pt_ctx* c) {
-  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_ray,
+  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_lights, c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_kmap, c->d_res, c->d_wstate, c->d_live, c->d_pool,
                   c->d_pix_of, c->d_accum, c->d_frame, c->d_tmin, c->d_ray_b, c->d_ps0_b, c->d_ps1_b, c->d_ps2_b,
@@ -1097,6 +1099,9 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   if ((rc = dalloc(c, &c->d_prims_ref, (size_t)s->n_prims * 6))) return rc;
   if ((rc = dalloc(c, &c->d_shade, (size_t)s->n_prims * SHADE_REC))) return rc;
   if ((rc = dalloc(c, &c->d_bsdfs, std::max(1, s->n_bsdfs)))) return rc;
+  if (s->n_lights > 1 && !s->lights) return fail(c, PT_E_INVALID, "n_lights > 1 without lights");
+  if (s->n_lights > 256) return fail(c, PT_E_UNSUPPORTED, "more than 256 lights");
+  if ((rc = dalloc(c, &c->d_lights, std::max(1, (int)s->n_lights)))) return rc;
   if ((rc = dalloc(c, &c->d_cnt, (size_t)s->n_nodes * NLANE * CSTRIDE))) return rc;
   if ((rc = dalloc(c, &c->d_qoff, (size_t)s->n_nodes * NLANE))) return rc;
   if ((rc = dalloc(c, &c->d_iprefix, (size_t)NLANE * (c->max_level_nodes + 1)))) return rc;
@@ -1173,6 +1178,9 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   HIPCHK(c, hipMemset(c->d_qoff, 0, (size_t)s->n_nodes * NLANE * 4));
   c->light = s->light;
   c->camera = s->camera;
+  c->n_lights = s->n_lights > 1 ? (uint32_t)s->n_lights : 0u;
+  if (c->n_lights)
+    HIPCHK(c, hipMemcpy(c->d_lights, s->lights, sizeof(pt_light) * c->n_lights, hipMemcpyHostToDevice));
   {  // origin_bound: 64 x the largest magnitude of the scene's vertices, sphere extents, camera, light
     double m = 0.0;
     auto upd = [&](double v) { m = std::max(m, std::fabs(v)); };
@@ -1296,6 +1304,15 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   // the reference cannot render at all: cu:1765 casts every primitive to Triangle)
   if (c->refa && c->has_sphere)
     return fail(c, PT_E_UNSUPPORTED, "PT_FLAG_REF_ARITH: the reference renders triangles only");
+  // (the reference's CUDA path takes exactly one light, read as an AreaLight, cu:1733-1751)
+  // the extended light model (several lights, directional / hemisphere
+  // lights): its own kernel variants, default arithmetic and one NEE sample
+  // per vertex only
+  const bool xl = c->n_lights > 0 || c->light.type == PT_LIGHT_DIRECTIONAL || c->light.type == PT_LIGHT_HEMISPHERE;
+  if (xl && c->refa)
+    return fail(c, PT_E_UNSUPPORTED, "PT_FLAG_REF_ARITH: the reference's CUDA path takes one area light (cu:1733-1751)");
+  if (xl && (P->flags & PT_FLAG_REF_SCHEDULE))
+    return fail(c, PT_E_UNSUPPORTED, "PT_FLAG_REF_SCHEDULE: the reference schedule samples one area light");
   const int max_bounces = ref_sched ? 2 : P->max_bounces;
   const int passes = max_bounces + 2;  // vertices per path at most
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
@@ -1321,6 +1338,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.pix_of = c->d_act_pix;
     S.light = c->light;
     S.cam = c->camera;
+    S.lights = c->d_lights;
+    S.n_lights = c->n_lights;
     S.npix = npix;
     S.div_npix = udiv_make(npix);
     S.div_width = udiv_make((uint32_t)P->width);
@@ -1356,7 +1375,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       const bool guided = (uint64_t)M < (uint64_t)c->path_guided_below * blocks * TPB;
       // (spheres: the sphere test compiled in; the reference arithmetic has none)
       const bool sph = c->has_sphere;
-      auto kpath = guided ? (kv == 0 ? (sph ? k_path_leaf<1, false, true, true> : k_path_leaf<1, false, true, false>)
+      auto kpath = xl ? (sph ? k_path_leaf<1, false, false, true, true> : k_path_leaf<1, false, false, false, true>)
+                 : guided ? (kv == 0 ? (sph ? k_path_leaf<1, false, true, true> : k_path_leaf<1, false, true, false>)
                              : kv == 1 ? (sph ? k_path_leaf<2, false, true, true> : k_path_leaf<2, false, true, false>)
                              : kv == 2 ? k_path_leaf<1, true, true, false> : k_path_leaf<2, true, true, false>)
                           : (kv == 0 ? (sph ? k_path_leaf<1, false, false, true> : k_path_leaf<1, false, false, false>)
@@ -1472,9 +1492,9 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
           }
           if (c->timing) {
             const auto e = c->pair(pt_ctx::K_SHADE, 0);
-            HIPCHK(c, pt_launch_shade_push(nsh, c->refa, Gc, c->stream, e.first, e.second, &S));
+            HIPCHK(c, pt_launch_shade_push(nsh, c->refa, xl, Gc, c->stream, e.first, e.second, &S));
           } else {
-            HIPCHK(c, pt_launch_shade_push(nsh, c->refa, Gc, c->stream, nullptr, nullptr, &S));
+            HIPCHK(c, pt_launch_shade_push(nsh, c->refa, xl, Gc, c->stream, nullptr, nullptr, &S));
           }
           if (comp) {
             hipLaunchKernelGGL(k_compact_wstate, dim3((Gc + TPB - 1) / TPB), dim3(TPB), 0, c->stream, S.wstate, Gc,

@@ -23,11 +23,14 @@ namespace {
 // S points at a pt::ShadeArgs of pt_device.hip (the same definition, from the
 // same header, so the same layout).  e0/e1: optional dispatch timestamps.
 // refa: PT_FLAG_REF_ARITH (the reference's literal arithmetic, shade.hip).
-hipError_t pt_launch_shade_push(int nsh, bool refa, unsigned grid, hipStream_t stream, hipEvent_t e0,
+// xl: the extended light model (several / directional / hemisphere lights;
+// one NEE sample per vertex, default arithmetic only).
+hipError_t pt_launch_shade_push(int nsh, bool refa, bool xl, unsigned grid, hipStream_t stream, hipEvent_t e0,
                                 hipEvent_t e1, const void* S) {
   const auto& A = *static_cast<const pt::ShadeArgs*>(S);
-  auto k = refa ? (nsh == 2 ? pt::k_shade_push<2, true> : pt::k_shade_push<1, true>)
-                : (nsh == 2 ? pt::k_shade_push<2, false> : pt::k_shade_push<1, false>);
+  auto k = xl ? pt::k_shade_push<1, false, true>
+              : refa ? (nsh == 2 ? pt::k_shade_push<2, true> : pt::k_shade_push<1, true>)
+                     : (nsh == 2 ? pt::k_shade_push<2, false> : pt::k_shade_push<1, false>);
   if (e0)
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(pt::TPB), 0, stream, e0, e1, 0, A);
   else

@@ -13,6 +13,7 @@
 //   DynamicScene::Sphere (centre, radius*scale)     src/dynamic_scene/sphere.cpp:9-17
 // The XML reader below is a minimal, self-contained DOM builder (the reference
 // vendors tinyxml2, which is not reused).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -607,13 +608,22 @@ struct Loader {
       }
       S.have_camera = true;
     }
-    // light: the reference accepts exactly one (cu:1734-1737); we take the first
-    // area or point light.
+    // Lights in scene-graph order (application.cpp:370-374 init_light ->
+    // DynamicScene::*Light::get_static_light): area (area_light.h:12-24 with
+    // the LightInfo defaults), point, directional (directional_light.h:14-19:
+    // -(transform * (direction, 1)) -- translation included, as the reference
+    // writes it -- then light.cpp:14-16 dirToLight = its negated unit vector),
+    // ambient (ambient_light.h -> InfiniteHemisphereLight, light.cpp:27-44).
+    // The CUDA path accepts exactly one (cu:1734-1737): `light` is the first
+    // area or point light, else the first of the others; with more than one
+    // every light is listed (pt_scene_desc.lights, light == lights[0]).
     S.light = pt_light{};
     S.light.type = PT_LIGHT_NONE;
+    S.lights.clear();
     for (auto& pl : lights) {
       const M4& T = pl.T;
-      if (pl.info.type == 3) {  // area_light.h:12-24 with LightInfo defaults
+      pt_light L{};
+      if (pl.info.type == 3) {
         V3 position = xform_point(T, V3(0, 0, 0), false);
         V3 direction = xform_point(T, V3(0, 0, -1), false) - position;
         direction = direction / direction.norm();  // Vector3D::normalize: *= 1/norm
@@ -622,31 +632,57 @@ struct Loader {
         V3 dim_x = cross(lup, ldir);
         V3 dx = xform_point(T, dim_x, false) - position;
         V3 dy = xform_point(T, dim_y, false) - position;
-        S.light.type = PT_LIGHT_AREA;
+        L.type = PT_LIGHT_AREA;
         for (int k = 0; k < 3; ++k) {
-          S.light.radiance[k] = pl.info.spectrum[k];
-          S.light.position[k] = (float)position[k];
-          S.light.direction[k] = (float)direction[k];
-          S.light.dim_x[k] = (float)dx[k];
-          S.light.dim_y[k] = (float)dy[k];
+          L.radiance[k] = pl.info.spectrum[k];
+          L.position[k] = (float)position[k];
+          L.direction[k] = (float)direction[k];
+          L.dim_x[k] = (float)dx[k];
+          L.dim_y[k] = (float)dy[k];
         }
         // area = |dim_x| * |dim_y| in fp32 (cu:1751)
-        float ax = S.light.dim_x[0] * S.light.dim_x[0] + S.light.dim_x[1] * S.light.dim_x[1] +
-                   S.light.dim_x[2] * S.light.dim_x[2];
-        float ay = S.light.dim_y[0] * S.light.dim_y[0] + S.light.dim_y[1] * S.light.dim_y[1] +
-                   S.light.dim_y[2] * S.light.dim_y[2];
-        S.light.area = sqrtf(ax) * sqrtf(ay);
-        break;
+        float ax = L.dim_x[0] * L.dim_x[0] + L.dim_x[1] * L.dim_x[1] + L.dim_x[2] * L.dim_x[2];
+        float ay = L.dim_y[0] * L.dim_y[0] + L.dim_y[1] * L.dim_y[1] + L.dim_y[2] * L.dim_y[2];
+        L.area = sqrtf(ax) * sqrtf(ay);
       } else if (pl.info.type == 4) {
         V3 position = xform_point(T, V3(0, 0, 0), false);
-        S.light.type = PT_LIGHT_POINT;
+        L.type = PT_LIGHT_POINT;
         for (int k = 0; k < 3; ++k) {
-          S.light.radiance[k] = pl.info.spectrum[k];
-          S.light.position[k] = (float)position[k];
+          L.radiance[k] = pl.info.spectrum[k];
+          L.position[k] = (float)position[k];
         }
+      } else if (pl.info.type == 2) {
+        V3 to_light = xform_point(T, V3(0, 0, -1), false);  // -(-(T (0,0,-1,1)))
+        to_light = to_light / to_light.norm();
+        L.type = PT_LIGHT_DIRECTIONAL;
+        for (int k = 0; k < 3; ++k) {
+          L.radiance[k] = pl.info.spectrum[k];
+          L.direction[k] = (float)to_light[k];
+        }
+      } else if (pl.info.type == 1) {
+        L.type = PT_LIGHT_HEMISPHERE;
+        for (int k = 0; k < 3; ++k) L.radiance[k] = pl.info.spectrum[k];
+      } else {
+        continue;  // spot lights: a stub in the reference (light.cpp:61-69)
+      }
+      S.lights.push_back(L);
+    }
+    // no light at all: Application::load adds the default AmbientLight
+    // (application.cpp:389-392; LightInfo's spectrum (1, 1, 1), light_info.cpp:11)
+    if (S.lights.empty()) {
+      pt_light L{};
+      L.type = PT_LIGHT_HEMISPHERE;
+      L.radiance[0] = L.radiance[1] = L.radiance[2] = 1.0f;
+      S.lights.push_back(L);
+    }
+    // `light`: the first area / point light (the CUDA path's), else the first
+    for (size_t i = 0; i < S.lights.size(); ++i)
+      if (S.lights[i].type == PT_LIGHT_AREA || S.lights[i].type == PT_LIGHT_POINT) {
+        std::rotate(S.lights.begin(), S.lights.begin() + i, S.lights.begin() + i + 1);
         break;
       }
-    }
+    if (!S.lights.empty()) S.light = S.lights[0];
+    if (S.lights.size() < 2) S.lights.clear();
     return true;
   }
 };

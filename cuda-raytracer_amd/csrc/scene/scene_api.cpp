@@ -274,6 +274,8 @@ int pt_scene_get_desc(const pt_scene* sc, pt_scene_desc* d) {
   d->bsdfs = S.dbsdfs.data();
   d->light = S.light;
   d->camera = S.camera;
+  d->n_lights = (int32_t)S.lights.size();
+  d->lights = S.lights.empty() ? nullptr : S.lights.data();
   return PT_OK;
 }
 

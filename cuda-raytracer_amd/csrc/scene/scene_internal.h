@@ -111,6 +111,7 @@ struct Scene {
   std::vector<Prim> prims;
   std::vector<Material> materials;  // one per scene object (cu:1694-1723)
   pt_light light{};
+  std::vector<pt_light> lights;  // every light when there are two or more (lights[0] == light)
   pt_camera camera{};
   bool have_camera = false;
   // COLLADA camera optics + view direction, for the Scotty3D framing

@@ -36,9 +36,9 @@ PT_FLAG_REF_GUIDE = 0x10         # reference quirk (ii)
 PT_FLAG_REF_SCHEDULE = 0x20      # reference quirk (vi): 2 bounces, NEE 2/2/1 weighted 0.5/0.5/1
 PT_FLAG_REF_ARITH = 0x40         # the reference kernels' literal arithmetic (pt_api.h)
 PT_FLAG_EXACT_LIGHT_PDF = 0x80   # area-light NEE with the normalised cosine (default: light.cpp:81-92)
-PT_API_VERSION = 3
+PT_API_VERSION = 4
 PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION, PT_BSDF_REFRACTION = 0, 1, 2, 3, 4
-PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT = 0, 1, 2
+PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT, PT_LIGHT_DIRECTIONAL, PT_LIGHT_HEMISPHERE = 0, 1, 2, 3, 4
 PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1
 PT_GPU_BVH_PLOC, PT_GPU_BVH_LBVH = 0, 1
 PT_POST_PROCESS_THRESHOLD = 32
@@ -82,7 +82,8 @@ class pt_scene_desc(C.Structure):
                 ("n_nodes", C.c_int32), ("nodes", C.POINTER(pt_node)),
                 ("n_levels", C.c_int32), ("level_start", C.POINTER(C.c_int32)),
                 ("n_bsdfs", C.c_int32), ("bsdfs", C.POINTER(pt_bsdf)),
-                ("light", pt_light), ("camera", pt_camera)]
+                ("light", pt_light), ("camera", pt_camera),
+                ("n_lights", C.c_int32), ("lights", C.POINTER(pt_light))]
 
 
 class pt_render_params(C.Structure):
@@ -349,6 +350,9 @@ def scene_to_arrays(scene: "Scene") -> dict:
         "bsdf_size": np.array([C.sizeof(pt_bsdf)], np.int32),
         "light": np.frombuffer(bytes(d.light), dtype=np.uint8).copy(),
         "camera": np.frombuffer(bytes(d.camera), dtype=np.uint8).copy(),
+        # every light when there are several (pt_scene_desc.lights), else empty
+        "lights": np.frombuffer(C.string_at(d.lights, C.sizeof(pt_light) * d.n_lights), dtype=np.uint8).copy()
+        if d.n_lights > 1 else np.zeros(0, np.uint8),
     }
 
 
@@ -400,6 +404,10 @@ class ArrayScene:
         d.bsdfs = a["bsdfs"].ctypes.data_as(C.POINTER(pt_bsdf))
         d.light = pt_light.from_buffer_copy(a["light"].tobytes())
         d.camera = pt_camera.from_buffer_copy(a["camera"].tobytes())
+        lights = a.get("lights")
+        if lights is not None and len(lights) >= 2 * C.sizeof(pt_light):
+            d.n_lights = len(lights) // C.sizeof(pt_light)
+            d.lights = lights.ctypes.data_as(C.POINTER(pt_light))
         d._owner = self  # the desc points into our arrays: keep them alive
         return d
 

@@ -51,8 +51,9 @@ extern "C" {
 /* 2: pt_bsdf grew `roughness` (36 B), pt_stats `culled_rays` (round 4);
  * PT_FLAG_EXACT_LIGHT_PDF and the light.cpp pdf as the default (round 5).
  * 3: pt_group_* (several GPUs of one process, RCCL gather; round 5).
+ * 4: pt_scene_desc.n_lights / lights, PT_LIGHT_DIRECTIONAL / _HEMISPHERE.
  * A client checks pt_api_version() == PT_API_VERSION before passing structs. */
-#define PT_API_VERSION 3
+#define PT_API_VERSION 4
 int pt_api_version(void);
 
 /* ---- error codes ---------------------------------------------------------- */
@@ -140,6 +141,14 @@ typedef struct pt_bsdf {
 #define PT_LIGHT_NONE 0
 #define PT_LIGHT_AREA 1
 #define PT_LIGHT_POINT 2
+/* Scotty3D's infinite lights (the CPU path tracer's; static_scene/light.cpp:
+ * 12-45), from COLLADA <directional> and <ambient> lights:
+ *   DIRECTIONAL: `direction` = the unit direction TOWARD the light
+ *     (DirectionalLight::dirToLight), pdf 1, shadow rays of infinite length;
+ *   HEMISPHERE: InfiniteHemisphereLight -- radiance from every direction of
+ *     the upper (+y) hemisphere, sampled uniformly (pdf 1 / 2 pi). */
+#define PT_LIGHT_DIRECTIONAL 3
+#define PT_LIGHT_HEMISPHERE 4
 
 /* CuEmitter (cudaRenderer.h:126-133) + kind. */
 typedef struct pt_light {
@@ -162,7 +171,14 @@ typedef struct pt_camera {
   float up[3];
 } pt_camera;
 
-/* Flattened scene handed to the device (what CudaRenderer::loadScene builds). */
+/* Flattened scene handed to the device (what CudaRenderer::loadScene builds).
+ * Lights: the reference's CUDA path takes exactly one (cu:1734-1737) --
+ * `light`.  A scene with several (the Scotty3D CPU path tracer sums over
+ * scene->lights, pathtracer.cpp:441-476) lists them all in lights[0 ..
+ * n_lights) with light == lights[0]; each next-event sample then picks one
+ * uniformly (the low byte of its first Philox word, weighted by the exact
+ * inverse of its selection probability), which has the sum's expectation.
+ * n_lights 0 or 1: `light` alone (lights may be NULL). */
 typedef struct pt_scene_desc {
   int32_t n_prims;
   const pt_prim* prims;
@@ -175,6 +191,8 @@ typedef struct pt_scene_desc {
   const pt_bsdf* bsdfs;
   pt_light light;
   pt_camera camera;
+  int32_t n_lights;
+  const pt_light* lights;
 } pt_scene_desc;
 
 /* ---- host-side scene loading (input adapter, runs on the CPU) -------------- */
@@ -474,6 +492,7 @@ PT_STATIC_ASSERT(sizeof(pt_node) == 128, "pt_node layout");
 PT_STATIC_ASSERT(sizeof(pt_bsdf) == 36, "pt_bsdf layout");
 PT_STATIC_ASSERT(sizeof(pt_light) == 76, "pt_light layout");
 PT_STATIC_ASSERT(sizeof(pt_camera) == 48, "pt_camera layout");
+PT_STATIC_ASSERT(sizeof(pt_scene_desc) == 208, "pt_scene_desc layout");
 PT_STATIC_ASSERT(sizeof(pt_render_params) == 44, "pt_render_params layout");
 PT_STATIC_ASSERT(sizeof(pt_stats) == 920, "pt_stats layout");
 #undef PT_STATIC_ASSERT

@@ -401,12 +401,26 @@ static uint64_t trace(const job_t* J, v3 o, v3 d, float tmax) {
 /* One NEE sample toward the scene light, kernelDirectLightRays cu:380-481.
  * weight < 0: unweighted (default schedule); else the reference schedule's
  * per-sample weight (cu:2515-2533). */
+/* sel: the low byte of the sample's first Philox word; with several lights
+ * (S->lights, n_lights > 1) it picks light k = floor(sel n / 256), whose
+ * contribution is weighted by 256 / cnt_k, the inverse of its probability
+ * (shade.hip nee_sample). */
 static int nee_sample(const pt_scene_desc* S, uint32_t flags, v3 T, v3 alb, v3 n, v3 pt, float ux, float uy,
-                      float weight, v3* C, v3* sw, float* stmax) {
+                      float weight, v3* C, v3* sw, float* stmax, uint32_t sel) {
   const float INV_PI = 0.318309886183790671f, EPS = 1e-3f;
-  if (S->light.type == PT_LIGHT_AREA) {
+  const pt_light* Lp = &S->light;
+  float lw = 1.0f;
+  if (S->n_lights > 1) {
+    const uint32_t nl = (uint32_t)S->n_lights, k = ((sel & 0xFFu) * nl) >> 8;
+    const uint32_t cnt = (256u * (k + 1u) + nl - 1u) / nl - (256u * k + nl - 1u) / nl;
+    lw = 256.0f / (float)cnt;
+    Lp = &S->lights[k];
+  }
+  const pt_light LL = *Lp;
+  const pt_light* const L = &LL;
+  if (L->type == PT_LIGHT_AREA) {
     float sx = ux - 0.5f, sy = uy - 0.5f;
-    v3 pos = ld3(S->light.position), dx = ld3(S->light.dim_x), dy = ld3(S->light.dim_y);
+    v3 pos = ld3(L->position), dx = ld3(L->dim_x), dy = ld3(L->dim_y);
     v3 lpt = mk(fmaf(sy, dy.x, fmaf(sx, dx.x, pos.x)), fmaf(sy, dy.y, fmaf(sx, dx.y, pos.y)),
                 fmaf(sy, dy.z, fmaf(sx, dx.z, pos.z)));
     v3 dv = sub(lpt, pt);
@@ -417,21 +431,22 @@ static int nee_sample(const pt_scene_desc* S, uint32_t flags, v3 T, v3 alb, v3 n
     /* AreaLight::sample_L, light.cpp:81-92: cosTheta = dot(d, direction) of
      * the unnormalised d, pdf = sqDist / (area |cosTheta|), one-sided;
      * PT_FLAG_EXACT_LIGHT_PDF: the normalised cosine (solid-angle pdf) */
-    float cu = dot(dv, ld3(S->light.direction));
+    float cu = dot(dv, ld3(L->direction));
     float cosl = cu * inv;
     float cosn = dot(n, w);
     if (dist > 1e-2f && cosl < -1e-2f && cosn > 0.0f) {
       /* cosn / pdf, pdf = sq / (area * -cosTheta), as one division */
       float lc = (flags & PT_FLAG_EXACT_LIGHT_PDF) ? cosl : cu;
-      float scale = ((cosn * (S->light.area * -lc)) / sq) * INV_PI;
+      float scale = ((cosn * (L->area * -lc)) / sq) * INV_PI;
       if (weight >= 0.0f) scale = scale * weight;
-      *C = scl(mulv(mulv(T, alb), ld3(S->light.radiance)), scale);
+      if (lw != 1.0f) scale = scale * lw;
+      *C = scl(mulv(mulv(T, alb), ld3(L->radiance)), scale);
       *sw = w;
       *stmax = dist - EPS;
       return 1;
     }
-  } else if (S->light.type == PT_LIGHT_POINT) {
-    v3 dv = sub(ld3(S->light.position), pt);
+  } else if (L->type == PT_LIGHT_POINT) {
+    v3 dv = sub(ld3(L->position), pt);
     float sq = dot(dv, dv);
     float dist = sqrtf(sq);
     float inv = 1.0f / dist;
@@ -440,9 +455,42 @@ static int nee_sample(const pt_scene_desc* S, uint32_t flags, v3 T, v3 alb, v3 n
     if (dist > 1e-2f && cosn > 0.0f) {
       float scale = cosn * INV_PI;
       if (weight >= 0.0f) scale = scale * weight;
-      *C = scl(mulv(mulv(T, alb), ld3(S->light.radiance)), scale);
+      if (lw != 1.0f) scale = scale * lw;
+      *C = scl(mulv(mulv(T, alb), ld3(L->radiance)), scale);
       *sw = w;
       *stmax = dist - EPS;
+      return 1;
+    }
+  } else if (L->type == PT_LIGHT_DIRECTIONAL) {
+    /* DirectionalLight::sample_L, light.cpp:18-24: wi = dirToLight, pdf 1,
+     * infinitely far */
+    v3 w = ld3(L->direction);
+    float cosn = dot(n, w);
+    if (cosn > 0.0f) {
+      float scale = cosn * INV_PI;
+      if (weight >= 0.0f) scale = scale * weight;
+      if (lw != 1.0f) scale = scale * lw;
+      *C = scl(mulv(mulv(T, alb), ld3(L->radiance)), scale);
+      *sw = w;
+      *stmax = INFINITY;
+      return 1;
+    }
+  } else if (L->type == PT_LIGHT_HEMISPHERE) {
+    /* InfiniteHemisphereLight::sample_L, light.cpp:36-44: a uniform direction
+     * of the upper (+y) hemisphere, pdf 1 / (2 pi): cos / pdf * albedo / pi =
+     * 2 cos albedo */
+    float sn, cs;
+    sincos2pi(uy, &sn, &cs);
+    float rr = sqrtf(fmaxf(0.0f, fmaf(-ux, ux, 1.0f)));
+    v3 w = mk(rr * cs, ux, rr * sn);
+    float cosn = dot(n, w);
+    if (cosn > 0.0f) {
+      float scale = cosn * 2.0f;
+      if (weight >= 0.0f) scale = scale * weight;
+      if (lw != 1.0f) scale = scale * lw;
+      *C = scl(mulv(mulv(T, alb), ld3(L->radiance)), scale);
+      *sw = w;
+      *stmax = INFINITY;
       return 1;
     }
   }
@@ -646,14 +694,16 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
       float stmax[2] = {-1.0f, -1.0f};
       for (int k = 0; k < nee; ++k) {
         float ux = u01(r.v[0]), uy = u01(r.v[1]);
+        uint32_t sel = r.v[0];
         if (k == 1) {
           u4 r2 = rng_nee2(J->seed, g, s, vtx);
           ux = u01(r2.v[0]);
           uy = u01(r2.v[1]);
+          sel = r2.v[0];
         }
         float weight = ref_sched ? (nee == 2 ? 0.5f : 1.0f) : -1.0f;
         have_sh[k] = refa ? nee_ref(S, T, alb, n, pt, ux, uy, weight, &C[k], &sw[k], &stmax[k])
-                          : nee_sample(S, J->flags, T, alb, n, pt, ux, uy, weight, &C[k], &sw[k], &stmax[k]);
+                          : nee_sample(S, J->flags, T, alb, n, pt, ux, uy, weight, &C[k], &sw[k], &stmax[k], sel);
       }
       float x, y, z, sn, cs;
       sincos2pi(u01(r.v[3]), &sn, &cs);

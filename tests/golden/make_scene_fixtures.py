@@ -35,6 +35,10 @@ SCENES = {
     "trigs10": "basic/trigs10.dae",
     "plane4": "basic/plane4.dae",
     "floating": "basic/floating.dae",
+    # directional + ambient (hemisphere) lights, spheres (the extended light model)
+    "sphere_diffuse": "basic/sphere_diffuse.dae",
+    "sphere7_diffuse": "basic/sphere7_diffuse.dae",
+    "carim_diffuse": "basic/carim_diffuse.dae",
 }
 
 
