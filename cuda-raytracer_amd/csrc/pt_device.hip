@@ -1149,8 +1149,12 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
         r[1] = r[2] = r[3] = r[4] = make_float4(0.f, 0.f, 0.f, 0.f);
         continue;
       }
-      const bool flat = n0[0] == n1[0] && n0[1] == n1[1] && n0[2] == n1[2] && n1[0] == n2[0] && n1[1] == n2[1] &&
-                        n1[2] == n2[2];
+      // flat: the three normals identical to the bit (not float ==, under
+      // which a +0 and a -0 component match: the reference arithmetic's
+      // blend then takes n2 for n0, below, and the signs of zero components
+      // of its normal could differ from cu:1213-1221's; the oracle decides the
+      // same way)
+      const bool flat = memcmp(n0, n1, 3 * sizeof(float)) == 0 && memcmp(n1, n2, 3 * sizeof(float)) == 0;
       const uint32_t m2 = meta | (flat ? 0u : SHADE_SMOOTH);
       float mf;
       memcpy(&mf, &m2, 4);
@@ -1300,6 +1304,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
   const uint32_t nsh = ref_sched ? 2u : 1u;
   c->refa = (P->flags & PT_FLAG_REF_ARITH) != 0;
   c->tmin = false;
+  bool compact_mem = true;  // the tail compaction's second set could be allocated (ensure_compact_set)
   // (glass is read as the reference reads it, a mirror: shade.hip; spheres
   // the reference cannot render at all: cu:1765 casts every primitive to Triangle)
   if (c->refa && c->has_sphere)
@@ -1550,10 +1555,18 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         // still left in a workgroup's block).  With the per-region slot counters
         // a compaction pass costs what a plain one does, so compacting early
         // pays: 70 / 65 against 50 / 50 measured +0.5 % CBbunny, +0.9 % dragon proxy
-        compact_next = c->compaction && unclaimed == 0 && ncomp < MAX_COMPACTIONS &&
+        compact_next = c->compaction && compact_mem && unclaimed == 0 && ncomp < MAX_COMPACTIONS &&
                        (uint64_t)nlive * 100 <= (uint64_t)nbound * (ncomp ? c->compact_pct : c->compact_first);
+        if (compact_next && ensure_compact_set(c) != PT_OK) {
+          // no memory for the second set: this render goes on without tail
+          // compaction (a speed measure only) instead of failing with earlier
+          // chunks already added to the accumulation and the sample count not
+          // advanced
+          (void)hipGetLastError();
+          compact_mem = false;
+          compact_next = false;
+        }
         if (compact_next) {
-          if ((rc = ensure_compact_set(c))) return rc;
           RAY[1] = c->d_ray_b;
           PS[0][1] = c->d_ps0_b;
           PS[1][1] = c->d_ps1_b;

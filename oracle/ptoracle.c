@@ -616,7 +616,8 @@ static v3 path_radiance(const job_t* J, uint32_t g, uint32_t s, uint64_t* nrays)
     } else {
       const pt_prim_shading* sh = &S->shading[prim];
       v3 n0 = ld3(sh->n0), n1 = ld3(sh->n1), n2 = ld3(sh->n2);
-      if (!refa && n0.x == n1.x && n0.y == n1.y && n0.z == n1.z && n1.x == n2.x && n1.y == n2.y && n1.z == n2.z) {
+      /* flat: the three normals identical to the bit (pt_load_scene's test) */
+      if (!refa && memcmp(sh->n0, sh->n1, 3 * sizeof(float)) == 0 && memcmp(sh->n1, sh->n2, 3 * sizeof(float)) == 0) {
         /* flat triangle: the barycentric blend is a positive multiple of n0 */
         ns = nrm(n0);
       } else { /* barycentric shading normal, cu:1213-1221 */
