@@ -13,8 +13,12 @@ A step is one full frame: every rank renders its interleaved 32x32 tiles of the
 1024x1024 image at 256 spp (strong scaling: the frame is fixed, ranks split it),
 then the framebuffer is gathered to rank 0 over RCCL and copied to the host
 (ms/frame ends with the accumulated image on the host; one
-rank: pt_get_image into a pinned buffer).  Rays are every ray cast (camera +
-extension + shadow), counted on the device.
+rank: pt_get_image into a pinned buffer).  Rays are the rays traced (camera +
+extension + shadow), counted on the device: SURVEY §8(d) counts the rays cast
+through the traversal, so camera rays that pt_render resolves on the host
+(pixels whose whole footprint misses the scene's root box: radiance 0, never
+launched; pt_stats.culled_rays) are reported beside the value as
+"culled_rays_per_frame", not in it.
 
 BASELINE config 5 (the dragon proxy at 2048x2048, 1024 spp) runs tiled over
 all ranks when n_gpus >= 8; on fewer GPUs the line carries it as single-GPU
@@ -108,6 +112,10 @@ def parse():
     p.add_argument("--config5", choices=["auto", "on", "off"], default="auto",
                    help="BASELINE config 5 (dragon proxy, 2048x2048, 1024 spp): tiled over all ranks when "
                         "n_gpus >= 8 (auto/on), else one GPU's whole frame and 1/8 tile share (on; auto at 1 GPU)")
+    p.add_argument("--config5-size", default="2048x2048x1024",
+                   help="WxHxSPP of config 5 (BASELINE: 2048x2048x1024; tests shrink it to run the 8-rank branch)")
+    p.add_argument("--save-config5", default=None,
+                   help="rank 0 saves config 5's gathered frame when it runs tiled over >= 8 ranks (.npy; tests)")
     p.add_argument("--no-1spp", action="store_true",
                    help="skip the ms_1spp frame (profiler runs: keeps per-launch averages to full frames)")
     p.add_argument("--stats-in-timed", action="store_true",
@@ -343,7 +351,9 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    rays = ctx.stats().rays  # device counters, no instrumentation needed
+    st0 = ctx.stats()  # device counters, no instrumentation needed
+    # traced rays only: camera rays culled on the host never reach the GPU
+    rays, culled = st0.rays - st0.culled_rays, st0.culled_rays
     instrumented_ms = None
     if not args.stats_in_timed:
         # per-kernel times of one more, instrumented frame (HIP events attached
@@ -374,21 +384,23 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
     # 32 B per visit + 4 B per id they push (into the levels below l0)
     l0 = next((l for l in range(1, 16) if V[l] > 0), 1)
     lvl_bytes = sum(32 * V[l] for l in range(1, 16)) + sum(4 * V[l] for l in range(l0 + 1, 16))
-    root_bytes = 40 * st.rays + 4 * V[l0]
+    traced = st.rays - st.culled_rays
+    root_bytes = 40 * traced + 4 * V[l0]
     lvl_launches = sum(st.level_launches[l] for l in range(1, 16))
     flop_ray, _ = root_leaf_flops(desc)
-    path_flops = flop_ray * st.rays
+    path_flops = flop_ray * traced
     if dist:
         rdev = dev if args.backend == "nccl" else "cpu"
         t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        r = torch.tensor([rays], dtype=torch.float64, device=rdev)
+        r = torch.tensor([rays, culled], dtype=torch.float64, device=rdev)
         dist.all_reduce(r)
-        rays = float(r.item())
-    if args.save_frame and rank == 0 and share is None and name == args.scene and not flags:
+        rays, culled = float(r[0].item()), float(r[1].item())
+    save = getattr(args, "save_path", None) or (args.save_frame if name == args.scene else None)
+    if save and rank == 0 and share is None and not flags:
         import numpy as np
-        np.save(args.save_frame, host.numpy())
+        np.save(save, host.numpy())
     ms_step = elapsed / args.steps * 1e3
     if st.ms_path >= lvl_ms:
         kernel, launches = "k_path_leaf", st.path_launches
@@ -452,6 +464,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
         "value": round(rays / elapsed / 1e6, 2),
         "ms_per_frame": round(ms_step, 2),
         "rays_per_frame": int(rays / args.steps),
+        "culled_rays_per_frame": int(culled / args.steps),
         "batch_paths": st.batch_paths,
         "scene_build_ms": round(build_ms, 1),
         "bvh": {"nodes": int(desc.n_nodes), "levels": int(desc.n_levels), "prims": int(desc.n_prims),
@@ -459,7 +472,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
         "roofline": roof,
         "roofline_other": others,
         "ms_1spp": None if ms_1spp is None else round(ms_1spp, 2),
-        "trace": {"visits_per_ray": round(st.visits / max(1, st.rays), 2),
+        "trace": {"visits_per_ray": round(st.visits / max(1, traced), 2),
                   "instrumented_frame_ms": None if instrumented_ms is None else round(instrumented_ms, 2),
                   "passes": int(st.passes),
                   "ms_per_pass": None if instrumented_ms is None else round(instrumented_ms / max(1, st.passes), 3),
@@ -500,6 +513,7 @@ def compact_line(head, others, cpu, args, world, detail_path=None):
     for o in others:
         r = o.get("roofline") or {}
         c = {"scene": o["scene"], "value": o["value"], "ms_per_frame": o["ms_per_frame"],
+             "culled_rays_per_frame": o["culled_rays_per_frame"],
              "roofline": {k: r.get(k) for k in ("kernel", "frac", "achieved", "traffic")}}
         if o.get("config"):
             c["config"] = o["config"]
@@ -528,6 +542,7 @@ def compact_line(head, others, cpu, args, world, detail_path=None):
         "ms_per_frame": head["ms_per_frame"],
         "ms_1spp": head.get("ms_1spp"),
         "rays_per_frame": head["rays_per_frame"],
+        "culled_rays_per_frame": head["culled_rays_per_frame"],
         "roofline": _short_roof(head["roofline"]),
         "roofline_other": [_short_roof(r) for r in head.get("roofline_other") or []],
         "trace": {k: tr.get(k) for k in ("visits_per_ray", "passes", "ms_per_pass", "ms_path", "ms_levels",
@@ -590,26 +605,28 @@ def main():
         others.append(o)
     import copy
     a5 = copy.copy(args)
-    a5.width = a5.height = 2048
-    a5.spp = 1024
+    a5.width, a5.height, a5.spp = (int(v) for v in args.config5_size.lower().split("x"))
+    a5.save_path = args.save_config5
     if world >= 8 and args.config5 in ("auto", "on"):
         # BASELINE config 5: the dragon proxy at 2048x2048, 1024 spp, the
         # framebuffer tiled over all ranks and gathered over RCCL
         a5.steps, a5.warmup = 1, 1
         o, _ = run_workload("dragon_proxy", a5, ctx, rank, world, dev, dist)
-        o["config"] = "config 5: 2048x2048 1024spp 8 bounces, tiles over all ranks + RCCL gather"
+        o["config"] = (f"config 5: {a5.width}x{a5.height} {a5.spp}spp {a5.bounces} bounces, tiles over all ranks "
+                       f"+ {'RCCL' if args.backend == 'nccl' else args.backend} gather")
         others.append(o)
     elif world == 1 and (args.config5 == "on" or (args.config5 == "auto" and args.configs)):
         # config 5's workload on ONE GPU (not a scaling figure): one rank's
         # share of the 8-GPU tiling (every 8th 32x32 tile), then the whole frame
-        a5.steps, a5.warmup = 1, 1
+        a5.steps, a5.warmup, a5.save_path = 1, 1, None
         o, _ = run_workload("dragon_proxy", a5, ctx, 0, 1, dev, None, share=(0, 8))
-        o["config"] = ("config 5 workload, single GPU: rank 0's 1/8 tile share of 2048x2048 1024spp 8 bounces "
-                       "(the per-GPU work of the 8-GPU run, no gather)")
+        o["config"] = (f"config 5 workload, single GPU: rank 0's 1/8 tile share of {a5.width}x{a5.height} "
+                       f"{a5.spp}spp {a5.bounces} bounces (the per-GPU work of the 8-GPU run, no gather)")
         others.append(o)
-        a5.warmup = 0
+        a5.warmup, a5.save_path = 0, args.save_config5
         o, _ = run_workload("dragon_proxy", a5, ctx, 0, 1, dev, None)
-        o["config"] = "config 5 workload, single GPU: the whole 2048x2048 1024spp 8-bounce frame on one MI355X"
+        o["config"] = (f"config 5 workload, single GPU: the whole {a5.width}x{a5.height} {a5.spp}spp "
+                       f"{a5.bounces}-bounce frame on one MI355X")
         others.append(o)
     if rank == 0:
         cpu = cpu_baseline(head_scene.desc(), args) if world == 1 and not args.no_cpu else None

@@ -73,6 +73,8 @@ struct ShadeArgs {
   pt_camera cam;
   const pt_light* lights;  // pt_scene_desc.lights on the device when n_lights > 1
   uint32_t n_lights;
+  const float* cbox;  // single-leaf scenes: the leaf's primitive-pair boxes (8 floats each)
+  int nclus;
   uint32_t N, npix, sample_base, seed;
   udiv div_npix, div_width;  // p / npix, pixel / width (N and width * height < 2^30)
   int width, height, max_bounces;
@@ -1189,6 +1191,22 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     __syncthreads();
     if (s_skip) return;
   }
+  // PT_ROOT_CLUSTER: the root pass's cluster members into LDS, straight from
+  // memory (no VGPRs; in flight across the shading below): 3 wave loads
+  __shared__ float4 s_rcm[PT_ROOT_CLUSTER && !REFA ? 4 * ROOT_CL_MAX : 1];
+  __shared__ uint32_t s_rci[PT_ROOT_CLUSTER && !REFA ? 2 * ROOT_CL_MAX : 1];
+  if constexpr (PT_ROOT_CLUSTER && !REFA) {
+    static_assert(4 * ROOT_CL_MAX == 2 * 64 && 2 * ROOT_CL_MAX == 64, "three wave-wide LDS loads");
+    typedef __attribute__((address_space(1))) const void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    if (S.T.nc > 0) {
+      const int l = tid & 63;
+      if (wave < 2)
+        __builtin_amdgcn_global_load_lds((gptr_t)(S.T.cmem + wave * 64 + l), (lptr_t)(s_rcm + wave * 64), 16, 0, 0);
+      else if (wave == 2)
+        __builtin_amdgcn_global_load_lds((gptr_t)(S.T.cinfo + l), (lptr_t)s_rci, 4, 0, 0);
+    }
+  }
   const uint32_t p = blockIdx.x * TPB + tid;
   bool new_ext = false, new_sh[NSH];
   RayV ext{mk(0, 0, 0), mk(0, 0, 1), -1.0f}, shr[NSH];
@@ -1295,7 +1313,8 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     anyhit[1 + s] = true;
     n += new_sh[s] ? 1u : 0u;
   }
-  root_pass<1 + NSH, REFA>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh);
+  root_pass<1 + NSH, REFA, false, true>(S.A, S.T, blockIdx.x & (NLANE - 1), id, o, d, tm, valid, anyhit, sh, s_rcm,
+                                        s_rci);
   count_rays(S.rcount, n, sh + MAX_ROOT_TARGETS * 8);
 #if PT_SHADE_TIMING
   __syncthreads();
@@ -1329,7 +1348,8 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
       S.ps0[id1[0]] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
       S.ps1[id1[0]] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
     }
-    root_pass<1, REFA>(S.A, S.T, blockIdx.x & (NLANE - 1), id1, o1, d1, tm1, valid1, anyhit1, sh);
+    root_pass<1, REFA, false, true>(S.A, S.T, blockIdx.x & (NLANE - 1), id1, o1, d1, tm1, valid1, anyhit1, sh, s_rcm,
+                                    s_rci);
     count_rays(S.rcount, st0 ? 1u : 0u, sh + MAX_ROOT_TARGETS * 8);
   }
 }
@@ -1530,6 +1550,62 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
       const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1) : tri_test<REFA>(r.o, r.d, q, bt);
       take_hit(tt, pstart + k, bt, bp);
     }
+  }
+  prim = bp < 0 ? PT_PRIM_NONE : (uint32_t)bp;
+  t = bt;
+}
+
+// PT_PATH_CLUSTER: the closest-hit loop tests the leaf's primitive clusters
+// (one primitive, or two consecutive triangles with nearly the same box: a
+// Cornell wall's halves; ShadeArgs::cbox, host-built, widened by the BVH
+// boxes' guard band: conservative as a leaf box is) only where the lane's ray
+// enters the cluster's box, from records staged in LDS (s_rec; per-lane
+// candidates, so vector reads).  An extension ray inside the Cornell box
+// enters the boxes of the wall it leaves through (and of the light in front of
+// the ceiling): 1-2 clusters of 6.  Candidates run in increasing index with
+// the strict test: the same hit as the full loop (a box missed holds no hit).
+// CBempty 85,000 -> 93,400 Mrays/s, CBspheres 56,950 -> 59,100 (interleaved
+// A/B, 2 runs each; fixed pairs (2i, 2i + 1) instead: CBspheres 50,200, a
+// sphere paired with the ceiling)
+#ifndef PT_PATH_CLUSTER
+#define PT_PATH_CLUSTER 1
+#endif
+constexpr int PATH_CL_PRIMS = 32;  // primitives staged in LDS at most
+template <bool SPH>
+__device__ __forceinline__ void leaf_closest_cl(const ShadeArgs& S, const float4* s_rec, const uint32_t* s_cl,
+                                                int pstart, int pcount, const RayV& r, uint32_t& prim, float& t) {
+  const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(r.d.x)), __builtin_amdgcn_rcpf(safe_dir(r.d.y)),
+                    __builtin_amdgcn_rcpf(safe_dir(r.d.z)));
+  const f3 oi = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
+  const CPTR(f4v) B = (const CPTR(f4v))S.cbox;
+  uint32_t cm = 0u;
+  for (int c = 0; c < S.nclus; ++c) {
+    const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
+    cm |= box_hit(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv, __builtin_inff()) ? (1u << c) : 0u;
+  }
+  float bt = r.tmax;
+  int bp = -1;
+  auto step = [&](int k) {
+    Prim q;
+    q.q0 = s_rec[4 * k];
+    q.q1 = s_rec[4 * k + 1];
+    q.q2 = s_rec[4 * k + 2];
+    q.q3 = s_rec[4 * k + 3];
+    if (SPH && prim_sphere<false>(q)) {
+      const float tt = sphere_test(r.o, r.d, q.q0, q.q1);
+      const bool take = (tt >= 0.0f) & (tt < bt);
+      bt = take ? tt : bt;
+      bp = take ? pstart + k : bp;
+    } else {
+      bw_closest_update(r.o, r.d, q, pstart + k, bt, bp);
+    }
+  };
+  while (cm) {
+    const int c = __builtin_ctz(cm);
+    cm &= cm - 1u;
+    const uint32_t fc = s_cl[c];  // first primitive | count << 16
+    step((int)(fc & 0xFFFFu));
+    if (fc >> 17) step((int)(fc & 0xFFFFu) + 1);
   }
   prim = bp < 0 ? PT_PRIM_NONE : (uint32_t)bp;
   t = bt;
@@ -1750,6 +1826,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       return;
     }
   }
+  // PT_PATH_CLUSTER: the leaf's records in LDS for the per-lane candidate loop
+  __shared__ float4 s_rec[PT_PATH_CLUSTER ? PATH_CL_PRIMS * 4 : 1];
+  __shared__ uint32_t s_cl[PT_PATH_CLUSTER ? PATH_CL_PRIMS : 1];
+  const bool use_cl = PT_PATH_CLUSTER && !REFA && S.nclus > 0 && pcount <= PATH_CL_PRIMS;
+  if (use_cl) {
+    for (int i = threadIdx.x; i < pcount * 4; i += TPB) s_rec[i] = S.prims[(size_t)pstart * 4 + i];
+    for (int i = threadIdx.x; i < S.nclus; i += TPB)
+      s_cl[i] = __float_as_uint(S.cbox[8 * i + 6]) | (__float_as_uint(S.cbox[8 * i + 7]) << 16);
+    __syncthreads();
+  }
   // rays traced by the wave (wave-uniform, counted from ballots: no VGPR)
   uint32_t nrays = 0;
   // wave-uniform: the path region this wave grabs from (its workgroup's, then
@@ -1857,7 +1943,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       float t = 0.0f;
       if (st.flags & F_EXT) {
         // (extension rays have tmax = inf: not carried across iterations)
-        leaf_closest<REFA, SPH>(S.prims, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t);
+        if (PT_PATH_CLUSTER && !REFA && use_cl)
+          leaf_closest_cl<SPH>(S, s_rec, s_cl, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t);
+        else
+          leaf_closest<REFA, SPH>(S.prims, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t);
       }
       bool clear[NSH];
 #pragma unroll

@@ -133,7 +133,19 @@ struct RootTable {
   // scalar loads instead of six dword loads per box from the node array
   float tb[6][MAX_ROOT_TARGETS];
   float ib[6][MAX_INLINE_LEAVES];
+  // candidate clusters of the inline leaves' primitives (PT_ROOT_CLUSTER,
+  // pt_device.hip root_clusters; nc = 0: none): cbox, 8 floats per cluster,
+  // its box as the rows above; cinfo[c] = first member | member count << 16,
+  // cinfo[ROOT_CL_MAX + m] = member m's primitive, its record at cmem[4m ..
+  // 4m + 3] (cmem: 4 ROOT_CL_MAX records, cinfo: 2 ROOT_CL_MAX words, zero-padded:
+  // copied whole into LDS by the shade kernel)
+  int nc;
+  int nc_shadow;  // nc, or 0: shadow rays take the leaf loop (PT_NO_ROOT_CLUSTER_SHADOW)
+  const float* cbox;
+  const float4* cmem;
+  const uint32_t* cinfo;
 };
+constexpr int ROOT_CL_MAX = 32;  // members (and so clusters) at most
 
 struct LevelArgs {
   int first;  // first node id of the level

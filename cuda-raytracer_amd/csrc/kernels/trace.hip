@@ -692,10 +692,30 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 #ifndef PT_ROOT_SELECT
 #define PT_ROOT_SELECT 0
 #endif
-template <int R, bool REFA = false, bool TMIN = false>
+// PT_ROOT_CLUSTER: an extension ray (closest hit) tests the inline leaves'
+// primitive clusters (RootTable::nc: host-built, guard-banded boxes as
+// conservative as the BVH's) only where it enters the cluster's box, each lane
+// its own candidates (the member records staged in LDS by the caller: lrec,
+// linfo = RootTable::cmem, cinfo; CL callers only).  The hit taken is
+// the lowest (t, primitive) over the primitives tested, which is the same over
+// any set that holds every primitive the ray hits: the leaf loop's result.
+// Shadow rays likewise (box tests over their segment, the pre-test on the
+// candidates, done at the first hit; RootTable::nc_shadow = 0 gives them the
+// leaf loop).  CBbunny's 18 inline primitives form 7 clusters (a wall's two
+// triangles, the light's two, the 6 bunny triangles that share a leaf with the
+// walls): the inline-leaf phase of a shade workgroup-pass 24,900 -> 11,150
+// cycles (extension rays 13,900 -> 6,300; PT_SHADE_TIMING), CBbunny 122 ->
+// 114.7 ms per frame, dragon proxy +0.5 %; uncached vector loads of the
+// records instead of LDS lost 2,000 cycles in that phase (the dependent
+// round trips per candidate).
+#ifndef PT_ROOT_CLUSTER
+#define PT_ROOT_CLUSTER 1
+#endif
+template <int R, bool REFA = false, bool TMIN = false, bool CL = false>
 __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T, int lane, const uint32_t (&id)[R],
                                           const f3 (&o)[R], const f3 (&d)[R], const float (&tmax)[R],
-                                          const bool (&valid)[R], const bool (&anyhit)[R], uint32_t* sh) {
+                                          const bool (&valid)[R], const bool (&anyhit)[R], uint32_t* sh,
+                                          const float4* lrec = nullptr, const uint32_t* linfo = nullptr) {
   float tm[R];
   bool pv[R];
   RP_STAMP(0);
@@ -705,57 +725,84 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
     int bp = -1;
     // hits before the ray's t_min do not count (pt_intersect; 0 otherwise)
     const float tlo = (TMIN && valid[j]) ? A.tmin[id[j]] : 0.0f;
+    // the closest-hit rule: ties go to the lowest primitive across the inline
+    // leaves too (their primitive ranges are not in increasing order)
+    auto test = [&](const Prim& q, int gi) {
+      float tt;
+      if (prim_sphere<REFA>(q)) {
+        tt = sphere_test(o[j], d[j], q.q0, q.q1, tlo);
+      } else if (anyhit[j] || PT_ROOT_EXT_PRETEST) {
+        // shadow rays: division-free pre-test (they mostly point away from
+        // the walls or end before them, see tri_outside)
+        float ndd, num;
+        plane_nd<REFA>(o[j], d[j], q, ndd, num);
+        tt = -1.0f;
+        if (!tri_outside<REFA>(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q, bt, tlo);
+      } else {
+        tt = tri_test<REFA>(o[j], d[j], q, bt, tlo);
+      }
+      if constexpr (PT_ROOT_SELECT) {
+        // (as selects: no exec-mask branch per primitive; bp < 0 is the
+        // largest unsigned value)
+        const bool take = (tt >= 0.0f) & ((tt < bt) | ((tt == bt) & ((uint32_t)gi < (uint32_t)bp)));
+        bt = take ? tt : bt;
+        bp = take ? gi : bp;
+      } else if (tt >= 0.0f && (tt < bt || (tt == bt && (bp < 0 || gi < bp)))) {
+        bt = tt;
+        bp = gi;
+      }
+    };
     if (T.ni > 0) {
       const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
                         __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
       const f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
-      for (int i = 0; i < T.ni; ++i) {
-        // the leaf's primitive range in the round trip of its box (the
-        // compiler would read it behind the box test: two more round trips)
-        const int pstart = T.istart[i], pcount = T.icount[i];
-        const float b0 = T.ib[0][i], b1 = T.ib[1][i], b2 = T.ib[2][i], b3 = T.ib[3][i], b4 = T.ib[4][i], b5 = T.ib[5][i];
-        if constexpr (PT_ROOT_RANGE_EARLY) asm volatile("" ::"s"(pstart), "s"(pcount));
-        if (!valid[j] || !box_hit(b0, b1, b2, b3, b4, b5, oi, inv, bt)) continue;
-        constexpr int PS = prim_stride<REFA>();
-        const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * PS);
-        auto test = [&](const Prim& q, int k) {
-          float tt;
-          if (prim_sphere<REFA>(q)) {
-            tt = sphere_test(o[j], d[j], q.q0, q.q1, tlo);
-          } else if (anyhit[j] || PT_ROOT_EXT_PRETEST) {
-            // shadow rays: division-free pre-test (they mostly point away from
-            // the walls or end before them, see tri_outside)
-            float ndd, num;
-            plane_nd<REFA>(o[j], d[j], q, ndd, num);
-            tt = -1.0f;
-            if (!tri_outside<REFA>(ndd, num, bt)) tt = tri_test<REFA>(o[j], d[j], q, bt, tlo);
-          } else {
-            tt = tri_test<REFA>(o[j], d[j], q, bt, tlo);
+      if (CL && !REFA && PT_ROOT_CLUSTER && (anyhit[j] ? T.nc_shadow : T.nc) > 0) {
+        if (valid[j]) {
+          const CPTR(f4v) B = (const CPTR(f4v))T.cbox;
+          uint32_t cm = 0u;
+          for (int c = 0; c < T.nc; ++c) {
+            const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
+            cm |= box_hit(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv, bt) ? (1u << c) : 0u;
           }
-          // ties go to the lowest primitive across the inline leaves too
-          // (their primitive ranges are not in increasing order)
-          if constexpr (PT_ROOT_SELECT) {
-            // (as selects: no exec-mask branch per primitive; bp < 0 is the
-            // largest unsigned value)
-            const bool take = (tt >= 0.0f) & ((tt < bt) | ((tt == bt) & ((uint32_t)(pstart + k) < (uint32_t)bp)));
-            bt = take ? tt : bt;
-            bp = take ? pstart + k : bp;
-          } else if (tt >= 0.0f && (tt < bt || (tt == bt && (bp < 0 || pstart + k < bp)))) {
-            bt = tt;
-            bp = pstart + k;
-          }
-        };
-        int kk = 0;
-        if constexpr (!REFA && PT_ROOT_PAIR) {
-          // two records per scalar round trip
-          for (; kk + 1 < pcount; kk += 2, P += 2 * PS) {
-            Prim qa, qb;
-            load_prim_pair(P, qa, qb);
-            test(qa, kk);
-            test(qb, kk + 1);
+          // (a shadow ray is done at its first hit)
+          while (cm && !(anyhit[j] && bp >= 0)) {
+            const int c = __builtin_ctz(cm);
+            cm &= cm - 1u;
+            const uint32_t fc = linfo[c];
+            const int m0 = (int)(fc & 0xFFFFu), m1 = m0 + (int)(fc >> 16);
+            for (int m = m0; m < m1; ++m) {
+              Prim q;
+              q.q0 = lrec[4 * m];
+              q.q1 = lrec[4 * m + 1];
+              q.q2 = lrec[4 * m + 2];
+              q.q3 = lrec[4 * m + 3];
+              test(q, (int)linfo[ROOT_CL_MAX + m]);
+            }
           }
         }
-        for (; kk < pcount; ++kk, P += PS) test(load_prim<REFA>(P), kk);
+      } else {
+        for (int i = 0; i < T.ni; ++i) {
+          // the leaf's primitive range in the round trip of its box (the
+          // compiler would read it behind the box test: two more round trips)
+          const int pstart = T.istart[i], pcount = T.icount[i];
+          const float b0 = T.ib[0][i], b1 = T.ib[1][i], b2 = T.ib[2][i], b3 = T.ib[3][i], b4 = T.ib[4][i],
+                      b5 = T.ib[5][i];
+          if constexpr (PT_ROOT_RANGE_EARLY) asm volatile("" ::"s"(pstart), "s"(pcount));
+          if (!valid[j] || !box_hit(b0, b1, b2, b3, b4, b5, oi, inv, bt)) continue;
+          constexpr int PS = prim_stride<REFA>();
+          const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * PS);
+          int kk = 0;
+          if constexpr (!REFA && PT_ROOT_PAIR) {
+            // two records per scalar round trip
+            for (; kk + 1 < pcount; kk += 2, P += 2 * PS) {
+              Prim qa, qb;
+              load_prim_pair(P, qa, qb);
+              test(qa, pstart + kk);
+              test(qb, pstart + kk + 1);
+            }
+          }
+          for (; kk < pcount; ++kk, P += PS) test(load_prim<REFA>(P), pstart + kk);
+        }
       }
     }
     if (valid[j]) {  // the whole 32-B record at once (one full half line per ray)

@@ -84,6 +84,11 @@ struct pt_ctx {
   pt_bsdf* d_bsdfs = nullptr;
   pt_light* d_lights = nullptr;  // pt_scene_desc.lights (n_lights > 1)
   uint32_t n_lights = 0;
+  float* d_cbox = nullptr;  // single-leaf scenes: boxes of the leaf's primitive pairs, 8 floats each
+  float* d_rcbox = nullptr;   // root pass: the inline primitives' clusters (RootTable::cbox, root_clusters)
+  float4* d_rcmem = nullptr;  // their member records (RootTable::cmem)
+  uint32_t* d_rcinfo = nullptr;  // their member ranges and primitive ids (RootTable::cinfo)
+  int nclus = 0;
 
   // wavefront buffers (sized for N paths = 2N ray slots)
   uint32_t cap_paths = 0;  // paths the buffers hold
@@ -219,7 +224,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 }
 
 static void free_all(pt_ctx* c) {
-  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_lights, c->d_ray,
+  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_lights, c->d_cbox, c->d_rcbox, c->d_rcmem, c->d_rcinfo, c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_kmap, c->d_res, c->d_wstate, c->d_live, c->d_pool,
                   c->d_pix_of, c->d_accum, c->d_frame, c->d_tmin, c->d_ray_b, c->d_ps0_b, c->d_ps1_b, c->d_ps2_b,
@@ -374,6 +379,132 @@ static void box_row(float (&b)[6][W], int i, const pt_node& parent, int k) {
   b[3][i] = parent.bmax_y[k];
   b[4][i] = parent.bmin_z[k];
   b[5][i] = parent.bmax_z[k];
+}
+
+// Primitive boxes and guard-banded cluster boxes (the candidate loops of
+// k_path_leaf and root_pass).
+static void prim_box(const pt_prim& p, double* lo, double* hi, bool& sph) {
+  const float* q = p.q;
+  uint32_t meta;
+  memcpy(&meta, &q[3], 4);
+  sph = (meta >> 28) == PT_PRIM_SPHERE;
+  for (int k = 0; k < 3; ++k) {
+    lo[k] = sph ? (double)q[k] - q[4] : std::min({(double)q[k], (double)q[4 + k], (double)q[8 + k]});
+    hi[k] = sph ? (double)q[k] + q[4] : std::max({(double)q[k], (double)q[4 + k], (double)q[8 + k]});
+  }
+}
+static double half_area(const double* lo, const double* hi) {
+  const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+  return x * y + y * z + z * x;
+}
+// {xmin, xmax, ymin, ymax, zmin, zmax} (box_hit's order), widened by G and
+// rounded outward to fp32
+static void push_guarded_box(std::vector<float>& cb, const double* lo, const double* hi, double G) {
+  for (int k = 0; k < 3; ++k) {
+    float fl = (float)(lo[k] - G), fh = (float)(hi[k] + G);
+    if ((double)fl > lo[k] - G) fl = std::nextafter(fl, -INFINITY);
+    if ((double)fh < hi[k] + G) fh = std::nextafter(fh, INFINITY);
+    cb.push_back(fl);
+    cb.push_back(fh);
+  }
+}
+static float int_bits(int32_t v) {
+  float f;
+  memcpy(&f, &v, 4);
+  return f;
+}
+
+// The root pass's candidate clusters (RootTable::nc, PT_ROOT_CLUSTER): the
+// inline leaves' primitives grouped bottom-up, merging the two clusters whose
+// union lowers the expected cost most, cost(C) = 1 box test + 2 n(C) A(C) / A
+// (a primitive test ~ 2 box tests, entered by the rays in proportion to the
+// box's surface area A(C) against the whole set's A), at most 8 members: a
+// Cornell wall's two triangles become one cluster, a far light or a few small
+// triangles next to each other another.  Boxes widened by G as the BVH's.
+static int root_clusters(pt_ctx* c, const pt_scene_desc* s, double G) {
+  RootTable& T = c->rt;
+  T.nc = T.nc_shadow = 0;
+  T.cbox = nullptr;
+  T.cmem = nullptr;
+  T.cinfo = nullptr;
+  if (c->root_leaf || T.ni == 0 || getenv("PT_NO_ROOT_CLUSTER")) return PT_OK;
+  struct Cl {
+    double lo[3], hi[3];
+    std::vector<int> mem;
+  };
+  std::vector<Cl> cl;
+  for (int i = 0; i < T.ni; ++i)
+    for (int k = 0; k < T.icount[i]; ++k) {
+      Cl x;
+      bool sph;
+      prim_box(s->prims[T.istart[i] + k], x.lo, x.hi, sph);
+      x.mem = {T.istart[i] + k};
+      cl.push_back(x);
+    }
+  if (cl.empty() || cl.size() > (size_t)ROOT_CL_MAX) return PT_OK;
+  double alo[3] = {INFINITY, INFINITY, INFINITY}, ahi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (const Cl& x : cl)
+    for (int k = 0; k < 3; ++k) {
+      alo[k] = std::min(alo[k], x.lo[k]);
+      ahi[k] = std::max(ahi[k], x.hi[k]);
+    }
+  const double A = half_area(alo, ahi);
+  if (!(A > 0.0)) return PT_OK;
+  auto cost = [&](const double* lo, const double* hi, size_t n) { return 1.0 + 2.0 * (double)n * half_area(lo, hi) / A; };
+  for (;;) {
+    double best = 0.0;
+    size_t ba = 0, bb = 0;
+    for (size_t a = 0; a < cl.size(); ++a)
+      for (size_t b = a + 1; b < cl.size(); ++b) {
+        const size_t n = cl[a].mem.size() + cl[b].mem.size();
+        if (n > 8) continue;
+        double lo[3], hi[3];
+        for (int k = 0; k < 3; ++k) {
+          lo[k] = std::min(cl[a].lo[k], cl[b].lo[k]);
+          hi[k] = std::max(cl[a].hi[k], cl[b].hi[k]);
+        }
+        const double save = cost(cl[a].lo, cl[a].hi, cl[a].mem.size()) + cost(cl[b].lo, cl[b].hi, cl[b].mem.size()) -
+                            cost(lo, hi, n);
+        if (save > best) {
+          best = save;
+          ba = a;
+          bb = b;
+        }
+      }
+    if (best <= 0.0) break;
+    for (int k = 0; k < 3; ++k) {
+      cl[ba].lo[k] = std::min(cl[ba].lo[k], cl[bb].lo[k]);
+      cl[ba].hi[k] = std::max(cl[ba].hi[k], cl[bb].hi[k]);
+    }
+    cl[ba].mem.insert(cl[ba].mem.end(), cl[bb].mem.begin(), cl[bb].mem.end());
+    cl.erase(cl.begin() + (long)bb);
+  }
+  std::vector<float> cb;
+  std::vector<uint32_t> info(2 * ROOT_CL_MAX, 0u);
+  uint32_t nm = 0;
+  for (size_t k = 0; k < cl.size(); ++k) {
+    push_guarded_box(cb, cl[k].lo, cl[k].hi, G);
+    cb.push_back(0.0f);
+    cb.push_back(0.0f);
+    info[k] = nm | (uint32_t)cl[k].mem.size() << 16;
+    for (int p : cl[k].mem) info[ROOT_CL_MAX + nm++] = (uint32_t)p;
+  }
+  int rc;
+  if ((rc = dalloc(c, &c->d_rcbox, cb.size()))) return rc;
+  if ((rc = dalloc(c, &c->d_rcmem, 4 * ROOT_CL_MAX))) return rc;
+  if ((rc = dalloc(c, &c->d_rcinfo, 2 * ROOT_CL_MAX))) return rc;
+  HIPCHK(c, hipMemcpy(c->d_rcbox, cb.data(), cb.size() * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_rcinfo, info.data(), info.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemset(c->d_rcmem, 0, 4 * ROOT_CL_MAX * sizeof(float4)));
+  for (uint32_t m = 0; m < nm; ++m)
+    HIPCHK(c, hipMemcpy(c->d_rcmem + 4 * m, c->d_prims + (size_t)4 * info[ROOT_CL_MAX + m], 4 * sizeof(float4),
+                        hipMemcpyDeviceToDevice));
+  T.nc = (int)cl.size();
+  T.nc_shadow = getenv("PT_NO_ROOT_CLUSTER_SHADOW") ? 0 : T.nc;
+  T.cbox = c->d_rcbox;
+  T.cmem = c->d_rcmem;
+  T.cinfo = c->d_rcinfo;
+  return PT_OK;
 }
 
 static void build_root_table(pt_ctx* c) {
@@ -1205,8 +1336,55 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     for (int k = 0; k < 3; ++k) {
       upd(s->camera.origin[k]);
       upd(s->light.position[k]);
+      for (int l = 0; l < (int)c->n_lights; ++l) upd(s->lights[l].position[k]);
     }
     c->origin_bound = 64.0 * m;
+    // single-leaf scenes: the root leaf's primitives in clusters of one, or
+    // two consecutive triangles whose union box is barely larger than either
+    // (a Cornell wall's two halves), each cluster's box widened by the BVH
+    // boxes' guard band G = 2^-14 M (scene_internal.h box_guard) and rounded
+    // outward: k_path_leaf's closest-hit loop (PT_PATH_CLUSTER) tests a lane's
+    // ray only against the clusters whose box it enters.  Conservative as the
+    // BVH's own leaf boxes are: a triangle-test hit lies within ~2^-18 M of its
+    // triangle for origins up to 64 M.  Record: {xmin, xmax, ymin, ymax, zmin,
+    // zmax} (box_hit's order), first primitive (leaf-relative), count.
+    c->nclus = 0;
+    if (c->root_leaf) {
+      const pt_node& r = c->nodes_host[0];
+      const double G = std::ldexp(m, -14);
+      std::vector<float> cb;
+      for (int i = 0; i < r.prim_count;) {
+        double lo[3], hi[3], lo2[3], hi2[3];
+        bool s1 = false, s2 = true;
+        prim_box(s->prims[r.prim_start + i], lo, hi, s1);
+        int cnt = 1;
+        if (i + 1 < r.prim_count) {
+          prim_box(s->prims[r.prim_start + i + 1], lo2, hi2, s2);
+          double ul[3], uh[3];
+          for (int k = 0; k < 3; ++k) {
+            ul[k] = std::min(lo[k], lo2[k]);
+            uh[k] = std::max(hi[k], hi2[k]);
+          }
+          if (!s1 && !s2 && half_area(ul, uh) <= 1.05 * std::max(half_area(lo, hi), half_area(lo2, hi2))) {
+            cnt = 2;
+            for (int k = 0; k < 3; ++k) {
+              lo[k] = ul[k];
+              hi[k] = uh[k];
+            }
+          }
+        }
+        push_guarded_box(cb, lo, hi, G);
+        cb.push_back(int_bits(i));
+        cb.push_back(int_bits(cnt));
+        i += cnt;
+      }
+      int rc2;
+      if ((rc2 = dalloc(c, &c->d_cbox, std::max<size_t>(8, cb.size())))) return rc2;
+      HIPCHK(c, hipMemcpy(c->d_cbox, cb.data(), cb.size() * sizeof(float), hipMemcpyHostToDevice));
+      c->nclus = (int)(cb.size() / 8);
+    }
+    int rc3;
+    if ((rc3 = root_clusters(c, s, std::ldexp(m, -14)))) return rc3;
   }
   c->have_scene = true;
   c->cull_valid = false;
@@ -1345,6 +1523,8 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.cam = c->camera;
     S.lights = c->d_lights;
     S.n_lights = c->n_lights;
+    S.cbox = c->d_cbox;
+    S.nclus = c->nclus;
     S.npix = npix;
     S.div_npix = udiv_make(npix);
     S.div_width = udiv_make((uint32_t)P->width);
