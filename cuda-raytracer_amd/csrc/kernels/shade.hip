@@ -1611,6 +1611,50 @@ __device__ __forceinline__ void leaf_closest_cl(const ShadeArgs& S, const float4
   t = bt;
 }
 
+// PT_PATH_CLUSTER_OCC: the shadow rays' occlusion query over the same
+// clusters (box tests over the segment [0, tmax], then the candidates' tests,
+// done at the first hit): CBempty 93,200 -> 101,000 Mrays/s, CBspheres
+// 59,080 -> 61,050 (interleaved A/B, 2 runs each)
+#ifndef PT_PATH_CLUSTER_OCC
+#define PT_PATH_CLUSTER_OCC 1
+#endif
+template <bool SPH>
+__device__ __forceinline__ bool leaf_occluded_cl(const ShadeArgs& S, const float4* s_rec, const uint32_t* s_cl,
+                                                 const RayV& r) {
+  const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(r.d.x)), __builtin_amdgcn_rcpf(safe_dir(r.d.y)),
+                    __builtin_amdgcn_rcpf(safe_dir(r.d.z)));
+  const f3 oi = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
+  const CPTR(f4v) B = (const CPTR(f4v))S.cbox;
+  uint32_t cm = 0u;
+  for (int c = 0; c < S.nclus; ++c) {
+    const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
+    cm |= box_hit(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv, r.tmax) ? (1u << c) : 0u;
+  }
+  bool hit = false;
+  auto test = [&](int k) -> bool {
+    Prim q;
+    q.q0 = s_rec[4 * k];
+    q.q1 = s_rec[4 * k + 1];
+    q.q2 = s_rec[4 * k + 2];
+    q.q3 = s_rec[4 * k + 3];
+    if (SPH && prim_sphere<false>(q)) {
+      const float tt = sphere_test(r.o, r.d, q.q0, q.q1);
+      return (tt >= 0.0f) & (tt <= r.tmax);
+    }
+    float ndd, num;
+    plane_nd<false>(r.o, r.d, q, ndd, num);
+    return !tri_outside<false>(ndd, num, r.tmax) && bw_occludes(r.o, r.d, q, num, ndd, r.tmax);
+  };
+  while (cm && !hit) {
+    const int c = __builtin_ctz(cm);
+    cm &= cm - 1u;
+    const uint32_t fc = s_cl[c];
+    hit = test((int)(fc & 0xFFFFu));
+    if (!hit && (fc >> 17)) hit = test((int)(fc & 0xFFFFu) + 1);
+  }
+  return hit;
+}
+
 // any primitive at t in [0, tmax]; triangles whose plane hit is certainly
 // outside [0, tmax] for every lane (tri_outside: shadow rays toward the light
 // mostly point away from the walls or end before them) cost no division
@@ -1962,7 +2006,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
             shr[s] = RayV{mk(q[0], q[TPB], q[2 * TPB]), mk(q[3 * TPB], q[4 * TPB], q[5 * TPB]), q[6 * TPB]};
             C[s] = mk(q[7 * TPB], q[8 * TPB], q[9 * TPB]);
           }
-          clear[s] = !leaf_occluded<REFA, SPH>(S.prims, pstart, pcount, shr[s]);
+          if (PT_PATH_CLUSTER && PT_PATH_CLUSTER_OCC && !REFA && use_cl)
+            clear[s] = !leaf_occluded_cl<SPH>(S, s_rec, s_cl, shr[s]);
+          else
+            clear[s] = !leaf_occluded<REFA, SPH>(S.prims, pstart, pcount, shr[s]);
         }
       }
       bool new_ext, new_sh[NSH];
