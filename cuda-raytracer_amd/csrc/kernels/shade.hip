@@ -1581,7 +1581,7 @@ __device__ __forceinline__ void leaf_closest_cl(const ShadeArgs& S, const float4
   uint32_t cm = 0u;
   for (int c = 0; c < S.nclus; ++c) {
     const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
-    cm |= box_hit(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv, __builtin_inff()) ? (1u << c) : 0u;
+    cm = mask_bit(cm, box_hit_open(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv), c);
   }
   float bt = r.tmax;
   int bp = -1;
@@ -1628,7 +1628,7 @@ __device__ __forceinline__ bool leaf_occluded_cl(const ShadeArgs& S, const float
   uint32_t cm = 0u;
   for (int c = 0; c < S.nclus; ++c) {
     const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
-    cm |= box_hit(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv, r.tmax) ? (1u << c) : 0u;
+    cm = mask_bit(cm, box_hit_seg(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv, r.tmax), c);
   }
   bool hit = false;
   auto test = [&](int k) -> bool {

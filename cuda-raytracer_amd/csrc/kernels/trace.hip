@@ -502,6 +502,32 @@ __device__ __forceinline__ bool box_hit(float bx0, float bx1, float by0, float b
   return tn <= tf;
 }
 
+// The same test for a ray without a far limit (tmax = +inf: its min is the
+// identity here, directions come through safe_dir, so no slab value is NaN)
+__device__ __forceinline__ bool box_hit_open(float bx0, float bx1, float by0, float by1, float bz0, float bz1,
+                                             const f3 oi, const f3 inv) {
+  float tx0 = __builtin_fmaf(bx0, inv.x, -oi.x), tx1 = __builtin_fmaf(bx1, inv.x, -oi.x);
+  float ty0 = __builtin_fmaf(by0, inv.y, -oi.y), ty1 = __builtin_fmaf(by1, inv.y, -oi.y);
+  float tz0 = __builtin_fmaf(bz0, inv.z, -oi.z), tz1 = __builtin_fmaf(bz1, inv.z, -oi.z);
+  float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+  float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+  return tn <= tf;
+}
+// ... and with a far limit as a second compare (tmax not NaN: a shadow
+// segment), which keeps tmax out of the per-box min (the compiler re-emits
+// its NaN canonicalisation inside the box loop otherwise)
+__device__ __forceinline__ bool box_hit_seg(float bx0, float bx1, float by0, float by1, float bz0, float bz1,
+                                            const f3 oi, const f3 inv, float tmax) {
+  float tx0 = __builtin_fmaf(bx0, inv.x, -oi.x), tx1 = __builtin_fmaf(bx1, inv.x, -oi.x);
+  float ty0 = __builtin_fmaf(by0, inv.y, -oi.y), ty1 = __builtin_fmaf(by1, inv.y, -oi.y);
+  float tz0 = __builtin_fmaf(bz0, inv.z, -oi.z), tz1 = __builtin_fmaf(bz1, inv.z, -oi.z);
+  float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+  float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+  return (tn <= tf) & (tn <= tmax);
+}
+// bit c of a mask from a per-lane condition: v_cndmask + v_lshl_or
+__device__ __forceinline__ uint32_t mask_bit(uint32_t m, bool h, int c) { return ((uint32_t)h << c) | m; }
+
 __device__ __forceinline__ float safe_dir(float x) {
   return fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x;
 }
