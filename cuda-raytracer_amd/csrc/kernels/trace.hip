@@ -502,15 +502,27 @@ __device__ __forceinline__ bool box_hit(float bx0, float bx1, float by0, float b
   return tn <= tf;
 }
 
+// one axis's two slab distances b * inv - oi.  PT_BOX_PK: in one
+// v_pk_fma_f32 -- packed fp32 FMAs issue at twice the rate of v_fma_f32 on
+// gfx950 (130 against 74 TFLOP/s on independent chains, scripts/cal/pk_rate.hip),
+// yet the cluster masks of k_path_leaf measured slower with them: CBempty
+// 103,800 -> 100,800 Mrays/s, CBspheres 64,850 -> 62,700 (interleaved A/B, 2
+// runs each); a cluster pair's two triangles on packed fp32 likewise lost
+// (their records and the ray's broadcast pairs spilled at 64 VGPRs)
+#ifndef PT_BOX_PK
+#define PT_BOX_PK 0
+#endif
+__device__ __forceinline__ f2v slab2(float b0, float b1, float inv, float oi) {
+  if constexpr (PT_BOX_PK) return __builtin_elementwise_fma(f2v{b0, b1}, f2v{inv, inv}, f2v{-oi, -oi});
+  return f2v{__builtin_fmaf(b0, inv, -oi), __builtin_fmaf(b1, inv, -oi)};
+}
 // The same test for a ray without a far limit (tmax = +inf: its min is the
 // identity here, directions come through safe_dir, so no slab value is NaN)
 __device__ __forceinline__ bool box_hit_open(float bx0, float bx1, float by0, float by1, float bz0, float bz1,
                                              const f3 oi, const f3 inv) {
-  float tx0 = __builtin_fmaf(bx0, inv.x, -oi.x), tx1 = __builtin_fmaf(bx1, inv.x, -oi.x);
-  float ty0 = __builtin_fmaf(by0, inv.y, -oi.y), ty1 = __builtin_fmaf(by1, inv.y, -oi.y);
-  float tz0 = __builtin_fmaf(bz0, inv.z, -oi.z), tz1 = __builtin_fmaf(bz1, inv.z, -oi.z);
-  float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-  float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+  const f2v tx = slab2(bx0, bx1, inv.x, oi.x), ty = slab2(by0, by1, inv.y, oi.y), tz = slab2(bz0, bz1, inv.z, oi.z);
+  float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fmaxf(fminf(tz.x, tz.y), 0.0f));
+  float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
   return tn <= tf;
 }
 // ... and with a far limit as a second compare (tmax not NaN: a shadow
@@ -518,11 +530,9 @@ __device__ __forceinline__ bool box_hit_open(float bx0, float bx1, float by0, fl
 // its NaN canonicalisation inside the box loop otherwise)
 __device__ __forceinline__ bool box_hit_seg(float bx0, float bx1, float by0, float by1, float bz0, float bz1,
                                             const f3 oi, const f3 inv, float tmax) {
-  float tx0 = __builtin_fmaf(bx0, inv.x, -oi.x), tx1 = __builtin_fmaf(bx1, inv.x, -oi.x);
-  float ty0 = __builtin_fmaf(by0, inv.y, -oi.y), ty1 = __builtin_fmaf(by1, inv.y, -oi.y);
-  float tz0 = __builtin_fmaf(bz0, inv.z, -oi.z), tz1 = __builtin_fmaf(bz1, inv.z, -oi.z);
-  float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-  float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+  const f2v tx = slab2(bx0, bx1, inv.x, oi.x), ty = slab2(by0, by1, inv.y, oi.y), tz = slab2(bz0, bz1, inv.z, oi.z);
+  float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fmaxf(fminf(tz.x, tz.y), 0.0f));
+  float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
   return (tn <= tf) & (tn <= tmax);
 }
 // bit c of a mask from a per-lane condition: v_cndmask + v_lshl_or
