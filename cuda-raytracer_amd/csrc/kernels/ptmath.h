@@ -103,10 +103,15 @@ struct u4 {
 #endif
 // M64: each 32x32 -> 64-bit product as one v_mad_u64_u32 instead of
 // v_mul_hi_u32 + v_mul_lo_u32 (same bits; faster, but 4 more VGPRs live)
+// (PT_DBG_PHILOX_ROUNDS: a timing-only diagnostic build with fewer rounds --
+// not the Philox4x32-10 stream, so no parity)
+#ifndef PT_DBG_PHILOX_ROUNDS
+#define PT_DBG_PHILOX_ROUNDS 10
+#endif
 template <bool M64 = false>
 __device__ __forceinline__ u4 philox(u4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < PT_DBG_PHILOX_ROUNDS; ++r) {
     uint32_t hi0, lo0, hi1, lo1;
     if constexpr (M64) {
       const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;

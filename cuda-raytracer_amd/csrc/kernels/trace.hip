@@ -747,6 +747,14 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 #ifndef PT_ROOT_CLUSTER
 #define PT_ROOT_CLUSTER 1
 #endif
+// PT_ROOT_OCC_AABB: shadow rays pick their candidate clusters by the overlap of
+// their segment's bounding box with the cluster boxes (shade.hip
+// PT_PATH_OCC_AABB).  Off: CBbunny 112.35 -> 113.2 ms per frame with it, the
+// dragon proxy unchanged (the root pass computes the slab test's reciprocals
+// for its target boxes anyway)
+#ifndef PT_ROOT_OCC_AABB
+#define PT_ROOT_OCC_AABB 0
+#endif
 template <int R, bool REFA = false, bool TMIN = false, bool CL = false>
 __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T, int lane, const uint32_t (&id)[R],
                                           const f3 (&o)[R], const f3 (&d)[R], const float (&tmax)[R],
@@ -796,9 +804,25 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
         if (valid[j]) {
           const CPTR(f4v) B = (const CPTR(f4v))T.cbox;
           uint32_t cm = 0u;
-          for (int c = 0; c < T.nc; ++c) {
-            const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
-            cm |= box_hit(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv, bt) ? (1u << c) : 0u;
+          if (anyhit[j] && PT_ROOT_OCC_AABB) {
+            // a shadow segment: its bounding box against the cluster boxes
+            // (k_path_leaf's PT_PATH_OCC_AABB, the same argument)
+            const float tm = fminf(bt, 0x1p127f);
+            const f3 e = mk(__builtin_fmaf(tm, d[j].x, o[j].x), __builtin_fmaf(tm, d[j].y, o[j].y),
+                            __builtin_fmaf(tm, d[j].z, o[j].z));
+            const f3 lo = mk(fminf(o[j].x, e.x), fminf(o[j].y, e.y), fminf(o[j].z, e.z));
+            const f3 hi = mk(fmaxf(o[j].x, e.x), fmaxf(o[j].y, e.y), fmaxf(o[j].z, e.z));
+            for (int c = 0; c < T.nc; ++c) {
+              const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
+              const bool ov =
+                  !((hi.x < b0.x) | (lo.x > b0.y) | (hi.y < b0.z) | (lo.y > b0.w) | (hi.z < b1.x) | (lo.z > b1.y));
+              cm = mask_bit(cm, ov, c);
+            }
+          } else {
+            for (int c = 0; c < T.nc; ++c) {
+              const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
+              cm |= box_hit(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv, bt) ? (1u << c) : 0u;
+            }
           }
           // (a shadow ray is done at its first hit)
           while (cm && !(anyhit[j] && bp >= 0)) {
