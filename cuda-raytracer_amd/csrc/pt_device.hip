@@ -1378,10 +1378,21 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
         cb.push_back(int_bits(cnt));
         i += cnt;
       }
+      // record nclus: the union of the cluster boxes (PT_PATH_EXT_AABB)
+      const int nc = (int)(cb.size() / 8);
+      float ub[6] = {INFINITY, -INFINITY, INFINITY, -INFINITY, INFINITY, -INFINITY};
+      for (int k = 0; k < nc; ++k)
+        for (int a = 0; a < 3; ++a) {
+          ub[2 * a] = std::min(ub[2 * a], cb[8 * k + 2 * a]);
+          ub[2 * a + 1] = std::max(ub[2 * a + 1], cb[8 * k + 2 * a + 1]);
+        }
+      cb.insert(cb.end(), ub, ub + 6);
+      cb.push_back(0.0f);
+      cb.push_back(0.0f);
       int rc2;
       if ((rc2 = dalloc(c, &c->d_cbox, std::max<size_t>(8, cb.size())))) return rc2;
       HIPCHK(c, hipMemcpy(c->d_cbox, cb.data(), cb.size() * sizeof(float), hipMemcpyHostToDevice));
-      c->nclus = (int)(cb.size() / 8);
+      c->nclus = nc;
     }
     int rc3;
     if ((rc3 = root_clusters(c, s, std::ldexp(m, -14)))) return rc3;
