@@ -56,11 +56,14 @@ def test_level_skip_off_matches(gpu_ctx, name, monkeypatch):
     assert np.array_equal(g_skip, pyoracle.intersect(d, rays, use_bvh=True))
 
 
-@pytest.mark.parametrize("env", [("PT_ENTRY_LEVEL", "1"), ("PT_ENTRY_LEVEL", "2"), ("PT_INLINE_MAX", "0")])
+@pytest.mark.parametrize("env", [("PT_ENTRY_LEVEL", "1"), ("PT_ENTRY_LEVEL", "2"), ("PT_INLINE_MAX", "0"),
+                                 ("PT_NO_ROOT_CLUSTER", "1"), ("PT_NO_ROOT_CLUSTER_SHADOW", "1")])
 def test_schedule_options_match(gpu_ctx, env, monkeypatch):
-    """Ray-entry queues below the root targets (PT_ENTRY_LEVEL) and the root
-    pass without inline leaves (PT_INLINE_MAX=0) give the same closest hits and
-    the same image as the default schedule."""
+    """Ray-entry queues below the root targets (PT_ENTRY_LEVEL), the root
+    pass without inline leaves (PT_INLINE_MAX=0) and the inline leaves tested
+    whole instead of by candidate clusters (PT_NO_ROOT_CLUSTER, for shadow
+    rays only PT_NO_ROOT_CLUSTER_SHADOW) give the same closest hits and the
+    same image as the default schedule."""
     sc = load_fixture("CBbunny")
     d = sc.desc()
     rays = np.concatenate([camera_rays(d, 20000, seed=27), interior_rays(d, 20000, seed=28)])
