@@ -425,16 +425,37 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
 // thread's column of sh_lds ([NSH][10][TPB]: o, d, tmax, C) as soon as the NEE
 // sample has made them, instead of staying in registers through the BSDF
 // sample (k_path_leaf: fewer VGPRs live at its peak)
-template <int NSH, bool M64 = false, bool KR = false, bool REFA = false, bool LDSSH = false, bool XL = false>
+// Occ: no immediate occlusion query (the shadow rays are traced later and
+// resolved at the path's next vertex)
+struct NoOcc {
+  __device__ bool operator()(const RayV&) const { return false; }
+};
+template <class T>
+struct imm_occ {
+  static constexpr bool value = true;
+};
+template <>
+struct imm_occ<NoOcc> {
+  static constexpr bool value = false;
+};
+template <int NSH, bool M64 = false, bool KR = false, bool REFA = false, bool LDSSH = false, bool XL = false,
+          class Occ = NoOcc>
 __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, PathState& st, const f3 o,
                                              const f3 d, uint32_t prim, float t, const bool (&clear)[NSH],
                                              f3 (&C)[NSH], bool& new_ext, RayV& ext, bool (&new_sh)[NSH],
-                                             RayV (&shr)[NSH], float* sh_lds = nullptr) {
+                                             RayV (&shr)[NSH], float* sh_lds = nullptr, const Occ& occ = Occ{}) {
+  // IMM (an occlusion query given, k_path_leaf): each NEE shadow ray is
+  // tested where it is made and its contribution added at once -- the same
+  // sum in the same order as resolving it at the next vertex, where it would
+  // be added first -- so nothing is pending: new_sh says which rays were cast
+  // (for the ray count), the flags carry no shadow bit
+  constexpr bool IMM = imm_occ<Occ>::value;
   const uint32_t flags = st.flags;
   // (LDSSH: the radiance and the throughput live in rows 10 NSH .. 10 NSH + 5
-  // of sh_lds, re-read where they are used; a memory clobber after each store
-  // keeps the compiler from carrying them in registers anyway)
-  float* const Lq = LDSSH ? sh_lds + (size_t)10 * NSH * TPB + threadIdx.x : nullptr;
+  // of sh_lds -- rows 0 .. 5 under IMM --, re-read where they are used; a
+  // memory clobber after each store keeps the compiler from carrying them in
+  // registers anyway)
+  float* const Lq = LDSSH ? sh_lds + (size_t)(IMM ? 0 : 10 * NSH) * TPB + threadIdx.x : nullptr;
   float* const Tq = LDSSH ? Lq + 3 * TPB : nullptr;
   f3 T = LDSSH ? mk(0.f, 0.f, 0.f) : st.T;
   auto Tv = [&]() { return LDSSH ? mk(Tq[0], Tq[TPB], Tq[2 * TPB]) : T; };
@@ -605,7 +626,18 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
               const float weight = NSH == 2 ? (nee == 2 ? 0.5f : 1.0f) : -1.0f;
               new_sh[s] = nee_sample<KR, REFA, XL>(S, Tv(), alb, n, pt, ux, uy, weight, C[s], shr[s],
                                                selw);
-              if constexpr (LDSSH) {
+              if constexpr (IMM) {
+                if (new_sh[s] && !occ(shr[s])) {
+                  if constexpr (LDSSH) L = mk(Lq[0], Lq[TPB], Lq[2 * TPB]);
+                  L = L + C[s];
+                  if constexpr (LDSSH) {
+                    Lq[0] = L.x;
+                    Lq[TPB] = L.y;
+                    Lq[2 * TPB] = L.z;
+                    asm volatile("" ::: "memory");
+                  }
+                }
+              } else if constexpr (LDSSH) {
                 float* q = sh_lds + (size_t)s * 10 * TPB + threadIdx.x;
                 q[0 * TPB] = shr[s].o.x;
                 q[1 * TPB] = shr[s].o.y;
@@ -714,7 +746,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
   }
   uint32_t fl = spec | (new_ext ? F_EXT : 0u) | ((vtx + 1u) << 8);
 #pragma unroll
-  for (int s = 0; s < NSH; ++s) fl |= new_sh[s] ? sh_bit(s) : 0u;
+  for (int s = 0; s < NSH; ++s) fl |= (new_sh[s] && !IMM) ? sh_bit(s) : 0u;
   st.flags = fl;
   ext.o = o_new;
   ext.d = d_new;
@@ -1692,6 +1724,15 @@ __device__ __forceinline__ bool leaf_occluded_cl(const ShadeArgs& S, const float
   return hit;
 }
 
+// PT_PATH_IMM_OCC: k_path_leaf tests each shadow ray where its NEE sample
+// makes it (shade_vertex's IMM) instead of keeping it pending in LDS until the
+// path's next vertex: no shadow ray in LDS (16 -> 6 KB of LDS per
+// workgroup), no iteration that only resolves a path's last shadow ray;
+// CBempty 18.07 -> 17.73 ms per frame, CBspheres within noise (interleaved
+// A/B, 2 runs each)
+#ifndef PT_PATH_IMM_OCC
+#define PT_PATH_IMM_OCC 1
+#endif
 // PT_PATH_OCC_AABB: a shadow segment against the clusters as an overlap test of its bounding box with each
 // cluster's box (6 compares with scalar bounds, combined on the scalar unit)
 // instead of the slab test, then the same per-lane candidate loop.
@@ -2000,8 +2041,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
     C[s] = mk(0, 0, 0);
   }
   // PT_PATH_LDS_SH: the pending shadow rays live in LDS between vertices
-  __shared__ float sh_lds[PT_PATH_LDS_SH ? (NSH * 10 + 6) * TPB : 1];
-  float* const Lq = sh_lds + (size_t)10 * NSH * TPB + threadIdx.x;  // (PT_PATH_LDS_SH: the radiance)
+  // PT_PATH_IMM_OCC: shadow rays tested where they are made (shade_vertex's
+  // IMM), none pending between vertices
+  constexpr bool IMMO = PT_PATH_IMM_OCC;
+  __shared__ float sh_lds[PT_PATH_LDS_SH ? ((IMMO ? 0 : NSH * 10) + 6) * TPB : 1];
+  float* const Lq = sh_lds + (size_t)(IMMO ? 0 : 10 * NSH) * TPB + threadIdx.x;  // (PT_PATH_LDS_SH: the radiance)
+  // the occlusion query of one shadow ray
+  auto occluded = [&](const RayV& r) -> bool {
+    if (PT_DBG_SKIP_OCC) return false;
+    if (PT_PATH_CLUSTER && PT_PATH_CLUSTER_OCC && PT_PATH_OCC_AABB && !REFA && use_cl)
+      return leaf_occluded_aabb<SPH>(S, s_rec, s_cl, r);
+    if (PT_PATH_CLUSTER && PT_PATH_CLUSTER_OCC && !REFA && use_cl) return leaf_occluded_cl<SPH>(S, s_rec, s_cl, r);
+    return leaf_occluded<REFA, SPH>(S.prims, pstart, pcount, r);
+  };
   for (;;) {
     // ---- refill idle lanes from the pool (new paths start at their camera ray)
     unsigned long long idle = __ballot(!active);
@@ -2073,8 +2125,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
     }
     // ---- one vertex of every active path: leaf tests, then shade
     nrays += (uint32_t)__popcll(__ballot(active && (st.flags & F_EXT)));
+    if constexpr (!IMMO) {
 #pragma unroll
-    for (int s = 0; s < NSH; ++s) nrays += (uint32_t)__popcll(__ballot(active && (st.flags & sh_bit(s))));
+      for (int s = 0; s < NSH; ++s) nrays += (uint32_t)__popcll(__ballot(active && (st.flags & sh_bit(s))));
+    }
+    uint32_t cast_sh = 0u;  // (IMMO: the shadow rays this vertex cast, counted below in uniform control flow)
     if (active) {
       uint32_t prim = PT_PRIM_NONE;
       float t = 0.0f;
@@ -2093,28 +2148,29 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
           shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
           C[s] = mk(0, 0, 0);
         }
-        if (st.flags & sh_bit(s)) {
-          if constexpr (PT_PATH_LDS_SH) {
+        if (!IMMO && (st.flags & sh_bit(s))) {
+          if constexpr (PT_PATH_LDS_SH && !IMMO) {
             const float* q = sh_lds + (size_t)s * 10 * TPB + threadIdx.x;
             shr[s] = RayV{mk(q[0], q[TPB], q[2 * TPB]), mk(q[3 * TPB], q[4 * TPB], q[5 * TPB]), q[6 * TPB]};
             C[s] = mk(q[7 * TPB], q[8 * TPB], q[9 * TPB]);
           }
-          if (PT_DBG_SKIP_OCC)
-            clear[s] = true;
-          else if (PT_PATH_CLUSTER && PT_PATH_CLUSTER_OCC && PT_PATH_OCC_AABB && !REFA && use_cl)
-            clear[s] = !leaf_occluded_aabb<SPH>(S, s_rec, s_cl, shr[s]);
-          else if (PT_PATH_CLUSTER && PT_PATH_CLUSTER_OCC && !REFA && use_cl)
-            clear[s] = !leaf_occluded_cl<SPH>(S, s_rec, s_cl, shr[s]);
-          else
-            clear[s] = !leaf_occluded<REFA, SPH>(S.prims, pstart, pcount, shr[s]);
+          clear[s] = !occluded(shr[s]);
         }
       }
       bool new_ext, new_sh[NSH];
       RayV e2, s2[NSH];
       // (the sample index is recomputed, not carried: one register less)
-      shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD, REFA, PT_PATH_LDS_SH, XL>(
-          S, S.sample_base + udiv_q(sh_p[threadIdx.x], S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2, new_sh, s2,
-          sh_lds);
+      if constexpr (IMMO) {
+        shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD, REFA, PT_PATH_LDS_SH, XL, decltype(occluded)>(
+            S, S.sample_base + udiv_q(sh_p[threadIdx.x], S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
+            new_sh, s2, sh_lds, occluded);
+#pragma unroll
+        for (int s = 0; s < NSH; ++s) cast_sh |= new_sh[s] ? 1u << s : 0u;  // (cast and resolved)
+      } else {
+        shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD, REFA, PT_PATH_LDS_SH, XL>(
+            S, S.sample_base + udiv_q(sh_p[threadIdx.x], S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
+            new_sh, s2, sh_lds);
+      }
       // (unconditional: without a new extension ray F_EXT is clear and ext is
       // not read again before the lane's next camera ray -- the old ray need
       // not stay live through shade_vertex)
@@ -2132,6 +2188,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
         put_res(S.ps1, sh_p[threadIdx.x], st.L);
         active = false;
       }
+    }
+    if constexpr (IMMO) {
+#pragma unroll
+      for (int s = 0; s < NSH; ++s) nrays += (uint32_t)__popcll(__ballot((cast_sh >> s) & 1u));
     }
   }
   // rays traced (R): one fire-and-forget atomic per wave into its lane's counter
