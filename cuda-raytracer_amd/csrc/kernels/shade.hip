@@ -439,7 +439,7 @@ struct imm_occ<NoOcc> {
   static constexpr bool value = false;
 };
 template <int NSH, bool M64 = false, bool KR = false, bool REFA = false, bool LDSSH = false, bool XL = false,
-          class Occ = NoOcc>
+          class Occ = NoOcc, bool EARLY = PT_RNG_EARLY>
 __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, PathState& st, const f3 o,
                                              const f3 d, uint32_t prim, float t, const bool (&clear)[NSH],
                                              f3 (&C)[NSH], bool& new_ext, RayV& ext, bool (&new_sh)[NSH],
@@ -508,7 +508,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
       // shading record's first load is in flight (they depend on the path
       // and vertex only)
       u4 u_early{0u, 0u, 0u, 0u};
-      if constexpr (PT_RNG_EARLY) u_early = rng<M64>(S.seed, g, sidx, vtx, 0);
+      if constexpr (EARLY) u_early = rng<M64>(S.seed, g, sidx, vtx, 0);
       const uint32_t meta = __float_as_uint(q0.w) & ~SHADE_SMOOTH;
       f3 ns;
       if ((meta >> 28) == PT_PRIM_SPHERE) {
@@ -584,7 +584,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           }
         }
       } else {
-        const u4 u = PT_RNG_EARLY ? u_early : rng<M64>(S.seed, g, sidx, vtx, 0);
+        const u4 u = EARLY ? u_early : rng<M64>(S.seed, g, sidx, vtx, 0);
         f3 dpdu, dpdv;
         if (S.flags & PT_FLAG_REF_GUIDE) {
           // reference quirk (ii): cu:572-574 (NaN when n is (0,-1,0)); n.y <
@@ -1874,6 +1874,16 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
 #ifndef PT_PATH_MAD64
 #define PT_PATH_MAD64 true  // Philox products as v_mad_u64_u32 (CBempty +1.4 %; k_shade_push would lose its 7th wave)
 #endif
+// PT_PATH_RNG_EARLY: k_path_leaf's shade_vertex computes the vertex's Philox
+// words up front (PT_RNG_EARLY, kept for k_shade_push); off in round 5 (in
+// k_path_leaf the shading record is an L2 hit and nothing waits on it long).
+// With the light held in registers (PT_PATH_LIGHT_RELOAD below), at the final
+// round-5 code: CBempty 17.66 -> 17.2 ms per frame, CBspheres 28.6 -> 26.6
+// (v_mul_hi_u32 + v_mul_lo_u32 instead of PT_PATH_MAD64 measured slower in
+// both kernels in that configuration)
+#ifndef PT_PATH_RNG_EARLY
+#define PT_PATH_RNG_EARLY 0
+#endif
 // paths a wave takes from the global counter at a time (CBempty: 128: -1.3 %,
 // 512: +1.6 %, 1024: +1.4 %, 2048: +0.1 % against 256; re-measured in round
 // 3: 1024 -0.3 %, 256 -1.2 % against 512)
@@ -1889,8 +1899,12 @@ constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
 // the light re-read from the kernel arguments at each NEE sample (light_of):
 // SGPR spills 34 -> 13, v_readlane reloads 42 -> 13 (CBempty +0.8 %,
 // CBspheres +1.1 %)
+// (round 5, at the final code: the light held in registers measured faster --
+// alone CBempty 17.55 -> 17.25 ms per frame, CBspheres 28.48 -> 27.03; with
+// PT_PATH_RNG_EARLY off as well see above -- so the reload is off; the
+// kernel-argument layout check stays for the camera reload)
 #ifndef PT_PATH_LIGHT_RELOAD
-#define PT_PATH_LIGHT_RELOAD true
+#define PT_PATH_LIGHT_RELOAD false
 #endif
 // 8 waves per SIMD with the pending shadow rays, their contributions, the
 // radiance and the throughput in LDS (PT_PATH_LDS_SH, 16 KB per workgroup):
@@ -1986,7 +2000,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
   // kernel-argument segment, so S must stay this kernel's FIRST parameter:
   // checked at every launch (wave-uniform, a few cached scalar loads); a
   // mismatch sets ERR_KERNARG and the kernel does nothing (pt_render fails)
-  if (PT_PATH_LIGHT_RELOAD || PT_PATH_CAM_RELOAD) {
+  if (PT_PATH_LIGHT_RELOAD || XL || PT_PATH_CAM_RELOAD) {
     const pt_light a = light_of<true>(S), b = S.light;
     const pt_camera ca = cam_of<true>(S), cb = S.cam;
     uint32_t wa[sizeof a / 4], wb[sizeof b / 4], wc[sizeof ca / 4], wd[sizeof cb / 4];
@@ -2044,6 +2058,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
   // PT_PATH_IMM_OCC: shadow rays tested where they are made (shade_vertex's
   // IMM), none pending between vertices
   constexpr bool IMMO = PT_PATH_IMM_OCC;
+  // (XL: the light re-read keeps the extended-light variants' registers down,
+  // 136 B of scratch without it)
+  constexpr bool M64P = PT_PATH_MAD64, LRP = PT_PATH_LIGHT_RELOAD || XL, EARLYP = PT_PATH_RNG_EARLY;
   __shared__ float sh_lds[PT_PATH_LDS_SH ? ((IMMO ? 0 : NSH * 10) + 6) * TPB : 1];
   float* const Lq = sh_lds + (size_t)(IMMO ? 0 : 10 * NSH) * TPB + threadIdx.x;  // (PT_PATH_LDS_SH: the radiance)
   // the occlusion query of one shadow ray
@@ -2103,7 +2120,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
         const uint32_t p = next + r;
         sh_p[threadIdx.x] = p;
         active = true;
-        const f3 dir = camera_dir<PT_PATH_MAD64, REFA, PT_PATH_CAM_RELOAD>(S, p, st.g);
+        const f3 dir = camera_dir<M64P, REFA, PT_PATH_CAM_RELOAD>(S, p, st.g);
         st.T = mk(1.0f, 1.0f, 1.0f);
         st.L = mk(0.0f, 0.0f, 0.0f);
         if constexpr (PT_PATH_LDS_SH) {
@@ -2161,13 +2178,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       RayV e2, s2[NSH];
       // (the sample index is recomputed, not carried: one register less)
       if constexpr (IMMO) {
-        shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD, REFA, PT_PATH_LDS_SH, XL, decltype(occluded)>(
+        shade_vertex<NSH, M64P, LRP, REFA, PT_PATH_LDS_SH, XL, decltype(occluded), EARLYP>(
             S, S.sample_base + udiv_q(sh_p[threadIdx.x], S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
             new_sh, s2, sh_lds, occluded);
 #pragma unroll
         for (int s = 0; s < NSH; ++s) cast_sh |= new_sh[s] ? 1u << s : 0u;  // (cast and resolved)
       } else {
-        shade_vertex<NSH, PT_PATH_MAD64, PT_PATH_LIGHT_RELOAD, REFA, PT_PATH_LDS_SH, XL>(
+        shade_vertex<NSH, M64P, LRP, REFA, PT_PATH_LDS_SH, XL, NoOcc, EARLYP>(
             S, S.sample_base + udiv_q(sh_p[threadIdx.x], S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
             new_sh, s2, sh_lds);
       }
