@@ -412,8 +412,9 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
                 "flop_per_launch": int(path_flops / max(1, launches)),
                 "valu_busy": pmc_valu_busy(name, kernel),
                 "note": "single-leaf BVH: paths run to completion in registers; FP32 VALU, not HBM, bounds it; "
-                        "achieved counts only the leaf's intersection flops (FMA = 2), valu_busy (PMC) is the "
-                        "share of SIMD cycles issuing any VALU instruction (shading, NEE, RNG included)"}
+                        "achieved counts the reference's intersection work per ray (every leaf primitive, FMA = 2; "
+                        "the kernel's candidate clusters execute only part of it, DESIGN.md §3/§4), valu_busy (PMC) "
+                        "is the share of SIMD cycles issuing any VALU instruction (shading, NEE, RNG included)"}
     else:
         kernel, launches = "k_trace_level", lvl_launches
         ach = (lvl_bytes / (lvl_ms * 1e-3) / 1e9) if lvl_ms > 0 else 0.0
