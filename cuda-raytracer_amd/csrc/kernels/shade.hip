@@ -1234,17 +1234,22 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   }
   // PT_ROOT_CLUSTER: the root pass's cluster members into LDS, straight from
   // memory (no VGPRs; in flight across the shading below): 3 wave loads
-  __shared__ float4 s_rcm[PT_ROOT_CLUSTER && !REFA ? 4 * ROOT_CL_MAX : 1];
-  __shared__ uint32_t s_rci[PT_ROOT_CLUSTER && !REFA ? 2 * ROOT_CL_MAX : 1];
-  if constexpr (PT_ROOT_CLUSTER && !REFA) {
-    static_assert(4 * ROOT_CL_MAX == 2 * 64 && 2 * ROOT_CL_MAX == 64, "three wave-wide LDS loads");
+  // (REFA: the reference-arithmetic records, 6 float4 each: 3 wave loads)
+  constexpr int RPS = REFA ? 6 : 4;
+  __shared__ float4 s_rcm[PT_ROOT_CLUSTER ? RPS * ROOT_CL_MAX : 1];
+  __shared__ uint32_t s_rci[PT_ROOT_CLUSTER ? 2 * ROOT_CL_MAX : 1];
+  if constexpr (PT_ROOT_CLUSTER) {
+    constexpr int NW = RPS * ROOT_CL_MAX / 64;  // wave loads of 64 records' float4s
+    static_assert(RPS * ROOT_CL_MAX % 64 == 0 && 2 * ROOT_CL_MAX == 64 && NW < TPB / 64,
+                  "wave-wide LDS loads: the records, then the info words");
     typedef __attribute__((address_space(1))) const void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
     if (S.T.nc > 0) {
       const int l = tid & 63;
-      if (wave < 2)
-        __builtin_amdgcn_global_load_lds((gptr_t)(S.T.cmem + wave * 64 + l), (lptr_t)(s_rcm + wave * 64), 16, 0, 0);
-      else if (wave == 2)
+      const float4* src = REFA ? S.T.cmem_ref : S.T.cmem;
+      if (wave < NW)
+        __builtin_amdgcn_global_load_lds((gptr_t)(src + wave * 64 + l), (lptr_t)(s_rcm + wave * 64), 16, 0, 0);
+      else if (wave == NW)
         __builtin_amdgcn_global_load_lds((gptr_t)(S.T.cinfo + l), (lptr_t)s_rci, 4, 0, 0);
     }
   }

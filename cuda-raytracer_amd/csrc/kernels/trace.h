@@ -143,6 +143,7 @@ struct RootTable {
   int nc_shadow;  // nc, or 0: shadow rays take the leaf loop (PT_NO_ROOT_CLUSTER_SHADOW)
   const float* cbox;
   const float4* cmem;
+  const float4* cmem_ref;  // the members' PT_FLAG_REF_ARITH records, 6 float4 each (6 ROOT_CL_MAX)
   const uint32_t* cinfo;
 };
 constexpr int ROOT_CL_MAX = 32;  // members (and so clusters) at most

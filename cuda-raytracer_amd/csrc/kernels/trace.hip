@@ -732,7 +732,7 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 // primitive clusters (RootTable::nc: host-built, guard-banded boxes as
 // conservative as the BVH's) only where it enters the cluster's box, each lane
 // its own candidates (the member records staged in LDS by the caller: lrec,
-// linfo = RootTable::cmem, cinfo; CL callers only).  The hit taken is
+// linfo = RootTable::cmem (REFA: cmem_ref), cinfo; CL callers only).  The hit taken is
 // the lowest (t, primitive) over the primitives tested, which is the same over
 // any set that holds every primitive the ray hits: the leaf loop's result.
 // Shadow rays likewise (box tests over their segment, the pre-test on the
@@ -800,7 +800,7 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
       const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
                         __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
       const f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
-      if (CL && !REFA && PT_ROOT_CLUSTER && (anyhit[j] ? T.nc_shadow : T.nc) > 0) {
+      if (CL && PT_ROOT_CLUSTER && (anyhit[j] ? T.nc_shadow : T.nc) > 0) {
         if (valid[j]) {
           const CPTR(f4v) B = (const CPTR(f4v))T.cbox;
           uint32_t cm = 0u;
@@ -832,10 +832,15 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
             const int m0 = (int)(fc & 0xFFFFu), m1 = m0 + (int)(fc >> 16);
             for (int m = m0; m < m1; ++m) {
               Prim q;
-              q.q0 = lrec[4 * m];
-              q.q1 = lrec[4 * m + 1];
-              q.q2 = lrec[4 * m + 2];
-              q.q3 = lrec[4 * m + 3];
+              constexpr int PS = prim_stride<REFA>();
+              q.q0 = lrec[PS * m];
+              q.q1 = lrec[PS * m + 1];
+              q.q2 = lrec[PS * m + 2];
+              q.q3 = lrec[PS * m + 3];
+              if constexpr (REFA) {
+                q.q4 = lrec[PS * m + 4];
+                q.q5 = lrec[PS * m + 5];
+              }
               test(q, (int)linfo[ROOT_CL_MAX + m]);
             }
           }

@@ -87,6 +87,7 @@ struct pt_ctx {
   float* d_cbox = nullptr;  // single-leaf scenes: boxes of the leaf's primitive pairs, 8 floats each
   float* d_rcbox = nullptr;   // root pass: the inline primitives' clusters (RootTable::cbox, root_clusters)
   float4* d_rcmem = nullptr;  // their member records (RootTable::cmem)
+  float4* d_rcmem_ref = nullptr;  // ... as PT_FLAG_REF_ARITH records (RootTable::cmem_ref)
   uint32_t* d_rcinfo = nullptr;  // their member ranges and primitive ids (RootTable::cinfo)
   int nclus = 0;
 
@@ -224,7 +225,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 }
 
 static void free_all(pt_ctx* c) {
-  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_lights, c->d_cbox, c->d_rcbox, c->d_rcmem, c->d_rcinfo, c->d_ray,
+  void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_lights, c->d_cbox, c->d_rcbox, c->d_rcmem, c->d_rcmem_ref, c->d_rcinfo, c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_kmap, c->d_res, c->d_wstate, c->d_live, c->d_pool,
                   c->d_pix_of, c->d_accum, c->d_frame, c->d_tmin, c->d_ray_b, c->d_ps0_b, c->d_ps1_b, c->d_ps2_b,
@@ -425,7 +426,7 @@ static int root_clusters(pt_ctx* c, const pt_scene_desc* s, double G) {
   RootTable& T = c->rt;
   T.nc = T.nc_shadow = 0;
   T.cbox = nullptr;
-  T.cmem = nullptr;
+  T.cmem = T.cmem_ref = nullptr;
   T.cinfo = nullptr;
   if (c->root_leaf || T.ni == 0 || getenv("PT_NO_ROOT_CLUSTER")) return PT_OK;
   struct Cl {
@@ -493,16 +494,22 @@ static int root_clusters(pt_ctx* c, const pt_scene_desc* s, double G) {
   if ((rc = dalloc(c, &c->d_rcbox, cb.size()))) return rc;
   if ((rc = dalloc(c, &c->d_rcmem, 4 * ROOT_CL_MAX))) return rc;
   if ((rc = dalloc(c, &c->d_rcinfo, 2 * ROOT_CL_MAX))) return rc;
+  if ((rc = dalloc(c, &c->d_rcmem_ref, 6 * ROOT_CL_MAX))) return rc;
+  HIPCHK(c, hipMemset(c->d_rcmem_ref, 0, 6 * ROOT_CL_MAX * sizeof(float4)));
   HIPCHK(c, hipMemcpy(c->d_rcbox, cb.data(), cb.size() * sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_rcinfo, info.data(), info.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIPCHK(c, hipMemset(c->d_rcmem, 0, 4 * ROOT_CL_MAX * sizeof(float4)));
-  for (uint32_t m = 0; m < nm; ++m)
+  for (uint32_t m = 0; m < nm; ++m) {
     HIPCHK(c, hipMemcpy(c->d_rcmem + 4 * m, c->d_prims + (size_t)4 * info[ROOT_CL_MAX + m], 4 * sizeof(float4),
                         hipMemcpyDeviceToDevice));
+    HIPCHK(c, hipMemcpy(c->d_rcmem_ref + 6 * m, c->d_prims_ref + (size_t)6 * info[ROOT_CL_MAX + m],
+                        6 * sizeof(float4), hipMemcpyDeviceToDevice));
+  }
   T.nc = (int)cl.size();
   T.nc_shadow = getenv("PT_NO_ROOT_CLUSTER_SHADOW") ? 0 : T.nc;
   T.cbox = c->d_rcbox;
   T.cmem = c->d_rcmem;
+  T.cmem_ref = c->d_rcmem_ref;
   T.cinfo = c->d_rcinfo;
   return PT_OK;
 }
