@@ -139,7 +139,10 @@ struct pt_ctx {
   int path_grid[4] = {0, 0, 0, 0};  // resident workgroups of k_path_leaf<1|2, refa>
   int path_guide = 4;               // k_path_leaf grab schedule (path_grab; PT_PATH_GUIDE)
   int path_regions = 8;             // k_path_leaf path regions / counters (PT_PATH_REGIONS)
-  int path_guided_below = 128;      // guided grabs below this many paths per resident lane (PT_PATH_GUIDED_BELOW)
+  // guided grabs below this many paths per resident lane (PT_PATH_GUIDED_BELOW;
+  // 0, off: at the round-5 kernels even one rank's 1/8 share ran faster
+  // without them, DESIGN.md §4 "path grabs by chunk size")
+  int path_guided_below = 0;
   uint32_t chunk_paths = 1u << 28;  // paths per chunk (PT_CHUNK_PATHS; tests force multi-chunk frames)
 
   // framebuffer
