@@ -370,3 +370,23 @@ def test_scotty_camera_render(gpu_ctx):
     o, _ = pyoracle.image(d, 64, 48, 2, max_bounces=6)
     assert np.array_equal(g, o) and o[..., :3].mean() > 0.01
 
+
+
+@pytest.mark.parametrize("name", ["CBempty", "CBspheres"])
+def test_guided_path_grabs_match(monkeypatch, name):
+    """The guided path-grab schedule of the single-leaf kernel (off by
+    default, PT_PATH_GUIDED_BELOW) gives the oracle's image too: scheduling
+    never changes a path's result."""
+    sc = load_fixture(name)
+    d = sc.desc()
+    monkeypatch.setenv("PT_PATH_GUIDED_BELOW", "100000")
+    ctx = ptrace.Context(0)
+    monkeypatch.delenv("PT_PATH_GUIDED_BELOW")
+    try:
+        ctx.load_scene(sc)
+        ctx.clear()
+        ctx.render(48, 48, 3, max_bounces=8, seed=15618)
+        o, _ = pyoracle.image(d, 48, 48, 3, max_bounces=8, seed=15618)
+        assert np.array_equal(ctx.get_image(), o)
+    finally:
+        ctx.close()
