@@ -406,6 +406,11 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
 #ifndef PT_DBG_SKIP_NEE
 #define PT_DBG_SKIP_NEE 0
 #endif
+// PT_DBG_OCC_MASK_ONLY: the occlusion query computes its candidate mask and
+// tests none of the candidates (timing only)
+#ifndef PT_DBG_OCC_MASK_ONLY
+#define PT_DBG_OCC_MASK_ONLY 0
+#endif
 // One path vertex (restated from cu:380-664, see header): resolves the NSH
 // shadow rays of the previous vertex (C[s] added when unoccluded), shades the
 // extension hit (prim != PT_PRIM_NONE at distance t along ext), and produces
@@ -1784,6 +1789,7 @@ __device__ __forceinline__ bool leaf_occluded_aabb(const ShadeArgs& S, const flo
     const bool ov = !((hi.x < b0.x) | (lo.x > b0.y) | (hi.y < b0.z) | (lo.y > b0.w) | (hi.z < b1.x) | (lo.z > b1.y));
     cm = mask_bit(cm, ov, c);
   }
+  if (PT_DBG_OCC_MASK_ONLY) return cm == 0xFFFFFFFFu;  // (timing diagnostic: the mask without its candidates)
   while (cm && !hit) {
     const int c = __builtin_ctz(cm);
     cm &= cm - 1u;
