@@ -1326,6 +1326,15 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     s_dir[1][tid] = dir.y;
     s_dir[2][tid] = dir.z;
   }
+  if constexpr (PT_ROOT_CLUSTER) {
+    // The LDS copies of the cluster records count against vmcnt, and a
+    // workgroup barrier waits only for lgkmcnt: each loader wave waits for its
+    // copy here, before the barrier that precedes root_pass's reads of s_rcm /
+    // s_rci by every wave (a tail workgroup's idle loader wave reaches it
+    // within a few hundred cycles of issuing the copy).
+    constexpr int NW = RPS * ROOT_CL_MAX / 64;
+    if (S.T.nc > 0 && wave <= NW) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unchanged
+  }
   __syncthreads();
   SHADE_STAMP(4);
   if (fr) {

@@ -302,14 +302,20 @@ int pt_group_render(pt_group* g, const pt_render_params* params) {
     // one grouped round: every member sends its sums (from its accumulation
     // buffer, which pt_render left complete) to member 0, which receives each
     // into its slice
+    // (a failing Send / Recv still closes the group before the error returns:
+    // an open group would swallow the next render's calls)
     GNCCL(g, g->rccl.GroupStart());
-    for (int32_t i = 0; i < n; ++i)
-      if (g->counts[i]) GNCCL(g, g->rccl.Send(sums[i], 4 * (size_t)g->counts[i], ncclFloat32, 0, g->comms[i], g->streams[i]));
-    for (int32_t i = 0; i < n; ++i)
+    ncclResult_t gr = ncclSuccess;
+    const char* what = "ncclSend";
+    for (int32_t i = 0; i < n && gr == ncclSuccess; ++i)
+      if (g->counts[i]) gr = g->rccl.Send(sums[i], 4 * (size_t)g->counts[i], ncclFloat32, 0, g->comms[i], g->streams[i]);
+    if (gr == ncclSuccess) what = "ncclRecv";
+    for (int32_t i = 0; i < n && gr == ncclSuccess; ++i)
       if (g->counts[i])
-        GNCCL(g, g->rccl.Recv(g->d_recv + g->offs[i], 4 * (size_t)g->counts[i], ncclFloat32, i, g->comms[0],
-                              g->streams[0]));
-    GNCCL(g, g->rccl.GroupEnd());
+        gr = g->rccl.Recv(g->d_recv + g->offs[i], 4 * (size_t)g->counts[i], ncclFloat32, i, g->comms[0], g->streams[0]);
+    const ncclResult_t er = g->rccl.GroupEnd();
+    if (gr != ncclSuccess) return gfail(g, PT_E_HIP, std::string(what) + ": " + g->rccl.GetErrorString(gr));
+    if (er != ncclSuccess) return gfail(g, PT_E_HIP, std::string("ncclGroupEnd: ") + g->rccl.GetErrorString(er));
     for (int32_t i = 1; i < n; ++i) {
       GHIP(g, hipSetDevice(g->dev[i]));
       GHIP(g, hipStreamSynchronize(g->streams[i]));

@@ -620,6 +620,9 @@ struct Loader {
     S.light = pt_light{};
     S.light.type = PT_LIGHT_NONE;
     S.lights.clear();
+    // (a spot light is a light instance too: it keeps the default ambient
+    // light out, application.cpp:389, though it adds no light itself)
+    const bool any_light = !lights.empty();
     for (auto& pl : lights) {
       const M4& T = pl.T;
       pt_light L{};
@@ -667,9 +670,10 @@ struct Loader {
       }
       S.lights.push_back(L);
     }
-    // no light at all: Application::load adds the default AmbientLight
-    // (application.cpp:389-392; LightInfo's spectrum (1, 1, 1), light_info.cpp:11)
-    if (S.lights.empty()) {
+    // no light instance at all: Application::load adds the default
+    // AmbientLight (application.cpp:389-392; LightInfo's spectrum (1, 1, 1),
+    // light_info.cpp:11)
+    if (!any_light) {
       pt_light L{};
       L.type = PT_LIGHT_HEMISPHERE;
       L.radiance[0] = L.radiance[1] = L.radiance[2] = 1.0f;

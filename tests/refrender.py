@@ -52,11 +52,12 @@ REFERENCE_IMAGES = {
                       "basic/carim_diffuse.dae"),
 }
 # Scenes the reference renders reproduce with no free factor (scale 1).  The
-# Cornell boxes carry one constant per scene file (their renders are 0.67-0.68
-# of this build's radiance on every wall, floor and ceiling, whatever the
-# distance to the light): the course's copies of those .dae files evidently
-# differed from this repository's (e.g. the light's radiance), so their scale
-# is fitted and only the structure is compared.
+# four Cornell boxes share one constant (rendered without emission through
+# specular bounces, as the reference renders were, they are 0.671-0.681 of
+# this build's radiance on every wall, floor and ceiling, whatever the
+# distance to the light; DESIGN.md §2.2 lists the hypotheses measured), so
+# their scale is fitted -- within that common band -- and the structure is
+# compared.
 EXACT = ("trigs1", "trigs5", "trigs10", "plane4", "floating", "sphere_diffuse", "sphere7_diffuse", "carim_diffuse")
 # A mesh without a material is DiffuseBSDF(1, 1, 1) in this repository
 # (src/dynamic_scene/mesh.cpp:37, what pt_scene_load_dae restates) but was

@@ -50,6 +50,27 @@ def test_group_frame_equals_single_context(gpu_ctx, devices, gather, kind):
         g.close()
 
 
+def test_group_rccl_over_distinct_devices(gpu_ctx):
+    """The grouped RCCL round over every visible GPU: skipped on
+    the one-GPU test boxes, so RCCL parity over several distinct devices is
+    unpinned until a multi-GPU machine runs it."""
+    import torch
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("one GPU visible: RCCL over distinct devices needs two or more")
+    sc = load_fixture("CBbunny")
+    ref = _single(gpu_ctx, sc)
+    g = ptrace.Group(list(range(min(n, 8))), ptrace.PT_GATHER_AUTO)
+    try:
+        assert g.gather_kind == ptrace.PT_GATHER_RCCL, g.note
+        g.load_scene(sc)
+        g.clear()
+        g.render(W, H, SPP, max_bounces=BOUNCES)
+        assert np.array_equal(g.get_image(), ref)
+    finally:
+        g.close()
+
+
 def test_group_rccl_refuses_a_shared_device():
     with pytest.raises(ptrace.PTError) as e:
         ptrace.Group([0, 0], ptrace.PT_GATHER_RCCL)

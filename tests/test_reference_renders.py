@@ -26,18 +26,33 @@ Cornell boxes -- what their reference renders establish (stated tolerances below
     flat in the distance to the light (max/min over distance quintiles
     <= 1.03), while the solid-angle pdf (PT_FLAG_EXACT_LIGHT_PDF) is off by
     the distance itself (>= 1.3 across the side walls);
+  * the renders count no emission reached through a specular bounce (round
+    6): rendered with PT_FLAG_NO_EMISSION (no emitter counted anywhere; the
+    light's own pixels are saturated in the reference and so outside the
+    compared regions), the four Cornell files share one factor, 0.671-0.681
+    at 64 spp, and CBspheres' ceiling, floor and side walls come within 1 %;
+    with this build's default (an emitter seen through a mirror or glass
+    counts) CBspheres' factor drops to 0.622, its ceiling sits 5 % low and
+    CBcoil's ceiling 7 % low -- the caustic paths the reference drops
+    (test_specular_emission_is_not_in_the_reference);
   * paths are not cut at the reference's "max depth 2": with 2 bounces the
     colour bleed and the ceiling (lit only indirectly) fall short (ceiling /
     floor ratio 1.14 at 2 bounces, 1.05 at 3, 1.02 at 4, 1.00 at 8), so the
     comparison renders 8 bounces, the bench's count;
-  * one factor per scene file remains: the reference's radiance is 0.67-0.68
-    x the oracle's on every wall, floor and ceiling of both diffuse scenes,
+  * one factor common to the four Cornell files remains, 0.677 +- 0.005,
     while the exact scenes above (the same tone map, camera, BSDF and light
-    code) need none -- the course's copies of the Cornell .dae files differed
-    from this repository's (e.g. in the light's radiance);
+    code) need none.  Hypotheses measured and rejected:
+    the light node's 0.6 x 0.8 scale (area, sample extent, axes swapped:
+    the factor stays 0.68-0.69 and the distance profiles get worse), the
+    log-average tone map left commented out at pathtracer.cpp:134 (image.h:
+    143-167: it would give 0.04-560), a starter-stub light sampler that
+    always returns the light's centre (sampler.cpp:7-12: hard shadows, worse
+    blocks), the coil's phong colour or the course default DiffuseBSDF(0.5)
+    in place of its <mirror> (the coil stays at 0.14-0.5);
   * residuals after that factor (documented, asserted as bands): the back
-    wall is 5-8 % brighter in the reference, the objects (bunny, spheres)
-    4-14 % darker.
+    wall is 4-8 % brighter in the reference, the objects (bunny, spheres)
+    4-14 % darker, two of CBcoil's three coil regions 0.29-0.31 and the third
+    0.6-0.76 of ours.
 """
 import numpy as np
 import pytest
@@ -72,9 +87,17 @@ def oracle_frame(name, fx, spp, flags=0, max_bounces=8):
     return img
 
 
-def check_diffuse(c, block_frac):
-    """The bands every diffuse scene meets (module docstring)."""
-    assert 0.655 <= c["scale"] <= 0.695, c["scale"]
+# The reference's emission rule for the Cornell renders (module docstring):
+# no emitter counted through a specular bounce.
+CORNELL_FLAGS = ptrace.PT_FLAG_NO_EMISSION
+SPECULAR = ["CBspheres", "CBcoil"]
+CORNELL_SCALE = (0.665, 0.690)  # the one factor common to the four Cornell files
+
+
+def check_cornell(c, block_frac, specular=False):
+    """The bands every Cornell scene meets (module docstring)."""
+    assert CORNELL_SCALE[0] <= c["scale"] <= CORNELL_SCALE[1], c["scale"]
+    mirrors = sorted(r for r in c["rel"] if c["role"][r] == rr.MIRROR)
     for r, v in c["rel"].items():
         role = c["role"][r]
         if role in (rr.SIDE, rr.FLOOR, rr.CEILING):
@@ -83,10 +106,19 @@ def check_diffuse(c, block_frac):
             assert np.all((v >= 1.0) & (v <= 1.10)), (r, v)
         elif role == rr.OBJECT:
             assert np.all((v >= 0.80) & (v <= 1.0)), (r, v)
+        elif role == rr.MIRROR and len(mirrors) == 2:  # CBspheres: the glass and mirror spheres
+            assert np.all(np.abs(v - 1.0) <= 0.06), (r, v)
+        elif role == rr.MIRROR:  # CBcoil's coil (measured 0.29-0.31, 0.29-0.31, 0.6-0.76)
+            assert np.all((v >= 0.25) & (v <= 0.85)), (r, v)
     for r, (near_far, mx) in c["spread"].items():
-        lim = 1.03 if c["role"][r] == rr.SIDE else 1.08
-        assert mx <= lim, (r, rr.ROLE_NAMES[c["role"][r]], near_far, mx)
+        role = c["role"][r]
+        lim = 1.03 if role == rr.SIDE else (1.13 if specular and role in (rr.FLOOR, rr.BACK) else 1.09)
+        assert mx <= lim, (r, rr.ROLE_NAMES[role], near_far, mx)
     assert (c["block_diff"] <= 8).mean() >= block_frac, (c["block_diff"] <= 8).mean()
+
+
+def check_diffuse(c, block_frac):
+    check_cornell(c, block_frac)
 
 
 def check_exact(c, converged=False):
@@ -118,17 +150,27 @@ def test_fixture_framing(fixture):
     assert 0.6 < float(fixture["CBspheres_lambertian"]["zoom"]) < 0.7
 
 
-@pytest.mark.parametrize("name", DIFFUSE)
+@pytest.mark.parametrize("name", DIFFUSE + SPECULAR)
 def test_oracle_matches_reference_render(fixture, name):
-    c = rr.compare(fixture[name], oracle_frame(name, fixture[name], SPP_CPU))
-    check_diffuse(c, block_frac=0.80)
+    c = rr.compare(fixture[name], oracle_frame(name, fixture[name], SPP_CPU, flags=CORNELL_FLAGS))
+    check_cornell(c, block_frac=0.80, specular=name in SPECULAR)
+
+
+def test_specular_emission_is_not_in_the_reference(fixture):
+    """The discriminating check for the emission rule: counting the emitter
+    through the spheres (this build's default) leaves CBspheres' factor
+    outside the common band and its ceiling >= 3 % below the other walls."""
+    c = rr.compare(fixture["CBspheres"], oracle_frame("CBspheres", fixture["CBspheres"], SPP_CPU))
+    assert c["scale"] < CORNELL_SCALE[0] - 0.02, c["scale"]
+    ceil = [v for r, v in c["rel"].items() if c["role"][r] == rr.CEILING]
+    assert len(ceil) == 1 and ceil[0].mean() <= 0.97, ceil
 
 
 def test_exact_light_pdf_does_not_match(fixture):
     """The discriminating check: the solid-angle pdf leaves the distance in
     the ratio (the reference's pdf is light.cpp:81-92's)."""
     c = rr.compare(fixture["CBbunny"], oracle_frame("CBbunny", fixture["CBbunny"], SPP_CPU,
-                                                    flags=ptrace.PT_FLAG_EXACT_LIGHT_PDF))
+                                                    flags=ptrace.PT_FLAG_EXACT_LIGHT_PDF | CORNELL_FLAGS))
     sides = [mx for r, (nf, mx) in c["spread"].items() if c["role"][r] == rr.SIDE]
     assert len(sides) == 2 and min(sides) >= 1.3, sides
 

@@ -157,3 +157,21 @@ def test_camera_scotty_framing():
     assert abs(np.linalg.norm(left) / np.linalg.norm(up) - 640 / 480) < 1e-5
     with pytest.raises(ptrace.PTError):
         ptrace.Scene.from_triangles(np.eye(3, dtype=np.float32).reshape(1, 9)).camera_scotty(64, 64)
+
+
+@pytest.mark.skipif(not REFERENCE_MEDIA.exists(), reason="reference media not present")
+def test_default_ambient_light_only_without_any_light(tmp_path):
+    """Application::load adds its default AmbientLight only when the scene has
+    no light instance at all (application.cpp:389-392): a spot light (a stub
+    in the reference, light.cpp:61-69) adds no light but keeps it out."""
+    text = (REFERENCE_MEDIA / "basic" / "floating.dae").read_text()
+    spot = tmp_path / "spot.dae"
+    spot.write_text(text.replace("<area>", "<spot>").replace("</area>", "</spot>"))
+    d = ptrace.Scene.load_dae(spot).desc()
+    assert d.light.type == ptrace.PT_LIGHT_NONE and d.n_lights == 0
+    dark = tmp_path / "dark.dae"
+    dark.write_text(text.replace('<instance_light url="#Area-light"/>', ""))
+    d = ptrace.Scene.load_dae(dark).desc()
+    assert d.light.type == ptrace.PT_LIGHT_HEMISPHERE and tuple(d.light.radiance) == (1.0, 1.0, 1.0)
+    d = ptrace.Scene.load_dae(REFERENCE_MEDIA / "basic" / "floating.dae").desc()
+    assert d.light.type == ptrace.PT_LIGHT_AREA
