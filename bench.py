@@ -81,6 +81,8 @@ VALU_PEAK_TFLOPS = 157.3    # MI355X FP32 vector peak, same guide
 # the plane offset 6, the division 1, P = o + t d 6, three edge tests 8 each;
 # sphere_test: o - c 3, b 5, c 6, disc 2, sqrt 1, the two roots 2)
 FLOP_TRI, FLOP_SPHERE = 42, 19
+# a cluster box (slab) test: 6 FMAs for the slab distances (compares free)
+FLOP_BOX = 12
 # the newest round's PMC summaries (scripts/profile_round.sh -> profiles/rNN/)
 PMC_DIR = max((d for d in (ROOT / "profiles").glob("r[0-9][0-9]") if any(d.glob("pmc_*.json"))),
               default=ROOT / "profiles" / "r02")
@@ -434,6 +436,31 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
                 "note": "achieved/frac: SURVEY 8(d)'s 32 B per visit + 4 B per push; line_frac: the same visits at "
                         "the 128-B line a random record gather fetches; traffic_gbs: PMC HBM bytes per launch / "
                         "average launch time"}
+    if kernel == "k_path_leaf" and not flags:
+        # the work the kernel executes: one more frame
+        # through the counting build (PT_FLAG_COUNT_TESTS, not timed: the
+        # counters cost it time), priced like the reference's work -- 42 flop
+        # per triangle candidate tested (an upper bound: a shadow candidate the
+        # division-free pre-test rejects does less), 19 per sphere, 12 per
+        # cluster box test (a slab test's 6 FMAs; the shadow rays' box-overlap
+        # tests do compares only) -- over the same launch time as `achieved`
+        ctx.reset_stats()
+        ctx.clear()
+        ctx.render(args.width, args.height, args.spp, max_bounces=args.bounces, seed=args.seed,
+                   batch_paths=args.batch, tile_size=args.tile, rank=t_rank, nranks=t_world,
+                   flags=ptrace.PT_FLAG_COUNT_TESTS)
+        sc = ctx.stats()
+        ntest = sc.prim_tests_tri + sc.prim_tests_sph
+        if ntest > 0 and st.ms_path > 0:
+            ex = FLOP_TRI * sc.prim_tests_tri + FLOP_SPHERE * sc.prim_tests_sph + FLOP_BOX * sc.cluster_box_tests
+            exa = ex / (st.ms_path * 1e-3) / 1e12
+            roof.update({"executed_flop": int(ex / max(1, launches)), "executed_achieved": round(exa, 2),
+                         "executed_frac": round(exa / VALU_PEAK_TFLOPS, 4),
+                         "executed_tests_per_ray": round(ntest / max(1, traced), 3),
+                         "leaf_tests_per_ray": int(desc.nodes[0].prim_count),
+                         "box_tests_per_ray": round(sc.cluster_box_tests / max(1, traced), 3)})
+            roof["note"] += ("; executed_*: the tests the kernel actually ran (PT_FLAG_COUNT_TESTS frame), "
+                             "42 flop per triangle candidate, 19 per sphere, 12 per cluster box test")
     if src:
         roof["traffic_source"] = src
     others = []
@@ -492,7 +519,8 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
 
 LINE_MAX = 12000  # the driver parses the stdout line; keep it well under its limit
 _ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "launches", "avg_launch_us",
-              "flop_per_launch", "bytes_per_launch", "valu_busy", "traffic_gbs", "line_frac")
+              "flop_per_launch", "bytes_per_launch", "valu_busy", "traffic_gbs", "line_frac", "executed_flop",
+              "executed_frac", "executed_tests_per_ray")
 
 
 def _short_roof(r, keys=_ROOF_KEYS):

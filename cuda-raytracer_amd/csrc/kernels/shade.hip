@@ -1615,6 +1615,13 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
   t = bt;
 }
 
+// PT_FLAG_COUNT_TESTS: the primitive tests and cluster box tests a lane
+// executes (the counting variant of k_path_leaf only, CNT; the timed kernels
+// carry none of it)
+struct TestCount {
+  uint32_t tri, sph, box;
+};
+
 // PT_PATH_CLUSTER: the closest-hit loop tests the leaf's primitive clusters
 // (one primitive, or two consecutive triangles with nearly the same box: a
 // Cornell wall's halves; ShadeArgs::cbox, host-built, widened by the BVH
@@ -1640,9 +1647,10 @@ constexpr int PATH_CL_PRIMS = 32;  // primitives staged in LDS at most
 #ifndef PT_PATH_EXT_AABB
 #define PT_PATH_EXT_AABB 0
 #endif
-template <bool SPH>
+template <bool SPH, bool CNT = false>
 __device__ __forceinline__ void leaf_closest_cl(const ShadeArgs& S, const float4* s_rec, const uint32_t* s_cl,
-                                                int pstart, int pcount, const RayV& r, uint32_t& prim, float& t) {
+                                                int pstart, int pcount, const RayV& r, uint32_t& prim, float& t,
+                                                TestCount* tc = nullptr) {
   const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(r.d.x)), __builtin_amdgcn_rcpf(safe_dir(r.d.y)),
                     __builtin_amdgcn_rcpf(safe_dir(r.d.z)));
   const f3 oi = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
@@ -1671,6 +1679,7 @@ __device__ __forceinline__ void leaf_closest_cl(const ShadeArgs& S, const float4
       cm = mask_bit(cm, box_hit_open(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv), c);
     }
   }
+  if constexpr (CNT) tc->box += (uint32_t)S.nclus;
   float bt = r.tmax;
   int bp = -1;
   auto step = [&](int k) {
@@ -1679,6 +1688,10 @@ __device__ __forceinline__ void leaf_closest_cl(const ShadeArgs& S, const float4
     q.q1 = s_rec[4 * k + 1];
     q.q2 = s_rec[4 * k + 2];
     q.q3 = s_rec[4 * k + 3];
+    if constexpr (CNT) {
+      if (SPH && prim_sphere<false>(q)) ++tc->sph;
+      else ++tc->tri;
+    }
     if (SPH && prim_sphere<false>(q)) {
       const float tt = sphere_test(r.o, r.d, q.q0, q.q1);
       const bool take = (tt >= 0.0f) & (tt < bt);
@@ -1767,9 +1780,9 @@ __device__ __forceinline__ bool leaf_occluded_cl(const ShadeArgs& S, const float
 #ifndef PT_PATH_OCC_AABB
 #define PT_PATH_OCC_AABB 1
 #endif
-template <bool SPH>
+template <bool SPH, bool CNT = false>
 __device__ __forceinline__ bool leaf_occluded_aabb(const ShadeArgs& S, const float4* s_rec, const uint32_t* s_cl,
-                                                   const RayV& r) {
+                                                   const RayV& r, TestCount* tc = nullptr) {
   // (an unbounded segment -- a directional or hemisphere light -- as one of
   // length 2^127: no hit lies beyond it, and e stays finite for a unit d)
   const float tm = fminf(r.tmax, 0x1p127f);
@@ -1784,6 +1797,10 @@ __device__ __forceinline__ bool leaf_occluded_aabb(const ShadeArgs& S, const flo
     q.q1 = s_rec[4 * k + 1];
     q.q2 = s_rec[4 * k + 2];
     q.q3 = s_rec[4 * k + 3];
+    if constexpr (CNT) {
+      if (SPH && prim_sphere<false>(q)) ++tc->sph;
+      else ++tc->tri;
+    }
     if (SPH && prim_sphere<false>(q)) {
       const float tt = sphere_test(r.o, r.d, q.q0, q.q1);
       return (tt >= 0.0f) & (tt <= r.tmax);
@@ -1792,6 +1809,7 @@ __device__ __forceinline__ bool leaf_occluded_aabb(const ShadeArgs& S, const flo
     plane_nd<false>(r.o, r.d, q, ndd, num);
     return !tri_outside<false>(ndd, num, r.tmax) && bw_occludes(r.o, r.d, q, num, ndd, r.tmax);
   };
+  if constexpr (CNT) tc->box += (uint32_t)S.nclus;
   uint32_t cm = 0u;
   for (int c = 0; c < S.nclus; ++c) {
     const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
@@ -2011,7 +2029,9 @@ static __device__ unsigned long long g_path_timing[PT_TIMING_WAVES * 8];
 // resident lanes (PT_PATH_GUIDED_BELOW paths per lane, default 128).
 // SPH: the leaf holds spheres (false: the sphere test is not compiled in; the
 // host picks the variant, pt_ctx::has_sphere)
-template <int NSH, bool REFA, bool GUIDED, bool SPH = true, bool XL = false>
+// CNT: the counting variant (PT_FLAG_COUNT_TESTS): executed tests into
+// rcount's lines (words 1-3 of each 128-B counter line)
+template <int NSH, bool REFA, bool GUIDED, bool SPH = true, bool XL = false, bool CNT = false>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
     uint32_t* __restrict__ work, uint32_t nreg, uint32_t tail_unit, uint32_t* __restrict__ err) {
@@ -2083,11 +2103,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
   constexpr bool M64P = PT_PATH_MAD64, LRP = PT_PATH_LIGHT_RELOAD || XL, EARLYP = PT_PATH_RNG_EARLY;
   __shared__ float sh_lds[PT_PATH_LDS_SH ? ((IMMO ? 0 : NSH * 10) + 6) * TPB : 1];
   float* const Lq = sh_lds + (size_t)(IMMO ? 0 : 10 * NSH) * TPB + threadIdx.x;  // (PT_PATH_LDS_SH: the radiance)
+  TestCount tc{0u, 0u, 0u};  // (CNT only)
   // the occlusion query of one shadow ray
   auto occluded = [&](const RayV& r) -> bool {
     if (PT_DBG_SKIP_OCC) return false;
     if (PT_PATH_CLUSTER && PT_PATH_CLUSTER_OCC && PT_PATH_OCC_AABB && !REFA && use_cl)
-      return leaf_occluded_aabb<SPH>(S, s_rec, s_cl, r);
+      return leaf_occluded_aabb<SPH, CNT>(S, s_rec, s_cl, r, &tc);
+    if constexpr (CNT) tc.tri += (uint32_t)pcount;  // (the full loop: an upper bound)
     if (PT_PATH_CLUSTER && PT_PATH_CLUSTER_OCC && !REFA && use_cl) return leaf_occluded_cl<SPH>(S, s_rec, s_cl, r);
     return leaf_occluded<REFA, SPH>(S.prims, pstart, pcount, r);
   };
@@ -2172,10 +2194,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       float t = 0.0f;
       if (st.flags & F_EXT) {
         // (extension rays have tmax = inf: not carried across iterations)
-        if (PT_PATH_CLUSTER && !REFA && use_cl)
-          leaf_closest_cl<SPH>(S, s_rec, s_cl, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t);
-        else
+        if (PT_PATH_CLUSTER && !REFA && use_cl) {
+          leaf_closest_cl<SPH, CNT>(S, s_rec, s_cl, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t, &tc);
+        } else {
+          if constexpr (CNT) tc.tri += (uint32_t)pcount;
           leaf_closest<REFA, SPH>(S.prims, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t);
+        }
       }
       bool clear[NSH];
 #pragma unroll
@@ -2236,6 +2260,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
   if (lid == 0 && w)
     atomicAdd(rcount + (size_t)((blockIdx.x * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16,
               (unsigned long long)w);
+  if constexpr (CNT) {  // the wave's executed tests (64-bit sums: a lane's u32 counts cannot overflow them)
+    unsigned long long v[3] = {tc.tri, tc.sph, tc.box};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v[j] += __shfl_xor(v[j], o);
+    }
+    if (lid == 0) {
+      unsigned long long* line = rcount + (size_t)((blockIdx.x * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16;
+      for (int j = 0; j < 3; ++j)
+        if (v[j]) atomicAdd(line + 1 + j, v[j]);
+    }
+  }
 #if PT_PATH_TIMING
   const uint32_t gw = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   if (lid == 0 && gw < PT_TIMING_WAVES) {

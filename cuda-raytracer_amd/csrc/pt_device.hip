@@ -795,7 +795,14 @@ static int read_device_stats(pt_ctx* c) {
   HIPCHK(c, hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   unsigned long long R = 0;
-  for (int s = 0; s < RCOUNT_SLOTS; ++s) R += rl[s * 16];
+  unsigned long long nt[3] = {0, 0, 0};  // PT_FLAG_COUNT_TESTS: words 1-3 of each counter line
+  for (int s = 0; s < RCOUNT_SLOTS; ++s) {
+    R += rl[s * 16];
+    for (int j = 0; j < 3; ++j) nt[j] += rl[s * 16 + 1 + j];
+  }
+  c->stats.prim_tests_tri = nt[0];
+  c->stats.prim_tests_sph = nt[1];
+  c->stats.cluster_box_tests = nt[2];
   c->stats.rays = R + c->host_rays;
   c->stats.culled_rays = c->host_rays;
   c->stats.visits = st[STAT_V] + R;
@@ -1588,6 +1595,10 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
                           : (kv == 0 ? (sph ? k_path_leaf<1, false, false, true> : k_path_leaf<1, false, false, false>)
                              : kv == 1 ? (sph ? k_path_leaf<2, false, false, true> : k_path_leaf<2, false, false, false>)
                              : kv == 2 ? k_path_leaf<1, true, false, false> : k_path_leaf<2, true, false, false>);
+      // PT_FLAG_COUNT_TESTS: the counting variant (default schedule and
+      // arithmetic, one light; the others count nothing)
+      if ((P->flags & PT_FLAG_COUNT_TESTS) && kv == 0 && !guided && !xl)
+        kpath = sph ? k_path_leaf<1, false, false, true, false, true> : k_path_leaf<1, false, false, false, false, true>;
       // guided grabs from nreg path regions (k_path_leaf path_grab): each
       // region's tail phases begin path_guide chunks per wave before its end
       const uint32_t nreg = (uint32_t)std::max(1, std::min<int>(c->path_regions, (int)std::min<uint32_t>(blocks, PATH_REGIONS_MAX)));

@@ -36,7 +36,8 @@ PT_FLAG_REF_GUIDE = 0x10         # reference quirk (ii)
 PT_FLAG_REF_SCHEDULE = 0x20      # reference quirk (vi): 2 bounces, NEE 2/2/1 weighted 0.5/0.5/1
 PT_FLAG_REF_ARITH = 0x40         # the reference kernels' literal arithmetic (pt_api.h)
 PT_FLAG_EXACT_LIGHT_PDF = 0x80   # area-light NEE with the normalised cosine (default: light.cpp:81-92)
-PT_API_VERSION = 4
+PT_FLAG_COUNT_TESTS = 0x100     # count the single-leaf path kernel's executed primitive tests (pt_stats)
+PT_API_VERSION = 5
 PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION, PT_BSDF_REFRACTION = 0, 1, 2, 3, 4
 PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT, PT_LIGHT_DIRECTIONAL, PT_LIGHT_HEMISPHERE = 0, 1, 2, 3, 4
 PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1
@@ -104,7 +105,8 @@ class pt_stats(C.Structure):
                 ("ms_path", C.c_double), ("path_launches", C.c_uint64),
                 ("shaded", C.c_uint64), ("ms_shade_push", C.c_double), ("shade_launches", C.c_uint64),
                 ("queue_factor", C.c_int32), ("pad_", C.c_int32),
-                ("ms_scan_level", C.c_double * 16), ("culled_rays", C.c_uint64)]
+                ("ms_scan_level", C.c_double * 16), ("culled_rays", C.c_uint64),
+                ("prim_tests_tri", C.c_uint64), ("prim_tests_sph", C.c_uint64), ("cluster_box_tests", C.c_uint64)]
 
 
 class pt_mesh_desc(C.Structure):

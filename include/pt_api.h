@@ -52,8 +52,10 @@ extern "C" {
  * PT_FLAG_EXACT_LIGHT_PDF and the light.cpp pdf as the default (round 5).
  * 3: pt_group_* (several GPUs of one process, RCCL gather; round 5).
  * 4: pt_scene_desc.n_lights / lights, PT_LIGHT_DIRECTIONAL / _HEMISPHERE.
+ * 5: PT_FLAG_COUNT_TESTS and pt_stats.prim_tests_tri / _sph, cluster_box_tests
+ *    (round 6).
  * A client checks pt_api_version() == PT_API_VERSION before passing structs. */
-#define PT_API_VERSION 4
+#define PT_API_VERSION 5
 int pt_api_version(void);
 
 /* ---- error codes ---------------------------------------------------------- */
@@ -318,6 +320,13 @@ int pt_set_camera(pt_ctx* ctx, const pt_camera* camera);
  * test_gpu_reference_renders.py).  This flag takes the normalised cosine,
  * the unbiased estimator of the irradiance, instead.                         */
 #define PT_FLAG_EXACT_LIGHT_PDF 0x80u
+/* Count the primitive tests the single-leaf path kernel executes (the
+ * candidate clusters skip most of the leaf: DESIGN.md §4) into
+ * pt_stats.prim_tests_tri / prim_tests_sph / cluster_box_tests.  A counting
+ * build of the kernel runs instead of the timed one (slower: its time is not
+ * the kernel's); results are unchanged.  The wavefront kernels and the
+ * reference-arithmetic, guided and extended-light path variants count nothing. */
+#define PT_FLAG_COUNT_TESTS 0x100u
 
 typedef struct pt_render_params {
   int32_t width, height;
@@ -462,6 +471,12 @@ typedef struct pt_stats {
                                provably misses the scene's root box: resolved
                                by pt_render's pixel test (radiance 0, no
                                further ray) and counted in `rays` as cast */
+  /* PT_FLAG_COUNT_TESTS (single-leaf path kernel): primitive tests executed
+   * -- a triangle candidate counts once whether or not its division-free
+   * pre-test rejects it -- and cluster box tests (one per cluster per ray) */
+  uint64_t prim_tests_tri;
+  uint64_t prim_tests_sph;
+  uint64_t cluster_box_tests;
 } pt_stats;
 int pt_get_stats(pt_ctx* ctx, pt_stats* out);
 int pt_reset_stats(pt_ctx* ctx);
@@ -494,6 +509,6 @@ PT_STATIC_ASSERT(sizeof(pt_light) == 76, "pt_light layout");
 PT_STATIC_ASSERT(sizeof(pt_camera) == 48, "pt_camera layout");
 PT_STATIC_ASSERT(sizeof(pt_scene_desc) == 208, "pt_scene_desc layout");
 PT_STATIC_ASSERT(sizeof(pt_render_params) == 44, "pt_render_params layout");
-PT_STATIC_ASSERT(sizeof(pt_stats) == 920, "pt_stats layout");
+PT_STATIC_ASSERT(sizeof(pt_stats) == 944, "pt_stats layout");
 #undef PT_STATIC_ASSERT
 #endif /* PT_API_H */

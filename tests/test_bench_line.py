@@ -81,3 +81,20 @@ def test_visible_gpus_from_sysfs(tmp_path):
     assert bench.visible_gpus(tmp_path, env={"HIP_VISIBLE_DEVICES": "0,1"}) == 2
     assert bench.visible_gpus(tmp_path, env={"ROCR_VISIBLE_DEVICES": ""}) == 0
     assert bench.visible_gpus(tmp_path / "missing", env={}) == 0
+
+
+def test_line_carries_executed_work():
+    """The k_path_leaf roofline reports the work the kernel executes (the
+    PT_FLAG_COUNT_TESTS frame: executed_flop per launch, executed_frac) beside
+    the reference's per-ray work (achieved / frac), VERDICT r5 item 3."""
+    head, others, cpu = _canned()
+    r = dict(head["roofline"])
+    r.update({"kernel": "k_path_leaf", "executed_flop": 123456789, "executed_achieved": 30.0,
+              "executed_frac": round(30.0 / bench.VALU_PEAK_TFLOPS, 4), "executed_tests_per_ray": 2.5})
+    head["roofline"] = r
+    out = json.loads(bench.compact_line(head, others, cpu, ARGS, 1))
+    ro = out["roofline"]
+    for k in ("executed_flop", "executed_frac", "executed_tests_per_ray", "frac", "achieved"):
+        assert k in ro, k
+    assert abs(ro["executed_frac"] - 30.0 / bench.VALU_PEAK_TFLOPS) < 1e-4
+    assert bench.FLOP_TRI == 42 and bench.FLOP_SPHERE == 19 and bench.FLOP_BOX == 12

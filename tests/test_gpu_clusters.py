@@ -130,3 +130,33 @@ def test_clustered_render_bit_exact(gpu_ctx, name, flags):
     assert o[..., :3].mean() > 1e-3
     diff = np.abs(g[..., :3] - o[..., :3])
     assert diff.max() == 0.0, (name, float(diff.max()), int((diff > 0).any(axis=-1).sum()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(SCENES) + ["CBempty", "CBspheres"])
+def test_counting_build_same_frame_and_counts(gpu_ctx, name):
+    """PT_FLAG_COUNT_TESTS (the bench's executed-work figures) runs the
+    counting build of k_path_leaf: the frame is the timed build's bit for bit;
+    every traced ray ran one box test per cluster (extension rays the slab
+    test, shadow segments the overlap test), and no ray tested more
+    primitives than the leaf holds."""
+    from conftest import load_fixture
+    sc = SCENES[name]() if name in SCENES else load_fixture(name)
+    d = sc.desc()
+    gpu_ctx.load_scene(sc)
+    imgs, st = [], None
+    for flags in (0, ptrace.PT_FLAG_COUNT_TESTS):
+        gpu_ctx.reset_stats()
+        gpu_ctx.clear()
+        gpu_ctx.render(96, 64, 8, max_bounces=8, seed=15618, flags=flags)
+        imgs.append(gpu_ctx.get_image())
+        st = gpu_ctx.stats()
+    assert np.array_equal(imgs[0], imgs[1])
+    traced = st.rays - st.culled_rays
+    assert traced > 0 and st.cluster_box_tests > 0
+    nclus = st.cluster_box_tests // traced
+    assert st.cluster_box_tests == nclus * traced and 1 <= nclus <= d.nodes[0].prim_count
+    tests = st.prim_tests_tri + st.prim_tests_sph
+    assert 0 < tests < d.nodes[0].prim_count * traced
+    if name == "CBspheres":
+        assert st.prim_tests_sph > 0
