@@ -34,7 +34,7 @@ __device__ __forceinline__ f3 normalize(f3 a) {
 }
 
 // ---- correctly rounded sqrt / reciprocal in a bounded range ----------------------
-// PT_FAST_SQRT: the compiler's IEEE sqrtf is 16 instructions -- v_sqrt_f32
+// The compiler's IEEE sqrtf is 16 instructions -- v_sqrt_f32
 // (within one ulp), the choice among s - ulp, s, s + ulp by the signs of two
 // fma residuals, plus a 2^32 pre-scaling of inputs below 2^-96 (where
 // v_sqrt_f32 loses accuracy) and a special-case select.  sqrt_rn keeps the
@@ -42,12 +42,9 @@ __device__ __forceinline__ f3 normalize(f3 a) {
 // 2^-96.  It is used only where the argument is provably 0 or >= 2^-96 (a
 // squared length of a near-unit vector, 1 - z^2 of a 24-bit uniform), or
 // where a tiny argument's result is discarded (a light sample closer than
-// 1e-2); the oracle takes IEEE sqrtf everywhere.
-#ifndef PT_FAST_SQRT
-#define PT_FAST_SQRT 1
-#endif
+// 1e-2); the oracle takes IEEE sqrtf everywhere.  (Round 4: CBempty +3.5 %
+// with sqrt_rn / rcp_rn against sqrtf and 1.0f / b.)
 __device__ __forceinline__ float sqrt_rn(float x) {
-  if constexpr (!PT_FAST_SQRT) return sqrtf(x);
   const float s = __builtin_amdgcn_sqrtf(x);
   const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
   const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
@@ -58,7 +55,6 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 // reciprocal-and-correction sequence without its range scaling and fixup
 // (trace.hip div_rn, the same 8-instruction form)
 __device__ __forceinline__ float rcp_rn(float b) {
-  if constexpr (!PT_FAST_SQRT) return 1.0f / b;
   const float y0 = __builtin_amdgcn_rcpf(b);
   const float e = __builtin_fmaf(-b, y0, 1.0f);
   const float y1 = __builtin_fmaf(e, y0, y0);
@@ -94,24 +90,16 @@ __device__ __forceinline__ uint32_t udiv_q(uint32_t n, udiv d) {
 struct u4 {
   uint32_t x, y, z, w;
 };
-// PT_PHILOX_KEYS_INLINE: the seed-dependent round keys k0 + r 0x9E3779B9 are
-// recomputed (one s_add each) at every call instead of being hoisted out of
-// the path loop as ten loop-invariant SGPRs, which the register allocator
-// then spills to VGPR lanes (a v_readlane per round)
-#ifndef PT_PHILOX_KEYS_INLINE
-#define PT_PHILOX_KEYS_INLINE 1
-#endif
+// The seed-dependent round keys k0 + r 0x9E3779B9 are recomputed (one s_add
+// each, an empty asm on k0) at every call instead of being hoisted out of the
+// path loop as ten loop-invariant SGPRs, which the register allocator then
+// spills to VGPR lanes (a v_readlane per round): CBempty +1 %, CBspheres +6 %.
 // M64: each 32x32 -> 64-bit product as one v_mad_u64_u32 instead of
 // v_mul_hi_u32 + v_mul_lo_u32 (same bits; faster, but 4 more VGPRs live)
-// (PT_DBG_PHILOX_ROUNDS: a timing-only diagnostic build with fewer rounds --
-// not the Philox4x32-10 stream, so no parity)
-#ifndef PT_DBG_PHILOX_ROUNDS
-#define PT_DBG_PHILOX_ROUNDS 10
-#endif
 template <bool M64 = false>
 __device__ __forceinline__ u4 philox(u4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < PT_DBG_PHILOX_ROUNDS; ++r) {
+  for (int r = 0; r < 10; ++r) {
     uint32_t hi0, lo0, hi1, lo1;
     if constexpr (M64) {
       const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
@@ -123,21 +111,15 @@ __device__ __forceinline__ u4 philox(u4 c, uint32_t k0, uint32_t k1) {
     }
     c = u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
-    if constexpr (PT_PHILOX_KEYS_INLINE) asm volatile("" : "+s"(k0));
+    asm volatile("" : "+s"(k0));
     k1 += 0xBB67AE85u;
   }
   return c;
 }
-// uniform in [0,1): top 24 bits, exact in fp32.  PT_U01_LDEXP: the scaling by
-// 2^-24 as v_ldexp_f32 (the same value: an integer below 2^24 scaled by a
-// power of two), so no VGPR holds the 2^-24 constant for packed multiplies
-#ifndef PT_U01_LDEXP
-#define PT_U01_LDEXP 1
-#endif
-__device__ __forceinline__ float u01(uint32_t v) {
-  if (PT_U01_LDEXP) return __builtin_ldexpf((float)(v >> 8), -24);
-  return (float)(v >> 8) * (1.0f / 16777216.0f);
-}
+// uniform in [0,1): top 24 bits, exact in fp32, scaled by 2^-24 as
+// v_ldexp_f32 (the same value as a multiply: an integer below 2^24 scaled by
+// a power of two), so no VGPR holds the 2^-24 constant for packed multiplies
+__device__ __forceinline__ float u01(uint32_t v) { return __builtin_ldexpf((float)(v >> 8), -24); }
 
 // Random numbers of one path vertex.  counter = (pixel, sample, 2*vertex+call, 'PT')
 template <bool M64 = false>

@@ -29,27 +29,16 @@ constexpr uint32_t F_SPEC = 4u;    // last scattering was specular
 constexpr uint32_t F_SHADOW2 = 8u; // second shadow ray pending in slot 2N + p (reference schedule)
 __device__ __forceinline__ uint32_t sh_bit(int s) { return s ? F_SHADOW2 : F_SHADOW; }
 constexpr float INV_PI = 0.318309886183790671f;
-#ifndef PT_RNG_EARLY
-#define PT_RNG_EARLY 1
-#endif
-#ifndef PT_INV_PI_SGPR
-#define PT_INV_PI_SGPR 1
-#endif
 constexpr float REF_DIFFUSE_MULT = 0.3183f;  // BSDF_DIFFUSE_MULTIPLIER, cu:272
 constexpr float EPS = 1e-3f;  // reference offsets (cu:593, 1224)
 constexpr int SHADE_REC = 5;  // float4 per hit-shading record (ShadeArgs::shade)
 constexpr uint32_t SHADE_SMOOTH = 1u << 27;  // shading-record meta bit: a triangle with distinct vertex normals
-// the diffuse sampling frame: Duff et al.'s branchless orthonormal basis and
-// the sampled direction left unnormalised (default arithmetic; 0: the
-// guide-vector frame and a normalised direction, rounds 1-3)
-#ifndef PT_ONB_DUFF
-#define PT_ONB_DUFF 1
-#endif
-// a flat triangle's shading record holds its normalised normal in the first
-// 16 B (host-computed, bit-identical to the device's normalize)
-#ifndef PT_FLAT_NS
-#define PT_FLAT_NS 1
-#endif
+// The diffuse sampling frame (default arithmetic) is Duff et al.'s
+// branchless orthonormal basis with the sampled direction left unnormalised
+// (round 4, +4.2 % CBempty; rounds 1-3 used a guide-vector frame and a
+// normalised direction).  A flat triangle's shading record holds its
+// normalised normal in the first 16 B (host-computed, bit-identical to the
+// device's normalize; round 4, +2 % CBempty).
 constexpr uint32_t ERR_KERNARG = 2u;  // pt_ctx::d_err bit: k_path_leaf's kernel-argument layout check failed
 
 // slot regions of the tail compaction (ShadeArgs::compact)
@@ -93,11 +82,7 @@ struct ShadeArgs {
   uint32_t* pool;     // POOLS dispensers, CSTRIDE apart (block counters)
   int passes;         // vertices per path at most (max_bounces + 2)
   unsigned long long* rcount;    // rays entering the traversal (RCOUNT_SLOTS counters)
-  uint32_t kshift;    // record-order key of a path: its hit primitive >> kshift (PT_SORT_WAVE)
-  // PT_SORT_KMAP: the key is kmap[hit primitive >> kmshift] instead, the root
-  // target whose subtree holds the primitive (KMAP_SIZE entries)
-  const uint32_t* __restrict__ kmap;
-  uint32_t kmshift;
+  uint32_t kshift;    // record-order key of a path: its hit primitive >> kshift (shade_slot)
   // Tail compaction (pt_render): once every path of the chunk has started and
   // few slots are still live, one shade pass writes the continuing paths'
   // state and new rays densely into a second set of buffers, and the passes
@@ -331,7 +316,7 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
       // (1/pi from an SGPR: as a literal the compiler paired it with another
       // product in a v_pk_mul_f32 and spilled the VGPR pair holding it)
       float inv_pi = INV_PI;
-      if constexpr (PT_INV_PI_SGPR) asm volatile("" : "+s"(inv_pi));
+      asm volatile("" : "+s"(inv_pi));
       const float lc = (S.flags & PT_FLAG_EXACT_LIGHT_PDF) ? cosl : cu;
       float scale = ((cosn * (L.area * -lc)) / sq) * inv_pi;
       if (weight >= 0.0f) scale = scale * weight;
@@ -397,20 +382,6 @@ __device__ __forceinline__ bool nee_sample(const ShadeArgs& S, const f3 T, const
   return false;
 }
 
-// timing-only diagnostic builds (no parity): PT_DBG_SKIP_OCC treats every
-// shadow ray as unoccluded without testing it, PT_DBG_SKIP_NEE takes no NEE
-// sample (the paths themselves are unchanged by either)
-#ifndef PT_DBG_SKIP_OCC
-#define PT_DBG_SKIP_OCC 0
-#endif
-#ifndef PT_DBG_SKIP_NEE
-#define PT_DBG_SKIP_NEE 0
-#endif
-// PT_DBG_OCC_MASK_ONLY: the occlusion query computes its candidate mask and
-// tests none of the candidates (timing only)
-#ifndef PT_DBG_OCC_MASK_ONLY
-#define PT_DBG_OCC_MASK_ONLY 0
-#endif
 // One path vertex (restated from cu:380-664, see header): resolves the NSH
 // shadow rays of the previous vertex (C[s] added when unoccluded), shades the
 // extension hit (prim != PT_PRIM_NONE at distance t along ext), and produces
@@ -444,7 +415,7 @@ struct imm_occ<NoOcc> {
   static constexpr bool value = false;
 };
 template <int NSH, bool M64 = false, bool KR = false, bool REFA = false, bool LDSSH = false, bool XL = false,
-          class Occ = NoOcc, bool EARLY = PT_RNG_EARLY>
+          class Occ = NoOcc, bool EARLY = true>
 __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, PathState& st, const f3 o,
                                              const f3 d, uint32_t prim, float t, const bool (&clear)[NSH],
                                              f3 (&C)[NSH], bool& new_ext, RayV& ext, bool (&new_sh)[NSH],
@@ -509,9 +480,9 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
       // distinct vertex normals (or the reference arithmetic's blend)
       const float4* Q = S.shade + (size_t)prim * SHADE_REC;
       const float4 q0 = Q[0];
-      // PT_RNG_EARLY: the vertex's Philox words are computed while the
-      // shading record's first load is in flight (they depend on the path
-      // and vertex only)
+      // EARLY: the vertex's Philox words are computed while the shading
+      // record's first load is in flight (they depend on the path and vertex
+      // only; the shade kernel: +0.1-0.6 % on every workload, round 4)
       u4 u_early{0u, 0u, 0u, 0u};
       if constexpr (EARLY) u_early = rng<M64>(S.seed, g, sidx, vtx, 0);
       const uint32_t meta = __float_as_uint(q0.w) & ~SHADE_SMOOTH;
@@ -523,13 +494,13 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
         if (!REFA && flat) {
           // flat triangle (n0 == n1 == n2): the barycentric blend is a
           // positive multiple of n0, so its normalisation is normalize(n0)
-          // (PT_FLAT_NS: computed on the host, pt_load_scene)
-          ns = PT_FLAT_NS ? xyz(q0) : normalize(xyz(q0));
+          // (computed on the host, pt_load_scene)
+          ns = xyz(q0);
         } else {
           const float4 q1 = Q[1], q2 = Q[2], q3 = Q[3], q4 = Q[4];
           const f3 n1 = mk(q1.w, q2.w, q3.w), n2 = xyz(q4);
           // (a flat triangle's first 16 B hold normalize(n0): its raw n0 is n2)
-          const f3 n0 = (PT_FLAT_NS && flat) ? n2 : xyz(q0);
+          const f3 n0 = flat ? n2 : xyz(q0);
           // barycentric shading normal (cu:1213-1221)
           const f3 A = xyz(q1), B = xyz(q2), Cv = xyz(q3);
           float total = length(cross(A - B, B - Cv));
@@ -597,7 +568,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           const f3 guide = (n.y <= 1e-4f) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
           dpdu = normalize(cross(guide, n));
           dpdv = normalize(cross(dpdu, n));
-        } else if (!REFA && PT_ONB_DUFF) {
+        } else if (!REFA) {
           // branchless orthonormal basis (Duff et al., JCGT 6(1), 2017):
           // dpdu x dpdv = n; one reciprocal of sign(n.z) + n.z in [1, 2]
           // instead of a cross product, a normalisation and a second cross
@@ -607,7 +578,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           const float sx = sg * n.x;
           dpdu = mk(__builtin_fmaf(sx * n.x, a, 1.0f), sg * b, -sx);
           dpdv = mk(b, __builtin_fmaf(n.y * n.y, a, sg), -n.y);
-        } else {
+        } else {  // (REFA without the guide quirk)
           const f3 guide = (fabsf(n.x) < 0.9f) ? mk(1.0f, 0.0f, 0.0f) : mk(0.0f, 1.0f, 0.0f);
           dpdu = normalize_u(cross(guide, n));  // (|cross|^2 >= 0.19)
           dpdv = cross(n, dpdu);
@@ -616,7 +587,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           const f3 alb = ld3(B.albedo);
           // next-event estimation toward the scene light (cu:380-481); the
           // reference schedule takes 2, 2, 1 samples at vertices 1, 2, 3
-          const int nee = (emitter || PT_DBG_SKIP_NEE) ? 0 : (NSH == 2 && vtx <= 2u) ? 2 : 1;
+          const int nee = emitter ? 0 : (NSH == 2 && vtx <= 2u) ? 2 : 1;
 #pragma unroll
           for (int s = 0; s < NSH; ++s) {
             if (s < nee) {
@@ -674,14 +645,10 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
             x = r * cs;
             y = r * sn;
           }
-          if (REFA || PT_ONB_DUFF) {  // cu:631-637: not normalised (the basis is orthonormal: |d_new| = 1 + O(ulp))
-            d_new = mk(__builtin_fmaf(y, dpdv.x, __builtin_fmaf(x, dpdu.x, n.x * z)),
-                       __builtin_fmaf(y, dpdv.y, __builtin_fmaf(x, dpdu.y, n.y * z)),
-                       __builtin_fmaf(y, dpdv.z, __builtin_fmaf(x, dpdu.z, n.z * z)));
-          } else {
-            d_new = normalize_u(mk(n.x * z + x * dpdu.x + y * dpdv.x, n.y * z + x * dpdu.y + y * dpdv.y,
-                                 n.z * z + x * dpdu.z + y * dpdv.z));
-          }
+          // cu:631-637: not normalised (the basis is orthonormal: |d_new| = 1 + O(ulp))
+          d_new = mk(__builtin_fmaf(y, dpdv.x, __builtin_fmaf(x, dpdu.x, n.x * z)),
+                     __builtin_fmaf(y, dpdv.y, __builtin_fmaf(x, dpdu.y, n.y * z)),
+                     __builtin_fmaf(y, dpdv.z, __builtin_fmaf(x, dpdu.z, n.z * z)));
           if (S.flags & PT_FLAG_COSINE_DIFFUSE) {
             Tset(mulv(Tv(), alb));
           } else {
@@ -759,26 +726,16 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
 }
 
 // A finished path's radiance in the chunk's result buffer: 12 B per path
-// (PT_RES12; the buffer is read once more by k_accum, 16 B per path -> 12 B is
-// a quarter of that stream), else a float4.
-#ifndef PT_RES12
-#define PT_RES12 1
-#endif
+// (the buffer is read once more by k_accum: 16 B per path -> 12 B is a quarter
+// of that stream; round 2, k_accum 0.74 -> ~0.5 ms per CBempty frame).
 struct res3 {
   float x, y, z;
 };
 __device__ __forceinline__ void put_res(float4* res, uint32_t P, const f3 L) {
-  if (PT_RES12)
-    reinterpret_cast<res3*>(res)[P] = res3{L.x, L.y, L.z};
-  else
-    res[P] = make_float4(L.x, L.y, L.z, 0.0f);
+  reinterpret_cast<res3*>(res)[P] = res3{L.x, L.y, L.z};
 }
 __device__ __forceinline__ f3 get_res(const float4* res, size_t P) {
-  if (PT_RES12) {
-    const res3 r = reinterpret_cast<const res3*>(res)[P];
-    return mk(r.x, r.y, r.z);
-  }
-  const float4 r = res[P];
+  const res3 r = reinterpret_cast<const res3*>(res)[P];
   return mk(r.x, r.y, r.z);
 }
 
@@ -790,14 +747,13 @@ __device__ __forceinline__ void path_pixel(const ShadeArgs& S, uint32_t P, uint3
 }
 
 // Philox products as v_mad_u64_u32 in the wavefront shade kernel too (the
-// same bits; k_path_leaf uses them, PT_PATH_MAD64)
-#ifndef PT_SHADE_MAD64
-#define PT_SHADE_MAD64 true
-#endif
+// same bits as k_path_leaf's; 62 VGPRs, still 8 waves; CBbunny / dragon proxy
+// +1.1 %, round 3)
+constexpr bool SHADE_MAD64 = true;
 // Slot states returned by shade_slot
 constexpr int SLOT_FREE = 0, SLOT_LIVE = 1, SLOT_ENDED = 2;
 
-// Record order (PT_SORT_WAVE): a wave writes its paths' new state and ray
+// Record order: a wave writes its paths' new state and ray
 // records back into its own 64 slots in the order of a key -- the primitive
 // the path's extension ray hit, in SORT_KEYS equal ranges of the BVH order,
 // i.e. roughly the subtree the new rays start in; camera rays, misses and
@@ -806,39 +762,19 @@ constexpr int SLOT_FREE = 0, SLOT_LIVE = 1, SLOT_ENDED = 2;
 // kernel's gather of consecutive queue entries shares 128-B lines instead of
 // fetching one line per ray.  The slots of a path change from pass to pass
 // within its wave; results do not depend on it (a permutation of the wave's
-// slots, read before any is written).
-#ifndef PT_SORT_WAVE
-#define PT_SORT_WAVE 3
-#endif
-#ifndef PT_SORT_KEY_BITS
-#define PT_SORT_KEY_BITS 4
-#endif
-constexpr uint32_t SORT_KEY_BITS = PT_SORT_KEY_BITS, SORT_KEYS = 1u << SORT_KEY_BITS;
-// Rank of this lane among the wave's active lanes ordered by (key, lane);
-// key in [0, SORT_KEYS].
-__device__ __forceinline__ uint32_t wave_key_rank(uint32_t key) {
-  uint32_t rank = 0, base = 0;
-#pragma unroll
-  for (uint32_t c = 0; c <= SORT_KEYS; ++c) {
-    const unsigned long long m = __ballot(key == c);
-    rank = key == c ? base + mbcnt64(m) : rank;
-    base += (uint32_t)__popcll(m);
-  }
-  return rank;
-}
-// PT_SORT_WAVE 3: the key is taken after shading -- the hit primitive's range
-// and the octant of the new extension ray's direction (PT_SORT_DIR) -- and
-// ranked through a per-wave LDS histogram (one LDS atomic per lane, a 64-lane
-// scan over the bins) instead of one ballot per key.  The order of lanes with
-// equal keys is the order the LDS serves the atomics in; results do not
-// depend on slots.
-#ifndef PT_SORT_DIR
-#define PT_SORT_DIR 0
-#endif
-constexpr uint32_t HIST_BINS = 256;  // >= SORT_KEYS * 8 + 1 (and > KMAP keys)
-#ifndef PT_SORT_KMAP
-#define PT_SORT_KMAP 0
-#endif
+// slots, read before any is written).  CBbunny level 2 19.6 -> 15.7 ms,
+// frame +3.9 %; dragon proxy +2.0 % (round 2).
+// The key is taken after shading and ranked through a per-wave LDS histogram
+// (one LDS atomic per lane, a 64-lane scan over the bins) instead of one
+// ballot per key (-1.5-2 ms of shade kernel, round 2).  The order of lanes
+// with equal keys is the order the LDS serves the atomics in; results do not
+// depend on slots.  Measured and dropped: the same order over the whole
+// workgroup (two barriers and an LDS scan: levels 1-2 % faster, but the shade
+// kernel lost its 8th wave, -2.7 % on CBbunny), 32 key ranges (within noise),
+// the octant of the new ray's direction in the key (within noise), the root
+// target whose subtree holds the primitive as the key (-1.2 %).
+constexpr uint32_t SORT_KEY_BITS = 4, SORT_KEYS = 1u << SORT_KEY_BITS;
+constexpr uint32_t HIST_BINS = 256;  // >= SORT_KEYS + 2
 __device__ __forceinline__ uint32_t wave_hist_rank(uint32_t key, bool act, uint32_t* bins) {
   const uint32_t ln = lane_id();
 #pragma unroll
@@ -867,54 +803,13 @@ __device__ __forceinline__ uint32_t wave_hist_rank(uint32_t key, bool act, uint3
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   return act ? bins[key] + r : 0u;
 }
-// The same over the whole workgroup (PT_SORT_WAVE 2): rank among the
-// workgroup's lanes with act set, ordered by (key, wave, lane).  Every thread
-// of the workgroup calls it (two barriers); kc: LDS [SORT_KEYS + 1][4].
-__device__ __forceinline__ uint32_t block_key_rank(uint32_t key, bool act, uint32_t (*kc)[4]) {
-  const uint32_t wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  uint32_t wr = 0;
-#pragma unroll
-  for (uint32_t c = 0; c <= SORT_KEYS; ++c) {
-    const unsigned long long m = __ballot(act && key == c);
-    wr = key == c ? mbcnt64(m) : wr;
-    if (ln == 0) kc[c][wave] = (uint32_t)__popcll(m);
-  }
-  __syncthreads();
-  if (wave == 0) {  // lane c: key c's base = exclusive scan of the per-key totals
-    uint32_t w[4] = {0, 0, 0, 0};
-    if (ln <= SORT_KEYS) {
-      w[0] = kc[ln][0];
-      w[1] = kc[ln][1];
-      w[2] = kc[ln][2];
-      w[3] = kc[ln][3];
-    }
-    const uint32_t tot = w[0] + w[1] + w[2] + w[3];
-    uint32_t inc = tot;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t v = __shfl_up(inc, off, 64);
-      if ((int)ln >= off) inc += v;
-    }
-    const uint32_t b = inc - tot;
-    if (ln <= SORT_KEYS) {
-      kc[ln][0] = b;
-      kc[ln][1] = b + w[0];
-      kc[ln][2] = b + w[0] + w[1];
-      kc[ln][3] = b + w[0] + w[1] + w[2];
-    }
-  }
-  __syncthreads();
-  return act ? kc[key][wave] + wr : 0u;
-}
-
 // Shade the path in slot p: read its state, hit words and rays, run
 // shade_vertex, write the new state and ray records.  Returns the new rays in
 // registers.  A path with nothing left to trace (or `passes` vertices done)
 // writes its radiance to res[P] and frees the slot.
-// q: the slot the path's state and new rays are written to (p, or with
-// PT_SORT_WAVE its place in the key order of the wave (1) or workgroup (2)).
-// Every thread of the workgroup calls this; act = the thread has a slot
-// (p < N).  kc: LDS for block_key_rank.
+// q: the slot the path's state and new rays are written to (its place in the
+// key order of the wave).  Every thread of the workgroup calls this; act = the
+// thread has a slot (p < N).  kc: LDS for the compaction pass's offsets.
 // sparse (workgroup-uniform): most of the workgroup's slots are free (the tail
 // of a chunk): the flags word is read first and only live slots read the rest
 // (a second, dependent round trip instead of ~100 B of loads per free slot)
@@ -1003,21 +898,7 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
     }
   }
   const uint32_t flags = act ? __float_as_uint(s0.w) : 0u;
-  if constexpr (PT_SORT_WAVE == 1 || PT_SORT_WAVE == 2) {
-    // (every load above has completed -- the asm uses -- before any thread
-    // passes the rank's barriers and writes slots other threads read)
-    const uint32_t hp = __float_as_uint(r1.z);
-    const bool key_hit = (flags & F_EXT) && hp != PT_PRIM_NONE;
-    const uint32_t key = key_hit ? min(hp >> S.kshift, SORT_KEYS - 1u) : SORT_KEYS;
-    if constexpr (PT_SORT_WAVE == 2) {
-      const uint32_t r = block_key_rank(key, act, kc);
-      if (act) q = blockIdx.x * TPB + r;
-    } else if (act) {
-      q = (p & ~63u) + wave_key_rank(key);
-    }
-  }
   const bool live = (flags & (F_EXT | F_SHADOW | F_SHADOW2)) != 0;
-  if (PT_SORT_WAVE != 3 && !live) return SLOT_FREE;
   const uint32_t P = __float_as_uint(s1.w);
   PathState st{xyz(s0), flags, xyz(s1), 0u};
   const bool ext_hit = (flags & F_EXT) && __float_as_uint(r1.z) != PT_PRIM_NONE;
@@ -1035,21 +916,17 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
     }
     const float t = ext_hit ? r1.w : 0.0f;
     const f3 o = ext_hit ? xyz(r0) : mk(0, 0, 0), d = ext_hit ? mk(r0.w, r1.x, r1.y) : mk(0, 0, 1);
-    shade_vertex<NSH, PT_SHADE_MAD64, false, REFA, false, XL>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext,
-                                                              new_sh, shr);
+    shade_vertex<NSH, SHADE_MAD64, false, REFA, false, XL>(S, sidx, st, o, d, prim, t, clear, C, new_ext, ext, new_sh,
+                                                           shr);
     // (vertices done = vtx - 1: the last one resolves shadow rays only)
     ended = !(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || ((st.flags >> 8) & 0xffu) - 1u >= (uint32_t)S.passes;
   }
-  if constexpr (PT_SORT_WAVE == 3) {  // (every lane of the wave: uniform control flow here)
+  {  // (every lane of the wave: uniform control flow here)
     // continuing paths first (those whose new ray hit something in key
     // order, then the rest), ended paths and free slots last
     const bool cont = live && !ended;
     uint32_t key = cont ? HIST_BINS - 2 : HIST_BINS - 1;
-    if (cont && new_ext && ext_hit) {
-      key = PT_SORT_KMAP ? S.kmap[prim >> S.kmshift] : min(prim >> S.kshift, SORT_KEYS - 1u);
-      if (PT_SORT_DIR)
-        key = (key << 3) | (ext.d.x < 0.0f ? 1u : 0u) | (ext.d.y < 0.0f ? 2u : 0u) | (ext.d.z < 0.0f ? 4u : 0u);
-    }
+    if (cont && new_ext && ext_hit) key = min(prim >> S.kshift, SORT_KEYS - 1u);
     const uint32_t r = wave_hist_rank(key, act, bins);
     if (act) q = (q & ~63u) + r;
     if (S.compact) {
@@ -1190,15 +1067,11 @@ __global__ __launch_bounds__(TPB) void k_camera_push(ShadeArgs S) {
 // at least 7 waves/SIMD (built without SLP vectorisation, pt_shade.hip, it
 // needs 64 VGPRs and runs 8; with SLP it needed 74, i.e. 6 waves:
 // CBbunny shade 101 -> 105 ms)
-#ifndef PT_SHADE_ATTR
-#define PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(7, 8)))
-#endif
-template <int NSH, bool REFA, bool XL = false>
+constexpr int SHADE_WAVES = 7;
 // a workgroup with fewer live slots than this reads its slots sparsely (shade_slot)
-#ifndef PT_SPARSE_LIVE
-#define PT_SPARSE_LIVE 128
-#endif
-__global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
+constexpr uint32_t SPARSE_LIVE = 128;
+template <int NSH, bool REFA, bool XL = false>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SHADE_WAVES, 8))) void k_shade_push(ShadeArgs S) {
   __shared__ uint32_t sh[MAX_ROOT_TARGETS * 8 + 4];
   __shared__ uint32_t s_free[4], s_live[4], s_busy[4], s_next, s_end, s_shaded, s_nb, s_nbn;
   __shared__ float s_dir[3][TPB];
@@ -1221,7 +1094,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     s_shaded = ws.w;
     s_skip = ws.z == 0 && ws.x >= ws.y;  // idle: unless a dispenser is still open (below)
     // (ws.z: the slots live after the last pass's regeneration)
-    s_sparse = ws.z < (uint32_t)PT_SPARSE_LIVE;
+    s_sparse = ws.z < SPARSE_LIVE;
   }
   __syncthreads();
   SHADE_STAMP(1);
@@ -1237,14 +1110,14 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     __syncthreads();
     if (s_skip) return;
   }
-  // PT_ROOT_CLUSTER: the root pass's cluster members into LDS, straight from
+  // The root pass's candidate-cluster members into LDS, straight from
   // memory (no VGPRs; in flight across the shading below): 3 wave loads
   // (REFA: the reference-arithmetic records, 6 float4 each: 3 wave loads)
   constexpr int RPS = REFA ? 6 : 4;
-  __shared__ float4 s_rcm[PT_ROOT_CLUSTER ? RPS * ROOT_CL_MAX : 1];
-  __shared__ uint32_t s_rci[PT_ROOT_CLUSTER ? 2 * ROOT_CL_MAX : 1];
-  if constexpr (PT_ROOT_CLUSTER) {
-    constexpr int NW = RPS * ROOT_CL_MAX / 64;  // wave loads of 64 records' float4s
+  __shared__ float4 s_rcm[RPS * ROOT_CL_MAX];
+  __shared__ uint32_t s_rci[2 * ROOT_CL_MAX];
+  constexpr int NW = RPS * ROOT_CL_MAX / 64;  // wave loads of 64 records' float4s
+  {
     static_assert(RPS * ROOT_CL_MAX % 64 == 0 && 2 * ROOT_CL_MAX == 64 && NW < TPB / 64,
                   "wave-wide LDS loads: the records, then the info words");
     typedef __attribute__((address_space(1))) const void* gptr_t;
@@ -1267,10 +1140,10 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
   }
   __shared__ uint32_t s_kc[SORT_KEYS + 1][4];
-  __shared__ uint32_t s_bins[PT_SORT_WAVE == 3 ? 4 * HIST_BINS : 1];
+  __shared__ uint32_t s_bins[4 * HIST_BINS];
   uint32_t q = p;  // where this lane's path state and new rays go
   int state = shade_slot<NSH, REFA, XL>(S, p, p < nin, q, new_ext, ext, new_sh, shr, s_kc,
-                                    s_bins + (PT_SORT_WAVE == 3 ? wave * HIST_BINS : 0), s_sparse != 0,
+                                    s_bins + wave * HIST_BINS, s_sparse != 0,
                                     S.dense != 0, pre);
   // ---- regeneration: free slots take the next paths in rank order, from the
   // current block and then from a newly claimed one
@@ -1321,20 +1194,17 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
   if ((uint32_t)tid < ns) {
     const uint32_t P = (uint32_t)tid < t1 ? next + (uint32_t)tid : s_nb + (uint32_t)tid - t1;
     uint32_t g;
-    const f3 dir = camera_dir<PT_SHADE_MAD64, REFA>(S, P, g);
+    const f3 dir = camera_dir<SHADE_MAD64, REFA>(S, P, g);
     s_dir[0][tid] = dir.x;
     s_dir[1][tid] = dir.y;
     s_dir[2][tid] = dir.z;
   }
-  if constexpr (PT_ROOT_CLUSTER) {
-    // The LDS copies of the cluster records count against vmcnt, and a
-    // workgroup barrier waits only for lgkmcnt: each loader wave waits for its
-    // copy here, before the barrier that precedes root_pass's reads of s_rcm /
-    // s_rci by every wave (a tail workgroup's idle loader wave reaches it
-    // within a few hundred cycles of issuing the copy).
-    constexpr int NW = RPS * ROOT_CL_MAX / 64;
-    if (S.T.nc > 0 && wave <= NW) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unchanged
-  }
+  // The LDS copies of the cluster records count against vmcnt, and a
+  // workgroup barrier waits only for lgkmcnt: each loader wave waits for its
+  // copy here, before the barrier that precedes root_pass's reads of s_rcm /
+  // s_rci by every wave (a tail workgroup's idle loader wave reaches it within
+  // a few hundred cycles of issuing the copy).
+  if (S.T.nc > 0 && wave <= NW) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unchanged
   __syncthreads();
   SHADE_STAMP(4);
   if (fr) {
@@ -1346,9 +1216,8 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
       S.ps1[q] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
       ext = RayV{ld3(S.cam.origin), mk(s_dir[0][rank], s_dir[1][rank], s_dir[2][rank]), __builtin_inff()};
       new_ext = true;
-    } else if (!S.compact && (state == SLOT_ENDED || (PT_SORT_WAVE && q != p))) {
-      // the slot stays free (with PT_SORT_WAVE slot q may have held another
-      // lane's path until now)
+    } else if (!S.compact && (state == SLOT_ENDED || q != p)) {
+      // the slot stays free (slot q may have held another lane's path until now)
       S.ps0[q] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
     }
   }
@@ -1404,7 +1273,7 @@ __global__ __launch_bounds__(TPB) PT_SHADE_ATTR void k_shade_push(ShadeArgs S) {
     if (st0) {
       const uint32_t P = next + (uint32_t)tid;
       uint32_t g;
-      d1[0] = camera_dir<PT_SHADE_MAD64, REFA>(S, P, g);
+      d1[0] = camera_dir<SHADE_MAD64, REFA>(S, P, g);
       S.ps0[id1[0]] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));
       S.ps1[id1[0]] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(P));
     }
@@ -1526,35 +1395,17 @@ __global__ __launch_bounds__(TPB) void k_compact_slots(float4* ps0, uint4* wstat
 // use the same primitive tests and tie rule as the leaf code of
 // process_item (trace.hip); results are bit-identical to the wavefront path.
 // SPH: the leaf may hold spheres (else the sphere branch is not compiled in)
-// PT_PATH_STRICT (extension rays, tmax = +inf): the triangle test admits only
-// t < the best so far, so a hit is a new best and the update is two selects
-// (no exec-mask branches: fewer SALU per primitive).  The same hits as
-// take_hit: a tie keeps the lower index either way, and the inclusive tmax
-// of take_hit matters only for a first hit at t = tmax = +inf, which no test
-// returns (an infinite t fails the barycentric test).
-#ifndef PT_PATH_STRICT
-#define PT_PATH_STRICT 1
-#endif
-// PT_PATH_PAIR: two primitive records per scalar round trip in the
-// single-leaf loops (default arithmetic; one wait and one loop step per pair)
-#ifndef PT_PATH_PAIR
-#define PT_PATH_PAIR 1
-#endif
-// PT_PATH_TRIM: the single-leaf closest-hit loop of the sphere-free kernel
-// drops the second t < bt compare and the -0 fix of the triangle test (both
-// redundant there): CBempty +1.5 %
-#ifndef PT_PATH_TRIM
-#define PT_PATH_TRIM 1
-#endif
-// PT_CLOSEST_DIRECT_SPH: the same two for the triangles of the sphere kernel
-#ifndef PT_CLOSEST_DIRECT_SPH
-#define PT_CLOSEST_DIRECT_SPH 1
-#endif
-// PT_CLOSEST_DIRECT: with the trim, the hit update is made inside the test
-// (bw_closest_update) instead of through its -1 / t result
-#ifndef PT_CLOSEST_DIRECT
-#define PT_CLOSEST_DIRECT 1
-#endif
+// The closest-hit loop is strict (extension rays, tmax = +inf): the triangle
+// test admits only t < the best so far, so a hit is a new best and the update
+// is two selects (no exec-mask branches: fewer SALU per primitive; round 4,
+// CBempty +3.7 %).  The same hits as take_hit: a tie keeps the lower index
+// either way, and the inclusive tmax of take_hit matters only for a first hit
+// at t = tmax = +inf, which no test returns (an infinite t fails the
+// barycentric test).  Default arithmetic: two primitive records per scalar
+// round trip (one wait and one loop step per pair: +1 %), and a triangle's
+// update made inside the test from its own compares (bw_closest_update: no
+// second t < bt compare, no -0 fix -- a -0 t only feeds compares and the hit
+// point; CBempty +1.5 %, then +1.6 %, CBspheres' triangles +2.6 %, round 4).
 template <bool REFA, bool SPH = true>
 __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, int pcount, const RayV& r,
                                              uint32_t& prim, float& t) {
@@ -1563,28 +1414,16 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
   constexpr int PS = prim_stride<REFA>();
   const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * PS);
   int k0 = 0;
-  if constexpr (PT_PATH_PAIR && PT_PATH_STRICT && !REFA) {
-    // (the strict test returns t < bt or -1 -- a sphere's t is checked --
-    // and t = -0 may stay: it only feeds compares and the hit point)
+  if constexpr (!REFA) {
     auto step = [&](const Prim& q, int k) {
-      // (the kernel with the sphere test compiled in keeps both: measured
-      // -0.9 % on CBspheres with the trim)
-      constexpr bool TRIM = PT_PATH_TRIM && !SPH;
-      if constexpr (TRIM && PT_BW_POINT && PT_CLOSEST_DIRECT) {
+      if (!SPH || !prim_sphere<REFA>(q)) {
         // the update straight from the test's compares (no -1 sentinel)
         bw_closest_update(r.o, r.d, q, pstart + k, bt, bp);
         return;
       }
-      if constexpr (SPH && !REFA && PT_BW_POINT && PT_CLOSEST_DIRECT_SPH) {
-        // (the sphere kernel: triangles the same way, spheres as before)
-        if (!prim_sphere<REFA>(q)) {
-          bw_closest_update(r.o, r.d, q, pstart + k, bt, bp);
-          return;
-        }
-      }
-      const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1)
-                                                     : tri_test<REFA, true, !TRIM>(r.o, r.d, q, bt);
-      const bool take = TRIM ? (tt >= 0.0f) : ((tt >= 0.0f) & (tt < bt));
+      // (a sphere's t is checked against bt here)
+      const float tt = sphere_test(r.o, r.d, q.q0, q.q1);
+      const bool take = (tt >= 0.0f) & (tt < bt);
       bt = take ? tt : bt;
       bp = take ? pstart + k : bp;
     };
@@ -1600,16 +1439,11 @@ __device__ __forceinline__ void leaf_closest(const float4* prims, int pstart, in
     const Prim q = load_prim<REFA>(P);
     // (a tri_outside pre-test does not pay here: extension rays of one wave
     // rarely all miss a plane, measured -7 % on CBempty)
-    if constexpr (PT_PATH_STRICT) {
-      const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1)
-                                                     : tri_test<REFA, true>(r.o, r.d, q, bt);
-      const bool take = (tt >= 0.0f) & (tt < bt);
-      bt = take ? tt : bt;
-      bp = take ? pstart + k : bp;
-    } else {
-      const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1) : tri_test<REFA>(r.o, r.d, q, bt);
-      take_hit(tt, pstart + k, bt, bp);
-    }
+    const float tt = (SPH && prim_sphere<REFA>(q)) ? sphere_test(r.o, r.d, q.q0, q.q1)
+                                                   : tri_test<REFA, true>(r.o, r.d, q, bt);
+    const bool take = (tt >= 0.0f) & (tt < bt);
+    bt = take ? tt : bt;
+    bp = take ? pstart + k : bp;
   }
   prim = bp < 0 ? PT_PRIM_NONE : (uint32_t)bp;
   t = bt;
@@ -1622,7 +1456,7 @@ struct TestCount {
   uint32_t tri, sph, box;
 };
 
-// PT_PATH_CLUSTER: the closest-hit loop tests the leaf's primitive clusters
+// Candidate clusters: the closest-hit loop tests the leaf's primitive clusters
 // (one primitive, or two consecutive triangles with nearly the same box: a
 // Cornell wall's halves; ShadeArgs::cbox, host-built, widened by the BVH
 // boxes' guard band: conservative as a leaf box is) only where the lane's ray
@@ -1633,20 +1467,13 @@ struct TestCount {
 // the strict test: the same hit as the full loop (a box missed holds no hit).
 // CBempty 85,000 -> 93,400 Mrays/s, CBspheres 56,950 -> 59,100 (interleaved
 // A/B, 2 runs each; fixed pairs (2i, 2i + 1) instead: CBspheres 50,200, a
-// sphere paired with the ceiling)
-#ifndef PT_PATH_CLUSTER
-#define PT_PATH_CLUSTER 1
-#endif
+// sphere paired with the ceiling).  Extension rays pick their candidates by
+// the slab test: by the overlap of the box of their segment to the exit from
+// the clusters' union box instead (as the shadow rays do), CBempty 17.9 ->
+// 18.7 ms per frame, CBspheres likewise -- a room-crossing segment's box
+// overlaps more walls than its slab test enters, and each extra candidate
+// costs a division (round 5).
 constexpr int PATH_CL_PRIMS = 32;  // primitives staged in LDS at most
-// PT_PATH_EXT_AABB: extension rays too pick their candidates by box overlap,
-// of the segment from the origin to the ray's exit from the clusters' union
-// box (every hit lies before that exit: the union box holds every cluster box).
-// Off: CBempty 17.9 -> 18.7 ms per frame with it, CBspheres likewise -- a
-// room-crossing segment's box overlaps more walls than its slab test enters,
-// and each extra candidate costs a division
-#ifndef PT_PATH_EXT_AABB
-#define PT_PATH_EXT_AABB 0
-#endif
 template <bool SPH, bool CNT = false>
 __device__ __forceinline__ void leaf_closest_cl(const ShadeArgs& S, const float4* s_rec, const uint32_t* s_cl,
                                                 int pstart, int pcount, const RayV& r, uint32_t& prim, float& t,
@@ -1656,28 +1483,9 @@ __device__ __forceinline__ void leaf_closest_cl(const ShadeArgs& S, const float4
   const f3 oi = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
   const CPTR(f4v) B = (const CPTR(f4v))S.cbox;
   uint32_t cm = 0u;
-  if constexpr (PT_PATH_EXT_AABB) {
-    // the ray's exit from the clusters' union box (record nclus) bounds every
-    // hit: the segment to it, boxed, against the cluster boxes
-    // (PT_PATH_OCC_AABB's overlap test)
-    const float4 u0 = f4(B[2 * S.nclus]), u1 = f4(B[2 * S.nclus + 1]);
-    const float fx0 = __builtin_fmaf(u0.x, inv.x, -oi.x), fx1 = __builtin_fmaf(u0.y, inv.x, -oi.x);
-    const float fy0 = __builtin_fmaf(u0.z, inv.y, -oi.y), fy1 = __builtin_fmaf(u0.w, inv.y, -oi.y);
-    const float fz0 = __builtin_fmaf(u1.x, inv.z, -oi.z), fz1 = __builtin_fmaf(u1.y, inv.z, -oi.z);
-    const float tf = fminf(fminf(fmaxf(fx0, fx1), fmaxf(fy0, fy1)), fmaxf(fz0, fz1));
-    const f3 e = mk(__builtin_fmaf(tf, r.d.x, r.o.x), __builtin_fmaf(tf, r.d.y, r.o.y), __builtin_fmaf(tf, r.d.z, r.o.z));
-    const f3 lo = mk(fminf(r.o.x, e.x), fminf(r.o.y, e.y), fminf(r.o.z, e.z));
-    const f3 hi = mk(fmaxf(r.o.x, e.x), fmaxf(r.o.y, e.y), fmaxf(r.o.z, e.z));
-    for (int c = 0; c < S.nclus; ++c) {
-      const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
-      const bool ov = !((hi.x < b0.x) | (lo.x > b0.y) | (hi.y < b0.z) | (lo.y > b0.w) | (hi.z < b1.x) | (lo.z > b1.y));
-      cm = mask_bit(cm, ov, c);
-    }
-  } else {
-    for (int c = 0; c < S.nclus; ++c) {
-      const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
-      cm = mask_bit(cm, box_hit_open(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv), c);
-    }
+  for (int c = 0; c < S.nclus; ++c) {
+    const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
+    cm = mask_bit(cm, box_hit_open(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv), c);
   }
   if constexpr (CNT) tc->box += (uint32_t)S.nclus;
   float bt = r.tmax;
@@ -1712,62 +1520,12 @@ __device__ __forceinline__ void leaf_closest_cl(const ShadeArgs& S, const float4
   t = bt;
 }
 
-// PT_PATH_CLUSTER_OCC: the shadow rays' occlusion query over the same
-// clusters (box tests over the segment [0, tmax], then the candidates' tests,
-// done at the first hit): CBempty 93,200 -> 101,000 Mrays/s, CBspheres
-// 59,080 -> 61,050 (interleaved A/B, 2 runs each)
-#ifndef PT_PATH_CLUSTER_OCC
-#define PT_PATH_CLUSTER_OCC 1
-#endif
-template <bool SPH>
-__device__ __forceinline__ bool leaf_occluded_cl(const ShadeArgs& S, const float4* s_rec, const uint32_t* s_cl,
-                                                 const RayV& r) {
-  const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(r.d.x)), __builtin_amdgcn_rcpf(safe_dir(r.d.y)),
-                    __builtin_amdgcn_rcpf(safe_dir(r.d.z)));
-  const f3 oi = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
-  const CPTR(f4v) B = (const CPTR(f4v))S.cbox;
-  uint32_t cm = 0u;
-  for (int c = 0; c < S.nclus; ++c) {
-    const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
-    cm = mask_bit(cm, box_hit_seg(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv, r.tmax), c);
-  }
-  bool hit = false;
-  auto test = [&](int k) -> bool {
-    Prim q;
-    q.q0 = s_rec[4 * k];
-    q.q1 = s_rec[4 * k + 1];
-    q.q2 = s_rec[4 * k + 2];
-    q.q3 = s_rec[4 * k + 3];
-    if (SPH && prim_sphere<false>(q)) {
-      const float tt = sphere_test(r.o, r.d, q.q0, q.q1);
-      return (tt >= 0.0f) & (tt <= r.tmax);
-    }
-    float ndd, num;
-    plane_nd<false>(r.o, r.d, q, ndd, num);
-    return !tri_outside<false>(ndd, num, r.tmax) && bw_occludes(r.o, r.d, q, num, ndd, r.tmax);
-  };
-  while (cm && !hit) {
-    const int c = __builtin_ctz(cm);
-    cm &= cm - 1u;
-    const uint32_t fc = s_cl[c];
-    hit = test((int)(fc & 0xFFFFu));
-    if (!hit && (fc >> 17)) hit = test((int)(fc & 0xFFFFu) + 1);
-  }
-  return hit;
-}
-
-// PT_PATH_IMM_OCC: k_path_leaf tests each shadow ray where its NEE sample
-// makes it (shade_vertex's IMM) instead of keeping it pending in LDS until the
-// path's next vertex: no shadow ray in LDS (16 -> 6 KB of LDS per
-// workgroup), no iteration that only resolves a path's last shadow ray;
-// CBempty 18.07 -> 17.73 ms per frame, CBspheres within noise (interleaved
-// A/B, 2 runs each)
-#ifndef PT_PATH_IMM_OCC
-#define PT_PATH_IMM_OCC 1
-#endif
-// PT_PATH_OCC_AABB: a shadow segment against the clusters as an overlap test of its bounding box with each
-// cluster's box (6 compares with scalar bounds, combined on the scalar unit)
-// instead of the slab test, then the same per-lane candidate loop.
+// The shadow rays' occlusion query over the same clusters, done at the first
+// hit (round 5: CBempty 93,200 -> 101,000 Mrays/s, CBspheres 59,080 ->
+// 61,050).  A shadow segment is tested against the clusters as an overlap
+// test of its bounding box with each cluster's box (6 compares with scalar
+// bounds, combined on the scalar unit) instead of the slab test, then the
+// same per-lane candidate loop.
 // Conservative as the slab test: a hit point fma(t, d, o) with t in [0, tmax]
 // lies between o and e = fma(tmax, d, o) on every axis (fma is monotone in
 // t), so within the segment's box; a cluster's box holds every point where
@@ -1777,9 +1535,6 @@ __device__ __forceinline__ bool leaf_occluded_cl(const ShadeArgs& S, const float
 // lanes that overlap it whenever any lane does, lost 8 %: a wave's 64 lanes
 // lie on every wall, and a grazing incident ray leaves its shadow ray's
 // origin within the band of its own wall)
-#ifndef PT_PATH_OCC_AABB
-#define PT_PATH_OCC_AABB 1
-#endif
 template <bool SPH, bool CNT = false>
 __device__ __forceinline__ bool leaf_occluded_aabb(const ShadeArgs& S, const float4* s_rec, const uint32_t* s_cl,
                                                    const RayV& r, TestCount* tc = nullptr) {
@@ -1816,7 +1571,6 @@ __device__ __forceinline__ bool leaf_occluded_aabb(const ShadeArgs& S, const flo
     const bool ov = !((hi.x < b0.x) | (lo.x > b0.y) | (hi.y < b0.z) | (lo.y > b0.w) | (hi.z < b1.x) | (lo.z > b1.y));
     cm = mask_bit(cm, ov, c);
   }
-  if (PT_DBG_OCC_MASK_ONLY) return cm == 0xFFFFFFFFu;  // (timing diagnostic: the mask without its candidates)
   while (cm && !hit) {
     const int c = __builtin_ctz(cm);
     cm &= cm - 1u;
@@ -1829,45 +1583,24 @@ __device__ __forceinline__ bool leaf_occluded_aabb(const ShadeArgs& S, const flo
 
 // any primitive at t in [0, tmax]; triangles whose plane hit is certainly
 // outside [0, tmax] for every lane (tri_outside: shadow rays toward the light
-// mostly point away from the walls or end before them) cost no division
-#ifndef PT_OCC_BITWISE
-#define PT_OCC_BITWISE 1
-#endif
-// PT_OCC_TRIM: the sphere-free kernel's occlusion loop takes its answer as a
-// bool from the test's own compares (bw_occludes), on the pre-test's num / ndd
-#ifndef PT_OCC_TRIM
-#define PT_OCC_TRIM 1
-#endif
+// mostly point away from the walls or end before them) cost no division;
+// the answer is a bitwise mask update (no exec-mask branch per primitive:
+// +1-2 %, round 4), a triangle's straight from the test's own compares
+// (bw_occludes) on the pre-test's num / ndd (+1.4 % CBempty, round 4)
 template <bool REFA, bool SPH = true>
 __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, int pcount, const RayV& r) {
   constexpr int PS = prim_stride<REFA>();
   const CPTR(f4v) P = (const CPTR(f4v))(prims + (size_t)pstart * PS);
   bool hit = false;
   int k0 = 0;
-  if constexpr (PT_PATH_PAIR && PT_OCC_BITWISE && !REFA) {
+  if constexpr (!REFA) {
     auto test = [&](const Prim& q) -> bool {
-      if constexpr (PT_OCC_TRIM && !SPH && PT_BW_POINT) {
-        // (a bool straight from the test's compares, on the pre-test's
-        // num / ndd)
+      if (!SPH || !prim_sphere<REFA>(q)) {
         float ndd, num;
         plane_nd<REFA>(r.o, r.d, q, ndd, num);
         return !tri_outside<REFA>(ndd, num, r.tmax) && bw_occludes(r.o, r.d, q, num, ndd, r.tmax);
       }
-      if constexpr (SPH && !REFA && PT_BW_POINT && PT_CLOSEST_DIRECT_SPH) {
-        if (!prim_sphere<REFA>(q)) {
-          float ndd, num;
-          plane_nd<REFA>(r.o, r.d, q, ndd, num);
-          return !tri_outside<REFA>(ndd, num, r.tmax) && bw_occludes(r.o, r.d, q, num, ndd, r.tmax);
-        }
-      }
-      float tt = -1.0f;
-      if (SPH && prim_sphere<REFA>(q)) {
-        tt = sphere_test(r.o, r.d, q.q0, q.q1);
-      } else {
-        float ndd, num;
-        plane_nd<REFA>(r.o, r.d, q, ndd, num);
-        if (!tri_outside<REFA>(ndd, num, r.tmax)) tt = tri_test<REFA>(r.o, r.d, q, r.tmax);
-      }
+      const float tt = sphere_test(r.o, r.d, q.q0, q.q1);
       return (tt >= 0.0f) & (tt <= r.tmax);
     };
     for (; k0 + 1 < pcount; k0 += 2, P += 2 * PS) {
@@ -1888,14 +1621,9 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
       plane_nd<REFA>(r.o, r.d, q, ndd, num);
       if (!tri_outside<REFA>(ndd, num, r.tmax)) tt = tri_test<REFA>(r.o, r.d, q, r.tmax);
     }
-    if constexpr (PT_OCC_BITWISE) {
-      // (no short-circuit: one mask update, no exec-mask branch per primitive)
-      hit = hit | ((tt >= 0.0f) & (tt <= r.tmax));
-      if (__ballot(!hit) == 0ull) break;  // every active lane is occluded
-    } else {
-      hit = hit || (tt >= 0.0f && tt <= r.tmax);
-      if (!__any(!hit)) break;  // every active lane is occluded
-    }
+    // (no short-circuit: one mask update, no exec-mask branch per primitive)
+    hit = hit | ((tt >= 0.0f) & (tt <= r.tmax));
+    if (__ballot(!hit) == 0ull) break;  // every active lane is occluded
   }
   return hit;
 }
@@ -1909,65 +1637,37 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
 // passes N and its lanes are idle.  Results do not depend on which lane runs a
 // path: random numbers are keyed by (pixel, sample, vertex) and each path
 // writes only its own slot ps1[p].
-#ifndef PT_PATH_MAD64
-#define PT_PATH_MAD64 true  // Philox products as v_mad_u64_u32 (CBempty +1.4 %; k_shade_push would lose its 7th wave)
-#endif
-// PT_PATH_RNG_EARLY: k_path_leaf's shade_vertex computes the vertex's Philox
-// words up front (PT_RNG_EARLY, kept for k_shade_push); off in round 5 (in
-// k_path_leaf the shading record is an L2 hit and nothing waits on it long).
-// With the light held in registers (PT_PATH_LIGHT_RELOAD below), at the final
-// round-5 code: CBempty 17.66 -> 17.2 ms per frame, CBspheres 28.6 -> 26.6
-// (v_mul_hi_u32 + v_mul_lo_u32 instead of PT_PATH_MAD64 measured slower in
-// both kernels in that configuration)
-#ifndef PT_PATH_RNG_EARLY
-#define PT_PATH_RNG_EARLY 0
-#endif
+// Philox products as v_mad_u64_u32 (CBempty +1.4 %).  The vertex's Philox
+// words are computed where they are used, not early as in k_shade_push (in
+// k_path_leaf the shading record is an L2 hit and nothing waits on it long);
+// with the light held in registers, at the final round-5 code: CBempty 17.66
+// -> 17.2 ms per frame, CBspheres 28.6 -> 26.6 (v_mul_hi_u32 + v_mul_lo_u32
+// instead of v_mad_u64_u32 measured slower in that configuration).
+constexpr bool PATH_MAD64 = true, PATH_RNG_EARLY = false;
 // paths a wave takes from the global counter at a time (CBempty: 128: -1.3 %,
 // 512: +1.6 %, 1024: +1.4 %, 2048: +0.1 % against 256; re-measured in round
-// 3: 1024 -0.3 %, 256 -1.2 % against 512)
-#ifndef PT_PATH_CHUNK
-#define PT_PATH_CHUNK 512
-#endif
-constexpr uint32_t PATH_CHUNK = PT_PATH_CHUNK;
+// 3: 1024 -0.3 %, 256 -1.2 % against 512; round 5: 1024 -0.5 %, 256 -1.6 %)
+constexpr uint32_t PATH_CHUNK = 512;
 
 // With all path state in registers: 6 waves per SIMD (80 VGPRs, no spills);
 // 7 waves (72 VGPRs) ran within 0.6 % of it but spilled ~20 VGPRs around the
 // shading code (~35 GB of scratch write-back per 1024^2 x 256 spp frame, PMC
-// WRITE_SIZE); 8 waves spilled ~60 and lost 10 %.
-// the light re-read from the kernel arguments at each NEE sample (light_of):
-// SGPR spills 34 -> 13, v_readlane reloads 42 -> 13 (CBempty +0.8 %,
-// CBspheres +1.1 %)
-// (round 5, at the final code: the light held in registers measured faster --
-// alone CBempty 17.55 -> 17.25 ms per frame, CBspheres 28.48 -> 27.03; with
-// PT_PATH_RNG_EARLY off as well see above -- so the reload is off; the
-// kernel-argument layout check stays for the camera reload)
-#ifndef PT_PATH_LIGHT_RELOAD
-#define PT_PATH_LIGHT_RELOAD false
-#endif
-// 8 waves per SIMD with the pending shadow rays, their contributions, the
-// radiance and the throughput in LDS (PT_PATH_LDS_SH, 16 KB per workgroup):
-// 64 VGPRs, 9 spilled; CBempty 51,700 -> 54,700 Mrays/s, CBspheres 38,500 ->
-// 40,800 (7 waves: 68 VGPRs without spills, 54,000; the same state in
-// registers at 6 waves: 80 VGPRs, see above)
-#ifndef PT_PATH_WAVES
-#define PT_PATH_WAVES 8
-#endif
-// the camera re-read from the kernel arguments at each path start (cam_of)
-#ifndef PT_PATH_CAM_RELOAD
-#define PT_PATH_CAM_RELOAD true
-#endif
-#ifndef PT_PATH_LDS_SH
-#define PT_PATH_LDS_SH 1
-#endif
-// refill idle lanes only when at least this many are idle (the camera-ray code
-// then runs masked once per PT_REFILL_MIN path ends instead of at every
-// iteration with an idle lane; the idle lanes wait meanwhile)
-#ifndef PT_REFILL_MIN
-#define PT_REFILL_MIN 1
-#endif
-// (PT_PATH_LIGHT_RELOAD reads the light from the kernel-argument segment at
-// offsetof(ShadeArgs, light): S must stay this kernel's FIRST parameter; a
-// -DPT_DBG_BOUNDS build checks it at run time)
+// WRITE_SIZE); 8 waves spilled ~60 and lost 10 %.  8 waves per SIMD with the
+// radiance and the throughput in LDS (16 KB per workgroup while the pending
+// shadow rays were kept there too): 64 VGPRs; CBempty 51,700 -> 54,700
+// Mrays/s, CBspheres 38,500 -> 40,800 (7 waves: 68 VGPRs without spills,
+// 54,000).
+constexpr int PATH_WAVES = 8;
+// The light: held in registers (round 5, at the final code: CBempty 17.55 ->
+// 17.25 ms per frame, CBspheres 28.48 -> 27.03 against re-reading it from the
+// kernel arguments at each NEE sample, which had cut SGPR spills 34 -> 13 in
+// round 2); the extended-light variants (XL) keep the re-read (their
+// registers).  The camera is re-read from the kernel arguments at each path
+// start (cam_of).  Both re-reads read the kernel-argument segment at
+// offsetof(ShadeArgs, ...): S must stay this kernel's FIRST parameter (checked
+// at every launch, below).  Refilling idle lanes only once k of a wave's 64
+// are idle measured slower (k = 4, 8, 16: CBempty -0.6 / +0.0 / -0.9 %,
+// CBspheres -0.2 / -0.2 / -2.3 %, round 5): every idle lane refills.
 // Guided path grabs: the k-th grab from the counter takes the range
 // [S[j] + (k - G[j]) c[j], ...) of the phase j with G[j] <= k < G[j+1]; the
 // chunk size halves as the unstarted paths run out (512 down to 64), so no
@@ -2032,7 +1732,7 @@ static __device__ unsigned long long g_path_timing[PT_TIMING_WAVES * 8];
 // CNT: the counting variant (PT_FLAG_COUNT_TESTS): executed tests into
 // rcount's lines (words 1-3 of each 128-B counter line)
 template <int NSH, bool REFA, bool GUIDED, bool SPH = true, bool XL = false, bool CNT = false>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES, 8))) void k_path_leaf(
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
     uint32_t* __restrict__ work, uint32_t nreg, uint32_t tail_unit, uint32_t* __restrict__ err) {
   const uint32_t lid = lane_id();
@@ -2040,7 +1740,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
   // kernel-argument segment, so S must stay this kernel's FIRST parameter:
   // checked at every launch (wave-uniform, a few cached scalar loads); a
   // mismatch sets ERR_KERNARG and the kernel does nothing (pt_render fails)
-  if (PT_PATH_LIGHT_RELOAD || XL || PT_PATH_CAM_RELOAD) {
+  {
     const pt_light a = light_of<true>(S), b = S.light;
     const pt_camera ca = cam_of<true>(S), cb = S.cam;
     uint32_t wa[sizeof a / 4], wb[sizeof b / 4], wc[sizeof ca / 4], wd[sizeof cb / 4];
@@ -2058,10 +1758,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       return;
     }
   }
-  // PT_PATH_CLUSTER: the leaf's records in LDS for the per-lane candidate loop
-  __shared__ float4 s_rec[PT_PATH_CLUSTER ? PATH_CL_PRIMS * 4 : 1];
-  __shared__ uint32_t s_cl[PT_PATH_CLUSTER ? PATH_CL_PRIMS : 1];
-  const bool use_cl = PT_PATH_CLUSTER && !REFA && S.nclus > 0 && pcount <= PATH_CL_PRIMS;
+  // candidate clusters: the leaf's records in LDS for the per-lane candidate loop
+  __shared__ float4 s_rec[PATH_CL_PRIMS * 4];
+  __shared__ uint32_t s_cl[PATH_CL_PRIMS];
+  const bool use_cl = !REFA && S.nclus > 0 && pcount <= PATH_CL_PRIMS;
   if (use_cl) {
     for (int i = threadIdx.x; i < pcount * 4; i += TPB) s_rec[i] = S.prims[(size_t)pstart * 4 + i];
     for (int i = threadIdx.x; i < S.nclus; i += TPB)
@@ -2094,29 +1794,26 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
     shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
     C[s] = mk(0, 0, 0);
   }
-  // PT_PATH_LDS_SH: the pending shadow rays live in LDS between vertices
-  // PT_PATH_IMM_OCC: shadow rays tested where they are made (shade_vertex's
-  // IMM), none pending between vertices
-  constexpr bool IMMO = PT_PATH_IMM_OCC;
+  // Shadow rays are tested where their NEE sample makes them (shade_vertex's
+  // IMM), none pending between vertices (round 5: no shadow ray in LDS, 16 ->
+  // 6 KB of LDS per workgroup, no iteration that only resolves a path's last
+  // shadow ray; CBempty 18.07 -> 17.73 ms per frame).  The path's radiance and
+  // throughput live in LDS (sh_lds, stride-1 columns).
   // (XL: the light re-read keeps the extended-light variants' registers down,
   // 136 B of scratch without it)
-  constexpr bool M64P = PT_PATH_MAD64, LRP = PT_PATH_LIGHT_RELOAD || XL, EARLYP = PT_PATH_RNG_EARLY;
-  __shared__ float sh_lds[PT_PATH_LDS_SH ? ((IMMO ? 0 : NSH * 10) + 6) * TPB : 1];
-  float* const Lq = sh_lds + (size_t)(IMMO ? 0 : 10 * NSH) * TPB + threadIdx.x;  // (PT_PATH_LDS_SH: the radiance)
+  constexpr bool M64P = PATH_MAD64, LRP = XL, EARLYP = PATH_RNG_EARLY;
+  __shared__ float sh_lds[6 * TPB];
+  float* const Lq = sh_lds + threadIdx.x;  // (the radiance, then the throughput)
   TestCount tc{0u, 0u, 0u};  // (CNT only)
   // the occlusion query of one shadow ray
   auto occluded = [&](const RayV& r) -> bool {
-    if (PT_DBG_SKIP_OCC) return false;
-    if (PT_PATH_CLUSTER && PT_PATH_CLUSTER_OCC && PT_PATH_OCC_AABB && !REFA && use_cl)
-      return leaf_occluded_aabb<SPH, CNT>(S, s_rec, s_cl, r, &tc);
+    if (use_cl) return leaf_occluded_aabb<SPH, CNT>(S, s_rec, s_cl, r, &tc);
     if constexpr (CNT) tc.tri += (uint32_t)pcount;  // (the full loop: an upper bound)
-    if (PT_PATH_CLUSTER && PT_PATH_CLUSTER_OCC && !REFA && use_cl) return leaf_occluded_cl<SPH>(S, s_rec, s_cl, r);
     return leaf_occluded<REFA, SPH>(S.prims, pstart, pcount, r);
   };
   for (;;) {
     // ---- refill idle lanes from the pool (new paths start at their camera ray)
-    unsigned long long idle = __ballot(!active);
-    if (PT_REFILL_MIN > 1 && __popcll(idle) < PT_REFILL_MIN && idle != ~0ull) idle = 0;
+    const unsigned long long idle = __ballot(!active);
     if (idle && next == end && !drained) {
 #if PT_PATH_TIMING
       const unsigned long long tg = wall_clock64();
@@ -2162,19 +1859,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
         const uint32_t p = next + r;
         sh_p[threadIdx.x] = p;
         active = true;
-        const f3 dir = camera_dir<M64P, REFA, PT_PATH_CAM_RELOAD>(S, p, st.g);
+        const f3 dir = camera_dir<M64P, REFA, true>(S, p, st.g);
         st.T = mk(1.0f, 1.0f, 1.0f);
         st.L = mk(0.0f, 0.0f, 0.0f);
-        if constexpr (PT_PATH_LDS_SH) {
-          Lq[0] = 0.0f;
-          Lq[TPB] = 0.0f;
-          Lq[2 * TPB] = 0.0f;
-          Lq[3 * TPB] = 1.0f;  // (the throughput)
-          Lq[4 * TPB] = 1.0f;
-          Lq[5 * TPB] = 1.0f;
-        }
+        Lq[0] = 0.0f;
+        Lq[TPB] = 0.0f;
+        Lq[2 * TPB] = 0.0f;
+        Lq[3 * TPB] = 1.0f;  // (the throughput)
+        Lq[4 * TPB] = 1.0f;
+        Lq[5 * TPB] = 1.0f;
         st.flags = F_EXT | (1u << 8);
-        ext = RayV{ld3(cam_of<PT_PATH_CAM_RELOAD>(S).origin), dir, __builtin_inff()};
+        ext = RayV{ld3(cam_of<true>(S).origin), dir, __builtin_inff()};
       }
       next += min((uint32_t)__popcll(idle), avail);
     }
@@ -2184,17 +1879,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
     }
     // ---- one vertex of every active path: leaf tests, then shade
     nrays += (uint32_t)__popcll(__ballot(active && (st.flags & F_EXT)));
-    if constexpr (!IMMO) {
-#pragma unroll
-      for (int s = 0; s < NSH; ++s) nrays += (uint32_t)__popcll(__ballot(active && (st.flags & sh_bit(s))));
-    }
-    uint32_t cast_sh = 0u;  // (IMMO: the shadow rays this vertex cast, counted below in uniform control flow)
+    uint32_t cast_sh = 0u;  // (the shadow rays this vertex cast, counted below in uniform control flow)
     if (active) {
       uint32_t prim = PT_PRIM_NONE;
       float t = 0.0f;
       if (st.flags & F_EXT) {
         // (extension rays have tmax = inf: not carried across iterations)
-        if (PT_PATH_CLUSTER && !REFA && use_cl) {
+        if (use_cl) {
           leaf_closest_cl<SPH, CNT>(S, s_rec, s_cl, pstart, pcount, RayV{ext.o, ext.d, __builtin_inff()}, prim, t, &tc);
         } else {
           if constexpr (CNT) tc.tri += (uint32_t)pcount;
@@ -2204,56 +1895,33 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAV
       bool clear[NSH];
 #pragma unroll
       for (int s = 0; s < NSH; ++s) {
-        clear[s] = false;
-        if constexpr (PT_PATH_LDS_SH) {  // (no value carried across iterations in registers)
-          shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};
-          C[s] = mk(0, 0, 0);
-        }
-        if (!IMMO && (st.flags & sh_bit(s))) {
-          if constexpr (PT_PATH_LDS_SH && !IMMO) {
-            const float* q = sh_lds + (size_t)s * 10 * TPB + threadIdx.x;
-            shr[s] = RayV{mk(q[0], q[TPB], q[2 * TPB]), mk(q[3 * TPB], q[4 * TPB], q[5 * TPB]), q[6 * TPB]};
-            C[s] = mk(q[7 * TPB], q[8 * TPB], q[9 * TPB]);
-          }
-          clear[s] = !occluded(shr[s]);
-        }
+        clear[s] = false;  // (no shadow ray pending from the last vertex)
+        shr[s] = RayV{mk(0, 0, 0), mk(0, 0, 1), -1.0f};  // (no value carried across iterations in registers)
+        C[s] = mk(0, 0, 0);
       }
       bool new_ext, new_sh[NSH];
       RayV e2, s2[NSH];
       // (the sample index is recomputed, not carried: one register less)
-      if constexpr (IMMO) {
-        shade_vertex<NSH, M64P, LRP, REFA, PT_PATH_LDS_SH, XL, decltype(occluded), EARLYP>(
-            S, S.sample_base + udiv_q(sh_p[threadIdx.x], S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
-            new_sh, s2, sh_lds, occluded);
+      shade_vertex<NSH, M64P, LRP, REFA, true, XL, decltype(occluded), EARLYP>(
+          S, S.sample_base + udiv_q(sh_p[threadIdx.x], S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
+          new_sh, s2, sh_lds, occluded);
 #pragma unroll
-        for (int s = 0; s < NSH; ++s) cast_sh |= new_sh[s] ? 1u << s : 0u;  // (cast and resolved)
-      } else {
-        shade_vertex<NSH, M64P, LRP, REFA, PT_PATH_LDS_SH, XL, NoOcc, EARLYP>(
-            S, S.sample_base + udiv_q(sh_p[threadIdx.x], S.div_npix), st, ext.o, ext.d, prim, t, clear, C, new_ext, e2,
-            new_sh, s2, sh_lds);
-      }
+      for (int s = 0; s < NSH; ++s) cast_sh |= new_sh[s] ? 1u << s : 0u;  // (cast and resolved)
       // (unconditional: without a new extension ray F_EXT is clear and ext is
       // not read again before the lane's next camera ray -- the old ray need
       // not stay live through shade_vertex)
       ext = e2;
-      if constexpr (!PT_PATH_LDS_SH) {
-#pragma unroll
-        for (int s = 0; s < NSH; ++s)
-          if (new_sh[s]) shr[s] = s2[s];
-      }
       // vertices done = vtx - 1 (shade_vertex advanced it); the path ends
       // after `passes` of them or when it has no ray left to trace
       const uint32_t done = ((st.flags >> 8) & 0xffu) - 1u;
       if (!(st.flags & (F_EXT | F_SHADOW | F_SHADOW2)) || done >= (uint32_t)passes) {
-        if constexpr (PT_PATH_LDS_SH) st.L = mk(Lq[0], Lq[TPB], Lq[2 * TPB]);
+        st.L = mk(Lq[0], Lq[TPB], Lq[2 * TPB]);
         put_res(S.ps1, sh_p[threadIdx.x], st.L);
         active = false;
       }
     }
-    if constexpr (IMMO) {
 #pragma unroll
-      for (int s = 0; s < NSH; ++s) nrays += (uint32_t)__popcll(__ballot((cast_sh >> s) & 1u));
-    }
+    for (int s = 0; s < NSH; ++s) nrays += (uint32_t)__popcll(__ballot((cast_sh >> s) & 1u));
   }
   // rays traced (R): one fire-and-forget atomic per wave into its lane's counter
   const uint32_t w = __builtin_amdgcn_readfirstlane(nrays);

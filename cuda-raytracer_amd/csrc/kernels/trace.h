@@ -25,29 +25,20 @@ constexpr uint32_t PT_PRIM_NONE = 0xFFFFFFFFu;
 constexpr int TPB = 256;          // threads per workgroup (4 waves)
 constexpr int RPT = 4;            // rays per thread in a traversal item
 constexpr int TILE = TPB * RPT;   // rays per traversal item
-// rays per lane of a wave item (2: same, 8: -30 % on the dragon proxy)
-#ifndef PT_RPTW
-#define PT_RPTW 4
-#endif
 // a level runs 1024-ray workgroup items when its (node, lane) queues hold
-// this many rays on average, wave items otherwise (dragon proxy levels: 512:
-// 135 ms, 1024: 130, 4096: 130, 16384: 131, wave items only: 132)
-#ifndef PT_BLOCK_MODE_RAYS
-#define PT_BLOCK_MODE_RAYS 4096
-#endif
-// level-kernel workgroups: 16384 (vs 8192: dragon proxy levels -4 %; 2048
-// -15 %, 32768 within noise)
-#ifndef PT_LEVEL_GRID
-#define PT_LEVEL_GRID 16384
-#endif
-constexpr int RPTW = PT_RPTW;     // rays per lane in a wave-sized item
+// this many rays on average, wave items otherwise (BLOCK_MODE_RAYS_PER_PAIR;
+// dragon proxy levels: 512: 135 ms, 1024: 130, 4096: 130, 16384: 131, wave
+// items only: 132).  Level-kernel workgroups LEVEL_GRID: 16384 (vs 8192:
+// dragon proxy levels -4 %; 2048 -15 %, 32768 within noise).  Rays per lane of
+// a wave item RPTW (2: same, 8: -30 % on the dragon proxy).
+constexpr int RPTW = 4;           // rays per lane in a wave-sized item
 constexpr int WTILE = 64 * RPTW;  // rays per wave item (levels >= 1)
 constexpr int NLANE = 8;          // queue lanes (one per XCD)
 constexpr int CSTRIDE = 32;       // u32 per queue counter: each (node, lane) counter owns a 128-B line
 constexpr uint32_t MODE_WAVE = 0, MODE_BLOCK = 1;
-constexpr uint32_t BLOCK_MODE_RAYS_PER_PAIR = PT_BLOCK_MODE_RAYS;  // level mode threshold (mean rays per queue lane)
-constexpr int LEVEL_GRID = PT_LEVEL_GRID;  // workgroups of the level kernel (64 per CU: the
-                                          // dispatcher's refill balances uneven items)
+constexpr uint32_t BLOCK_MODE_RAYS_PER_PAIR = 4096;  // level mode threshold (mean rays per queue lane)
+constexpr int LEVEL_GRID = 16384;  // workgroups of the level kernel (64 per CU: the
+                                   // dispatcher's refill balances uneven items)
 constexpr int RCOUNT_SLOTS = 64;  // ray counters (u64, 128 B apart), indexed by workgroup & 63
 
 // device statistics slots (unsigned long long)
@@ -119,7 +110,6 @@ __host__ __device__ inline size_t cnt_idx(int node, int lane) { return ((size_t)
 // shadow ray occluded by one is never queued); every other ray is pushed into
 // the queues of the targets (nodes of one level, 1 or 2) whose boxes it hits.
 constexpr int MAX_ROOT_TARGETS = 16, MAX_INLINE_LEAVES = 4;
-constexpr uint32_t KMAP_BITS = 8, KMAP_SIZE = 1u << KMAP_BITS;  // record-order key map (shade.hip)
 struct RootTable {
   int nt;                          // queue targets
   int tnode[MAX_ROOT_TARGETS];     // target node ids

@@ -108,7 +108,7 @@ __device__ __forceinline__ bool prim_sphere(const Prim& q) {
 // plane hit (a wave skips the inside test when no lane has t in [tlo, tbest]),
 // the inside test predicated.  A ray parallel to the plane has t = +-inf or
 // NaN and misses.
-// t = num / den of the Baldwin-Weber test.  PT_FAST_DIV: the compiler's IEEE
+// t = num / den of the Baldwin-Weber test: the compiler's IEEE
 // division sequence (reciprocal, one refinement, quotient, two residual
 // corrections) without its range scaling (v_div_scale x 2) and special-case
 // fixup (v_div_fixup): 8 instead of 11 instructions and the same bits wherever
@@ -122,12 +122,8 @@ __device__ __forceinline__ bool prim_sphere(const Prim& q) {
 // plane to 29 decimal places).  The oracle divides with IEEE `/`; the GPU
 // parity tests check the two agree, tests/test_gpu_regress.py checks the
 // division itself down to |num| = 2^-100 bit for bit and to 2^-126 within
-// one ulp.
-#ifndef PT_FAST_DIV
-#define PT_FAST_DIV 1
-#endif
+// one ulp.  (Round 3: CBempty +1.5-3 %, the wavefront scenes +1.2-1.5 %.)
 __device__ __forceinline__ float div_rn(float a, float b) {
-  if constexpr (!PT_FAST_DIV) return a / b;
   const float y0 = __builtin_amdgcn_rcpf(b);
   const float e = __builtin_fmaf(-b, y0, 1.0f);
   const float y1 = __builtin_fmaf(e, y0, y0);
@@ -169,10 +165,8 @@ __device__ __forceinline__ float bw_plane(const f3 o, const float4 W) {
 }
 // STRICT: a hit needs t < tbest (the caller's best so far, no hit yet at
 // tbest = +inf, which no hit reaches): then every hit returned is a new best
-// PT_BW_POINT (default; the oracle's form): u and v from the hit point
-#ifndef PT_BW_POINT
-#define PT_BW_POINT 1
-#endif
+// u and v from the hit point, the oracle's form (round 4: 9 FMAs for both
+// instead of 14 for U(o) + t U.d and V(o) + t V.d; CBempty +5.4 %)
 // ZFIX: a hit at t = -0 is returned as +0 (the {prim, t} keys order t by its
 // bits); false where t only feeds comparisons and the hit point
 template <bool STRICT = false, bool ZFIX = true>
@@ -180,17 +174,9 @@ __device__ __forceinline__ float bw_test(const f3 o, const f3 d, const float4 U,
                                          float tbest, float tlo = 0.0f) {
   const float t = div_rn(-bw_plane(o, W), fdot(W.x, W.y, W.z, d.x, d.y, d.z));
   if (!(t >= tlo) | (STRICT ? !(t < tbest) : (t > tbest))) return -1.0f;
-  float u, v;
-  if constexpr (PT_BW_POINT) {
-    // barycentrics of the plane hit P = o + t d: U(P), V(P) (9 FMAs for
-    // both instead of 14 for U(o) + t U.d and V(o) + t V.d)
-    const f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
-    u = bw_plane(P, U);
-    v = bw_plane(P, V);
-  } else {
-    u = __builtin_fmaf(t, fdot(U.x, U.y, U.z, d.x, d.y, d.z), bw_plane(o, U));
-    v = __builtin_fmaf(t, fdot(V.x, V.y, V.z, d.x, d.y, d.z), bw_plane(o, V));
-  }
+  // barycentrics of the plane hit P = o + t d: U(P), V(P)
+  const f3 P = mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
+  const float u = bw_plane(P, U), v = bw_plane(P, V);
   // (unordered compares: a NaN u or v -- a ray parallel to the plane, t =
   // +-inf -- is a miss)
   const bool miss = !(u >= 0.0f) | !(v >= 0.0f) | !(u + v <= 1.0f);
@@ -227,22 +213,14 @@ __device__ __forceinline__ float tri_test_ref(const f3 o, const f3 d, const floa
   return t == 0.0f ? 0.0f : t;
 }
 // A triangle's closest-hit test in the record's arithmetic.
-// The U and V rows of a Baldwin-Weber record.  PT_UV_PAIRS: the record holds
-// them interleaved, {Ux, Vx, Uy, Vy}{Uz, Vz, Uw, Vw}{W} (bw_prim_records), so
-// the packed u / v evaluation (v_pk_fma_f32 with an SGPR pair operand) reads
-// each (U_k, V_k) pair straight from the record's SGPRs instead of copying
-// them into place (6 s_mov per primitive)
-#ifndef PT_UV_PAIRS
-#define PT_UV_PAIRS 1
-#endif
+// The U and V rows of a Baldwin-Weber record.  The record holds them
+// interleaved, {Ux, Vx, Uy, Vy}{Uz, Vz, Uw, Vw}{W} (bw_prim_records), so the
+// packed u / v evaluation (v_pk_fma_f32 with an SGPR pair operand) reads each
+// (U_k, V_k) pair straight from the record's SGPRs instead of copying them
+// into place (6 s_mov per primitive; round 4, +1-2 % on the single-leaf scenes)
 __device__ __forceinline__ void bw_uv(const Prim& q, float4& U, float4& V) {
-  if constexpr (PT_UV_PAIRS) {
-    U = make_float4(q.q0.x, q.q0.z, q.q1.x, q.q1.z);
-    V = make_float4(q.q0.y, q.q0.w, q.q1.y, q.q1.w);
-  } else {
-    U = q.q0;
-    V = q.q1;
-  }
+  U = make_float4(q.q0.x, q.q0.z, q.q1.x, q.q1.z);
+  V = make_float4(q.q0.y, q.q0.w, q.q1.y, q.q1.w);
 }
 template <bool REFA, bool STRICT = false, bool ZFIX = true>
 __device__ __forceinline__ float tri_test(const f3 o, const f3 d, const Prim& q, float tbest, float tlo = 0.0f) {
@@ -372,15 +350,8 @@ __device__ __forceinline__ f2v bw_test2(const f3x2& o, const f3x2& d, const floa
                                         f2v tbest, f2v tlo) {
   const f2v nm = -bw_plane2(o, W), dn = fdot2(sp3(W.x, W.y, W.z), d);
   const f2v t = f2v{div_rn(nm[0], dn[0]), div_rn(nm[1], dn[1])};
-  f2v u, v;
-  if constexpr (PT_BW_POINT) {
-    const f3x2 P{fma2(t, d.x, o.x), fma2(t, d.y, o.y), fma2(t, d.z, o.z)};
-    u = bw_plane2(P, U);
-    v = bw_plane2(P, V);
-  } else {
-    u = fma2(t, fdot2(sp3(U.x, U.y, U.z), d), bw_plane2(o, U));
-    v = fma2(t, fdot2(sp3(V.x, V.y, V.z), d), bw_plane2(o, V));
-  }
+  const f3x2 P{fma2(t, d.x, o.x), fma2(t, d.y, o.y), fma2(t, d.z, o.z)};
+  const f2v u = bw_plane2(P, U), v = bw_plane2(P, V);
   const f2v uv = u + v;
   const f2v tz = t + sp(0.0f);
   f2v r;
@@ -394,10 +365,8 @@ __device__ __forceinline__ f2v bw_test2(const f3x2& o, const f3x2& d, const floa
 }
 // The strict two-ray test with the hit update inside (default arithmetic):
 // where tri_test2<false, true> would return t >= 0 for ray i, bt_i = t (-0 as
-// +0: the keys order t by its bits) and bp_i = idx
-#ifndef PT_LEVEL_DIRECT
-#define PT_LEVEL_DIRECT 1
-#endif
+// +0: the keys order t by its bits) and bp_i = idx (round 4: the level
+// kernels' two-ray leaf test +1.1-1.5 % on the wavefront scenes)
 __device__ __forceinline__ void bw_update2(const f3x2& o, const f3x2& d, const Prim& q, f2v tlo, int idx, float& bt0,
                                            float& bt1, int& bp0, int& bp1) {
   float4 U, V;
@@ -435,33 +404,23 @@ __device__ __forceinline__ f2v tri_test2(const f3x2& o, const f3x2& d, const Pri
 // beats {bt, bp} -- nearer, or as near as the incoming key while this leaf has
 // no hit yet (its primitives are tested in increasing index order, so the
 // first of equal hits is the lowest).  A lane without a ray has bt < 0 and
-// takes nothing.  PT_SELECT_UPDATE: as two selects (no exec-mask branch).
-#ifndef PT_SELECT_UPDATE
-#define PT_SELECT_UPDATE 0  // (selects: leaf levels -3 to -7 %, CBempty -0.5 %)
-#endif
+// takes nothing.  (As two selects instead of the branch: leaf levels -3 to
+// -7 %, CBempty -0.5 %.)
 __device__ __forceinline__ void take_hit(float t, int k, float& bt, int& bp) {
-#if PT_SELECT_UPDATE
-  const bool take = (t >= 0.0f) & ((t < bt) | ((t == bt) & (bp < 0)));
-  bt = take ? t : bt;
-  bp = take ? k : bp;
-#else
   if (t >= 0.0f && (t < bt || (t == bt && bp < 0))) {
     bt = t;
     bp = k;
   }
-#endif
 }
 
-// PT_LEVEL_STRICT (the level kernels' leaf loops): the running best starts one
+// The strict leaf loops of the level kernels: the running best starts one
 // ulp above the ray's tmax (the key's t from the leaves already visited) and
 // the triangle tests admit only t below it, so "t <= tmax, and a first hit at
 // t == tmax counts" becomes "t < best", every hit the test returns is a new
 // best, and the update is a compare and two selects.  The same hits as
 // take_hit: equal t within a leaf keeps the lower index (tested first), a
-// hit at the incoming tmax still reaches the key's atomicMin.
-#ifndef PT_LEVEL_STRICT
-#define PT_LEVEL_STRICT 1
-#endif
+// hit at the incoming tmax still reaches the key's atomicMin (round 4: levels
+// +1 %).
 __device__ __forceinline__ float next_up(float x) {  // (x >= 0, or negative for an empty lane: unchanged)
   return x >= 0.0f && x < __builtin_inff() ? __uint_as_float(__float_as_uint(x) + 1u) : x;
 }
@@ -502,18 +461,14 @@ __device__ __forceinline__ bool box_hit(float bx0, float bx1, float by0, float b
   return tn <= tf;
 }
 
-// one axis's two slab distances b * inv - oi.  PT_BOX_PK: in one
-// v_pk_fma_f32 -- packed fp32 FMAs issue at twice the rate of v_fma_f32 on
-// gfx950 (130 against 74 TFLOP/s on independent chains, scripts/cal/pk_rate.hip),
-// yet the cluster masks of k_path_leaf measured slower with them: CBempty
-// 103,800 -> 100,800 Mrays/s, CBspheres 64,850 -> 62,700 (interleaved A/B, 2
-// runs each); a cluster pair's two triangles on packed fp32 likewise lost
-// (their records and the ray's broadcast pairs spilled at 64 VGPRs)
-#ifndef PT_BOX_PK
-#define PT_BOX_PK 0
-#endif
+// one axis's two slab distances b * inv - oi, as two v_fma_f32 (in one
+// v_pk_fma_f32 instead -- packed fp32 FMAs issue at twice the rate of
+// v_fma_f32 on gfx950, 130 against 74 TFLOP/s on independent chains,
+// scripts/cal/pk_rate.hip -- the cluster masks of k_path_leaf measured slower:
+// CBempty 103,800 -> 100,800 Mrays/s, CBspheres 64,850 -> 62,700, round 5; a
+// cluster pair's two triangles on packed fp32 likewise lost: their records
+// and the ray's broadcast pairs spilled at 64 VGPRs)
 __device__ __forceinline__ f2v slab2(float b0, float b1, float inv, float oi) {
-  if constexpr (PT_BOX_PK) return __builtin_elementwise_fma(f2v{b0, b1}, f2v{inv, inv}, f2v{-oi, -oi});
   return f2v{__builtin_fmaf(b0, inv, -oi), __builtin_fmaf(b1, inv, -oi)};
 }
 // The same test for a ray without a far limit (tmax = +inf: its min is the
@@ -715,20 +670,10 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 //     here (the callers write the empty r1 of invalid slots);
 //  3. a shadow ray (anyhit) occluded by an inline leaf is done: not queued;
 //     the others are pushed into the targets' queues with the tightened tmax.
-#ifndef PT_ROOT_EXT_PRETEST
-#define PT_ROOT_EXT_PRETEST 0
-#endif
-#ifndef PT_ROOT_PAIR
-#define PT_ROOT_PAIR 1
-#endif
-#ifndef PT_ROOT_RANGE_EARLY
-#define PT_ROOT_RANGE_EARLY 1
-#endif
-// (selects measured slower: CBbunny -2.4 %, dragon proxy -0.6 %, round 4)
-#ifndef PT_ROOT_SELECT
-#define PT_ROOT_SELECT 0
-#endif
-// PT_ROOT_CLUSTER: an extension ray (closest hit) tests the inline leaves'
+// (The hit update as selects measured slower: CBbunny -2.4 %, dragon proxy
+// -0.6 %, round 4; a division-free pre-test for extension rays too: CBbunny
+// shade +3.7 ms, round 4.)
+// Candidate clusters: an extension ray (closest hit) tests the inline leaves'
 // primitive clusters (RootTable::nc: host-built, guard-banded boxes as
 // conservative as the BVH's) only where it enters the cluster's box, each lane
 // its own candidates (the member records staged in LDS by the caller: lrec,
@@ -743,18 +688,11 @@ __device__ __forceinline__ void push_children(const TraceArgs& A, const Tg& tg, 
 // cycles (extension rays 13,900 -> 6,300; PT_SHADE_TIMING), CBbunny 122 ->
 // 114.7 ms per frame, dragon proxy +0.5 %; uncached vector loads of the
 // records instead of LDS lost 2,000 cycles in that phase (the dependent
-// round trips per candidate).
-#ifndef PT_ROOT_CLUSTER
-#define PT_ROOT_CLUSTER 1
-#endif
-// PT_ROOT_OCC_AABB: shadow rays pick their candidate clusters by the overlap of
-// their segment's bounding box with the cluster boxes (shade.hip
-// PT_PATH_OCC_AABB).  Off: CBbunny 112.35 -> 113.2 ms per frame with it, the
+// round trips per candidate).  Shadow rays pick their candidates by the slab
+// test too: the segment-box overlap k_path_leaf uses (shade.hip
+// leaf_occluded_aabb) measured CBbunny 112.35 -> 113.2 ms per frame, the
 // dragon proxy unchanged (the root pass computes the slab test's reciprocals
-// for its target boxes anyway)
-#ifndef PT_ROOT_OCC_AABB
-#define PT_ROOT_OCC_AABB 0
-#endif
+// for its target boxes anyway).
 template <int R, bool REFA = false, bool TMIN = false, bool CL = false>
 __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T, int lane, const uint32_t (&id)[R],
                                           const f3 (&o)[R], const f3 (&d)[R], const float (&tmax)[R],
@@ -775,7 +713,7 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
       float tt;
       if (prim_sphere<REFA>(q)) {
         tt = sphere_test(o[j], d[j], q.q0, q.q1, tlo);
-      } else if (anyhit[j] || PT_ROOT_EXT_PRETEST) {
+      } else if (anyhit[j]) {
         // shadow rays: division-free pre-test (they mostly point away from
         // the walls or end before them, see tri_outside)
         float ndd, num;
@@ -785,13 +723,7 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
       } else {
         tt = tri_test<REFA>(o[j], d[j], q, bt, tlo);
       }
-      if constexpr (PT_ROOT_SELECT) {
-        // (as selects: no exec-mask branch per primitive; bp < 0 is the
-        // largest unsigned value)
-        const bool take = (tt >= 0.0f) & ((tt < bt) | ((tt == bt) & ((uint32_t)gi < (uint32_t)bp)));
-        bt = take ? tt : bt;
-        bp = take ? gi : bp;
-      } else if (tt >= 0.0f && (tt < bt || (tt == bt && (bp < 0 || gi < bp)))) {
+      if (tt >= 0.0f && (tt < bt || (tt == bt && (bp < 0 || gi < bp)))) {
         bt = tt;
         bp = gi;
       }
@@ -800,29 +732,13 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
       const f3 inv = mk(__builtin_amdgcn_rcpf(safe_dir(d[j].x)), __builtin_amdgcn_rcpf(safe_dir(d[j].y)),
                         __builtin_amdgcn_rcpf(safe_dir(d[j].z)));
       const f3 oi = mk(o[j].x * inv.x, o[j].y * inv.y, o[j].z * inv.z);
-      if (CL && PT_ROOT_CLUSTER && (anyhit[j] ? T.nc_shadow : T.nc) > 0) {
+      if (CL && (anyhit[j] ? T.nc_shadow : T.nc) > 0) {
         if (valid[j]) {
           const CPTR(f4v) B = (const CPTR(f4v))T.cbox;
           uint32_t cm = 0u;
-          if (anyhit[j] && PT_ROOT_OCC_AABB) {
-            // a shadow segment: its bounding box against the cluster boxes
-            // (k_path_leaf's PT_PATH_OCC_AABB, the same argument)
-            const float tm = fminf(bt, 0x1p127f);
-            const f3 e = mk(__builtin_fmaf(tm, d[j].x, o[j].x), __builtin_fmaf(tm, d[j].y, o[j].y),
-                            __builtin_fmaf(tm, d[j].z, o[j].z));
-            const f3 lo = mk(fminf(o[j].x, e.x), fminf(o[j].y, e.y), fminf(o[j].z, e.z));
-            const f3 hi = mk(fmaxf(o[j].x, e.x), fmaxf(o[j].y, e.y), fmaxf(o[j].z, e.z));
-            for (int c = 0; c < T.nc; ++c) {
-              const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
-              const bool ov =
-                  !((hi.x < b0.x) | (lo.x > b0.y) | (hi.y < b0.z) | (lo.y > b0.w) | (hi.z < b1.x) | (lo.z > b1.y));
-              cm = mask_bit(cm, ov, c);
-            }
-          } else {
-            for (int c = 0; c < T.nc; ++c) {
-              const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
-              cm |= box_hit(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv, bt) ? (1u << c) : 0u;
-            }
+          for (int c = 0; c < T.nc; ++c) {
+            const float4 b0 = f4(B[2 * c]), b1 = f4(B[2 * c + 1]);
+            cm |= box_hit(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, oi, inv, bt) ? (1u << c) : 0u;
           }
           // (a shadow ray is done at its first hit)
           while (cm && !(anyhit[j] && bp >= 0)) {
@@ -852,13 +768,13 @@ __device__ __forceinline__ void root_pass(const TraceArgs& A, const RootTable& T
           const int pstart = T.istart[i], pcount = T.icount[i];
           const float b0 = T.ib[0][i], b1 = T.ib[1][i], b2 = T.ib[2][i], b3 = T.ib[3][i], b4 = T.ib[4][i],
                       b5 = T.ib[5][i];
-          if constexpr (PT_ROOT_RANGE_EARLY) asm volatile("" ::"s"(pstart), "s"(pcount));
+          asm volatile("" ::"s"(pstart), "s"(pcount));
           if (!valid[j] || !box_hit(b0, b1, b2, b3, b4, b5, oi, inv, bt)) continue;
           constexpr int PS = prim_stride<REFA>();
           const CPTR(f4v) P = (const CPTR(f4v))(A.prims + (size_t)pstart * PS);
           int kk = 0;
-          if constexpr (!REFA && PT_ROOT_PAIR) {
-            // two records per scalar round trip
+          if constexpr (!REFA) {
+            // two records per scalar round trip (round 4: +0.8 % on CBbunny)
             for (; kk + 1 < pcount; kk += 2, P += 2 * PS) {
               Prim qa, qb;
               load_prim_pair(P, qa, qb);
@@ -944,7 +860,7 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
     int bp[RPT];
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
-      bt[j] = PT_LEVEL_STRICT ? next_up(tmax[j]) : tmax[j];
+      bt[j] = next_up(tmax[j]);
       bp[j] = -1;
     }
     constexpr int PS = prim_stride<REFA>();
@@ -955,25 +871,23 @@ __device__ __forceinline__ uint32_t process_item(const TraceArgs& A, int node, u
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {
           if (j >= nj) break;
-          if constexpr (PT_LEVEL_STRICT) take_strict(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
-          else take_hit(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
+          take_strict(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
         }
       } else {
 #pragma unroll
         for (int j = 0; j < RPT; j += 2) {
           if (j >= nj) break;
-          if constexpr (!REFA && PT_LEVEL_STRICT && PT_BW_POINT && PT_LEVEL_DIRECT) {
+          if constexpr (!REFA) {
             // (the update inside the test, no -1 sentinel)
             bw_update2(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{tlo[j], tlo[j + 1]}, pstart + k, bt[j],
                        bt[j + 1], bp[j], bp[j + 1]);
             continue;
           }
-          const f2v t2 = tri_test2<REFA, PT_LEVEL_STRICT>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q,
-                                                          f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
+          const f2v t2 = tri_test2<REFA, true>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{bt[j], bt[j + 1]},
+                                               f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
-            if constexpr (PT_LEVEL_STRICT) take_strict(t2[i], pstart + k, bt[j + i], bp[j + i]);
-            else take_hit(t2[i], pstart + k, bt[j + i], bp[j + i]);
+            take_strict(t2[i], pstart + k, bt[j + i], bp[j + i]);
           }
         }
       }
@@ -1199,7 +1113,7 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     int bp[RPTW];
 #pragma unroll
     for (int j = 0; j < RPTW; ++j) {
-      bt[j] = PT_LEVEL_STRICT ? next_up(tmax[j]) : tmax[j];
+      bt[j] = next_up(tmax[j]);
       bp[j] = -1;
     }
     constexpr int PS = prim_stride<REFA>();
@@ -1211,25 +1125,23 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 #pragma unroll
         for (int j = 0; j < RPTW; ++j) {
           if (j >= nj) break;
-          if constexpr (PT_LEVEL_STRICT) take_strict(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
-          else take_hit(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
+          take_strict(sphere_test(o[j], d[j], q.q0, q.q1, tlo[j]), pstart + k, bt[j], bp[j]);
         }
       } else {
 #pragma unroll
         for (int j = 0; j < RPTW; j += 2) {
           if (j >= nj) break;
-          if constexpr (!REFA && PT_LEVEL_STRICT && PT_BW_POINT && PT_LEVEL_DIRECT) {
+          if constexpr (!REFA) {
             // (the update inside the test, no -1 sentinel)
             bw_update2(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{tlo[j], tlo[j + 1]}, pstart + k, bt[j],
                        bt[j + 1], bp[j], bp[j + 1]);
             continue;
           }
-          const f2v t2 = tri_test2<REFA, PT_LEVEL_STRICT>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q,
-                                                          f2v{bt[j], bt[j + 1]}, f2v{tlo[j], tlo[j + 1]});
+          const f2v t2 = tri_test2<REFA, true>(pair3(o[j], o[j + 1]), pair3(d[j], d[j + 1]), q, f2v{bt[j], bt[j + 1]},
+                                               f2v{tlo[j], tlo[j + 1]});
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
-            if constexpr (PT_LEVEL_STRICT) take_strict(t2[i], pstart + k, bt[j + i], bp[j + i]);
-            else take_hit(t2[i], pstart + k, bt[j + i], bp[j + i]);
+            take_strict(t2[i], pstart + k, bt[j + i], bp[j + i]);
           }
         }
       }
@@ -1312,23 +1224,20 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
 // 5 waves per SIMD (<= 96 VGPRs): the two-level push needs 91 without spills
 // (at 6 waves, 80 VGPRs, it spilled 19; round 1's one-level push: 6 waves
 // +2-3 % over 4, 7 waves spilled and lost 4 %)
-#ifndef PT_LEVEL_ATTR
-#define PT_LEVEL_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
-#endif
+constexpr int LEVEL_WAVES = 5;
 // LEAF: a level whose queued nodes are all leaves (the levels between two
 // real levels hold only the leaf rays of the real level above them): the
-// leaf-only code needs fewer registers and runs PT_LEAF_WAVES waves per SIMD
+// leaf-only code needs fewer registers and runs LEAF_WAVES waves per SIMD
 // (8, round 3: 64 VGPRs, 4 spilled, against 68 at 7 waves: the leaf levels'
-// share of the dragon proxy's levels ~1 % faster)
-#ifndef PT_LEAF_WAVES
-#define PT_LEAF_WAVES 8
-#endif
+// share of the dragon proxy's levels ~1 % faster; round 5: 7 waves -0.3-0.5 %)
+constexpr int LEAF_WAVES = 8;
 // TMIN: the rays carry a t_min (pt_intersect with t_min > 0 somewhere in the
 // batch): hits before it do not count (TraceArgs::tmin)
 template <bool REFA, bool LEAF, bool BLOCK = true, bool TMIN = false>
 __device__ __forceinline__ void trace_level_body(const TraceArgs& A, const LevelArgs& L);
 template <bool REFA, bool TMIN = false>
-__global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, LevelArgs L) {
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(LEVEL_WAVES, 8))) void k_trace_level(TraceArgs A,
+                                                                                                           LevelArgs L) {
   trace_level_body<REFA, false, true, TMIN>(A, L);
 }
 // The real levels of the two-level traversal always run wave items (their
@@ -1337,17 +1246,15 @@ __global__ __launch_bounds__(TPB) PT_LEVEL_ATTR void k_trace_level(TraceArgs A, 
 // VGPRs, 5 spilled): dragon proxy level 6 30.1 -> 28.4 ms, frame +0.9 %
 // (at 5 waves it measured the same as k_trace_level); round 3: 7 waves (72
 // VGPRs, 6 spilled) with the leaf kernel at 8: levels -1.5 to -3 % on the
-// dragon proxy trees and bunny.dae
-#ifndef PT_REAL_WAVES
-#define PT_REAL_WAVES 7
-#endif
-#define PT_REAL_ATTR __attribute__((amdgpu_waves_per_eu(PT_REAL_WAVES, 8)))
+// dragon proxy trees and bunny.dae (round 5: 6 waves -0.3-0.5 %)
+constexpr int REAL_WAVES = 7;
 template <bool REFA, bool TMIN = false>
-__global__ __launch_bounds__(TPB) PT_REAL_ATTR void k_trace_real(TraceArgs A, LevelArgs L) {
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(REAL_WAVES, 8))) void k_trace_real(TraceArgs A,
+                                                                                                         LevelArgs L) {
   trace_level_body<REFA, false, false, TMIN>(A, L);
 }
 template <bool REFA, bool TMIN = false>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PT_LEAF_WAVES, 8))) void k_trace_leaves(
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(LEAF_WAVES, 8))) void k_trace_leaves(
     TraceArgs A, LevelArgs L) {
   trace_level_body<REFA, true, true, TMIN>(A, L);
 }
@@ -1426,10 +1333,7 @@ __device__ __forceinline__ void trace_level_body(const TraceArgs& A, const Level
 // processed).  Same closest-hit rules as the level kernels (min of the {t,
 // prim} key, ties to the lowest primitive; a shadow ray stops at its first
 // occluder), so the result does not depend on the traversal order.
-#ifndef PT_DFS_STACK
-#define PT_DFS_STACK 32
-#endif
-constexpr int DFS_STACK = PT_DFS_STACK;  // per-lane stack entries (the host checks 3 x subtree depth fits)
+constexpr int DFS_STACK = 32;  // per-lane stack entries (the host checks 3 x subtree depth fits)
 __device__ __forceinline__ bool box_hit_t(float bx0, float bx1, float by0, float by1, float bz0, float bz1,
                                           const f3 oi, const f3 inv, float tmax, float& tn) {
   float tx0 = __builtin_fmaf(bx0, inv.x, -oi.x), tx1 = __builtin_fmaf(bx1, inv.x, -oi.x);
@@ -1565,10 +1469,7 @@ __global__ __launch_bounds__(TPB) void k_trace_dfs(TraceArgs A, LevelArgs L) {
 // Each thread owns SCAN_NPT consecutive nodes of a chunk of 1024 * SCAN_NPT:
 // their counter loads are issued together, and a level that fits one chunk
 // (all but the widest) keeps its counts in registers between the passes.
-#ifndef PT_SCAN_NPT
-#define PT_SCAN_NPT 2
-#endif
-constexpr int SCAN_NPT = PT_SCAN_NPT;
+constexpr int SCAN_NPT = 2;
 // A node's child ids and prim_count in two 16-B loads (pt_node: child[4] at
 // byte 96, {prim_start, prim_count, level, ref_id} at 112).
 __device__ __forceinline__ void load_links(const TraceArgs& A, int node, int4& ch, int& pc) {

@@ -392,10 +392,7 @@ __global__ void k_prim_records(const float* __restrict__ pos, const float* __res
 // range (as the radix tree's nodes do).
 // search window radius; visits per ray on the dragon proxy: 2: 5.16, 3: 5.22,
 // 4: 4.89, 8: 5.11, 16: 5.21, 32: 5.22 (the radix tree: 6.93, host SAH: 4.36)
-#ifndef PT_PLOC_R
-#define PT_PLOC_R 4
-#endif
-constexpr int PLOC_R = PT_PLOC_R;
+constexpr int PLOC_R = 4;
 
 __device__ __forceinline__ float union_area(const Box& a, const Box& b) {
   const float x = fmaxf(a.hi[0], b.hi[0]) - fminf(a.lo[0], b.lo[0]);

@@ -126,8 +126,6 @@ struct pt_ctx {
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
   uint32_t* d_work = nullptr;  // k_path_leaf path-region counters (128 B apart)
-  uint32_t* d_kmap = nullptr;  // record-order key map (KMAP_SIZE): root target of primitive i << kmap_shift
-  uint32_t kmap_shift = 0;
   float4* d_res = nullptr;     // per-path radiance of a chunk
   size_t res_cap = 0;
   uint4* d_wstate = nullptr;   // per shade workgroup {block next, block end, live slots, shaded vertices}
@@ -230,7 +228,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_lights, c->d_cbox, c->d_rcbox, c->d_rcmem, c->d_rcmem_ref, c->d_rcinfo, c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
-                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_kmap, c->d_res, c->d_wstate, c->d_live, c->d_pool,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live, c->d_pool,
                   c->d_pix_of, c->d_accum, c->d_frame, c->d_tmin, c->d_ray_b, c->d_ps0_b, c->d_ps1_b, c->d_ps2_b,
                   c->d_ps3_b, c->d_compact, c->d_act_pix, c->d_act_slot};
   for (void* p : ptrs)
@@ -255,10 +253,7 @@ static constexpr uint32_t CBLK = 2 * CREGIONS;
 static constexpr uint32_t LIVE_WORDS = 2 + CREGIONS;
 // paths per chunk: pt_ctx::chunk_paths (per-path radiance buffer: 12 B each);
 // POLL_GROUP passes are queued between two reads of the finished-path count
-#ifndef PT_POLL_GROUP
-#define PT_POLL_GROUP 4
-#endif
-static constexpr int POLL_GROUP = PT_POLL_GROUP;
+static constexpr int POLL_GROUP = 4;
 // ray-id queues hold ID_FACTOR x qfactor ids per ray slot and region (the
 // entry queues qfactor entries of 32 B).  Queues live in QREGIONS rotating
 // regions: the scan of level l allocates its targets' queues (levels l + 1 and,
@@ -269,14 +264,8 @@ static constexpr size_t QREGIONS = 3;
 // Ray entries below the root targets' level measured -3 % on CBbunny and
 // +1.5-4 % on the dragon proxy trees (the leaf-heavy levels are bound by the
 // leaf loop and the closest-hit atomics, not by the ray gathers): off by default.
-#ifndef PT_ENTRY_LEVEL_DEFAULT
-#define PT_ENTRY_LEVEL_DEFAULT 0
-#endif
-static constexpr int ENTRY_LEVEL_DEFAULT = PT_ENTRY_LEVEL_DEFAULT;
-#ifndef PT_SCAN_MULTI_MIN_DEFAULT
-#define PT_SCAN_MULTI_MIN_DEFAULT 512
-#endif
-static constexpr int SCAN_MULTI_MIN_DEFAULT = PT_SCAN_MULTI_MIN_DEFAULT;
+static constexpr int ENTRY_LEVEL_DEFAULT = 0;  // (env PT_ENTRY_LEVEL)
+static constexpr int SCAN_MULTI_MIN_DEFAULT = 512;  // (env PT_SCAN_MULTI_MIN)
 static uint32_t max_batch_paths(const pt_ctx* c, uint32_t slots_per_path) {
   // u32 entry offsets: both halves of the entry queues, and the root's id
   // queues (<= 16 targets x every ray, see root_per_lane)
@@ -914,13 +903,9 @@ static std::vector<float4> bw_prim_records(const pt_scene_desc* s) {
     } else {
       double r[12];
       bw_rows(q, r);
-      if (PT_UV_PAIRS) {  // U and V interleaved (trace.hip bw_uv)
-        o[0] = make_float4((float)r[0], (float)r[4], (float)r[1], (float)r[5]);
-        o[1] = make_float4((float)r[2], (float)r[6], (float)r[3], (float)r[7]);
-      } else {
-        o[0] = make_float4((float)r[0], (float)r[1], (float)r[2], (float)r[3]);
-        o[1] = make_float4((float)r[4], (float)r[5], (float)r[6], (float)r[7]);
-      }
+      // U and V interleaved (trace.hip bw_uv)
+      o[0] = make_float4((float)r[0], (float)r[4], (float)r[1], (float)r[5]);
+      o[1] = make_float4((float)r[2], (float)r[6], (float)r[3], (float)r[7]);
       o[2] = make_float4((float)r[8], (float)r[9], (float)r[10], (float)r[11]);
     }
     o[3] = make_float4(q[3], 0.f, 0.f, 0.f);
@@ -1127,7 +1112,6 @@ int pt_create(pt_ctx** out, int device) {
   if (const char* q = getenv("PT_COMPACT_FIRST")) {
     c->compact_first = std::min(100, std::max(1, atoi(q)));
   }
-  c->compaction = c->compaction && PT_SORT_WAVE == 3;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return PT_E_HIP;
@@ -1137,7 +1121,6 @@ int pt_create(pt_ctx** out, int device) {
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, PATH_REGIONS_MAX * PATH_CTR_STRIDE * 4) != hipSuccess ||
-      hipMalloc((void**)&c->d_kmap, KMAP_SIZE * 4) != hipSuccess ||
       hipMalloc((void**)&c->d_live, LIVE_WORDS * 4) != hipSuccess ||
       hipMalloc((void**)&c->d_compact, MAX_COMPACTIONS * CBLK * 4) != hipSuccess ||
       hipMalloc((void**)&c->d_pool, POOLS * CSTRIDE * 4) != hipSuccess ||
@@ -1216,32 +1199,6 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   for (int i = 0; i < s->n_bsdfs; ++i)
     if (s->bsdfs[i].type == PT_BSDF_GLASS || s->bsdfs[i].type == PT_BSDF_REFRACTION) c->has_glass = true;
   build_root_table(c);
-  {  // record-order key map: the root target whose subtree holds primitive i << kmap_shift
-    uint32_t b = 0;
-    while ((1u << b) < (uint32_t)c->n_prims) ++b;
-    c->kmap_shift = b > KMAP_BITS ? b - KMAP_BITS : 0u;
-    std::vector<uint32_t> km(KMAP_SIZE, (uint32_t)MAX_ROOT_TARGETS);
-    for (int t = 0; t < c->rt.nt; ++t) {
-      int lo = INT32_MAX, hi = -1;
-      std::vector<int> st{c->rt.tnode[t]};
-      while (!st.empty()) {
-        const pt_node& n = c->nodes_host[st.back()];
-        st.pop_back();
-        if (n.prim_count > 0) {
-          lo = std::min(lo, n.prim_start);
-          hi = std::max(hi, n.prim_start + n.prim_count);
-        } else {
-          for (int k = 0; k < 4; ++k)
-            if (n.child[k] >= 0) st.push_back(n.child[k]);
-        }
-      }
-      for (uint32_t i = 0; i < KMAP_SIZE; ++i) {
-        const int p = (int)(i << c->kmap_shift);
-        if (p >= lo && p < hi) km[i] = (uint32_t)t;
-      }
-    }
-    HIPCHK(c, hipMemcpy(c->d_kmap, km.data(), KMAP_SIZE * 4, hipMemcpyHostToDevice));
-  }
   if ((rc = dalloc(c, &c->d_nodes, s->n_nodes))) return rc;
   if ((rc = dalloc(c, &c->d_prims, (size_t)s->n_prims * prim_stride<false>()))) return rc;
   if ((rc = dalloc(c, &c->d_prims_ref, (size_t)s->n_prims * 6))) return rc;
@@ -1306,7 +1263,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
       const uint32_t m2 = meta | (flat ? 0u : SHADE_SMOOTH);
       float mf;
       memcpy(&mf, &m2, 4);
-      if (flat && PT_FLAT_NS) {
+      if (flat) {
         // a flat triangle's shading normal normalize(n0) (ptmath.h normalize:
         // n0 * (1 / sqrt(fma-chain dot)), correctly rounded fp32 here as on
         // the device), so the kernels read it instead of computing it; the
@@ -1571,8 +1528,6 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       while ((1u << b) < (uint32_t)c->n_prims) ++b;
       S.kshift = b > SORT_KEY_BITS ? b - SORT_KEY_BITS : 0u;
     }
-    S.kmap = c->d_kmap;
-    S.kmshift = c->kmap_shift;
     if (c->root_leaf) {
       // single-leaf tree: every path runs to completion in one kernel
       // (persistent waves with path regeneration, output res[P])
