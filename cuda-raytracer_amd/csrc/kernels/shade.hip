@@ -75,6 +75,10 @@ struct ShadeArgs {
   // writes res[P] and starts the next unstarted path
   float4* res;        // per-path radiance of the chunk
   uint32_t M;         // paths in the chunk
+  // k_path_leaf's path grabs: chunk size, paths per region, regions, the
+  // regions' counters (re-read from the kernel-argument segment at each grab)
+  uint32_t grab_chunk, grab_region, grab_nreg;
+  uint32_t* grab_work;
   // paths are handed out in blocks of POOL_BLOCK consecutive paths (one sample
   // of 256 owned pixels): block c comes from dispenser c % POOLS
   uint4* wstate;      // per workgroup: {next, end} of its current block, live slots after its last pass,
@@ -1644,9 +1648,12 @@ __device__ __forceinline__ bool leaf_occluded(const float4* prims, int pstart, i
 // -> 17.2 ms per frame, CBspheres 28.6 -> 26.6 (v_mul_hi_u32 + v_mul_lo_u32
 // instead of v_mad_u64_u32 measured slower in that configuration).
 constexpr bool PATH_MAD64 = true, PATH_RNG_EARLY = false;
-// paths a wave takes from the global counter at a time (CBempty: 128: -1.3 %,
-// 512: +1.6 %, 1024: +1.4 %, 2048: +0.1 % against 256; re-measured in round
-// 3: 1024 -0.3 %, 256 -1.2 % against 512; round 5: 1024 -0.5 %, 256 -1.6 %)
+// paths a wave takes from the global counter at a time for a whole frame
+// (CBempty: 128: -1.3 %, 512: +1.6 %, 1024: +1.4 %, 2048: +0.1 % against 256;
+// re-measured in round 3: 1024 -0.3 %, 256 -1.2 % against 512; round 5: 1024
+// -0.5 %, 256 -1.6 %); the guided schedule's largest chunk.  The plain grabs
+// take the launch's `chunk` (pt_ctx::path_chunk_for: smaller for a small
+// launch, whose tail is about one chunk's time)
 constexpr uint32_t PATH_CHUNK = 512;
 
 // With all path state in registers: 6 waves per SIMD (80 VGPRs, no spills);
@@ -1668,49 +1675,23 @@ constexpr int PATH_WAVES = 8;
 // at every launch, below).  Refilling idle lanes only once k of a wave's 64
 // are idle measured slower (k = 4, 8, 16: CBempty -0.6 / +0.0 / -0.9 %,
 // CBspheres -0.2 / -0.2 / -2.3 %, round 5): every idle lane refills.
-// Guided path grabs: the k-th grab from the counter takes the range
-// [S[j] + (k - G[j]) c[j], ...) of the phase j with G[j] <= k < G[j+1]; the
-// chunk size halves as the unstarted paths run out (512 down to 64), so no
-// wave takes a large chunk late.  Waves on one SIMD run at very different
-// speeds (1/8 share of a CBempty frame: 2 to 24 chunks per wave, PMC timing
-// build), and a slow wave's last 512-path chunk ran up to 0.9 ms after the
-// counter was exhausted.  The paths are split into path regions, one per
-// counter (128 B apart; a workgroup starts on region blockIdx % nreg and
-// moves on when it is empty): one counter for all waves queued the grabs,
-// each a same-address device atomic (2-100 us under contention, timing
-// build).  1/8 share of a CBempty frame: 5.18 ms (one counter, 512-path
-// chunks) -> 5.03 (guide 4) -> 4.89 (guide 4, 8 regions); ideal 4.59;
-// CBspheres 6.32 -> 5.88 ms; full frames within noise.
-constexpr int PATH_PHASES = 4;
+// Path grabs (round 6): the launch's paths are split into `grab_nreg`
+// contiguous path regions of `grab_region` paths, one counter each (128 B
+// apart); a wave takes `grab_chunk` paths at a time from its region (its
+// workgroup's, blockIdx % nreg) and moves on to the next region when that one
+// is dry; it exits once every region is.  One counter for the whole launch
+// saturated near 90 M grabs/s (a CBempty frame in 128-path chunks took 24.5
+// instead of 16.8 ms), and a launch's tail is about one chunk's time: the
+// host picks the chunk by the launch's paths per resident lane (pt_render).
+// The grab's operands are re-read from the kernel-argument segment and the
+// wave's region state lives in LDS, so the path loop holds none of them in
+// SGPRs (held there they spilled 64 SGPRs to VGPR lanes instead of 28, and a
+// whole frame ran 8 % slower).  Round 2-5's guided schedule (chunks halving
+// from 512 to 64 as the paths ran out, its phase arithmetic in SGPRs) is gone:
+// it lost on whole frames (2.6 %) and, at the round-5 kernels, on the 1/8
+// share too.
 constexpr uint32_t PATH_REGIONS_MAX = 32;
 constexpr uint32_t PATH_CTR_STRIDE = 32;  // u32s between region counters (128 B)
-
-// The k-th grab of path region [lo, hi): phase j hands out chunks of
-// PATH_CHUNK >> j and begins tail_unit * (PATH_CHUNK >> (j - 1)) paths before
-// hi (tail_unit = the region's waves x the guide factor; 0: one phase).
-// Returns false once the region's paths are all handed out.
-__device__ __forceinline__ bool path_grab(uint32_t lo, uint32_t hi, uint32_t tail_unit, uint32_t k, uint32_t& b,
-                                          uint32_t& e) {
-  uint32_t s0 = lo, g = 0;
-#pragma unroll
-  for (int j = 0; j < PATH_PHASES; ++j) {
-    const uint32_t c = PATH_CHUNK >> j;
-    uint32_t s1 = hi;
-    if (j + 1 < PATH_PHASES) {
-      const uint64_t rem = (uint64_t)tail_unit * (PATH_CHUNK >> j);
-      s1 = rem >= (uint64_t)(hi - s0) ? s0 : hi - (uint32_t)rem;
-    }
-    const uint32_t n = (s1 - s0 + c - 1) / c;
-    if (k - g < n) {
-      b = s0 + (k - g) * c;
-      e = min(b + c, s1);
-      return true;
-    }
-    g += n;
-    s0 = s1;
-  }
-  return false;
-}
 
 // PT_PATH_TIMING (diagnostic build only): per-wave wall-clock marks (entry,
 // first empty grab, exit, chunks taken) for pt_dbg_path_timing
@@ -1721,20 +1702,14 @@ __device__ __forceinline__ bool path_grab(uint32_t lo, uint32_t hi, uint32_t tai
 constexpr uint32_t PT_TIMING_WAVES = 16384;
 static __device__ unsigned long long g_path_timing[PT_TIMING_WAVES * 8];
 #endif
-// GUIDED: the guided grabs above; otherwise every grab is PATH_CHUNK paths
-// from one counter (work[0]).  The guided schedule's bookkeeping costs SGPRs
-// (52 spilled instead of 30) and a whole 1024^2 x 256 spp CBempty frame 2.6 %
-// (35.9 -> 36.8 ms), while it shortens the tail of small chunks (a 1/8 share:
-// 5.05 -> 4.89 ms): the host takes it only when the chunk is small against the
-// resident lanes (PT_PATH_GUIDED_BELOW paths per lane, default 128).
 // SPH: the leaf holds spheres (false: the sphere test is not compiled in; the
 // host picks the variant, pt_ctx::has_sphere)
 // CNT: the counting variant (PT_FLAG_COUNT_TESTS): executed tests into
 // rcount's lines (words 1-3 of each 128-B counter line)
-template <int NSH, bool REFA, bool GUIDED, bool SPH = true, bool XL = false, bool CNT = false>
+template <int NSH, bool REFA, bool SPH = true, bool XL = false, bool CNT = false>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES, 8))) void k_path_leaf(
     ShadeArgs S, int pstart, int pcount, int passes, unsigned long long* __restrict__ rcount,
-    uint32_t* __restrict__ work, uint32_t nreg, uint32_t tail_unit, uint32_t* __restrict__ err) {
+    uint32_t* __restrict__ err) {
   const uint32_t lid = lane_id();
   // light_of<true> reads the light at offsetof(ShadeArgs, light) of the
   // kernel-argument segment, so S must stay this kernel's FIRST parameter:
@@ -1770,9 +1745,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES,
   }
   // rays traced by the wave (wave-uniform, counted from ballots: no VGPR)
   uint32_t nrays = 0;
-  // wave-uniform: the path region this wave grabs from (its workgroup's, then
-  // the next ones as they run out) and how many regions it has found empty
-  uint32_t reg = blockIdx.x % nreg, tried = 0;
+  // per wave: the path region it grabs from (its workgroup's, then the next
+  // ones as they run dry) and how many regions it has found dry
+  __shared__ uint32_t s_grab[TPB / 64][2];
+  if (lid == 0) {
+    s_grab[threadIdx.x >> 6][0] = blockIdx.x % S.grab_nreg;
+    s_grab[threadIdx.x >> 6][1] = 0u;
+  }
 #if PT_PATH_TIMING
   const unsigned long long tm0 = wall_clock64();
   unsigned long long tm_drain = 0, tm_grab = 0, tm_grab_max = 0;
@@ -1818,32 +1797,38 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES,
 #if PT_PATH_TIMING
       const unsigned long long tg = wall_clock64();
 #endif
-      uint32_t b = 0, e = 0;
-      if constexpr (!GUIDED) {
-        if (lid == 0) b = atomicAdd(work, PATH_CHUNK);
-        b = __builtin_amdgcn_readfirstlane(b);
-        drained = b >= S.N;
-        next = drained ? 0u : b;
-        end = drained ? 0u : min(b + PATH_CHUNK, S.N);
-      } else {
+      uint32_t b = 0, e = 0, dry = 0;
       if (lid == 0) {
+        // (the grab's operands from the kernel-argument segment, opaque to the
+        // compiler: not held in SGPRs across the path loop)
+        const CPTR(char) kp = (const CPTR(char))__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kp));
+        const CPTR(uint32_t) ga = (const CPTR(uint32_t))(kp + offsetof(ShadeArgs, grab_chunk));
+        const uint32_t chunk = ga[0], region = ga[1], nreg = ga[2];
+        typedef uint32_t* wptr_t;
+        uint32_t* const work = *(const CPTR(wptr_t))(kp + offsetof(ShadeArgs, grab_work));
+        uint32_t* const gs = s_grab[threadIdx.x >> 6];
+        uint32_t reg = gs[0], tried = gs[1];
         while (tried < nreg) {
-          const uint32_t k = atomicAdd(work + reg * PATH_CTR_STRIDE, 1u);
-          const uint32_t lo = (uint32_t)((uint64_t)S.N * reg / nreg);
-          const uint32_t hi = (uint32_t)((uint64_t)S.N * (reg + 1) / nreg);
-          if (path_grab(lo, hi, tail_unit, k, b, e)) break;
+          const uint32_t lo = reg * region, hi = min(lo + region, S.N);
+          const uint32_t k = atomicAdd(work + reg * PATH_CTR_STRIDE, chunk);
+          if (k < hi - lo) {
+            b = lo + k;
+            e = min(b + chunk, hi);
+            break;
+          }
           reg = reg + 1 == nreg ? 0u : reg + 1;
           ++tried;
         }
+        gs[0] = reg;
+        gs[1] = tried;
+        dry = tried >= nreg ? 1u : 0u;
       }
       b = __builtin_amdgcn_readfirstlane(b);
       e = __builtin_amdgcn_readfirstlane(e);
-      reg = __builtin_amdgcn_readfirstlane(reg);
-      tried = __builtin_amdgcn_readfirstlane(tried);
-      drained = tried >= nreg;
+      drained = __builtin_amdgcn_readfirstlane(dry) != 0u;
       next = drained ? 0u : b;
       end = drained ? 0u : e;
-      }
 #if PT_PATH_TIMING
       const unsigned long long dt = wall_clock64() - tg;
       tm_grab += dt;

@@ -135,12 +135,8 @@ struct pt_ctx {
   uint32_t* h_poll = nullptr;  // pinned: {live, err} x 2 poll slots
   hipEvent_t ev_poll[2] = {};
   int path_grid[4] = {0, 0, 0, 0};  // resident workgroups of k_path_leaf<1|2, refa>
-  int path_guide = 4;               // k_path_leaf grab schedule (path_grab; PT_PATH_GUIDE)
   int path_regions = 8;             // k_path_leaf path regions / counters (PT_PATH_REGIONS)
-  // guided grabs below this many paths per resident lane (PT_PATH_GUIDED_BELOW;
-  // 0, off: at the round-5 kernels even one rank's 1/8 share ran faster
-  // without them, DESIGN.md §4 "path grabs by chunk size")
-  int path_guided_below = 0;
+  uint32_t path_chunk = 0;  // k_path_leaf's grab size (0: path_chunk_for; env PT_PATH_CHUNK)
   uint32_t chunk_paths = 1u << 28;  // paths per chunk (PT_CHUNK_PATHS; tests force multi-chunk frames)
 
   // framebuffer
@@ -266,6 +262,16 @@ static constexpr size_t QREGIONS = 3;
 // leaf loop and the closest-hit atomics, not by the ray gathers): off by default.
 static constexpr int ENTRY_LEVEL_DEFAULT = 0;  // (env PT_ENTRY_LEVEL)
 static constexpr int SCAN_MULTI_MIN_DEFAULT = 512;  // (env PT_SCAN_MULTI_MIN)
+// k_path_leaf's grab size for a launch of M paths over `blocks` resident
+// workgroups: a launch's tail is about one chunk's time, and more grabs cost
+// counter atomics (DESIGN.md §4 "path grabs"): 512 paths for a whole frame
+// (>= 256 paths per resident lane), 256 down to 128 per lane, 128 below (one
+// rank's 1/8 share of a 1024^2 x 256 spp frame: 64 per lane)
+static uint32_t path_chunk_for(uint32_t M, uint32_t blocks) {
+  const uint64_t lanes = (uint64_t)std::max<uint32_t>(1, blocks) * TPB;
+  return (uint64_t)M >= 256 * lanes ? 512u : (uint64_t)M >= 96 * lanes ? 256u : 128u;
+}
+
 static uint32_t max_batch_paths(const pt_ctx* c, uint32_t slots_per_path) {
   // u32 entry offsets: both halves of the entry queues, and the root's id
   // queues (<= 16 targets x every ray, see root_per_lane)
@@ -1097,9 +1103,8 @@ int pt_create(pt_ctx** out, int device) {
   // initial queue factor (doubles whenever a level overflows; PT_QFACTOR=1
   // exercises that path in the tests)
   if (const char* q = getenv("PT_QFACTOR")) c->qfactor = std::max(1, atoi(q));
-  if (const char* q = getenv("PT_PATH_GUIDE")) c->path_guide = std::max(0, atoi(q));
   if (const char* q = getenv("PT_PATH_REGIONS")) c->path_regions = std::max(1, atoi(q));
-  if (const char* q = getenv("PT_PATH_GUIDED_BELOW")) c->path_guided_below = std::max(0, atoi(q));
+  if (const char* q = getenv("PT_PATH_CHUNK")) c->path_chunk = (uint32_t)std::min(4096, std::max(64, atoi(q)));
   // paths per chunk (a frame of npix x spp paths runs in ceil(spp / (chunk / npix))
   // chunks, summed per pixel in sample order across them): tests set it small
   if (const char* q = getenv("PT_CULL")) c->cull = atoi(q) != 0;
@@ -1137,8 +1142,8 @@ int pt_create(pt_ctx** out, int device) {
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[0], k_path_leaf<1, false, true>, TPB, 0);
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[1], k_path_leaf<2, false, true>, TPB, 0);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[2], k_path_leaf<1, true, true, false>, TPB, 0);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[3], k_path_leaf<2, true, true, false>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[2], k_path_leaf<1, true, false>, TPB, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb[3], k_path_leaf<2, true, false>, TPB, 0);
     for (int i = 0; i < 4; ++i) c->path_grid[i] = std::max(1, ncu * std::max(1, nb[i]));
   }
   *out = c;
@@ -1539,29 +1544,27 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       const uint32_t want = (M + 4 * PATH_CHUNK - 1) / (4 * PATH_CHUNK);
       const int kv = (nsh == 2 ? 1 : 0) + (c->refa ? 2 : 0);
       const uint32_t blocks = std::min<uint32_t>(want, c->path_grid[kv]);
-      // guided grabs only for chunks that are small against the resident lanes
-      const bool guided = (uint64_t)M < (uint64_t)c->path_guided_below * blocks * TPB;
       // (spheres: the sphere test compiled in; the reference arithmetic has none)
       const bool sph = c->has_sphere;
-      auto kpath = xl ? (sph ? k_path_leaf<1, false, false, true, true> : k_path_leaf<1, false, false, false, true>)
-                 : guided ? (kv == 0 ? (sph ? k_path_leaf<1, false, true, true> : k_path_leaf<1, false, true, false>)
-                             : kv == 1 ? (sph ? k_path_leaf<2, false, true, true> : k_path_leaf<2, false, true, false>)
-                             : kv == 2 ? k_path_leaf<1, true, true, false> : k_path_leaf<2, true, true, false>)
-                          : (kv == 0 ? (sph ? k_path_leaf<1, false, false, true> : k_path_leaf<1, false, false, false>)
-                             : kv == 1 ? (sph ? k_path_leaf<2, false, false, true> : k_path_leaf<2, false, false, false>)
-                             : kv == 2 ? k_path_leaf<1, true, false, false> : k_path_leaf<2, true, false, false>);
+      auto kpath = xl ? (sph ? k_path_leaf<1, false, true, true> : k_path_leaf<1, false, false, true>)
+                      : (kv == 0 ? (sph ? k_path_leaf<1, false, true> : k_path_leaf<1, false, false>)
+                         : kv == 1 ? (sph ? k_path_leaf<2, false, true> : k_path_leaf<2, false, false>)
+                         : kv == 2 ? k_path_leaf<1, true, false> : k_path_leaf<2, true, false>);
       // PT_FLAG_COUNT_TESTS: the counting variant (default schedule and
       // arithmetic, one light; the others count nothing)
-      if ((P->flags & PT_FLAG_COUNT_TESTS) && kv == 0 && !guided && !xl)
-        kpath = sph ? k_path_leaf<1, false, false, true, false, true> : k_path_leaf<1, false, false, false, false, true>;
-      // guided grabs from nreg path regions (k_path_leaf path_grab): each
-      // region's tail phases begin path_guide chunks per wave before its end
+      if ((P->flags & PT_FLAG_COUNT_TESTS) && kv == 0 && !xl)
+        kpath = sph ? k_path_leaf<1, false, true, false, true> : k_path_leaf<1, false, false, false, true>;
+      // path grabs (shade.hip k_path_leaf): nreg regions, chunks of 512 paths
+      // for a whole frame, fewer when the launch has few paths per resident
+      // lane (its tail is about one chunk's time)
       const uint32_t nreg = (uint32_t)std::max(1, std::min<int>(c->path_regions, (int)std::min<uint32_t>(blocks, PATH_REGIONS_MAX)));
-      const uint32_t tail_unit = (uint32_t)std::min<uint64_t>(
-          ((uint64_t)blocks * (TPB / 64) + nreg - 1) / nreg * (uint64_t)c->path_guide, 1u << 22);
+      S.grab_chunk = c->path_chunk ? c->path_chunk : path_chunk_for(M, blocks);
+      S.grab_nreg = nreg;
+      S.grab_region = (M + nreg - 1) / nreg;
+      S.grab_work = c->d_work;
       HIPCHK(c, hipMemsetAsync(c->d_work, 0, (size_t)nreg * PATH_CTR_STRIDE * 4, c->stream));
-      c->launch(pt_ctx::K_PATH, 0, kpath, dim3(blocks), dim3(TPB), S,
-                root.prim_start, root.prim_count, passes, c->d_rcount, c->d_work, nreg, tail_unit, c->d_err);
+      c->launch(pt_ctx::K_PATH, 0, kpath, dim3(blocks), dim3(TPB), S, root.prim_start, root.prim_count, passes,
+                c->d_rcount, c->d_err);
       HIPCHK(c, hipMemcpyAsync(c->h_poll, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
       path_err = true;
       c->stats.passes += passes;

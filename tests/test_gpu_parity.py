@@ -373,20 +373,29 @@ def test_scotty_camera_render(gpu_ctx):
 
 
 @pytest.mark.parametrize("name", ["CBempty", "CBspheres"])
-def test_guided_path_grabs_match(monkeypatch, name):
-    """The guided path-grab schedule of the single-leaf kernel (off by
-    default, PT_PATH_GUIDED_BELOW) gives the oracle's image too: scheduling
-    never changes a path's result."""
+@pytest.mark.parametrize("chunk,regions", [(64, 1), (128, 3), (4096, 32)])
+def test_path_grab_schedules_match(monkeypatch, name, chunk, regions):
+    """Other path-grab schedules of the single-leaf kernel (grab size,
+    path regions: PT_PATH_CHUNK / PT_PATH_REGIONS) give the oracle's image
+    too: scheduling never changes a path's result, and every path is taken
+    exactly once (the ray count equals the default schedule's)."""
     sc = load_fixture(name)
     d = sc.desc()
-    monkeypatch.setenv("PT_PATH_GUIDED_BELOW", "100000")
-    ctx = ptrace.Context(0)
-    monkeypatch.delenv("PT_PATH_GUIDED_BELOW")
-    try:
-        ctx.load_scene(sc)
-        ctx.clear()
-        ctx.render(48, 48, 3, max_bounces=8, seed=15618)
-        o, _ = pyoracle.image(d, 48, 48, 3, max_bounces=8, seed=15618)
-        assert np.array_equal(ctx.get_image(), o)
-    finally:
-        ctx.close()
+    counts = []
+    for env in ({}, {"PT_PATH_CHUNK": str(chunk), "PT_PATH_REGIONS": str(regions)}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        ctx = ptrace.Context(0)
+        for k in env:
+            monkeypatch.delenv(k)
+        try:
+            ctx.load_scene(sc)
+            ctx.clear()
+            ctx.reset_stats()
+            ctx.render(48, 48, 3, max_bounces=8, seed=15618)
+            o, _ = pyoracle.image(d, 48, 48, 3, max_bounces=8, seed=15618)
+            assert np.array_equal(ctx.get_image(), o)
+            counts.append(ctx.stats().rays)
+        finally:
+            ctx.close()
+    assert counts[0] == counts[1]
