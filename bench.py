@@ -13,7 +13,10 @@ A step is one full frame: every rank renders its interleaved 32x32 tiles of the
 1024x1024 image at 256 spp (strong scaling: the frame is fixed, ranks split it),
 then the framebuffer is gathered to rank 0 over RCCL and copied to the host
 (ms/frame ends with the accumulated image on the host; one
-rank: pt_get_image into a pinned buffer).  Rays are the rays traced (camera +
+rank: pt_get_image_async into a pinned buffer, more ranks: a non-blocking
+copy of the gathered frame; either copy overlaps the next frame's rendering,
+and the last frame's copy is waited for inside the timed region).  Rays are
+the rays traced (camera +
 extension + shadow), counted on the device: SURVEY §8(d) counts the rays cast
 through the traversal, so camera rays that pt_render resolves on the host
 (pixels whose whole footprint misses the scene's root box: radiance 0, never
@@ -336,9 +339,11 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
             sums[0] = ptdist.local_sums_tensor(ctx, sdev, out=sums[0])
             img = ptdist.gather_frame(sums[0], args.width, args.height, args.tile, args.spp)
             if img is not None:
-                host.copy_(img)
+                # (queued on torch's stream: overlaps the next frame's
+                # rendering on the library's stream, like get_image_async)
+                host.copy_(img, non_blocking=True)
         else:
-            ctx.get_image(out=host)
+            ctx.get_image_async(out=host)
 
     for _ in range(args.warmup):
         frame(False)
@@ -349,6 +354,8 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         frame(args.stats_in_timed)
+    ctx.wait_image()  # (the last frame's image is on the host inside the timed region)
+    torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -363,6 +370,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
         ctx.reset_stats()
         t1 = time.perf_counter()
         frame(True)
+        ctx.wait_image()
         torch.cuda.synchronize()
         instrumented_ms = (time.perf_counter() - t1) * 1e3
     st = ctx.stats()

@@ -157,6 +157,14 @@ struct pt_ctx {
   float4* d_accum = nullptr;
   float4* d_frame = nullptr;  // row-major frame staged for pt_get_image (k_frame)
   size_t frame_cap = 0;
+  // pt_get_image_async: two alternating staged frames, their copies to the
+  // host on copy_stream (ev_fr: staged on `stream`, ev_cp: copy done)
+  hipStream_t copy_stream = nullptr;
+  float4* d_frame_a[2] = {nullptr, nullptr};
+  size_t frame_cap_a[2] = {0, 0};
+  hipEvent_t ev_fr[2] = {}, ev_cp[2] = {};
+  bool cp_queued[2] = {false, false};
+  int fidx = 0;
   int32_t samples = 0;
 
   pt_stats stats{};
@@ -225,7 +233,7 @@ static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_lights, c->d_cbox, c->d_rcbox, c->d_rcmem, c->d_rcmem_ref, c->d_rcinfo, c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live, c->d_pool,
-                  c->d_pix_of, c->d_accum, c->d_frame, c->d_tmin, c->d_ray_b, c->d_ps0_b, c->d_ps1_b, c->d_ps2_b,
+                  c->d_pix_of, c->d_accum, c->d_frame, c->d_frame_a[0], c->d_frame_a[1], c->d_tmin, c->d_ray_b, c->d_ps0_b, c->d_ps1_b, c->d_ps2_b,
                   c->d_ps3_b, c->d_compact, c->d_act_pix, c->d_act_slot};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -1123,6 +1131,11 @@ int pt_create(pt_ctx** out, int device) {
   }
   for (auto& e : c->ev) hipEventCreate(&e);
   for (auto& e : c->ev_poll) hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (int k = 0; k < 2; ++k) {
+    hipEventCreateWithFlags(&c->ev_fr[k], hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->ev_cp[k], hipEventDisableTiming);
+  }
+  if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) c->copy_stream = nullptr;
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, PATH_REGIONS_MAX * PATH_CTR_STRIDE * 4) != hipSuccess ||
@@ -1154,7 +1167,13 @@ void pt_destroy(pt_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
   free_all(c);
+  for (int k = 0; k < 2; ++k) {
+    if (c->ev_fr[k]) hipEventDestroy(c->ev_fr[k]);
+    if (c->ev_cp[k]) hipEventDestroy(c->ev_cp[k]);
+  }
+  if (c->copy_stream) hipStreamDestroy(c->copy_stream);
   for (auto& e : c->evpool) hipEventDestroy(e);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
@@ -1830,6 +1849,48 @@ int pt_get_image(pt_ctx* c, float* rgba, size_t n_floats) {
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(rgba, c->d_frame, npx * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PT_OK;
+}
+
+int pt_get_image_async(pt_ctx* c, float* rgba, size_t n_floats) {
+  if (!c || !rgba) return PT_E_INVALID;
+  if (!c->copy_stream) return fail(c, PT_E_HIP, "pt_get_image_async: no copy stream");
+  const size_t npx = (size_t)c->fb_w * c->fb_h;
+  if (npx * 4 > n_floats) return fail(c, PT_E_INVALID, "image buffer too small");
+  if (npx == 0) return PT_OK;
+  hipSetDevice(c->device);
+  int rc;
+  const int k = c->fidx;
+  if (npx > c->frame_cap_a[k]) {
+    if (c->cp_queued[k]) HIPCHK(c, hipEventSynchronize(c->ev_cp[k]));
+    if ((rc = dalloc(c, &c->d_frame_a[k], npx))) return rc;
+    c->frame_cap_a[k] = npx;
+  }
+  // the staged frame k is rewritten only after its last copy has read it
+  if (c->cp_queued[k]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_cp[k], 0));
+  const uint32_t npix = (uint32_t)c->pix_of.size();
+  if (npix < npx) HIPCHK(c, hipMemsetAsync(c->d_frame_a[k], 0, npx * sizeof(float4), c->stream));
+  const float ns = (float)(c->samples > 0 ? c->samples : 1);
+  if (npix)
+    hipLaunchKernelGGL(k_frame, dim3((npix + TPB - 1) / TPB), dim3(TPB), 0, c->stream, (const float4*)c->d_accum,
+                       (const uint32_t*)c->d_pix_of, npix, ns, c->d_frame_a[k]);
+  HIPCHK(c, hipGetLastError());
+  // (pt_clear / pt_render on `stream` after this point cannot change the
+  // staged frame: the copy reads d_frame_a[k], not the accumulation)
+  HIPCHK(c, hipEventRecord(c->ev_fr[k], c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->ev_fr[k], 0));
+  HIPCHK(c, hipMemcpyAsync(rgba, c->d_frame_a[k], npx * sizeof(float4), hipMemcpyDeviceToHost, c->copy_stream));
+  HIPCHK(c, hipEventRecord(c->ev_cp[k], c->copy_stream));
+  c->cp_queued[k] = true;
+  c->fidx = k ^ 1;
+  return PT_OK;
+}
+
+int pt_wait_image(pt_ctx* c) {
+  if (!c) return PT_E_INVALID;
+  hipSetDevice(c->device);
+  for (int k = 0; k < 2; ++k)
+    if (c->cp_queued[k]) HIPCHK(c, hipEventSynchronize(c->ev_cp[k]));
   return PT_OK;
 }
 

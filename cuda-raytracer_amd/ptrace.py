@@ -121,7 +121,7 @@ API_SYMBOLS = [
     "pt_api_version", "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_from_mesh_ex", "pt_scene_build_gpu", "pt_scene_build_gpu_ex", "pt_scene_camera_scotty", "pt_scene_free", "pt_scene_get_desc",
     "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
-    "pt_clear", "pt_get_image", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex", "pt_copy_owned_sums",
+    "pt_clear", "pt_get_image", "pt_get_image_async", "pt_wait_image", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex", "pt_copy_owned_sums",
     "pt_get_stats", "pt_reset_stats", "pt_median_filter", "pt_get_display_image", "pt_tonemap",
     "pt_write_png", "pt_write_pfm", "pt_check_division", "pt_check_fast_math",
     "pt_group_create", "pt_group_destroy", "pt_group_last_error", "pt_group_gather_kind", "pt_group_size",
@@ -173,6 +173,8 @@ def _load():
         "pt_render": (C.c_int, [P, C.POINTER(pt_render_params)]),
         "pt_clear": (C.c_int, [P]),
         "pt_get_image": (C.c_int, [P, C.POINTER(C.c_float), SZ]),
+        "pt_get_image_async": (C.c_int, [P, C.POINTER(C.c_float), SZ]),
+        "pt_wait_image": (C.c_int, [P]),
         "pt_owned_pixels": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32), SZ, C.POINTER(P)]),
         "pt_samples": (C.c_int, [P, C.POINTER(I32)]),
         "pt_copy_owned_sums": (C.c_int, [P, P, SZ, I32]),
@@ -482,6 +484,21 @@ class Context:
         n = C.c_int32()
         self._chk(LIB.pt_samples(self.h, C.byref(n)))
         return n.value
+
+    def get_image_async(self, out):
+        """Queue the frame's copy into `out` (a host buffer: numpy array or
+        torch CPU tensor, ideally pinned) and return at once; the next clear /
+        render overlaps the copy.  `out` holds the frame after wait_image."""
+        if isinstance(out, np.ndarray):
+            assert out.dtype == np.float32 and out.flags.c_contiguous
+            self._chk(LIB.pt_get_image_async(self.h, _ptr(out, C.c_float), out.size))
+        else:  # torch tensor
+            assert out.dtype.is_floating_point and out.is_contiguous() and out.device.type == "cpu"
+            self._chk(LIB.pt_get_image_async(self.h, C.cast(out.data_ptr(), C.POINTER(C.c_float)), out.numel()))
+        return out
+
+    def wait_image(self):
+        self._chk(LIB.pt_wait_image(self.h))
 
     def get_image(self, out=None):
         """The accumulated frame (H, W, 4) float32 on the host.  `out`: an

@@ -52,8 +52,8 @@ extern "C" {
  * PT_FLAG_EXACT_LIGHT_PDF and the light.cpp pdf as the default (round 5).
  * 3: pt_group_* (several GPUs of one process, RCCL gather; round 5).
  * 4: pt_scene_desc.n_lights / lights, PT_LIGHT_DIRECTIONAL / _HEMISPHERE.
- * 5: PT_FLAG_COUNT_TESTS and pt_stats.prim_tests_tri / _sph, cluster_box_tests
- *    (round 6).
+ * 5: PT_FLAG_COUNT_TESTS and pt_stats.prim_tests_tri / _sph, cluster_box_tests;
+ *    pt_get_image_async / pt_wait_image (round 6).
  * A client checks pt_api_version() == PT_API_VERSION before passing structs. */
 #define PT_API_VERSION 5
 int pt_api_version(void);
@@ -350,6 +350,15 @@ int pt_clear(pt_ctx* ctx);
 /* Copy the current image (accumulated radiance / samples) of the whole frame,
  * width*height*4 floats.  Pixels this rank does not own are 0. */
 int pt_get_image(pt_ctx* ctx, float* rgba, size_t n_floats);
+/* pt_get_image without the wait (round 6): the frame is assembled on the
+ * device by the same kernel, and its copy into `rgba` (host memory, ideally
+ * pinned) is queued on a copy stream of the context; the call returns at
+ * once, and a following pt_clear / pt_render overlaps the copy (it reads a
+ * staged frame of its own; two alternate).  `rgba` holds the frame after
+ * pt_wait_image, which waits for every queued copy.  No reference
+ * counterpart: getImage (cu:1539-1570) is synchronous. */
+int pt_get_image_async(pt_ctx* ctx, float* rgba, size_t n_floats);
+int pt_wait_image(pt_ctx* ctx);
 /* Owned-pixel view for the multi-GPU gather: *n_pixels owned pixels, their
  * global indices (row*width+col, host array filled if not NULL) and a device
  * pointer to their float4 radiance sums (not divided by spp). */

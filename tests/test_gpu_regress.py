@@ -338,3 +338,29 @@ def test_bench_eight_ranks_config5_branch(tmp_path):
     assert c1.shape == (64, 96, 4) and c1[..., :3].mean() > 0
     assert np.array_equal(h1, h8)
     assert np.array_equal(c1, c8)
+
+
+def test_async_image_overlaps_next_frame(gpu_ctx):
+    """pt_get_image_async (the bench's frame readback): the copy of frame A
+    is queued, frame B is cleared and rendered while it may still run, and
+    after pt_wait_image both host buffers hold exactly what the synchronous
+    pt_get_image returns for each frame (the copy reads a staged frame of its
+    own, two alternate, so the next clear / render cannot change it)."""
+    import torch
+    gpu_ctx.load_scene(load_fixture("CBgems"))
+    W, H = 160, 96
+    want = []
+    for spp, seed in ((3, 15618), (2, 7)):
+        gpu_ctx.clear()
+        gpu_ctx.render(W, H, spp, max_bounces=6, seed=seed)
+        want.append(gpu_ctx.get_image())
+    bufs = [torch.empty((H, W, 4), dtype=torch.float32, pin_memory=True) for _ in range(3)]
+    for k, (spp, seed) in enumerate(((3, 15618), (2, 7), (3, 15618))):
+        gpu_ctx.clear()
+        gpu_ctx.render(W, H, spp, max_bounces=6, seed=seed)
+        gpu_ctx.get_image_async(bufs[k])
+    gpu_ctx.wait_image()
+    assert np.array_equal(bufs[0].numpy(), want[0])
+    assert np.array_equal(bufs[1].numpy(), want[1])
+    assert np.array_equal(bufs[2].numpy(), want[0])
+    assert not np.array_equal(want[0], want[1])
