@@ -123,6 +123,9 @@ def parse():
                    help="rank 0 saves config 5's gathered frame when it runs tiled over >= 8 ranks (.npy; tests)")
     p.add_argument("--no-1spp", action="store_true",
                    help="skip the ms_1spp frame (profiler runs: keeps per-launch averages to full frames)")
+    p.add_argument("--no-executed", action="store_true",
+                   help="skip the PT_FLAG_COUNT_TESTS frame of k_path_leaf workloads (profiler runs: its counting "
+                        "kernel would join the profiled kernel's per-launch averages)")
     p.add_argument("--stats-in-timed", action="store_true",
                    help="record per-kernel HIP events inside the timed steps (default: one extra instrumented frame)")
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -444,7 +447,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
                 "note": "achieved/frac: SURVEY 8(d)'s 32 B per visit + 4 B per push; line_frac: the same visits at "
                         "the 128-B line a random record gather fetches; traffic_gbs: PMC HBM bytes per launch / "
                         "average launch time"}
-    if kernel == "k_path_leaf" and not flags:
+    if kernel == "k_path_leaf" and not flags and not args.no_executed:
         # the work the kernel executes: one more frame
         # through the counting build (PT_FLAG_COUNT_TESTS, not timed: the
         # counters cost it time), priced like the reference's work -- 42 flop

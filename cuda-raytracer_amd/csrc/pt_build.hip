@@ -7,10 +7,15 @@
 //   1. primitive boxes and centroids             k_prim_bounds
 //   2. centroid bounds (ordered-int atomics)     k_reduce_bounds
 //   3. 63-bit Morton codes, radix sort           k_morton + hipcub
-//   4. binary tree: PLOC agglomerative clustering (default, k_ploc_*: mutual
-//      nearest neighbours by union box area in a Morton-order window, then a
-//      depth-first renumbering of the primitives), or the radix tree of
-//      Karras 2012 (PT_GPU_BVH=lbvh; k_karras)
+//   4. binary tree: top-down binned SAH with the reference's split rule
+//      (default since round 6, PT_GPU_BVH_SAH, k_sah_*: 12 planes per axis
+//      over each node's centroid extent, cost 5 + 2 (SA_l n_l + SA_r n_r) /
+//      SA, level-synchronous; the dragon proxy's frames as fast as on the
+//      host SAH tree), PLOC agglomerative clustering over Morton order
+//      (PT_GPU_BVH_PLOC, k_ploc_*: mutual nearest neighbours by union box
+//      area in a Morton-order window, then a depth-first renumbering of the
+//      primitives), or the radix tree of Karras 2012 (PT_GPU_BVH_LBVH;
+//      k_karras)
 //   5. node boxes: made by the merges (PLOC) or bottom-up (k_bottom_up)
 //   6. 4-wide collapse, one kernel per level:    k_wide_count / scan / k_wide_emit
 //      a node with <= max_leaf primitives is a leaf; otherwise its wide
@@ -27,6 +32,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cfloat>
+#include <climits>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -210,8 +216,11 @@ __global__ void k_bottom_up(const Box* __restrict__ pbox, const uint32_t* __rest
   }
 }
 
-__device__ __forceinline__ int2 node_range(int v, int n, const int2* __restrict__ range) {
-  return v >= n - 1 ? make_int2(v - (n - 1), v - (n - 1)) : range[v];
+// sah: the top-down SAH tree (every node id has a range; a node of more than
+// max_leaf primitives always has two children), else leaves are the ids
+// n - 1 .. 2n - 2 (radix tree, PLOC)
+__device__ __forceinline__ int2 node_range(int v, int n, const int2* __restrict__ range, bool sah = false) {
+  return (!sah && v >= n - 1) ? make_int2(v - (n - 1), v - (n - 1)) : range[v];
 }
 
 // the wide children (binary node ids) of binary node v; 0 for a wide leaf.
@@ -225,9 +234,9 @@ __device__ __forceinline__ float box_area(const Box& b) {
 }
 __device__ __forceinline__ int wide_children(int v, int n, int max_leaf, const int2* __restrict__ child,
                                              const int2* __restrict__ range, const Box* __restrict__ nbox,
-                                             int (&out)[4]) {
-  const int2 r = node_range(v, n, range);
-  if (v >= n - 1 || r.y - r.x + 1 <= max_leaf) return 0;
+                                             int (&out)[4], bool sah) {
+  const int2 r = node_range(v, n, range, sah);
+  if ((!sah && v >= n - 1) || r.y - r.x + 1 <= max_leaf) return 0;
   const int2 c = child[v];
   out[0] = c.x;
   out[1] = c.y;
@@ -237,7 +246,7 @@ __device__ __forceinline__ int wide_children(int v, int n, int max_leaf, const i
     float ba = -1.0f;
     for (int j = 0; j < m; ++j) {
       const int u = out[j];
-      if (u >= n - 1) continue;
+      if (!sah && u >= n - 1) continue;
       const int2 ru = range[u];
       if (ru.y - ru.x + 1 <= max_leaf) continue;
       const float a = box_area(nbox[u]);
@@ -257,27 +266,27 @@ __device__ __forceinline__ int wide_children(int v, int n, int max_leaf, const i
 // 6a. children per frontier node
 __global__ void k_wide_count(const int* __restrict__ front, int m, int n, int max_leaf,
                              const int2* __restrict__ child, const int2* __restrict__ range,
-                             const Box* __restrict__ nbox, uint32_t* __restrict__ cnt) {
+                             const Box* __restrict__ nbox, uint32_t* __restrict__ cnt, bool sah) {
   const int f = blockIdx.x * TPB + threadIdx.x;
   if (f >= m) return;
   int out[4];
-  cnt[f] = (uint32_t)wide_children(front[f], n, max_leaf, child, range, nbox, out);
+  cnt[f] = (uint32_t)wide_children(front[f], n, max_leaf, child, range, nbox, out, sah);
 }
 
 // 6b. write the level's pt_node records and the next frontier
 __global__ void k_wide_emit(const int* __restrict__ front, int m, int n, int max_leaf, int level, int base,
                             int next_base, const int2* __restrict__ child, const int2* __restrict__ range,
                             const Box* __restrict__ nbox, const uint32_t* __restrict__ off, pt_node* __restrict__ nodes,
-                            int* __restrict__ next) {
+                            int* __restrict__ next, bool sah) {
   const int f = blockIdx.x * TPB + threadIdx.x;
   if (f >= m) return;
   const int v = front[f];
   int out[4];
-  const int k = wide_children(v, n, max_leaf, child, range, nbox, out);
+  const int k = wide_children(v, n, max_leaf, child, range, nbox, out, sah);
   pt_node d;
   d.level = level;
   d.ref_id = v;
-  const int2 r = node_range(v, n, range);
+  const int2 r = node_range(v, n, range, sah);
   d.prim_start = k ? 0 : r.x;
   d.prim_count = k ? 0 : r.y - r.x + 1;
 #pragma unroll
@@ -511,6 +520,364 @@ __global__ void k_ploc_remap(int n, int2* __restrict__ child, const uint32_t* __
   }
 }
 
+// ---- 4''-5''. top-down binned SAH (the reference's split rule, bvh.cpp:48-230,
+// level-synchronous on the device).  A node of more than max_leaf primitives
+// is split by one of 12 planes per axis, evenly spaced over its centroids'
+// extent (plane p at lo + p (hi - lo) / 13), minimising the reference's cost
+// 5 + 2 (SA_l / SA) n_l + 2 (SA_r / SA) n_r; a node whose planes all cost at
+// least a leaf's 2 n (coincident centroids) is split at the middle of its
+// range instead (the reference keeps it as a larger leaf).  Per level: the
+// centroid extents of the nodes being split (k_sah_cbounds), their 13 bins per
+// axis (count and box: k_sah_bin), the best plane and the two children
+// (k_sah_split), then a stable partition of each node's primitive range
+// (k_sah_flags, a scan, k_sah_scatter).  Node ids count up in creation order
+// (the root is 0); every node has a range of the sorted primitives, and the
+// 4-wide collapse reads the tree in its `sah` mode.
+constexpr int SAH_BINS = 13;  // 12 planes
+constexpr int SAH_CNT = 2 * 3 * SAH_BINS;  // bin records per node: counts (u32) and boxes (6 ordered u32)
+
+struct SahSplit {  // per node being split
+  int axis;        // -1: split at the middle of the range
+  int plane;       // 1..12: the left child holds bins 0 .. plane - 1
+  int nl;          // primitives of the left child
+  int pad;
+  Box bl, br;
+};
+
+// the slot (index into the level's list of nodes being split, sorted by range
+// start) whose range holds position i, or -1
+__device__ __forceinline__ int sah_slot(const int2* __restrict__ srange, int m, int i) {
+  int lo = 0, hi = m - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (srange[mid].x <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  return (m > 0 && srange[lo].x <= i && i <= srange[lo].y) ? lo : -1;
+}
+
+// (the accumulating kernels below reduce in LDS when all of a workgroup's
+// positions lie in one node's range -- every workgroup of the top levels,
+// where one node's bins would otherwise take ~10^5 same-address atomics --
+// and flush once; mixed workgroups use global atomics)
+__device__ __forceinline__ int block_uniform_slot(int s) {
+  __shared__ int lo, hi;
+  if (threadIdx.x == 0) {
+    lo = INT_MAX;
+    hi = INT_MIN;
+  }
+  __syncthreads();
+  atomicMin(&lo, s);
+  atomicMax(&hi, s);
+  __syncthreads();
+  return lo == hi ? lo : -2;  // (-1: no slot in the whole workgroup)
+}
+
+__global__ void k_sah_cbounds(const uint32_t* __restrict__ P, int n, const float* __restrict__ cen,
+                              const int2* __restrict__ srange, int m, uint32_t* __restrict__ cb) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  const int s = i < n ? sah_slot(srange, m, i) : -1;
+  const int u = block_uniform_slot(i < n ? s : (blockIdx.x * TPB < n ? sah_slot(srange, m, blockIdx.x * TPB) : -1));
+  __shared__ uint32_t L[6];
+  if (u >= 0 && threadIdx.x < 6) L[threadIdx.x] = threadIdx.x < 3 ? 0xFFFFFFFFu : 0u;
+  __syncthreads();
+  if (s >= 0) {
+    const uint32_t pr = P[i];
+    uint32_t* const dst = u >= 0 ? L : cb + s * 6;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t o = f2ord(cen[(size_t)pr * 3 + k]);
+      atomicMin(&dst[k], o);
+      atomicMax(&dst[3 + k], o);
+    }
+  }
+  if (u >= 0) {
+    __syncthreads();
+    if (threadIdx.x < 3) atomicMin(&cb[u * 6 + threadIdx.x], L[threadIdx.x]);
+    else if (threadIdx.x < 6) atomicMax(&cb[u * 6 + threadIdx.x], L[threadIdx.x]);
+  }
+}
+
+// bin of centroid c among the 12 planes of [lo, hi]: the number of planes
+// strictly below c (0 .. 12); a primitive is left of plane p iff its bin < p
+__device__ __forceinline__ int sah_bin(float c, float lo, float hi) {
+  const float step = (hi - lo) / 13.0f;
+  int b = 0;
+#pragma unroll
+  for (int p = 1; p <= 12; ++p) b += (fmaf((float)p, step, lo) < c) ? 1 : 0;
+  return b;
+}
+
+__global__ void k_sah_bin(const uint32_t* __restrict__ P, int n, const float* __restrict__ cen,
+                          const Box* __restrict__ pbox, const int2* __restrict__ srange, int m,
+                          const uint32_t* __restrict__ cb, uint32_t* __restrict__ bins) {
+  constexpr int NB = SAH_CNT * 4;  // u32 per node: [axis][bin]: count, then lo[3], hi[3] (ordered), pad
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  const int s = i < n ? sah_slot(srange, m, i) : -1;
+  const int u = block_uniform_slot(i < n ? s : (blockIdx.x * TPB < n ? sah_slot(srange, m, blockIdx.x * TPB) : -1));
+  __shared__ uint32_t L[NB];
+  if (u >= 0)
+    for (int t = threadIdx.x; t < NB; t += TPB) {
+      const int f = t & 7;
+      L[t] = (f >= 1 && f <= 3) ? 0xFFFFFFFFu : 0u;
+    }
+  __syncthreads();
+  if (s >= 0) {
+    const uint32_t pr = P[i];
+    const Box b = pbox[pr];
+    uint32_t* const B = u >= 0 ? L : bins + (size_t)s * NB;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int j = sah_bin(cen[(size_t)pr * 3 + k], ord2f(cb[s * 6 + k]), ord2f(cb[s * 6 + 3 + k]));
+      uint32_t* const r = B + (k * SAH_BINS + j) * 8;
+      atomicAdd(&r[0], 1u);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        atomicMin(&r[1 + a], f2ord(b.lo[a]));
+        atomicMax(&r[4 + a], f2ord(b.hi[a]));
+      }
+    }
+  }
+  if (u >= 0) {
+    __syncthreads();
+    uint32_t* const G = bins + (size_t)u * NB;
+    for (int t = threadIdx.x; t < NB; t += TPB) {
+      const int f = t & 7;
+      if (f == 0) {
+        if (L[t]) atomicAdd(&G[t], L[t]);
+      } else if (f <= 3) {
+        if (L[t] != 0xFFFFFFFFu) atomicMin(&G[t], L[t]);
+      } else if (f <= 6) {
+        if (L[t]) atomicMax(&G[t], L[t]);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float box_sa(const Box& b) {
+  const float x = b.hi[0] - b.lo[0], y = b.hi[1] - b.lo[1], z = b.hi[2] - b.lo[2];
+  return 2.0f * (x * y + y * z + z * x);
+}
+__device__ __forceinline__ void box_grow(Box& a, const uint32_t* r) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    a.lo[k] = fminf(a.lo[k], ord2f(r[1 + k]));
+    a.hi[k] = fmaxf(a.hi[k], ord2f(r[4 + k]));
+  }
+}
+
+// one thread per node being split: the best plane (axes in order, strict <:
+// the first minimum, as the reference's loops), the children's boxes
+__global__ void k_sah_split(const int* __restrict__ snode, int m, const int2* __restrict__ srange,
+                            const Box* __restrict__ nbox, const uint32_t* __restrict__ bins,
+                            SahSplit* __restrict__ out) {
+  const int s = blockIdx.x * TPB + threadIdx.x;
+  if (s >= m) return;
+  const int2 r = srange[s];
+  const int cnt = r.y - r.x + 1;
+  const double total_sa = (double)box_sa(nbox[snode[s]]);
+  const uint32_t* const B = bins + (size_t)s * SAH_CNT * 4;
+  const float leaf_cost = 2.0f * (float)cnt;
+  double best = leaf_cost;
+  SahSplit o;
+  o.axis = -1;
+  o.plane = 0;
+  o.nl = cnt / 2;
+  o.pad = 0;
+  for (int k = 0; k < 3; ++k) {
+    Box L[SAH_BINS], R;
+    uint32_t nL[SAH_BINS];
+    Box acc;
+    uint32_t c = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      acc.lo[a] = FLT_MAX;
+      acc.hi[a] = -FLT_MAX;
+    }
+    for (int j = 0; j < SAH_BINS; ++j) {  // L[j]: bins 0 .. j - 1 (left of plane j)
+      L[j] = acc;
+      nL[j] = c;
+      const uint32_t* rr = B + (k * SAH_BINS + j) * 8;
+      if (rr[0]) {
+        box_grow(acc, rr);
+        c += rr[0];
+      }
+    }
+    R.lo[0] = R.lo[1] = R.lo[2] = FLT_MAX;
+    R.hi[0] = R.hi[1] = R.hi[2] = -FLT_MAX;
+    Box Rp[SAH_BINS];
+    for (int j = SAH_BINS - 1; j >= 1; --j) {  // Rp[j]: bins j .. 12 (right of plane j)
+      const uint32_t* rr = B + (k * SAH_BINS + j) * 8;
+      if (rr[0]) box_grow(R, rr);
+      Rp[j] = R;
+    }
+    for (int p = 1; p < SAH_BINS; ++p) {
+      const int nl = (int)nL[p], nr = cnt - nl;
+      if (nl == 0 || nr == 0) continue;
+      const double cost = 5.0 + ((double)box_sa(L[p]) / total_sa) * nl * 2 + ((double)box_sa(Rp[p]) / total_sa) * nr * 2;
+      if (cost < best) {
+        best = cost;
+        o.axis = k;
+        o.plane = p;
+        o.nl = nl;
+        o.bl = L[p];
+        o.br = Rp[p];
+      }
+    }
+  }
+  out[s] = o;
+}
+
+// children of the split nodes: ids base + 2 s, base + 2 s + 1; a child of
+// more than max_leaf primitives is split at the next level (flag)
+__global__ void k_sah_children(const int* __restrict__ snode, int m, const int2* __restrict__ srange,
+                                  const SahSplit* __restrict__ sp, int base, int max_leaf, int2* __restrict__ child,
+                               int2* __restrict__ range, uint32_t* __restrict__ more) {
+  const int s = blockIdx.x * TPB + threadIdx.x;
+  if (s >= m) return;
+  const int2 r = srange[s];
+  const SahSplit o = sp[s];
+  const int l = base + 2 * s, rr = l + 1;
+  child[snode[s]] = make_int2(l, rr);
+  range[l] = make_int2(r.x, r.x + o.nl - 1);
+  range[rr] = make_int2(r.x + o.nl, r.y);
+  child[l] = child[rr] = make_int2(-1, -1);
+  more[2 * s] = o.nl > max_leaf ? 1u : 0u;
+  more[2 * s + 1] = (r.y - r.x + 1 - o.nl) > max_leaf ? 1u : 0u;
+}
+
+// left flags of the positions in split ranges (0 elsewhere)
+__global__ void k_sah_flags(const uint32_t* __restrict__ P, int n, const float* __restrict__ cen,
+                            const int2* __restrict__ srange, int m, const uint32_t* __restrict__ cb,
+                            const SahSplit* __restrict__ sp, uint32_t* __restrict__ left) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  const int s = sah_slot(srange, m, i);
+  uint32_t f = 0;
+  if (s >= 0) {
+    const SahSplit o = sp[s];
+    if (o.axis < 0) {
+      f = (i - srange[s].x) < o.nl ? 1u : 0u;
+    } else {
+      const int k = o.axis;
+      f = sah_bin(cen[(size_t)P[i] * 3 + k], ord2f(cb[s * 6 + k]), ord2f(cb[s * 6 + 3 + k])) < o.plane ? 1u : 0u;
+    }
+  }
+  left[i] = f;
+}
+
+// stable partition of each split range (left primitives first, in order)
+__global__ void k_sah_scatter(const uint32_t* __restrict__ P, int n, const int2* __restrict__ srange, int m,
+                              const SahSplit* __restrict__ sp, const uint32_t* __restrict__ left,
+                              const uint32_t* __restrict__ lscan, uint32_t* __restrict__ P2) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  const int s = sah_slot(srange, m, i);
+  if (s < 0) {
+    P2[i] = P[i];
+    return;
+  }
+  const int first = srange[s].x;
+  const uint32_t lr = lscan[i] - lscan[first];  // left primitives before i in the range
+  const int pos = left[i] ? first + (int)lr : first + sp[s].nl + (i - first - (int)lr);
+  P2[pos] = P[i];
+}
+
+// the children's boxes as the unions of their primitives' boxes, after the
+// partition (the middle split of coincident centroids has no bins to take
+// them from): ordered-u32 atomics into cbu[6 per child], then k_sah_child_box
+__global__ void k_sah_child_acc(const uint32_t* __restrict__ P, int n, const Box* __restrict__ pbox,
+                                const int2* __restrict__ srange, int m, const SahSplit* __restrict__ sp,
+                                uint32_t* __restrict__ cbu) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  const int s = i < n ? sah_slot(srange, m, i) : -1;
+  const int c = s >= 0 ? 2 * s + ((i - srange[s].x) < sp[s].nl ? 0 : 1) : -1;
+  // (uniform child: the workgroup's positions in one child's range)
+  const int u = block_uniform_slot(i < n ? c : (blockIdx.x * TPB < n ? c : -1));
+  __shared__ uint32_t L[6];
+  if (u >= 0 && threadIdx.x < 6) L[threadIdx.x] = threadIdx.x < 3 ? 0xFFFFFFFFu : 0u;
+  __syncthreads();
+  if (c >= 0) {
+    const Box b = pbox[P[i]];
+    uint32_t* const dst = u >= 0 ? L : cbu + c * 6;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      atomicMin(&dst[k], f2ord(b.lo[k]));
+      atomicMax(&dst[3 + k], f2ord(b.hi[k]));
+    }
+  }
+  if (u >= 0) {
+    __syncthreads();
+    if (threadIdx.x < 3) atomicMin(&cbu[u * 6 + threadIdx.x], L[threadIdx.x]);
+    else if (threadIdx.x < 6) atomicMax(&cbu[u * 6 + threadIdx.x], L[threadIdx.x]);
+  }
+}
+__global__ void k_sah_child_box(int m2, int base, const uint32_t* __restrict__ cbu, Box* __restrict__ nbox) {
+  const int c = blockIdx.x * TPB + threadIdx.x;
+  if (c >= m2) return;
+  Box b;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    b.lo[k] = ord2f(cbu[c * 6 + k]);
+    b.hi[k] = ord2f(cbu[c * 6 + 3 + k]);
+  }
+  nbox[base + c] = b;
+}
+__global__ void k_sah_init_cbu(int m2, uint32_t* __restrict__ cbu) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  if (i < m2 * 6) cbu[i] = (i % 6) < 3 ? 0xFFFFFFFFu : 0u;
+}
+
+// the root's box: the union of the primitive boxes
+__global__ void k_root_box(const Box* __restrict__ pbox, int n, uint32_t* __restrict__ rb) {
+  __shared__ uint32_t s[6];
+  if (threadIdx.x < 3) s[threadIdx.x] = 0xFFFFFFFFu;
+  else if (threadIdx.x < 6) s[threadIdx.x] = 0u;
+  __syncthreads();
+  for (int i = blockIdx.x * TPB + threadIdx.x; i < n; i += gridDim.x * TPB) {
+    const Box b = pbox[i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      atomicMin(&s[k], f2ord(b.lo[k]));
+      atomicMax(&s[3 + k], f2ord(b.hi[k]));
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) atomicMin(&rb[threadIdx.x], s[threadIdx.x]);
+  else if (threadIdx.x < 6) atomicMax(&rb[threadIdx.x], s[threadIdx.x]);
+}
+__global__ void k_root_init(const uint32_t* __restrict__ rb, int n, Box* __restrict__ nbox, int2* __restrict__ range,
+                            int2* __restrict__ child) {
+  Box b;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    b.lo[k] = ord2f(rb[k]);
+    b.hi[k] = ord2f(rb[3 + k]);
+  }
+  nbox[0] = b;
+  range[0] = make_int2(0, n - 1);
+  child[0] = make_int2(-1, -1);
+}
+__global__ void k_sah_init_bins(int m, uint32_t* __restrict__ cb, uint32_t* __restrict__ bins) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  if (i < m * 6) cb[i] = (i % 6) < 3 ? 0xFFFFFFFFu : 0u;
+  if (i < m * SAH_CNT * 4) {
+    const int f = i & 7;  // count, lo[3] (min: init high), hi[3] (max: init low), pad
+    bins[i] = (f >= 1 && f <= 3) ? 0xFFFFFFFFu : 0u;
+  }
+}
+// the next level's split list: compacted children with more than max_leaf
+// primitives (their ids base + t and ranges), kept in range order
+__global__ void k_sah_next(int m2, int base, const uint32_t* __restrict__ more, const uint32_t* __restrict__ mscan,
+                           const int2* __restrict__ range, int* __restrict__ snode2, int2* __restrict__ srange2) {
+  const int t = blockIdx.x * TPB + threadIdx.x;
+  if (t >= m2) return;
+  if (more[t]) {
+    snode2[mscan[t]] = base + t;
+    srange2[mscan[t]] = range[base + t];
+  }
+}
+
 struct DevBuf {
   std::vector<void*> ptrs;
   ~DevBuf() {
@@ -572,16 +939,85 @@ static int build_on_device(const pt_mesh_desc* md, int max_leaf, int builder, pt
                      d_cen);
   hipLaunchKernelGGL(k_reduce_bounds, dim3(std::min(1024, (n + TPB - 1) / TPB)), dim3(TPB), 0, st, d_cen, n,
                      d_bounds);
-  hipLaunchKernelGGL(k_morton, g, dim3(TPB), 0, st, d_cen, n, d_bounds, d_key, d_idx);
-  size_t tmp_bytes = 0;
-  BCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, d_key, d_key2, d_idx, d_idx2, n, 0, 63, st));
-  void* d_tmp = B.alloc<uint8_t>(tmp_bytes);
-  if (!d_tmp) return PT_E_HIP;
-  BCHK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp_bytes, d_key, d_key2, d_idx, d_idx2, n, 0, 63, st));
-  // binary tree: PLOC or the radix tree
+  // binary tree: top-down SAH, PLOC or the radix tree (the last two over
+  // the primitives in Morton order)
+  const bool sah = builder == PT_GPU_BVH_SAH;
+  if (!sah) {
+    hipLaunchKernelGGL(k_morton, g, dim3(TPB), 0, st, d_cen, n, d_bounds, d_key, d_idx);
+    size_t tmp_bytes = 0;
+    BCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, d_key, d_key2, d_idx, d_idx2, n, 0, 63, st));
+    void* d_tmp = B.alloc<uint8_t>(tmp_bytes);
+    if (!d_tmp) return PT_E_HIP;
+    BCHK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp_bytes, d_key, d_key2, d_idx, d_idx2, n, 0, 63, st));
+  }
   const bool ploc = n > 1 && builder == PT_GPU_BVH_PLOC;
   uint32_t* d_sorted = d_idx2;  // final primitive order
-  if (ploc) {
+  if (sah) {
+    // ids count up from the root (0): at most 2 n - 1 nodes, each with a range
+    int2* d_child2 = B.alloc<int2>(2 * (size_t)n);
+    int2* d_range2 = B.alloc<int2>(2 * (size_t)n);
+    const int smax = n / (max_leaf + 1) + 1;  // nodes split in one level (disjoint ranges of > max_leaf)
+    uint32_t *d_P = B.alloc<uint32_t>(n), *d_P2 = B.alloc<uint32_t>(n), *d_left = B.alloc<uint32_t>(n + 1),
+             *d_lscan = B.alloc<uint32_t>(n + 1), *d_more = B.alloc<uint32_t>(2 * (size_t)smax + 1),
+             *d_mscan = B.alloc<uint32_t>(2 * (size_t)smax + 1), *d_cb = B.alloc<uint32_t>(6 * (size_t)smax),
+             *d_bins = B.alloc<uint32_t>((size_t)smax * SAH_CNT * 4), *d_rb = B.alloc<uint32_t>(6),
+             *d_cbu = B.alloc<uint32_t>(12 * (size_t)smax);
+    int *d_snode = B.alloc<int>(smax), *d_snode2 = B.alloc<int>(smax);
+    int2 *d_srange = B.alloc<int2>(smax), *d_srange2 = B.alloc<int2>(smax);
+    SahSplit* d_sp = B.alloc<SahSplit>(smax);
+    size_t sb = 0;
+    BCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, d_left, d_lscan, n + 1, st));
+    void* d_sscan = B.alloc<uint8_t>(sb);
+    if (!d_child2 || !d_range2 || !d_P || !d_P2 || !d_left || !d_lscan || !d_more || !d_mscan || !d_cb || !d_bins ||
+        !d_rb || !d_cbu || !d_snode || !d_snode2 || !d_srange || !d_srange2 || !d_sp || !d_sscan)
+      return PT_E_HIP;
+    d_child = d_child2;
+    d_range = d_range2;
+    std::vector<uint32_t> iota(n);
+    for (int i = 0; i < n; ++i) iota[i] = (uint32_t)i;
+    BCHK(hipMemcpyAsync(d_P, iota.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    BCHK(hipMemcpyAsync(d_rb, binit, sizeof(binit), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_root_box, dim3(std::min(1024, (n + TPB - 1) / TPB)), dim3(TPB), 0, st, d_pbox, n, d_rb);
+    hipLaunchKernelGGL(k_root_init, dim3(1), dim3(1), 0, st, d_rb, n, d_nbox, d_range, d_child);
+    int m = n > max_leaf ? 1 : 0, next_id = 1;
+    if (m) {
+      const int zero = 0;
+      const int2 r0 = make_int2(0, n - 1);
+      BCHK(hipMemcpyAsync(d_snode, &zero, 4, hipMemcpyHostToDevice, st));
+      BCHK(hipMemcpyAsync(d_srange, &r0, sizeof(r0), hipMemcpyHostToDevice, st));
+    }
+    for (int level = 0; m > 0; ++level) {
+      if (level > 4 * 64 || m > smax) return PT_E_INVALID;
+      const dim3 gm((m + TPB - 1) / TPB), gb(((size_t)m * SAH_CNT * 4 + TPB - 1) / TPB);
+      hipLaunchKernelGGL(k_sah_init_bins, gb, dim3(TPB), 0, st, m, d_cb, d_bins);
+      hipLaunchKernelGGL(k_sah_cbounds, g, dim3(TPB), 0, st, d_P, n, d_cen, d_srange, m, d_cb);
+      hipLaunchKernelGGL(k_sah_bin, g, dim3(TPB), 0, st, d_P, n, d_cen, d_pbox, d_srange, m, d_cb, d_bins);
+      hipLaunchKernelGGL(k_sah_split, gm, dim3(TPB), 0, st, d_snode, m, d_srange, d_nbox, d_bins, d_sp);
+      hipLaunchKernelGGL(k_sah_children, gm, dim3(TPB), 0, st, d_snode, m, d_srange, d_sp, next_id, max_leaf, d_child,
+                         d_range, d_more);
+      hipLaunchKernelGGL(k_sah_flags, g, dim3(TPB), 0, st, d_P, n, d_cen, d_srange, m, d_cb, d_sp, d_left);
+      BCHK(hipcub::DeviceScan::ExclusiveSum(d_sscan, sb, d_left, d_lscan, n, st));
+      hipLaunchKernelGGL(k_sah_scatter, g, dim3(TPB), 0, st, d_P, n, d_srange, m, d_sp, d_left, d_lscan, d_P2);
+      std::swap(d_P, d_P2);
+      const int m2 = 2 * m;
+      hipLaunchKernelGGL(k_sah_init_cbu, dim3((m2 * 6 + TPB - 1) / TPB), dim3(TPB), 0, st, m2, d_cbu);
+      hipLaunchKernelGGL(k_sah_child_acc, g, dim3(TPB), 0, st, d_P, n, d_pbox, d_srange, m, d_sp, d_cbu);
+      hipLaunchKernelGGL(k_sah_child_box, dim3((m2 + TPB - 1) / TPB), dim3(TPB), 0, st, m2, next_id, d_cbu, d_nbox);
+      BCHK(hipMemsetAsync(d_more + m2, 0, 4, st));
+      BCHK(hipcub::DeviceScan::ExclusiveSum(d_sscan, sb, d_more, d_mscan, m2 + 1, st));
+      uint32_t next_m = 0;
+      BCHK(hipMemcpyAsync(&next_m, d_mscan + m2, 4, hipMemcpyDeviceToHost, st));
+      hipLaunchKernelGGL(k_sah_next, dim3((m2 + TPB - 1) / TPB), dim3(TPB), 0, st, m2, next_id, d_more, d_mscan,
+                         d_range, d_snode2, d_srange2);
+      BCHK(hipStreamSynchronize(st));
+      BCHK(hipGetLastError());
+      next_id += m2;
+      m = (int)next_m;
+      std::swap(d_snode, d_snode2);
+      std::swap(d_srange, d_srange2);
+    }
+    d_sorted = d_P;
+  } else if (ploc) {
     int *d_clus = B.alloc<int>(n), *d_clus2 = B.alloc<int>(n), *d_nn = B.alloc<int>(n);
     uint32_t *d_lead = B.alloc<uint32_t>(n), *d_lrank = B.alloc<uint32_t>(n), *d_keep = B.alloc<uint32_t>(n),
              *d_kpos = B.alloc<uint32_t>(n), *d_pcnt = B.alloc<uint32_t>(n), *d_start = B.alloc<uint32_t>(n),
@@ -636,7 +1072,7 @@ static int build_on_device(const pt_mesh_desc* md, int max_leaf, int builder, pt
   BCHK(hipGetLastError());
 
   // 6. level-synchronous 4-wide collapse
-  const int root = n > 1 ? 0 : n - 1;  // a single primitive: the root is leaf 0
+  const int root = (n > 1 || sah) ? 0 : n - 1;  // a single primitive: the root is leaf 0
   BCHK(hipMemcpyAsync(d_front, &root, 4, hipMemcpyHostToDevice, st));
   size_t scan_bytes = 0;
   BCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, d_cnt, d_off, 2 * n + 1, st));
@@ -649,12 +1085,12 @@ static int build_on_device(const pt_mesh_desc* md, int max_leaf, int builder, pt
     const dim3 gm((m + TPB - 1) / TPB);
     BCHK(hipMemsetAsync(d_cnt + m, 0, 4, st));
     hipLaunchKernelGGL(k_wide_count, gm, dim3(TPB), 0, st, d_front, m, n, max_leaf, d_child, d_range, d_nbox,
-                       d_cnt);
+                       d_cnt, sah);
     BCHK(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_cnt, d_off, m + 1, st));
     uint32_t next_m = 0;
     BCHK(hipMemcpyAsync(&next_m, d_off + m, 4, hipMemcpyDeviceToHost, st));
     hipLaunchKernelGGL(k_wide_emit, gm, dim3(TPB), 0, st, d_front, m, n, max_leaf, level, base, base + m, d_child,
-                       d_range, d_nbox, d_off, d_nodes, d_next);
+                       d_range, d_nbox, d_off, d_nodes, d_next, sah);
     BCHK(hipStreamSynchronize(st));
     BCHK(hipGetLastError());
     base += m;
@@ -683,7 +1119,7 @@ static int build_on_device(const pt_mesh_desc* md, int max_leaf, int builder, pt
 
 extern "C" int pt_scene_build_gpu(const pt_mesh_desc* mesh, int32_t device, int32_t max_leaf, pt_scene** out,
                                   double* build_ms) {
-  return pt_scene_build_gpu_ex(mesh, device, max_leaf, PT_GPU_BVH_PLOC, out, build_ms);
+  return pt_scene_build_gpu_ex(mesh, device, max_leaf, PT_GPU_BVH_SAH, out, build_ms);
 }
 
 extern "C" int pt_scene_build_gpu_ex(const pt_mesh_desc* mesh, int32_t device, int32_t max_leaf, int32_t builder,
@@ -691,7 +1127,7 @@ extern "C" int pt_scene_build_gpu_ex(const pt_mesh_desc* mesh, int32_t device, i
   if (!out) return PT_E_INVALID;
   *out = nullptr;
   if (max_leaf < 1 || max_leaf > 64) return PT_E_INVALID;
-  if (builder != PT_GPU_BVH_PLOC && builder != PT_GPU_BVH_LBVH) return PT_E_INVALID;
+  if (builder != PT_GPU_BVH_PLOC && builder != PT_GPU_BVH_LBVH && builder != PT_GPU_BVH_SAH) return PT_E_INVALID;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PT_E_NODEVICE;
   if (device < 0 || device >= ndev) return PT_E_INVALID;

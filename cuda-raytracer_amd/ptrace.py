@@ -41,7 +41,7 @@ PT_API_VERSION = 5
 PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION, PT_BSDF_REFRACTION = 0, 1, 2, 3, 4
 PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT, PT_LIGHT_DIRECTIONAL, PT_LIGHT_HEMISPHERE = 0, 1, 2, 3, 4
 PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1
-PT_GPU_BVH_PLOC, PT_GPU_BVH_LBVH = 0, 1
+PT_GPU_BVH_PLOC, PT_GPU_BVH_LBVH, PT_GPU_BVH_SAH = 0, 1, 2
 PT_POST_PROCESS_THRESHOLD = 32
 
 
@@ -248,7 +248,7 @@ class Scene:
 
     @classmethod
     def from_mesh(cls, positions, bsdfs, normals=None, tri_bsdf=None, spheres=None, sphere_bsdf=None,
-                  light=None, camera=None, gpu_device=None, max_leaf=32, builder="ploc"):
+                  light=None, camera=None, gpu_device=None, max_leaf=32, builder="sah"):
         """General flattened input (pt_scene_from_mesh): triangles (n, 9),
         optional vertex normals (n, 9), per-triangle bsdf ids, spheres (m, 4)
         and a list of pt_bsdf.  gpu_device=k builds the BVH on GPU k
@@ -286,7 +286,7 @@ class Scene:
             rc = LIB.pt_scene_from_mesh(C.byref(m), C.byref(h))
         else:
             ms = C.c_double()
-            b = {"ploc": PT_GPU_BVH_PLOC, "lbvh": PT_GPU_BVH_LBVH}[builder]
+            b = {"ploc": PT_GPU_BVH_PLOC, "lbvh": PT_GPU_BVH_LBVH, "sah": PT_GPU_BVH_SAH}[builder]
             rc = LIB.pt_scene_build_gpu_ex(C.byref(m), gpu_device, max_leaf, b, C.byref(h), C.byref(ms))
         if rc != PT_OK:
             raise PTError(rc, "pt_scene_from_mesh failed" if gpu_device is None else "pt_scene_build_gpu failed")

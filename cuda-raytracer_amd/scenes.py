@@ -9,8 +9,9 @@ CBbunny.npz): the Cornell box walls and area light once, three copies of the
 side by side on the floor) and a tessellated mirror sphere (60 x 120 UV
 sphere, 14,160 triangles) under the light: 99,900 triangles in total, run
 through the same reference BVH build (pt_scene_from_mesh) or, as
-"dragon_proxy_gpubvh", through the GPU build (pt_scene_build_gpu: PLOC
-clustering; "dragon_proxy_lbvh" is the same scene with the radix tree).
+"dragon_proxy_gpubvh", through the GPU build (pt_scene_build_gpu: the
+top-down SAH; "dragon_proxy_ploc" / "dragon_proxy_lbvh" are the same scene
+with PLOC clustering / the radix tree).
 
 bunny_lit(): bunny.dae (config 4's wide-level scene) with CBbunny's light.
 rebuilt(name, ...): any fixture rebuilt from its meshes (host or GPU build).
@@ -86,7 +87,7 @@ def fixture_arrays(name):
             "bsdfs": bsdfs, "light": light, "camera": camera}
 
 
-def rebuilt(name, gpu_device=None, max_leaf=32, builder="ploc"):
+def rebuilt(name, gpu_device=None, max_leaf=32, builder="sah"):
     """Fixture `name` rebuilt from its meshes: the host SAH build
     (pt_scene_from_mesh) or the GPU build (gpu_device=k)."""
     a = fixture_arrays(name)
@@ -145,10 +146,12 @@ def dragon_proxy_arrays():
     return (np.concatenate(out_p), np.concatenate(out_n), np.concatenate(out_b), bsdfs, light, camera)
 
 
-def dragon_proxy(gpu_device=None, max_leaf=32, builder="ploc"):
+def dragon_proxy(gpu_device=None, max_leaf=32, builder="sah"):
     """The ~100k-triangle config-4/5 scene as a ptrace.Scene: the reference's
-    host SAH build, or (gpu_device=k) the GPU build ("ploc" clustering or the
-    "lbvh" radix tree) with wide leaves of <= max_leaf primitives (32, the
+    host SAH build, or (gpu_device=k) the GPU build ("sah": the reference's
+    12-plane SAH split rule, level-synchronous on the device, the default
+    since round 6; "ploc" clustering; the "lbvh" radix tree) with wide leaves
+    of <= max_leaf primitives (32, the
     reference's leaf size; the radix tree: 5,073 Mrays/s vs 4,918 at 16 and
     4,556 at 8 on the dragon proxy)."""
     pos, nrm, tb, bsdfs, light, camera = dragon_proxy_arrays()
@@ -164,6 +167,10 @@ def load(name):
         return dragon_proxy(gpu_device=0)
     if name == "dragon_proxy_lbvh":
         return dragon_proxy(gpu_device=0, builder="lbvh")
+    if name == "dragon_proxy_sah":
+        return dragon_proxy(gpu_device=0, builder="sah")
+    if name == "dragon_proxy_ploc":
+        return dragon_proxy(gpu_device=0, builder="ploc")
     if name == "bunny":
         return bunny_lit()
     return ptrace.ArrayScene.load(FIXTURES / f"{name}.npz")

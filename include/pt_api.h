@@ -235,9 +235,11 @@ int pt_scene_from_mesh_ex(const pt_mesh_desc* mesh, int32_t max_leaf, pt_scene**
  * on the device collapsed to the 4-wide, level-major layout (wide leaves hold
  * <= max_leaf primitives; the reference's host SAH build, bvh.cpp:48-337, is
  * pt_scene_from_mesh).  *build_ms (optional) receives the build's wall time.
- * pt_scene_build_gpu uses PT_GPU_BVH_PLOC. */
+ * pt_scene_build_gpu uses PT_GPU_BVH_SAH (round 6; PLOC before). */
 #define PT_GPU_BVH_PLOC 0 /* agglomerative clustering in Morton order (PLOC) */
 #define PT_GPU_BVH_LBVH 1 /* Karras radix tree over Morton codes            */
+#define PT_GPU_BVH_SAH 2  /* top-down binned SAH, the reference's 12-plane
+                             split rule (bvh.cpp:48-230), level-synchronous */
 int pt_scene_build_gpu(const pt_mesh_desc* mesh, int32_t device, int32_t max_leaf, pt_scene** out,
                        double* build_ms);
 int pt_scene_build_gpu_ex(const pt_mesh_desc* mesh, int32_t device, int32_t max_leaf, int32_t builder,

@@ -48,7 +48,8 @@ def _check_layout(sc, max_leaf):
     assert (covered == 1).all()
 
 
-@pytest.mark.parametrize("max_leaf,builder", [(4, "ploc"), (8, "ploc"), (32, "ploc"), (8, "lbvh"), (32, "lbvh")])
+@pytest.mark.parametrize("max_leaf,builder", [(4, "ploc"), (8, "ploc"), (32, "ploc"), (8, "lbvh"), (32, "lbvh"),
+                                              (4, "sah"), (8, "sah"), (32, "sah")])
 def test_gpu_build_dragon_proxy(gpu_ctx, max_leaf, builder):
     t = time.perf_counter()
     host = scenes.dragon_proxy()
@@ -86,7 +87,7 @@ def test_gpu_build_small_and_spheres(gpu_ctx):
         b.albedo[k] = 0.5
     rng = np.random.default_rng(9)
     cases = [(1, 0, False), (0, 1, False), (2, 3, False), (37, 5, False), (5000, 0, False), (300, 0, True)]
-    for (n_tris, n_sph, dup), builder in [(c, bld) for c in cases for bld in ("ploc", "lbvh")]:
+    for (n_tris, n_sph, dup), builder in [(c, bld) for c in cases for bld in ("ploc", "lbvh", "sah")]:
         tris = None
         if n_tris:  # small triangles scattered in the box (big ones only for the tiny cases)
             size = 2.0 if n_tris < 100 else 0.15
