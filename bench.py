@@ -15,7 +15,10 @@ then the framebuffer is gathered to rank 0 over RCCL and copied to the host
 (ms/frame ends with the accumulated image on the host; one
 rank: pt_get_image_async into a pinned buffer, more ranks: a non-blocking
 copy of the gathered frame; either copy overlaps the next frame's rendering,
-and the last frame's copy is waited for inside the timed region).  Rays are
+and the last frame's copy is waited for inside the timed region).  Timed
+frames are queued with PT_FLAG_ASYNC: on the single-leaf scenes one frame's
+path kernel runs while the previous frame's per-path results are summed
+(same sums, same order); the wavefront scenes render synchronously.  Rays are
 the rays traced (camera +
 extension + shadow), counted on the device: SURVEY §8(d) counts the rays cast
 through the traversal, so camera rays that pt_render resolves on the host
@@ -100,7 +103,7 @@ def _ordinal(n):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scene", default="CBempty", help="headline scene (configs[1] = CBempty)")
     p.add_argument("--configs", default="CBspheres,CBbunny,bunny,dragon_proxy,dragon_proxy_gpubvh",
@@ -335,7 +338,7 @@ def run_workload(name, args, ctx, rank, world, dev, dist, share=None, flags=0):
         ctx.clear()
         ctx.render(args.width, args.height, args.spp, max_bounces=args.bounces, seed=args.seed,
                    batch_paths=args.batch, tile_size=args.tile, rank=t_rank, nranks=t_world,
-                   flags=flags | (ptrace.PT_FLAG_STATS if stats else 0))
+                   flags=flags | (ptrace.PT_FLAG_STATS if stats else ptrace.PT_FLAG_ASYNC))
         if world > 1 or args.force_gather:
             # RCCL gathers device tensors; gloo (tests) host tensors
             sdev = dev if args.backend == "nccl" else "cpu"

@@ -69,4 +69,18 @@ __global__ __launch_bounds__(TPB) void k_frame(const float4* __restrict__ accum,
   frame[pix_of[q]] = make_float4(a.x / ns, a.y / ns, a.z / ns, 1.0f);
 }
 
+// Zero n float4s / n words on the context's stream.  Kernels of ours rather
+// than hipMemsetAsync: the runtime's fill kernel, queued while a frame's copy
+// to the host runs on the copy stream (pt_get_image_async), does not start
+// until that copy is nearly done (~300 us: a 16 MB accumulation buffer, or
+// the 4-byte path-grab counters in front of the next frame's path kernel).
+__global__ __launch_bounds__(TPB) void k_zero(float4* __restrict__ p, uint32_t n) {
+  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+  if (i < n) p[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+__global__ __launch_bounds__(TPB) void k_zero_u32(uint32_t* __restrict__ p, uint32_t n) {
+  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+  if (i < n) p[i] = 0u;
+}
+
 }  // namespace pt

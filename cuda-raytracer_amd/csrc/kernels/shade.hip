@@ -118,6 +118,13 @@ struct ShadeArgs {
   // diagnostic build only (PT_SHADE_TIMING=1, env PT_SHADE_TIMING): per-phase
   // cycle sums of k_shade_push, 64 x 16 counters; else null
   unsigned long long* tprof;
+  // k_path_leaf's first acc_blocks workgroups (0: none) sum the previous
+  // launch's per-path results -- acc_npix pixels x acc_spp samples in acc_res
+  // -- into acc_dst[acc_slot[q]], k_accum's sums (pipelined frames, pt_render)
+  const float4* acc_res;
+  float4* acc_dst;
+  const uint32_t* acc_slot;
+  uint32_t acc_npix, acc_spp, acc_blocks;
 };
 
 #ifndef PT_SHADE_TIMING
@@ -741,6 +748,24 @@ __device__ __forceinline__ void put_res(float4* res, uint32_t P, const f3 L) {
 __device__ __forceinline__ f3 get_res(const float4* res, size_t P) {
   const res3 r = reinterpret_cast<const res3*>(res)[P];
   return mk(r.x, r.y, r.z);
+}
+
+// Sum each active pixel's samples of this batch into the accumulation buffer
+// (slot[q]: its owned slot; culled pixels add exact zeros, so they are not
+// touched), in sample order (deterministic; replaces kernelUpdateSSImage +
+// kernelReconstructImage + kernelAccumulate, cu:666-742).
+__device__ __forceinline__ void accum_pixel(const float4* __restrict__ ps1, float4* accum,
+                                            const uint32_t* __restrict__ slot, uint32_t npix, uint32_t spp_b,
+                                            uint32_t q) {
+  const uint32_t o = slot[q];
+  float4 a = accum[o];
+  for (uint32_t j = 0; j < spp_b; ++j) {
+    const f3 l = get_res(ps1, (size_t)j * npix + q);
+    a.x = a.x + l.x;
+    a.y = a.y + l.y;
+    a.z = a.z + l.z;
+  }
+  accum[o] = a;
 }
 
 // Pixel and sample of path P of the chunk.
@@ -1733,6 +1758,26 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES,
       return;
     }
   }
+  // Pipelined frames (pt_render, PT_FLAG_ASYNC): the first acc_blocks
+  // workgroups sum the previous launch's results (k_accum's work, its sums
+  // bit for bit) and exit.  Dispatched first, they hold a few of the slots
+  // the path workgroups would take while the rest start paths; the path
+  // workgroups behind them start as they exit (persistent waves grab their
+  // paths, so a late start only means fewer grabs).  Memory-bound sums beside
+  // the VALU-bound paths instead of a bandwidth-bound k_accum after them.
+  // (Measured and rejected: the frame's copy to the host carried the same way
+  // by leading workgroups writing the pinned buffer -- 16.53 against 16.42 ms
+  // per CBempty frame with the copy on the copy stream.)
+  {
+    const uint32_t na = S.acc_blocks;
+    if (blockIdx.x < na) {
+      const uint32_t n = S.acc_npix;
+      for (uint32_t q = blockIdx.x * TPB + threadIdx.x; q < n; q += na * TPB)
+        accum_pixel(S.acc_res, S.acc_dst, S.acc_slot, n, S.acc_spp, q);
+      return;
+    }
+  }
+  const uint32_t wg = blockIdx.x - S.acc_blocks;  // (the path workgroup's index)
   // candidate clusters: the leaf's records in LDS for the per-lane candidate loop
   __shared__ float4 s_rec[PATH_CL_PRIMS * 4];
   __shared__ uint32_t s_cl[PATH_CL_PRIMS];
@@ -1749,7 +1794,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES,
   // ones as they run dry) and how many regions it has found dry
   __shared__ uint32_t s_grab[TPB / 64][2];
   if (lid == 0) {
-    s_grab[threadIdx.x >> 6][0] = blockIdx.x % S.grab_nreg;
+    s_grab[threadIdx.x >> 6][0] = wg % S.grab_nreg;
     s_grab[threadIdx.x >> 6][1] = 0u;
   }
 #if PT_PATH_TIMING
@@ -1911,7 +1956,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES,
   // rays traced (R): one fire-and-forget atomic per wave into its lane's counter
   const uint32_t w = __builtin_amdgcn_readfirstlane(nrays);
   if (lid == 0 && w)
-    atomicAdd(rcount + (size_t)((blockIdx.x * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16,
+    atomicAdd(rcount + (size_t)((wg * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16,
               (unsigned long long)w);
   if constexpr (CNT) {  // the wave's executed tests (64-bit sums: a lane's u32 counts cannot overflow them)
     unsigned long long v[3] = {tc.tri, tc.sph, tc.box};
@@ -1921,13 +1966,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES,
       for (int o = 32; o > 0; o >>= 1) v[j] += __shfl_xor(v[j], o);
     }
     if (lid == 0) {
-      unsigned long long* line = rcount + (size_t)((blockIdx.x * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16;
+      unsigned long long* line = rcount + (size_t)((wg * 4 + (threadIdx.x >> 6)) & (RCOUNT_SLOTS - 1)) * 16;
       for (int j = 0; j < 3; ++j)
         if (v[j]) atomicAdd(line + 1 + j, v[j]);
     }
   }
 #if PT_PATH_TIMING
-  const uint32_t gw = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const uint32_t gw = wg * (TPB / 64) + (threadIdx.x >> 6);
   if (lid == 0 && gw < PT_TIMING_WAVES) {
     unsigned long long* o = g_path_timing + (size_t)gw * 8;
     o[0] = tm0;
@@ -1940,23 +1985,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES,
 #endif
 }
 
-// Sum each active pixel's samples of this batch into the accumulation buffer
-// (slot[q]: its owned slot; culled pixels add exact zeros, so they are not
-// touched), in sample order (deterministic; replaces kernelUpdateSSImage +
-// kernelReconstructImage + kernelAccumulate, cu:666-742).
+// (accum_pixel for every active pixel of a batch)
 __global__ __launch_bounds__(TPB) void k_accum(const float4* __restrict__ ps1, float4* accum,
                                                const uint32_t* __restrict__ slot, uint32_t npix, uint32_t spp_b) {
   const uint32_t q = blockIdx.x * TPB + threadIdx.x;
-  if (q >= npix) return;
-  const uint32_t o = slot[q];
-  float4 a = accum[o];
-  for (uint32_t j = 0; j < spp_b; ++j) {
-    const f3 l = get_res(ps1, (size_t)j * npix + q);
-    a.x = a.x + l.x;
-    a.y = a.y + l.y;
-    a.z = a.z + l.z;
-  }
-  accum[o] = a;
+  if (q < npix) accum_pixel(ps1, accum, slot, npix, spp_b, q);
 }
 
 // Repack pt_intersect's 8-float rays {o, tmax, d, 0} into ray records.

@@ -128,6 +128,31 @@ struct pt_ctx {
   uint32_t* d_work = nullptr;  // k_path_leaf path-region counters (128 B apart)
   float4* d_res = nullptr;     // per-path radiance of a chunk
   size_t res_cap = 0;
+  bool async_pending = false;  // frames queued with PT_FLAG_ASYNC (or a synchronous one's work) not yet waited for
+  // Pipelined single-leaf frames (PT_FLAG_ASYNC): a launch's per-path results
+  // are summed by the leading workgroups of the next launch (k_path_leaf,
+  // ShadeArgs::acc_*) or by flush_sums; acc_on: such sums are pending (job
+  // acc_job).  The results alternate between two slots (d_res, d_res_b; res_k
+  // the next one), pt_clear between two accumulation buffers while sums or
+  // images are pending on the current one, and an image requested before its
+  // sums are made (pt_get_image_async) waits in img_job until they are.
+  struct AccJob {
+    const float4* res;
+    float4* dst;
+    uint32_t npix, spp;
+  } acc_job{};
+  bool acc_on = false;
+  float4* d_res_b = nullptr;
+  size_t res_cap_b = 0;
+  int res_k = 0;
+  float4* d_accum_b = nullptr;
+  struct ImgJob {
+    const float4* acc;
+    float* rgba;
+    float ns;
+  } img_job[2]{};
+  int n_img = 0;
+  int acc_blocks = 64;  // k_path_leaf's leading sum workgroups (env PT_ACC_BLOCKS; a multiple of 8)
   uint4* d_wstate = nullptr;   // per shade workgroup {block next, block end, live slots, shaded vertices}
   uint32_t* d_pool = nullptr;  // POOLS path-block dispensers, CSTRIDE apart
   size_t wstate_cap = 0;
@@ -218,6 +243,32 @@ static int fail(pt_ctx* ctx, int code, const std::string& m) {
   return code;
 }
 
+// Wait for the frames queued since the last wait (PT_FLAG_ASYNC, and a
+// synchronous single-leaf frame's own work) and report their failure: the
+// kernel-argument check of k_path_leaf sets ERR_KERNARG in d_err (sticky
+// across queued frames: reset only when nothing is pending).
+static int flush_sums(pt_ctx* c);
+static int serve_images(pt_ctx* c);
+
+// Zero `bytes` (a multiple of 4) on the context's stream (post.hip k_zero_u32:
+// not hipMemsetAsync, which waits behind an image copy on the copy stream).
+static hipError_t zero_async(pt_ctx* c, void* p, size_t bytes) {
+  const uint32_t n = (uint32_t)(bytes / 4);
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_zero_u32, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, (uint32_t*)p, n);
+  return hipGetLastError();
+}
+static int drain(pt_ctx* c) {
+  if (!c->async_pending) return PT_OK;
+  if (int rc = flush_sums(c)) return rc;
+  c->async_pending = false;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  uint32_t e = 0;
+  HIPCHK(c, hipMemcpy(&e, c->d_err, 4, hipMemcpyDeviceToHost));
+  if (e & ERR_KERNARG) return fail(c, PT_E_HIP, "k_path_leaf: ShadeArgs is not the kernel's first argument (light_of<true>)");
+  return PT_OK;
+}
+
 template <class T>
 static int dalloc(pt_ctx* ctx, T** p, size_t count) {
   if (*p) {
@@ -232,7 +283,7 @@ static int dalloc(pt_ctx* ctx, T** p, size_t count) {
 static void free_all(pt_ctx* c) {
   void* ptrs[] = {c->d_nodes, c->d_prims,  c->d_prims_ref, c->d_shade, c->d_bsdfs,   c->d_lights, c->d_cbox, c->d_rcbox, c->d_rcmem, c->d_rcmem_ref, c->d_rcinfo, c->d_ray,
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
-                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_wstate, c->d_live, c->d_pool,
+                  c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_res_b, c->d_accum_b, c->d_wstate, c->d_live, c->d_pool,
                   c->d_pix_of, c->d_accum, c->d_frame, c->d_frame_a[0], c->d_frame_a[1], c->d_tmin, c->d_ray_b, c->d_ps0_b, c->d_ps1_b, c->d_ps2_b,
                   c->d_ps3_b, c->d_compact, c->d_act_pix, c->d_act_slot};
   for (void* p : ptrs)
@@ -1116,6 +1167,8 @@ int pt_create(pt_ctx** out, int device) {
   // paths per chunk (a frame of npix x spp paths runs in ceil(spp / (chunk / npix))
   // chunks, summed per pixel in sample order across them): tests set it small
   if (const char* q = getenv("PT_CULL")) c->cull = atoi(q) != 0;
+  // (A/B: PT_ACC_BLOCKS=0 sums each pipelined launch by a k_accum of its own)
+  if (const char* q = getenv("PT_ACC_BLOCKS")) c->acc_blocks = atoi(q) <= 0 ? 0 : std::max(8, std::min(4096, atoi(q) / 8 * 8));
   if (const char* q = getenv("PT_CHUNK_PATHS")) c->chunk_paths = (uint32_t)std::min<long long>(1ll << 28, std::max(1ll, atoll(q)));
   // tail compaction needs the wave record order's continuing-first ranks
   if (const char* q = getenv("PT_COMPACT")) {
@@ -1190,6 +1243,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   if (!c || !s || s->n_prims <= 0 || s->n_nodes <= 0 || s->n_levels <= 0) return fail(c, PT_E_INVALID, "empty scene");
   hipSetDevice(c->device);
   int rc;
+  if ((rc = drain(c))) return rc;
   c->n_prims = s->n_prims;
   c->n_nodes = s->n_nodes;
   c->n_levels = s->n_levels;
@@ -1415,9 +1469,24 @@ int pt_set_camera(pt_ctx* c, const pt_camera* cam) {
 int pt_clear(pt_ctx* c) {
   if (!c) return PT_E_INVALID;
   hipSetDevice(c->device);
-  if (c->d_accum && !c->pix_of.empty())
-    HIPCHK(c, hipMemsetAsync(c->d_accum, 0, c->pix_of.size() * sizeof(float4), c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // (queued, not waited for: ordered after the frames before it on `stream`,
+  // where their sums are made, so a pipelined next frame is not held up)
+  if (c->d_accum && !c->pix_of.empty()) {
+    const uint32_t n = (uint32_t)c->pix_of.size();
+    // sums or an image still pending on the current buffer: the next frame
+    // accumulates into the other one
+    bool pending = c->acc_on && c->acc_job.dst == c->d_accum;
+    for (int i = 0; i < c->n_img; ++i) pending = pending || c->img_job[i].acc == c->d_accum;
+    if (pending) {
+      if (!c->d_accum_b) {
+        int rc;
+        if ((rc = dalloc(c, &c->d_accum_b, n))) return rc;
+      }
+      std::swap(c->d_accum, c->d_accum_b);
+    }
+    hipLaunchKernelGGL(k_zero, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, c->d_accum, n);
+    HIPCHK(c, hipGetLastError());
+  }
   c->samples = 0;
   return PT_OK;
 }
@@ -1425,6 +1494,7 @@ int pt_clear(pt_ctx* c) {
 int pt_reset_stats(pt_ctx* c) {
   if (!c) return PT_E_INVALID;
   hipSetDevice(c->device);
+  if (int rc = drain(c)) return rc;
   HIPCHK(c, hipMemset(c->d_stats, 0, STAT_COUNT * 8));
   HIPCHK(c, hipMemset(c->d_rcount, 0, RCOUNT_SLOTS * 16 * 8));
   memset(&c->stats, 0, sizeof(c->stats));
@@ -1435,7 +1505,9 @@ int pt_reset_stats(pt_ctx* c) {
 int pt_get_stats(pt_ctx* c, pt_stats* out) {
   if (!c || !out) return PT_E_INVALID;
   hipSetDevice(c->device);
-  int rc = read_device_stats(c);
+  int rc = drain(c);
+  if (rc) return rc;
+  rc = read_device_stats(c);
   c->stats.n_levels = c->n_levels;
   c->stats.queue_factor = (int32_t)c->qfactor;
   *out = c->stats;
@@ -1456,9 +1528,16 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     return fail(c, PT_E_UNSUPPORTED, "image larger than 2^30 pixels");
   hipSetDevice(c->device);
   int rc;
+  const bool fb_change = P->width != c->fb_w || P->height != c->fb_h || tile != c->fb_tile || rank != c->fb_rank ||
+                         nranks != c->fb_nranks;
+  const bool cull_stale = !c->cull_valid || memcmp(&c->cull_cam, &c->camera, sizeof(pt_camera)) != 0;
+  // PT_FLAG_ASYNC: single-leaf scenes, uninstrumented frames, and nothing the
+  // queued frames read is re-uploaded (owned / culled pixel lists)
+  const bool async = (P->flags & PT_FLAG_ASYNC) && c->root_leaf && !(P->flags & PT_FLAG_STATS) && !fb_change &&
+                     !cull_stale;
+  if (!async && (rc = drain(c))) return rc;
   // framebuffer / owned pixels
-  if (P->width != c->fb_w || P->height != c->fb_h || tile != c->fb_tile || rank != c->fb_rank ||
-      nranks != c->fb_nranks) {
+  if (fb_change) {
     build_owned_pixels(c, P->width, P->height, tile, rank, nranks);
     c->cull_valid = false;
     c->fb_w = P->width;
@@ -1468,6 +1547,10 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     c->fb_nranks = nranks;
     if ((rc = dalloc(c, &c->d_pix_of, c->pix_of.size()))) return rc;
     if ((rc = dalloc(c, &c->d_accum, c->pix_of.size()))) return rc;
+    if (c->d_accum_b) {  // (re-made at its first use, pt_clear)
+      hipFree(c->d_accum_b);
+      c->d_accum_b = nullptr;
+    }
     if (!c->pix_of.empty())
       HIPCHK(c, hipMemcpy(c->d_pix_of, c->pix_of.data(), c->pix_of.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemset(c->d_accum, 0, std::max<size_t>(1, c->pix_of.size()) * sizeof(float4)));
@@ -1507,22 +1590,30 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     return fail(c, PT_E_UNSUPPORTED, "PT_FLAG_REF_SCHEDULE: the reference schedule samples one area light");
   const int max_bounces = ref_sched ? 2 : P->max_bounces;
   const int passes = max_bounces + 2;  // vertices per path at most
-  HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+  // (d_err collects the queued frames' failures: reset when none is pending)
+  if (!c->async_pending) HIPCHK(c, zero_async(c, c->d_err, 4));
   c->timing = (P->flags & PT_FLAG_STATS) != 0;
   const bool timed = c->timing;
 
   hipEvent_t t0 = c->ev[6], t1 = c->ev[7];
   HIPCHK(c, hipEventRecord(t0, c->stream));
-  bool first = true, path_err = false;
+  bool first = true;
   // chunks of spp_c samples of every owned pixel: M = npix * spp_c paths, each
   // path's radiance lands in res[j * npix + q] and is summed in sample order
   for (int done = 0; done < P->spp;) {
     const uint32_t spp_c = std::min<uint32_t>(std::max<uint32_t>(1, c->chunk_paths / npix), (uint32_t)(P->spp - done));
     const uint32_t M = npix * spp_c;
-    if ((size_t)M > c->res_cap) {
-      if ((rc = dalloc(c, &c->d_res, M))) return rc;
-      c->res_cap = M;
+    // per-path results: slot res_k of two when frames are pipelined (the
+    // previous launch's slot is summed while this one is written), else slot 0
+    const int rk = async ? c->res_k : 0;
+    float4*& res_slot = rk ? c->d_res_b : c->d_res;
+    size_t& res_cap = rk ? c->res_cap_b : c->res_cap;
+    if ((size_t)M > res_cap) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));  // (queued launches may still read it)
+      if ((rc = dalloc(c, &res_slot, M))) return rc;
+      res_cap = M;
     }
+    float4* const res = res_slot;
     ShadeArgs S;
     S.prims = c->refa ? c->d_prims_ref : c->d_prims;
     S.shade = c->d_shade;
@@ -1544,8 +1635,13 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.flags = P->flags;
     S.rcount = c->d_rcount;
     S.sample_base = (uint32_t)(P->sample_offset + done);
-    S.res = c->d_res;
+    S.res = res;
     S.M = M;
+    S.acc_blocks = 0;  // (k_path_leaf's leading sum workgroups: none unless set below)
+    S.acc_res = nullptr;
+    S.acc_dst = nullptr;
+    S.acc_slot = nullptr;
+    S.acc_npix = S.acc_spp = 0;
     S.passes = passes;
     {  // record-order keys: SORT_KEYS equal primitive ranges (BVH order, so ~subtrees)
       uint32_t b = 0;
@@ -1558,7 +1654,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       const pt_node& root = c->nodes_host[0];
       S.ray = nullptr;
       S.ps0 = S.ps2 = S.ps3 = nullptr;
-      S.ps1 = c->d_res;
+      S.ps1 = res;
       S.N = M;
       const uint32_t want = (M + 4 * PATH_CHUNK - 1) / (4 * PATH_CHUNK);
       const int kv = (nsh == 2 ? 1 : 0) + (c->refa ? 2 : 0);
@@ -1581,11 +1677,28 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
       S.grab_nreg = nreg;
       S.grab_region = (M + nreg - 1) / nreg;
       S.grab_work = c->d_work;
-      HIPCHK(c, hipMemsetAsync(c->d_work, 0, (size_t)nreg * PATH_CTR_STRIDE * 4, c->stream));
-      c->launch(pt_ctx::K_PATH, 0, kpath, dim3(blocks), dim3(TPB), S, root.prim_start, root.prim_count, passes,
-                c->d_rcount, c->d_err);
-      HIPCHK(c, hipMemcpyAsync(c->h_poll, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
-      path_err = true;
+      HIPCHK(c, zero_async(c, c->d_work, (size_t)nreg * PATH_CTR_STRIDE * 4));
+      // pipelined: the previous launch's sums in this launch's leading workgroups
+      if (async && c->acc_on && c->acc_blocks == 0)
+        if ((rc = flush_sums(c))) return rc;
+      if (async && c->acc_on) {
+        S.acc_blocks = (uint32_t)c->acc_blocks;
+        S.acc_res = c->acc_job.res;
+        S.acc_dst = c->acc_job.dst;
+        S.acc_slot = c->d_act_slot;
+        S.acc_npix = c->acc_job.npix;
+        S.acc_spp = c->acc_job.spp;
+      }
+      c->launch(pt_ctx::K_PATH, 0, kpath, dim3(blocks + S.acc_blocks), dim3(TPB), S, root.prim_start, root.prim_count,
+                passes, c->d_rcount, c->d_err);
+      HIPCHK(c, hipGetLastError());
+      c->async_pending = true;
+      if (async) {  // (this launch's sums: pending; the images that waited for the previous ones: queued)
+        c->acc_on = true;
+        c->acc_job = pt_ctx::AccJob{res, c->d_accum, npix, spp_c};
+        c->res_k = rk ^ 1;
+        if ((rc = serve_images(c))) return rc;
+      }
       c->stats.passes += passes;
       if (first) c->stats.batch_paths = (int32_t)M;
     } else {
@@ -1678,7 +1791,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
           if (comp) {
             // this pass writes the continuing paths densely into the other
             // set; the live slots are at most the last poll's count
-            HIPCHK(c, hipMemsetAsync(c->d_compact + ncomp * CBLK, 0, CREGIONS * 4, c->stream));
+            HIPCHK(c, zero_async(c, c->d_compact + ncomp * CBLK, CREGIONS * 4));
             S.compact = c->d_compact + ncomp * CBLK;
             S.creg = c->d_live + 2;  // (the regions' bounds from the k_live_sum just before)
             bind(cur, 1 - cur);
@@ -1706,7 +1819,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
             compact_next = false;
           }
         }
-        HIPCHK(c, hipMemsetAsync(c->d_live, 0, LIVE_WORDS * 4, c->stream));
+        HIPCHK(c, zero_async(c, c->d_live, LIVE_WORDS * 4));
         hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, Gc,
                            (const uint32_t*)c->d_pool, nblocks, c->d_live, (unsigned long long*)nullptr);
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 4 * (g & 1), c->d_live, 8, hipMemcpyDeviceToHost, c->stream));
@@ -1773,7 +1886,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         if (max_batch_paths(c, 1 + nsh) / 2 < 4096)
           return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded (u32 queue offsets)");
         c->qfactor *= 2;
-        HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+        HIPCHK(c, zero_async(c, c->d_err, 4));
         continue;
       }
       if (!finished) return fail(c, PT_E_HIP, "paths did not finish within the pass bound");
@@ -1798,18 +1911,24 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, Gc,
                            (const uint32_t*)c->d_pool, nblocks, c->d_live, c->d_stats + STAT_SHADED);
     }
-    c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)c->d_res,
-              c->d_accum, (const uint32_t*)c->d_act_slot, npix, spp_c);
-    HIPCHK(c, hipGetLastError());
+    if (!async) {  // (pipelined: the sums are pending, see above)
+      c->launch(pt_ctx::K_ACCUM, 0, k_accum, dim3((npix + TPB - 1) / TPB), dim3(TPB), (const float4*)res,
+                c->d_accum, (const uint32_t*)c->d_act_slot, npix, spp_c);
+      HIPCHK(c, hipGetLastError());
+    }
     done += (int)spp_c;
     first = false;
     c->stats.batches++;
   }
   HIPCHK(c, hipEventRecord(t1, c->stream));
+  if (async) {  // (queued: pt_sync and the other waiting calls report its failure)
+    c->samples += P->spp;
+    return PT_OK;
+  }
   HIPCHK(c, hipEventSynchronize(t1));
-  if (path_err && (c->h_poll[0] & ERR_KERNARG)) {
+  if ((rc = drain(c))) {
     c->timing = false;
-    return fail(c, PT_E_HIP, "k_path_leaf: ShadeArgs is not the kernel's first argument (light_of<true>)");
+    return rc;
   }
   float total = 0;
   hipEventElapsedTime(&total, t0, t1);
@@ -1836,12 +1955,13 @@ int pt_get_image(pt_ctx* c, float* rgba, size_t n_floats) {
   if (npx == 0) return PT_OK;
   hipSetDevice(c->device);
   int rc;
+  if ((rc = drain(c))) return rc;
   if (npx > c->frame_cap) {
     if ((rc = dalloc(c, &c->d_frame, npx))) return rc;
     c->frame_cap = npx;
   }
   const uint32_t npix = (uint32_t)c->pix_of.size();
-  if (npix < npx) HIPCHK(c, hipMemsetAsync(c->d_frame, 0, npx * sizeof(float4), c->stream));
+  if (npix < npx) HIPCHK(c, zero_async(c, c->d_frame, npx * sizeof(float4)));
   const float ns = (float)(c->samples > 0 ? c->samples : 1);
   if (npix)
     hipLaunchKernelGGL(k_frame, dim3((npix + TPB - 1) / TPB), dim3(TPB), 0, c->stream, (const float4*)c->d_accum,
@@ -1852,13 +1972,10 @@ int pt_get_image(pt_ctx* c, float* rgba, size_t n_floats) {
   return PT_OK;
 }
 
-int pt_get_image_async(pt_ctx* c, float* rgba, size_t n_floats) {
-  if (!c || !rgba) return PT_E_INVALID;
-  if (!c->copy_stream) return fail(c, PT_E_HIP, "pt_get_image_async: no copy stream");
+// The frame of accumulation buffer `acc` (sums / ns) assembled into staged
+// frame fidx on `stream` and copied to rgba on copy_stream.
+static int queue_image(pt_ctx* c, const float4* acc, float* rgba, float ns) {
   const size_t npx = (size_t)c->fb_w * c->fb_h;
-  if (npx * 4 > n_floats) return fail(c, PT_E_INVALID, "image buffer too small");
-  if (npx == 0) return PT_OK;
-  hipSetDevice(c->device);
   int rc;
   const int k = c->fidx;
   if (npx > c->frame_cap_a[k]) {
@@ -1869,10 +1986,11 @@ int pt_get_image_async(pt_ctx* c, float* rgba, size_t n_floats) {
   // the staged frame k is rewritten only after its last copy has read it
   if (c->cp_queued[k]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_cp[k], 0));
   const uint32_t npix = (uint32_t)c->pix_of.size();
-  if (npix < npx) HIPCHK(c, hipMemsetAsync(c->d_frame_a[k], 0, npx * sizeof(float4), c->stream));
-  const float ns = (float)(c->samples > 0 ? c->samples : 1);
+  if (npix < npx)
+    hipLaunchKernelGGL(k_zero, dim3((uint32_t)((npx + TPB - 1) / TPB)), dim3(TPB), 0, c->stream, c->d_frame_a[k],
+                       (uint32_t)npx);
   if (npix)
-    hipLaunchKernelGGL(k_frame, dim3((npix + TPB - 1) / TPB), dim3(TPB), 0, c->stream, (const float4*)c->d_accum,
+    hipLaunchKernelGGL(k_frame, dim3((npix + TPB - 1) / TPB), dim3(TPB), 0, c->stream, acc,
                        (const uint32_t*)c->d_pix_of, npix, ns, c->d_frame_a[k]);
   HIPCHK(c, hipGetLastError());
   // (pt_clear / pt_render on `stream` after this point cannot change the
@@ -1886,12 +2004,62 @@ int pt_get_image_async(pt_ctx* c, float* rgba, size_t n_floats) {
   return PT_OK;
 }
 
+static int serve_images(pt_ctx* c) {
+  for (int i = 0; i < c->n_img; ++i)
+    if (int rc = queue_image(c, c->img_job[i].acc, c->img_job[i].rgba, c->img_job[i].ns)) return rc;
+  c->n_img = 0;
+  return PT_OK;
+}
+
+// The pending sums of the last pipelined launch as a k_accum of their own
+// (no launch follows to carry them), then the images waiting for them.
+static int flush_sums(pt_ctx* c) {
+  if (c->acc_on) {
+    const pt_ctx::AccJob& j = c->acc_job;
+    hipLaunchKernelGGL(k_accum, dim3((j.npix + TPB - 1) / TPB), dim3(TPB), 0, c->stream, j.res, j.dst,
+                       (const uint32_t*)c->d_act_slot, j.npix, j.spp);
+    HIPCHK(c, hipGetLastError());
+    c->acc_on = false;
+  }
+  return serve_images(c);
+}
+
+int pt_get_image_async(pt_ctx* c, float* rgba, size_t n_floats) {
+  if (!c || !rgba) return PT_E_INVALID;
+  if (!c->copy_stream) return fail(c, PT_E_HIP, "pt_get_image_async: no copy stream");
+  const size_t npx = (size_t)c->fb_w * c->fb_h;
+  if (npx * 4 > n_floats) return fail(c, PT_E_INVALID, "image buffer too small");
+  if (npx == 0) return PT_OK;
+  hipSetDevice(c->device);
+  const float ns = (float)(c->samples > 0 ? c->samples : 1);
+  if (c->acc_on && c->acc_job.dst == c->d_accum) {
+    // its sums are pending (pipelined frames): the frame is assembled after
+    // the launch that makes them (two requests at most; a third flushes them)
+    if (c->n_img == 2)
+      if (int rc = flush_sums(c)) return rc;
+    if (c->acc_on) {
+      c->img_job[c->n_img++] = pt_ctx::ImgJob{c->d_accum, rgba, ns};
+      return PT_OK;
+    }
+  }
+  return queue_image(c, c->d_accum, rgba, ns);
+}
+
 int pt_wait_image(pt_ctx* c) {
   if (!c) return PT_E_INVALID;
   hipSetDevice(c->device);
+  // (the frames the copies come from, their pending sums and images queued
+  // first: their failure)
+  if (int rc = drain(c)) return rc;
   for (int k = 0; k < 2; ++k)
     if (c->cp_queued[k]) HIPCHK(c, hipEventSynchronize(c->ev_cp[k]));
   return PT_OK;
+}
+
+int pt_sync(pt_ctx* c) {
+  if (!c) return PT_E_INVALID;
+  hipSetDevice(c->device);
+  return drain(c);
 }
 
 int pt_copy_owned_sums(pt_ctx* c, void* dst, size_t n_bytes, int32_t dst_on_device) {
@@ -1900,6 +2068,7 @@ int pt_copy_owned_sums(pt_ctx* c, void* dst, size_t n_bytes, int32_t dst_on_devi
   if (n_bytes < need) return fail(c, PT_E_INVALID, "pt_copy_owned_sums: buffer too small");
   if (need == 0) return PT_OK;
   hipSetDevice(c->device);
+  if (int rc = drain(c)) return rc;
   HIPCHK(c, hipMemcpyAsync(dst, c->d_accum, need, dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
                            c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1946,7 +2115,11 @@ int pt_owned_pixels(pt_ctx* c, int32_t* n_pixels, int32_t* pixel_index, size_t m
   *n_pixels = (int32_t)c->pix_of.size();
   if (pixel_index)
     for (size_t i = 0; i < c->pix_of.size() && i < max_idx; ++i) pixel_index[i] = (int32_t)c->pix_of[i];
-  if (device_sums) *device_sums = c->d_accum;
+  if (device_sums) {  // (complete sums: the caller reads them on streams of its own)
+    hipSetDevice(c->device);
+    if (int rc = drain(c)) return rc;
+    *device_sums = c->d_accum;
+  }
   return PT_OK;
 }
 
@@ -1956,6 +2129,8 @@ int pt_intersect_ex(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits, uin
   if (c) c->ray_cur = nullptr;  // (a failed render may have left the compaction's second set bound)
   if (!c || (!rays && n > 0) || (!hits && n > 0) || n < 0) return PT_E_INVALID;
   if (!c->have_scene) return fail(c, PT_E_NOSCENE, "no scene loaded");
+  hipSetDevice(c->device);
+  if (int rc = drain(c)) return rc;
   c->refa = (flags & PT_FLAG_REF_ARITH) != 0;
   if (c->refa && c->has_sphere)
     return fail(c, PT_E_UNSUPPORTED, "PT_FLAG_REF_ARITH: the reference intersects triangles only");
@@ -2000,7 +2175,7 @@ int pt_intersect_ex(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits, uin
   HIPCHK(c, hipMalloc((void**)&d_in, (size_t)n * 32));  // rays in, then hit keys out
   for (;;) {
     HIPCHK(c, hipMemcpyAsync(d_in, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+    HIPCHK(c, zero_async(c, c->d_err, 4));
     hipLaunchKernelGGL(k_load_rays, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, d_in, c->d_ray,
                        (uint32_t)n);
     hipEventRecord(c->ev[6], c->stream);

@@ -37,7 +37,8 @@ PT_FLAG_REF_SCHEDULE = 0x20      # reference quirk (vi): 2 bounces, NEE 2/2/1 we
 PT_FLAG_REF_ARITH = 0x40         # the reference kernels' literal arithmetic (pt_api.h)
 PT_FLAG_EXACT_LIGHT_PDF = 0x80   # area-light NEE with the normalised cosine (default: light.cpp:81-92)
 PT_FLAG_COUNT_TESTS = 0x100     # count the single-leaf path kernel's executed primitive tests (pt_stats)
-PT_API_VERSION = 5
+PT_FLAG_ASYNC = 0x200           # queue a single-leaf frame and return (pt_sync / the waiting calls report it)
+PT_API_VERSION = 6
 PT_BSDF_DIFFUSE, PT_BSDF_MIRROR, PT_BSDF_GLASS, PT_BSDF_EMISSION, PT_BSDF_REFRACTION = 0, 1, 2, 3, 4
 PT_LIGHT_NONE, PT_LIGHT_AREA, PT_LIGHT_POINT, PT_LIGHT_DIRECTIONAL, PT_LIGHT_HEMISPHERE = 0, 1, 2, 3, 4
 PT_PRIM_TRIANGLE, PT_PRIM_SPHERE = 0, 1
@@ -121,7 +122,7 @@ API_SYMBOLS = [
     "pt_api_version", "pt_scene_load_dae", "pt_scene_from_triangles", "pt_scene_from_mesh", "pt_scene_from_mesh_ex", "pt_scene_build_gpu", "pt_scene_build_gpu_ex", "pt_scene_camera_scotty", "pt_scene_free", "pt_scene_get_desc",
     "pt_scene_level_counts", "pt_scene_sorted_to_input", "pt_create", "pt_destroy",
     "pt_last_error", "pt_device_count", "pt_load_scene", "pt_set_camera", "pt_render",
-    "pt_clear", "pt_get_image", "pt_get_image_async", "pt_wait_image", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex", "pt_copy_owned_sums",
+    "pt_clear", "pt_get_image", "pt_get_image_async", "pt_wait_image", "pt_sync", "pt_owned_pixels", "pt_samples", "pt_intersect", "pt_intersect_ex", "pt_copy_owned_sums",
     "pt_get_stats", "pt_reset_stats", "pt_median_filter", "pt_get_display_image", "pt_tonemap",
     "pt_write_png", "pt_write_pfm", "pt_check_division", "pt_check_fast_math",
     "pt_group_create", "pt_group_destroy", "pt_group_last_error", "pt_group_gather_kind", "pt_group_size",
@@ -175,6 +176,7 @@ def _load():
         "pt_get_image": (C.c_int, [P, C.POINTER(C.c_float), SZ]),
         "pt_get_image_async": (C.c_int, [P, C.POINTER(C.c_float), SZ]),
         "pt_wait_image": (C.c_int, [P]),
+        "pt_sync": (C.c_int, [P]),
         "pt_owned_pixels": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32), SZ, C.POINTER(P)]),
         "pt_samples": (C.c_int, [P, C.POINTER(I32)]),
         "pt_copy_owned_sums": (C.c_int, [P, P, SZ, I32]),
@@ -499,6 +501,10 @@ class Context:
 
     def wait_image(self):
         self._chk(LIB.pt_wait_image(self.h))
+
+    def sync(self):
+        """Wait for the frames queued with PT_FLAG_ASYNC (raises their failure)."""
+        self._chk(LIB.pt_sync(self.h))
 
     def get_image(self, out=None):
         """The accumulated frame (H, W, 4) float32 on the host.  `out`: an

@@ -54,8 +54,9 @@ extern "C" {
  * 4: pt_scene_desc.n_lights / lights, PT_LIGHT_DIRECTIONAL / _HEMISPHERE.
  * 5: PT_FLAG_COUNT_TESTS and pt_stats.prim_tests_tri / _sph, cluster_box_tests;
  *    pt_get_image_async / pt_wait_image (round 6).
+ * 6: PT_FLAG_ASYNC and pt_sync (pipelined single-leaf frames, round 6).
  * A client checks pt_api_version() == PT_API_VERSION before passing structs. */
-#define PT_API_VERSION 5
+#define PT_API_VERSION 6
 int pt_api_version(void);
 
 /* ---- error codes ---------------------------------------------------------- */
@@ -329,6 +330,19 @@ int pt_set_camera(pt_ctx* ctx, const pt_camera* camera);
  * the kernel's); results are unchanged.  The wavefront kernels and the
  * reference-arithmetic, guided and extended-light path variants count nothing. */
 #define PT_FLAG_COUNT_TESTS 0x100u
+/* Queue the frame and return (round 6; no reference counterpart: renderFrame,
+ * cu:2499-2533, returns when the frame is done).  Single-leaf scenes only
+ * (the wavefront renderer polls the device between passes and stays
+ * synchronous; PT_FLAG_STATS renders too): the path kernel of a frame runs
+ * on a stream of its own and writes one of two per-path result buffers, so
+ * the next frame's path kernel starts while the previous frame's results are
+ * summed into the accumulation buffer (same sums, same order, same bits).
+ * pt_clear and pt_get_image_async queue behind it without waiting; every
+ * other call on the context (pt_sync, pt_wait_image, pt_get_image,
+ * pt_get_stats, pt_load_scene, a synchronous pt_render, ...) first waits for
+ * the queued frames and reports a failure of theirs.  pt_stats.ms_total is
+ * not measured for an asynchronous frame. */
+#define PT_FLAG_ASYNC 0x200u
 
 typedef struct pt_render_params {
   int32_t width, height;
@@ -345,9 +359,12 @@ typedef struct pt_render_params {
 
 /* Render params->spp samples per owned pixel and ADD them to the context's
  * accumulation buffer (progressive, like renderAccumulate, cu:2419-2457).
- * Blocks until the GPU work is complete. */
+ * Blocks until the GPU work is complete (unless PT_FLAG_ASYNC). */
 int pt_render(pt_ctx* ctx, const pt_render_params* params);
-/* Zero the accumulation buffer and sample count (kernelClearAccumulate, cu:744). */
+/* Wait for every frame queued with PT_FLAG_ASYNC; PT_OK or its failure. */
+int pt_sync(pt_ctx* ctx);
+/* Zero the accumulation buffer and sample count (kernelClearAccumulate, cu:744).
+ * Queued on the context's stream (ordered after the frames before it). */
 int pt_clear(pt_ctx* ctx);
 /* Copy the current image (accumulated radiance / samples) of the whole frame,
  * width*height*4 floats.  Pixels this rank does not own are 0. */

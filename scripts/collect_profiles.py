@@ -7,6 +7,7 @@ after scripts/profile_round.sh came back in gpurun_out/):
 * bench_default.json                      the bench line (gpurun_out/bench.log)
 * bench_detail.json                       its detail side file (gpurun_out/bench_detail.json)
 * rocprof_kernel_stats_<scene>.csv        rocprofv3 --stats of one frame per workload
+* detail_<scene>.json                     that run's bench detail file (per-level visits)
 * pmc_<scene>.json                        per-kernel PMC totals (scripts/pmc_summary.py)
 """
 import glob
@@ -41,6 +42,9 @@ def main():
         stats = glob.glob(str(d / "**" / "*kernel_stats.csv"), recursive=True)
         if stats:
             shutil.copy(stats[0], dst / f"rocprof_kernel_stats_{sc}.csv")
+        det = OUT / f"prof_{sc}.detail.json"  # (that run's per-level visits: scripts/dev/level_table.py)
+        if det.exists():
+            shutil.copy(det, dst / f"detail_{sc}.json")
     scenes = sorted({p.name[len("pmc_"):].rsplit("_", 1)[0] for p in OUT.glob("pmc_*") if p.is_dir()})
     for sc in scenes:
         files = sorted(glob.glob(str(OUT / f"pmc_{sc}_[0-9]*" / "**" / "*counter_collection.csv"), recursive=True))

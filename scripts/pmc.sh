@@ -10,7 +10,7 @@ IFS=';' read -ra P <<< "${PASSES:-FETCH_SIZE;WRITE_SIZE}"
 n=0
 for c in "${P[@]}"; do
   timeout -s KILL 600 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${TAG}_$n -o run -- \
-    python bench.py --steps 1 --warmup 0 --no-cpu --no-1spp --no-executed ${PMC_ARGS:-} > gpurun_out/pmc_${TAG}_$n.log 2>&1
+    python bench.py --steps 1 --warmup 0 --no-cpu --no-1spp --no-executed --detail-out gpurun_out/pmc_${TAG}_$n.detail.json ${PMC_ARGS:-} > gpurun_out/pmc_${TAG}_$n.log 2>&1
   rc=$?; echo "=== pmc [$c] rc=$rc"
   [ $rc -ne 0 ] && { tail -20 gpurun_out/pmc_${TAG}_$n.log; exit $rc; }
   n=$((n+1))

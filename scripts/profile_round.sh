@@ -16,7 +16,7 @@ if [ -z "$NO_BENCH" ]; then
 fi
 [ -z "$NO_PROF" ] && for sc in $SCENES; do
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$sc -o run --output-format csv -- \
-    python bench.py --scene $sc --configs none --config5 off --ref-arith none --steps 1 --warmup 0 --no-cpu --no-1spp --no-executed \
+    python bench.py --scene $sc --configs none --config5 off --ref-arith none --steps 1 --warmup 0 --no-cpu --no-1spp --no-executed --detail-out gpurun_out/prof_$sc.detail.json \
     > gpurun_out/prof_$sc.log 2>&1 || { echo "rocprof $sc rc=$?"; exit 1; }
   echo "rocprof $sc ok"
 done

@@ -27,16 +27,21 @@ def _scene(name):
     return scenes.load(name)
 
 
-def _ctx_with_chunk(chunk):
-    old = os.environ.get("PT_CHUNK_PATHS")
-    os.environ["PT_CHUNK_PATHS"] = str(chunk)
+def _ctx_with_env(**env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
     try:
         return ptrace.Context(0)
     finally:
-        if old is None:
-            del os.environ["PT_CHUNK_PATHS"]
-        else:
-            os.environ["PT_CHUNK_PATHS"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def _ctx_with_chunk(chunk):
+    return _ctx_with_env(PT_CHUNK_PATHS=chunk)
 
 
 @pytest.fixture(scope="module")
@@ -72,6 +77,87 @@ def test_multi_chunk_frame_bit_exact(gpu_ctx, chunk_ctxs, name):
         assert len(bad) == 0, f"{name} chunk {key}: {len(bad)} values differ, max {np.abs(g - o).max()}"
         assert ctx.stats().rays == orays
         assert np.isfinite(g).all() and o[..., :3].mean() > 1e-3
+
+
+@pytest.mark.parametrize("name", ["CBempty", "CBbunny"])
+def test_async_frames_across_chunks(gpu_ctx, chunk_ctxs, name):
+    """PT_FLAG_ASYNC (the bench's timed frames): a single-leaf launch's per-path
+    results are summed by the next launch's leading workgroups (two result
+    buffers alternate; pt_clear switches accumulation buffers while sums or
+    images are pending; an image waits for its sums) -- progressive renders
+    (two calls, 6 + 10 samples) and a cleared second frame, queued back to
+    back with their image copies, equal the synchronous renders bit for bit,
+    on every chunking, with 8 leading workgroups and with none (a k_accum per
+    launch); the wavefront renderer (CBbunny) ignores the flag.  The counters
+    read after the queued frames cover all of them."""
+    import torch
+    W, H, B = 96, 80, 8
+    sc = _scene(name)
+    gpu_ctx.load_scene(sc)
+    want, rays = [], []
+    for seed in (SEED, 7):
+        gpu_ctx.reset_stats()
+        gpu_ctx.clear()
+        gpu_ctx.render(W, H, 6, max_bounces=B, seed=seed)
+        gpu_ctx.render(W, H, 10, max_bounces=B, seed=seed, sample_offset=6)
+        want.append(gpu_ctx.get_image())
+        rays.append(gpu_ctx.stats().rays)
+    A = ptrace.PT_FLAG_ASYNC
+    extra = [("acc8", _ctx_with_env(PT_ACC_BLOCKS=8)), ("acc0", _ctx_with_env(PT_ACC_BLOCKS=0))]
+    for key, ctx in [("1chunk", gpu_ctx)] + list(chunk_ctxs.items()) + extra:
+        ctx.load_scene(sc)
+        ctx.clear()
+        ctx.render(W, H, 16, max_bounces=B, seed=SEED)  # (camera culling, framebuffer: set up synchronously)
+        ctx.reset_stats()
+        bufs = [torch.empty((H, W, 4), dtype=torch.float32, pin_memory=True) for _ in range(3)]
+        for k, seed in enumerate((SEED, 7, SEED)):
+            ctx.clear()
+            ctx.render(W, H, 6, max_bounces=B, seed=seed, flags=A)
+            ctx.render(W, H, 10, max_bounces=B, seed=seed, sample_offset=6, flags=A)
+            ctx.get_image_async(bufs[k])
+        ctx.wait_image()
+        for k, w in enumerate((0, 1, 0)):
+            bad = np.argwhere(bufs[k].numpy() != want[w])
+            assert len(bad) == 0, f"{name} {key} frame {k}: {len(bad)} values differ"
+        assert ctx.stats().rays == 2 * rays[0] + rays[1]  # (pt_get_stats waits for the queued frames)
+        ctx.sync()
+        assert ctx.samples() == 16
+    for _, ctx in extra:
+        ctx.close()
+    assert not np.array_equal(want[0], want[1])
+
+
+def test_async_images_between_progressive_renders(gpu_ctx):
+    """An image requested while its frame's sums are pending (PT_FLAG_ASYNC)
+    shows the samples rendered when it was requested, not those of a later
+    progressive render into the same accumulation buffer; three requests in
+    a row (two wait at most, the third flushes the sums) give the same
+    frame."""
+    import torch
+    W, H, B = 96, 80, 8
+    gpu_ctx.load_scene(_scene("CBempty"))
+    gpu_ctx.clear()
+    gpu_ctx.render(W, H, 6, max_bounces=B, seed=SEED)
+    img6 = gpu_ctx.get_image()
+    gpu_ctx.render(W, H, 10, max_bounces=B, seed=SEED, sample_offset=6)
+    img16 = gpu_ctx.get_image()
+    A = ptrace.PT_FLAG_ASYNC
+    bufs = [torch.empty((H, W, 4), dtype=torch.float32, pin_memory=True) for _ in range(5)]
+    gpu_ctx.clear()
+    gpu_ctx.render(W, H, 6, max_bounces=B, seed=SEED, flags=A)
+    gpu_ctx.get_image_async(bufs[0])
+    gpu_ctx.render(W, H, 10, max_bounces=B, seed=SEED, sample_offset=6, flags=A)
+    for b in bufs[1:4]:
+        gpu_ctx.get_image_async(b)
+    gpu_ctx.clear()  # (the next frame's buffer: the pending images keep theirs)
+    gpu_ctx.render(W, H, 6, max_bounces=B, seed=SEED, flags=A)
+    gpu_ctx.get_image_async(bufs[4])
+    gpu_ctx.wait_image()
+    assert np.array_equal(bufs[0].numpy(), img6)
+    for b in bufs[1:4]:
+        assert np.array_equal(b.numpy(), img16)
+    assert np.array_equal(bufs[4].numpy(), img6)
+    assert not np.array_equal(img6, img16)
 
 
 def test_multi_chunk_wavefront_with_batches(chunk_ctxs):
