@@ -64,6 +64,7 @@ struct ShadeArgs {
   uint32_t n_lights;
   const float* cbox;  // single-leaf scenes: the leaf's primitive-pair boxes (8 floats each)
   int nclus;
+  uint32_t sph_cl;  // the clusters that hold a sphere (bit c: cluster c; spheres are clusters of one)
   uint32_t N, npix, sample_base, seed;
   udiv div_npix, div_width;  // p / npix, pixel / width (N and width * height < 2^30)
   int width, height, max_bounces;
@@ -670,52 +671,53 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           o_new = mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y),
                      __builtin_fmaf(n.z, EPS, pt.z));  // cu:593
           spec = 0;
-        } else if (B.type == PT_BSDF_MIRROR) {
-          if constexpr (REFA) {
-            // cu:1234 wi = normalize(dot(dpdu, -d), dot(dpdv, -d), dot(n, -d));
-            // cu:643-650 wo = (-wi.x, -wi.y, wi.z) back to world space
-            const f3 md = mk(-d.x, -d.y, -d.z);
-            const f3 wi = normalize(mk(dot(dpdu, md), dot(dpdv, md), dot(n, md)));
-            const float wx = -wi.x, wy = -wi.y, wz = wi.z;
-            d_new = mk(__builtin_fmaf(wy, dpdv.x, __builtin_fmaf(wx, dpdu.x, n.x * wz)),
-                       __builtin_fmaf(wy, dpdv.y, __builtin_fmaf(wx, dpdu.y, n.y * wz)),
-                       __builtin_fmaf(wy, dpdv.z, __builtin_fmaf(wx, dpdu.z, n.z * wz)));
-            o_new = mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y), __builtin_fmaf(n.z, EPS, pt.z));
-          } else {
-            const float dn = dot(d, n);
-            d_new = normalize_u(d - n * (2.0f * dn));  // (unit d, n: |d_new| ~ 1)
-            o_new = mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y), __builtin_fmaf(n.z, EPS, pt.z));
-          }
+        } else if (REFA) {  // (a mirror: glass is read as one under REFA, above)
+          // cu:1234 wi = normalize(dot(dpdu, -d), dot(dpdv, -d), dot(n, -d));
+          // cu:643-650 wo = (-wi.x, -wi.y, wi.z) back to world space
+          const f3 md = mk(-d.x, -d.y, -d.z);
+          const f3 wi = normalize(mk(dot(dpdu, md), dot(dpdv, md), dot(n, md)));
+          const float wx = -wi.x, wy = -wi.y, wz = wi.z;
+          d_new = mk(__builtin_fmaf(wy, dpdv.x, __builtin_fmaf(wx, dpdu.x, n.x * wz)),
+                     __builtin_fmaf(wy, dpdv.y, __builtin_fmaf(wx, dpdu.y, n.y * wz)),
+                     __builtin_fmaf(wy, dpdv.z, __builtin_fmaf(wx, dpdu.z, n.z * wz)));
+          o_new = mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y), __builtin_fmaf(n.z, EPS, pt.z));
           Tset(mulv(Tv(), ld3(B.albedo)));
           spec = F_SPEC;
-        } else {  // PT_BSDF_GLASS / _REFRACTION (Fresnel-weighted reflect / refract, bsdf.h:167-212)
-          const float ior = B.ior;
-          const float eta = front ? rcp_rn(ior) : ior;  // (an index of refraction: normal range)
-          const float cosi = -dot(d, n);
-          const float sin2t = (eta * eta) * (1.0f - cosi * cosi);
+        } else {
+          // PT_BSDF_MIRROR, and _GLASS / _REFRACTION (Fresnel-weighted reflect /
+          // refract, bsdf.h:167-212) -- one body with the reflected and the
+          // refracted direction selected before a single normalisation (a
+          // wave's lanes at mirror, reflecting and refracting vertices ran
+          // three bodies with a normalisation each)
+          const float dn = dot(d, n);
           bool refl = true;
-          float cost = 0.0f;
-          if (sin2t < 1.0f) {
-            cost = sqrt_rn(1.0f - sin2t);  // (sin2t < 1: 1 - sin2t >= 2^-24)
-            float r0 = div_rn(1.0f - ior, 1.0f + ior);  // (1 - ior: 0 or >= 2^-24 in magnitude)
-            r0 = r0 * r0;
-            const float c = front ? cosi : cost;
-            const float m = 1.0f - c;
-            const float F = __builtin_fmaf(1.0f - r0, ((m * m) * (m * m)) * m, r0);
-            // u.x: a glass vertex takes no NEE sample, so the vertex's first
-            // Philox word is free (no second Philox call in a divergent branch)
-            refl = u01(u.x) < F;
+          float eta = 1.0f, cost = 0.0f;
+          if (B.type != PT_BSDF_MIRROR) {
+            const float ior = B.ior;
+            eta = front ? rcp_rn(ior) : ior;  // (an index of refraction: normal range)
+            const float cosi = -dn;
+            const float sin2t = (eta * eta) * (1.0f - cosi * cosi);
+            if (sin2t < 1.0f) {
+              cost = sqrt_rn(1.0f - sin2t);  // (sin2t < 1: 1 - sin2t >= 2^-24)
+              float r0 = div_rn(1.0f - ior, 1.0f + ior);  // (1 - ior: 0 or >= 2^-24 in magnitude)
+              r0 = r0 * r0;
+              const float c = front ? cosi : cost;
+              const float m = 1.0f - c;
+              const float F = __builtin_fmaf(1.0f - r0, ((m * m) * (m * m)) * m, r0);
+              // u.x: a glass vertex takes no NEE sample, so the vertex's first
+              // Philox word is free (no second Philox call in a divergent branch)
+              refl = u01(u.x) < F;
+            }
           }
-          if (refl) {
-            const float dn = dot(d, n);
-            d_new = normalize_u(d - n * (2.0f * dn));
-            Tset(mulv(Tv(), ld3(B.albedo)));
-            o_new = mk(__builtin_fmaf(n.x, EPS, pt.x), __builtin_fmaf(n.y, EPS, pt.y), __builtin_fmaf(n.z, EPS, pt.z));
-          } else {
-            d_new = normalize_u(d * eta + n * (eta * cosi - cost));  // (|.| ~ 1: Snell's refracted direction)
-            Tset(mulv(Tv(), ld3(B.transmittance)));
-            o_new = mk(__builtin_fmaf(-n.x, EPS, P.x), __builtin_fmaf(-n.y, EPS, P.y), __builtin_fmaf(-n.z, EPS, P.z));
-          }
+          // reflected: d - 2 (d.n) n; refracted (Snell): eta d + (eta cosi - cost) n
+          const float kr = 2.0f * dn, kt = eta * -dn - cost;
+          const f3 v = refl ? mk(d.x - n.x * kr, d.y - n.y * kr, d.z - n.z * kr)
+                            : mk(d.x * eta + n.x * kt, d.y * eta + n.y * kt, d.z * eta + n.z * kt);
+          d_new = normalize_u(v);  // (|v| ~ 1)
+          Tset(mulv(Tv(), refl ? ld3(B.albedo) : ld3(B.transmittance)));
+          const float oe = refl ? EPS : -EPS;
+          const f3 ob = refl ? pt : P;
+          o_new = mk(__builtin_fmaf(n.x, oe, ob.x), __builtin_fmaf(n.y, oe, ob.y), __builtin_fmaf(n.z, oe, ob.z));
           spec = F_SPEC;
         }
         new_ext = (vtx <= (uint32_t)S.max_bounces) && (T.x > 0.0f || T.y > 0.0f || T.z > 0.0f);
@@ -1538,12 +1540,53 @@ __device__ __forceinline__ void leaf_closest_cl(const ShadeArgs& S, const float4
       bw_closest_update(r.o, r.d, q, pstart + k, bt, bp);
     }
   };
-  while (cm) {
-    const int c = __builtin_ctz(cm);
-    cm &= cm - 1u;
-    const uint32_t fc = s_cl[c];  // first primitive | count << 16
-    step((int)(fc & 0xFFFFu));
-    if (fc >> 17) step((int)(fc & 0xFFFFu) + 1);
+  if constexpr (SPH) {
+    // the triangle candidates, then the spheres: two per-lane loops instead
+    // of one whose iterations ran both tests whenever a wave's lanes were at
+    // a triangle and at a sphere.  A sphere takes a tie with the best so far
+    // by the lower index: the hit of the loop in index order.
+    uint32_t cs = cm & S.sph_cl;
+    cm &= ~S.sph_cl;
+    while (cm) {
+      const int c = __builtin_ctz(cm);
+      cm &= cm - 1u;
+      const uint32_t fc = s_cl[c];  // first primitive | count << 16
+      Prim q;
+      const int k = (int)(fc & 0xFFFFu);
+      q.q0 = s_rec[4 * k];
+      q.q1 = s_rec[4 * k + 1];
+      q.q2 = s_rec[4 * k + 2];
+      q.q3 = s_rec[4 * k + 3];
+      if constexpr (CNT) ++tc->tri;
+      bw_closest_update(r.o, r.d, q, pstart + k, bt, bp);
+      if (fc >> 17) {
+        q.q0 = s_rec[4 * k + 4];
+        q.q1 = s_rec[4 * k + 5];
+        q.q2 = s_rec[4 * k + 6];
+        q.q3 = s_rec[4 * k + 7];
+        if constexpr (CNT) ++tc->tri;
+        bw_closest_update(r.o, r.d, q, pstart + k + 1, bt, bp);
+      }
+    }
+    while (cs) {
+      const int c = __builtin_ctz(cs);
+      cs &= cs - 1u;
+      const int k = (int)(s_cl[c] & 0xFFFFu);
+      if constexpr (CNT) ++tc->sph;
+      const float tt = sphere_test(r.o, r.d, s_rec[4 * k], s_rec[4 * k + 1]);
+      const int gi = pstart + k;
+      const bool take = (tt >= 0.0f) & ((tt < bt) | ((tt == bt) & (gi < bp)));
+      bt = take ? tt : bt;
+      bp = take ? gi : bp;
+    }
+  } else {
+    while (cm) {
+      const int c = __builtin_ctz(cm);
+      cm &= cm - 1u;
+      const uint32_t fc = s_cl[c];  // first primitive | count << 16
+      step((int)(fc & 0xFFFFu));
+      if (fc >> 17) step((int)(fc & 0xFFFFu) + 1);
+    }
   }
   prim = bp < 0 ? PT_PRIM_NONE : (uint32_t)bp;
   t = bt;
@@ -1600,12 +1643,28 @@ __device__ __forceinline__ bool leaf_occluded_aabb(const ShadeArgs& S, const flo
     const bool ov = !((hi.x < b0.x) | (lo.x > b0.y) | (hi.y < b0.z) | (lo.y > b0.w) | (hi.z < b1.x) | (lo.z > b1.y));
     cm = mask_bit(cm, ov, c);
   }
+  // (SPH: the triangle candidates, then the spheres, as in leaf_closest_cl)
+  uint32_t cs = 0u;
+  if constexpr (SPH) {
+    cs = cm & S.sph_cl;
+    cm &= ~S.sph_cl;
+  }
   while (cm && !hit) {
     const int c = __builtin_ctz(cm);
     cm &= cm - 1u;
     const uint32_t fc = s_cl[c];
     hit = test((int)(fc & 0xFFFFu));
     if (!hit && (fc >> 17)) hit = test((int)(fc & 0xFFFFu) + 1);
+  }
+  if constexpr (SPH) {
+    while (cs && !hit) {
+      const int c = __builtin_ctz(cs);
+      cs &= cs - 1u;
+      const int k = (int)(s_cl[c] & 0xFFFFu);
+      if constexpr (CNT) ++tc->sph;
+      const float tt = sphere_test(r.o, r.d, s_rec[4 * k], s_rec[4 * k + 1]);
+      hit = (tt >= 0.0f) & (tt <= r.tmax);
+    }
   }
   return hit;
 }

@@ -90,6 +90,7 @@ struct pt_ctx {
   float4* d_rcmem_ref = nullptr;  // ... as PT_FLAG_REF_ARITH records (RootTable::cmem_ref)
   uint32_t* d_rcinfo = nullptr;  // their member ranges and primitive ids (RootTable::cinfo)
   int nclus = 0;
+  uint32_t sph_clmask = 0;  // the single-leaf clusters that hold a sphere (bit c: cluster c)
 
   // wavefront buffers (sized for N paths = 2N ray slots)
   uint32_t cap_paths = 0;  // paths the buffers hold
@@ -1401,6 +1402,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     // triangle for origins up to 64 M.  Record: {xmin, xmax, ymin, ymax, zmin,
     // zmax} (box_hit's order), first primitive (leaf-relative), count.
     c->nclus = 0;
+    c->sph_clmask = 0;
     if (c->root_leaf) {
       const pt_node& r = c->nodes_host[0];
       const double G = std::ldexp(m, -14);
@@ -1425,6 +1427,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
             }
           }
         }
+        if (s1 && cb.size() / 8 < 32) c->sph_clmask |= 1u << (cb.size() / 8);
         push_guarded_box(cb, lo, hi, G);
         cb.push_back(int_bits(i));
         cb.push_back(int_bits(cnt));
@@ -1625,6 +1628,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     S.n_lights = c->n_lights;
     S.cbox = c->d_cbox;
     S.nclus = c->nclus;
+    S.sph_cl = c->sph_clmask;
     S.npix = npix;
     S.div_npix = udiv_make(npix);
     S.div_width = udiv_make((uint32_t)P->width);
