@@ -1083,6 +1083,45 @@ __device__ __forceinline__ void push_two_level(const TraceArgs& A, int node, con
   }
 }
 
+#ifndef PT_DBG_LINES
+#define PT_DBG_LINES 0
+#endif
+#if PT_DBG_LINES
+// diagnostic build only: how many distinct memory lines a wave item's ray
+// record gathers touch, for records of 32 B (4 per 128-B line, as built), 16 B
+// (8 per line) and 8 B (16 per line): g_dbg_lines[4 kind + {rays, lines32,
+// lines16, lines8}], kind 0 interior, 1 leaf items
+static __device__ unsigned long long g_dbg_lines[8];
+template <int R>
+__device__ __forceinline__ void dbg_count_lines(const uint32_t (&id)[R], const bool (&valid)[R], bool leaf) {
+  const uint32_t lid = lane_id();
+  uint32_t nl[3] = {0, 0, 0}, nv = 0;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    bool dup[3] = {false, false, false};
+    for (int jj = 0; jj <= j; ++jj) {
+      for (int k = 0; k < 64; ++k) {
+        const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)id[jj], k);
+        const bool ov = __builtin_amdgcn_readlane((int)valid[jj], k) != 0;
+        const bool before = jj < j || (uint32_t)k < lid;
+        if (!ov || !before) continue;
+        dup[0] |= (o >> 2) == (id[j] >> 2);
+        dup[1] |= (o >> 3) == (id[j] >> 3);
+        dup[2] |= (o >> 4) == (id[j] >> 4);
+      }
+    }
+    nv += (uint32_t)__popcll(__ballot(valid[j]));
+#pragma unroll
+    for (int g = 0; g < 3; ++g) nl[g] += (uint32_t)__popcll(__ballot(valid[j] && !dup[g]));
+  }
+  if (lid == 0) {
+    unsigned long long* c = g_dbg_lines + (leaf ? 4 : 0);
+    atomicAdd(c, (unsigned long long)nv);
+    for (int g = 0; g < 3; ++g) atomicAdd(c + 1 + g, (unsigned long long)nl[g]);
+  }
+}
+#endif
+
 template <bool REFA = false, bool LEAF = false, bool TMIN = false>
 __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint32_t base, int n, int lane, bool ids,
                                              bool out_ids, bool two_level) {
@@ -1103,6 +1142,9 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     if (valid[j]) load_ray(A, ids, base + (uint32_t)i, id[j], o[j], d[j], tmax[j]);
   }
   const int nj = (n + 63) >> 6;  // ray groups with at least one valid lane (uniform)
+#if PT_DBG_LINES
+  if (ids) dbg_count_lines<RPTW>(id, valid, nd->prim_count > 0);
+#endif
   float tlo[RPTW];  // the rays' t_min (pt_intersect; TMIN only)
 #pragma unroll
   for (int j = 0; j < RPTW; ++j) tlo[j] = (TMIN && valid[j]) ? A.tmin[id[j]] : 0.0f;

@@ -1099,6 +1099,16 @@ int pt_dbg_path_timing(unsigned long long* out, int nwaves) {
                                                                                                  : PT_E_HIP;
 }
 #endif
+#if PT_DBG_LINES
+// diagnostic build only: the level items' record-line counts (read, then reset)
+int pt_dbg_lines(unsigned long long* out8) {
+  if (!out8) return PT_E_INVALID;
+  if (hipDeviceSynchronize() != hipSuccess) return PT_E_HIP;
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_dbg_lines), 64) != hipSuccess) return PT_E_HIP;
+  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_lines), z, 64) == hipSuccess ? PT_OK : PT_E_HIP;
+}
+#endif
 
 int pt_check_division(pt_ctx* c, const float* num, const float* den, float* q, int32_t n) {
   if (!c || !num || !den || !q || n < 0) return PT_E_INVALID;
