@@ -1866,6 +1866,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES,
   uint32_t next = 0, end = 0;
   bool drained = false;
   bool active = false;
+  // Camera rays made in batches (round 6): the wave computes the camera rays
+  // of the pool's next up to 64 paths with every lane at once into a ring in
+  // LDS (s_cam: {dir, pixel} and the path, per wave), and idle lanes start
+  // their paths from the ring's head -- the same path for the same lane as
+  // taking them straight from the pool.  Made where a lane refills, the camera
+  // ray cost the wave a whole divergent camera_dir per iteration (~15 of 64
+  // lanes refill at each vertex of a ~4-vertex mean path).
+  __shared__ float4 s_cam[TPB / 64][64];
+  __shared__ uint32_t s_camp[TPB / 64][64];
+  float4* const cam_ring = s_cam[threadIdx.x >> 6];
+  uint32_t* const camp_ring = s_camp[threadIdx.x >> 6];
+  uint32_t fhead = 0, fcount = 0;  // (wave-uniform) ring head and entries
   // the lane's path index lives in LDS between its uses (camera ray, sample
   // index, result): one VGPR less across the vertex loop
   __shared__ uint32_t sh_p[TPB];
@@ -1895,9 +1907,26 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES,
     return leaf_occluded<REFA, SPH>(S.prims, pstart, pcount, r);
   };
   for (;;) {
-    // ---- refill idle lanes from the pool (new paths start at their camera ray)
+    // ---- refill idle lanes from the camera-ray ring (new paths start at their camera ray)
     const unsigned long long idle = __ballot(!active);
-    if (idle && next == end && !drained) {
+    const uint32_t nidle = (uint32_t)__popcll(idle);
+    // top the ring up in batches until it holds a ray for every idle lane (or
+    // the paths have run out): at most a few rounds, fully active
+    while (idle && fcount < nidle && !(drained && next == end)) {
+      if (next < end) {
+        const uint32_t m = min(64u - fcount, end - next);
+        if (lid < m) {
+          const uint32_t p = next + lid;
+          uint32_t g;
+          const f3 dir = camera_dir<M64P, REFA, true>(S, p, g);
+          const uint32_t at = (fhead + fcount + lid) & 63u;
+          cam_ring[at] = make_float4(dir.x, dir.y, dir.z, __uint_as_float(g));
+          camp_ring[at] = p;
+        }
+        fcount += m;
+        next += m;
+        continue;
+      }
 #if PT_PATH_TIMING
       const unsigned long long tg = wall_clock64();
 #endif
@@ -1941,14 +1970,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES,
       else ++nchunks;
 #endif
     }
-    if (idle && next < end) {
+    if (idle && fcount) {
       const uint32_t r = mbcnt64(idle);
-      const uint32_t avail = end - next;
-      if (!active && r < avail) {
-        const uint32_t p = next + r;
+      if (!active && r < fcount) {
+        const uint32_t at = (fhead + r) & 63u;
+        const float4 c = cam_ring[at];
+        const uint32_t p = camp_ring[at];
         sh_p[threadIdx.x] = p;
         active = true;
-        const f3 dir = camera_dir<M64P, REFA, true>(S, p, st.g);
+        const f3 dir = mk(c.x, c.y, c.z);
+        st.g = __float_as_uint(c.w);
         st.T = mk(1.0f, 1.0f, 1.0f);
         st.L = mk(0.0f, 0.0f, 0.0f);
         Lq[0] = 0.0f;
@@ -1960,12 +1991,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PATH_WAVES,
         st.flags = F_EXT | (1u << 8);
         ext = RayV{ld3(cam_of<true>(S).origin), dir, __builtin_inff()};
       }
-      next += min((uint32_t)__popcll(idle), avail);
+      const uint32_t used = min(nidle, fcount);
+      fhead = (fhead + used) & 63u;
+      fcount -= used;
     }
-    if (!__any(active)) {
-      if (drained) break;
-      continue;  // (pool was empty: the next iteration grabs a chunk)
-    }
+    if (!__any(active)) break;  // (the paths have run out: the ring is filled whenever any remain)
     // ---- one vertex of every active path: leaf tests, then shade
     nrays += (uint32_t)__popcll(__ballot(active && (st.flags & F_EXT)));
     uint32_t cast_sh = 0u;  // (the shadow rays this vertex cast, counted below in uniform control flow)

@@ -1,0 +1,12 @@
+cd ${GRAFT_REPO_ROOT:-/root/repo}
+export TMPDIR=/tmp
+make -s -C cuda-raytracer_amd check || exit 3
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_all.log 2>&1
+rc=$?; echo "tests rc=$rc: $(tail -1 gpurun_out/t_all.log)"; [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" gpurun_out/t_all.log | head -30; exit $rc; }
+for i in 1 2; do
+timeout -k 10 300 python bench.py --no-cpu --configs CBspheres --config5 off --ref-arith none --steps 10 > gpurun_out/b$i.log 2>&1 || exit 1
+python -c "
+import json
+d=[json.loads(l) for l in open('gpurun_out/b$i.log') if l.startswith('{')][-1]
+print('CBempty', d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'], [ (c['scene'], c['value'], c['ms_per_frame']) for c in d['configs']])"
+done
