@@ -82,5 +82,11 @@ __global__ __launch_bounds__(TPB) void k_zero_u32(uint32_t* __restrict__ p, uint
   const uint32_t i = blockIdx.x * TPB + threadIdx.x;
   if (i < n) p[i] = 0u;
 }
+// (a small device-to-device copy as a kernel of ours, for the same reason)
+__global__ __launch_bounds__(TPB) void k_copy_u32(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                  uint32_t n) {
+  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
 
 }  // namespace pt

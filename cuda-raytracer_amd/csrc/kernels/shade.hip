@@ -490,6 +490,13 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
       // the record's first 16 B answer spheres ({centre, meta}) and flat
       // triangles ({n0, meta}); the rest is read only for a triangle with
       // distinct vertex normals (or the reference arithmetic's blend)
+#ifdef PT_DBG_BOUNDS
+      if (prim >= S.A.dbg_nprims) {
+        printf("PT_DBG_BOUNDS shade prim %u vs %u (flags %x, t %g, block %d thread %d)\n", prim, S.A.dbg_nprims,
+               st.flags, t, (int)blockIdx.x, (int)threadIdx.x);
+        prim = 0u;
+      }
+#endif
       const float4* Q = S.shade + (size_t)prim * SHADE_REC;
       const float4 q0 = Q[0];
       // EARLY: the vertex's Philox words are computed while the shading
@@ -984,6 +991,13 @@ __device__ __forceinline__ int shade_slot(const ShadeArgs& S, uint32_t p, bool a
     }
     if (!live) return SLOT_FREE;
   }
+#ifdef PT_DBG_BOUNDS
+  if (q >= S.N || (ended && P >= S.M)) {
+    printf("PT_DBG_BOUNDS shade_slot q %u (N %u) P %u (M %u) ended %d compact %d block %d thread %d\n", q, S.N, P,
+           S.M, (int)ended, S.compact ? 1 : 0, (int)blockIdx.x, (int)threadIdx.x);
+    return SLOT_FREE;
+  }
+#endif
   if (ended) {
     new_ext = false;
 #pragma unroll
@@ -1241,6 +1255,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SHADE_WAVES
   if (fr) {
     uint32_t rank = mbcnt64(mf);
     for (int w = 0; w < wave; ++w) rank += s_free[w];
+#ifdef PT_DBG_BOUNDS
+    if (q >= S.N) printf("PT_DBG_BOUNDS regen q %u (N %u) block %d thread %d\n", q, S.N, (int)blockIdx.x, (int)threadIdx.x);
+#endif
     if (rank < ns) {
       const uint32_t P = rank < t1 ? next + rank : s_nb + rank - t1;
       S.ps0[q] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(F_EXT | (1u << 8)));

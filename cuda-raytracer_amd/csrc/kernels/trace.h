@@ -69,6 +69,7 @@ struct TraceArgs {
   uint32_t dbg_nslots;               // ray records
   uint32_t dbg_nnodes;
   uint64_t dbg_qids;                 // ids in q (all regions)
+  uint32_t dbg_nprims;               // primitives (hit keys, shading records)
 };
 #ifdef PT_DBG_BOUNDS
 #define PT_CHECK(cond, what, a, b)                                                                  \

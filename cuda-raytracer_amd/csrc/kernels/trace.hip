@@ -1127,6 +1127,14 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
                                              bool out_ids, bool two_level) {
   const uint32_t lid = lane_id();
   const CPTR(pt_node) nd = (const CPTR(pt_node))(A.nodes + node);
+#ifdef PT_DBG_BOUNDS
+  if (ids && (uint64_t)base + (uint64_t)n > A.dbg_qids) {
+    if (lid == 0)
+      printf("PT_DBG_BOUNDS process_wave queue read node %d lane %d base %u n %d vs %llu ids\n", node, lane, base, n,
+             (unsigned long long)A.dbg_qids);
+    return;
+  }
+#endif
   uint32_t id[RPTW];
   f3 o[RPTW], d[RPTW];
   float tmax[RPTW];
@@ -1139,6 +1147,16 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
     o[j] = mk(0.f, 0.f, 0.f);
     d[j] = mk(1.f, 0.f, 0.f);
     tmax[j] = -1.0f;
+#ifdef PT_DBG_BOUNDS
+    if (valid[j] && ids) {
+      const uint32_t qi = A.q[base + (uint32_t)i];
+      if (qi >= A.dbg_nslots) {
+        printf("PT_DBG_BOUNDS process_wave ray id %u vs %u (node %d lane %d base %u i %d n %d)\n", qi, A.dbg_nslots,
+               node, lane, base, i, n);
+        valid[j] = false;
+      }
+    }
+#endif
     if (valid[j]) load_ray(A, ids, base + (uint32_t)i, id[j], o[j], d[j], tmax[j]);
   }
   const int nj = (n + 63) >> 6;  // ray groups with at least one valid lane (uniform)

@@ -124,6 +124,11 @@ struct pt_ctx {
   int scan_multi_min = 0;          // levels with more nodes use k_scan_count + k_scan_alloc
   int dfs_level = 1 << 20;         // the DFS cut: this real level's rays finish their subtrees depth-first
   unsigned long long* d_rcount = nullptr;  // valid root rays: RCOUNT_SLOTS counters, one 128-B line each
+  // the ray and statistics counters as a wavefront chunk started: restored
+  // when the chunk is re-run after a queue overflow (its abandoned passes
+  // counted rays and visits)
+  unsigned long long* d_rcount_bak = nullptr;
+  unsigned long long* d_stats_bak = nullptr;
   unsigned long long* d_stats = nullptr;
   uint32_t* d_err = nullptr;
   uint32_t* d_work = nullptr;  // k_path_leaf path-region counters (128 B apart)
@@ -210,6 +215,17 @@ struct pt_ctx {
     } else {
       hipLaunchKernelGGL(kernel, grid, block, 0, stream, args...);
     }
+    if (dbg_sync) sync_check(cls, level, grid.x);
+  }
+  // PT_DEBUG_SYNC (environment, read at pt_create; a debugging aid): every
+  // kernel launch is waited for and a failure reported on stderr with the
+  // kernel class, level and grid -- the first kernel that faults, not the
+  // next synchronising call
+  bool dbg_sync = false;
+  void sync_check(int cls, int level, unsigned grid) {
+    const hipError_t e = hipStreamSynchronize(stream);
+    if (e != hipSuccess)
+      fprintf(stderr, "PT_DEBUG_SYNC: kernel class %d level %d grid %u: %s\n", cls, level, grid, hipGetErrorString(e));
   }
   bool timing = false;
   std::vector<hipEvent_t> evpool;
@@ -259,6 +275,13 @@ static hipError_t zero_async(pt_ctx* c, void* p, size_t bytes) {
   hipLaunchKernelGGL(k_zero_u32, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, (uint32_t*)p, n);
   return hipGetLastError();
 }
+static hipError_t copy_async(pt_ctx* c, void* dst, const void* src, size_t bytes) {
+  const uint32_t n = (uint32_t)(bytes / 4);
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_copy_u32, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, (const uint32_t*)src,
+                     (uint32_t*)dst, n);
+  return hipGetLastError();
+}
 static int drain(pt_ctx* c) {
   if (!c->async_pending) return PT_OK;
   if (int rc = flush_sums(c)) return rc;
@@ -286,7 +309,7 @@ static void free_all(pt_ctx* c) {
                   c->d_ps0,    c->d_ps1,     c->d_ps2,     c->d_ps3,     c->d_q,   c->d_qe,   c->d_cnt,
                   c->d_qoff,  c->d_iprefix, c->d_nitems, c->d_icnt, c->d_scan_aux, c->d_rcount, c->d_stats,  c->d_err, c->d_work, c->d_res, c->d_res_b, c->d_accum_b, c->d_wstate, c->d_live, c->d_pool,
                   c->d_pix_of, c->d_accum, c->d_frame, c->d_frame_a[0], c->d_frame_a[1], c->d_tmin, c->d_ray_b, c->d_ps0_b, c->d_ps1_b, c->d_ps2_b,
-                  c->d_ps3_b, c->d_compact, c->d_act_pix, c->d_act_slot};
+                  c->d_ps3_b, c->d_compact, c->d_act_pix, c->d_act_slot, c->d_rcount_bak, c->d_stats_bak};
   for (void* p : ptrs)
     if (p) hipFree(p);
 }
@@ -708,6 +731,7 @@ static TraceArgs trace_args(pt_ctx* c) {
   A.dbg_nslots = (uint32_t)std::min<size_t>((size_t)c->cap_paths * c->cap_spp, 0xFFFFFFFFu);
   A.dbg_nnodes = (uint32_t)c->n_nodes;
   A.dbg_qids = (uint64_t)QREGIONS * c->qcap;
+  A.dbg_nprims = (uint32_t)c->n_prims;
   return A;
 }
 
@@ -1180,6 +1204,7 @@ int pt_create(pt_ctx** out, int device) {
   if (const char* q = getenv("PT_CULL")) c->cull = atoi(q) != 0;
   // (A/B: PT_ACC_BLOCKS=0 sums each pipelined launch by a k_accum of its own)
   if (const char* q = getenv("PT_ACC_BLOCKS")) c->acc_blocks = atoi(q) <= 0 ? 0 : std::max(8, std::min(4096, atoi(q) / 8 * 8));
+  c->dbg_sync = getenv("PT_DEBUG_SYNC") != nullptr;
   if (const char* q = getenv("PT_CHUNK_PATHS")) c->chunk_paths = (uint32_t)std::min<long long>(1ll << 28, std::max(1ll, atoll(q)));
   // tail compaction needs the wave record order's continuing-first ranks
   if (const char* q = getenv("PT_COMPACT")) {
@@ -1202,6 +1227,8 @@ int pt_create(pt_ctx** out, int device) {
   if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) c->copy_stream = nullptr;
   if (hipMalloc((void**)&c->d_stats, STAT_COUNT * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_rcount, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
+      hipMalloc((void**)&c->d_rcount_bak, RCOUNT_SLOTS * 16 * 8) != hipSuccess ||
+      hipMalloc((void**)&c->d_stats_bak, STAT_COUNT * 8) != hipSuccess ||
       hipMalloc((void**)&c->d_err, 4) != hipSuccess || hipMalloc((void**)&c->d_work, PATH_REGIONS_MAX * PATH_CTR_STRIDE * 4) != hipSuccess ||
       hipMalloc((void**)&c->d_live, LIVE_WORDS * 4) != hipSuccess ||
       hipMalloc((void**)&c->d_compact, MAX_COMPACTIONS * CBLK * 4) != hipSuccess ||
@@ -1376,6 +1403,7 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
   HIPCHK(c, hipMemset(c->d_qoff, 0, (size_t)s->n_nodes * NLANE * 4));
   c->light = s->light;
   c->camera = s->camera;
+  c->cull_valid = false;  // (the culled pixels depend on the scene's box, not only on the camera)
   c->n_lights = s->n_lights > 1 ? (uint32_t)s->n_lights : 0u;
   if (c->n_lights)
     HIPCHK(c, hipMemcpy(c->d_lights, s->lights, sizeof(pt_light) * c->n_lights, hipMemcpyHostToDevice));
@@ -1718,6 +1746,11 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     } else {
       // N path slots run the chunk's M paths: a slot whose path ends starts the
       // next one in the same shade kernel, so every pass traces a full pool
+      // (the counters as the chunk starts, for a re-run after a queue overflow)
+      HIPCHK(c, copy_async(c, c->d_rcount_bak, c->d_rcount, RCOUNT_SLOTS * 16 * 8));
+      HIPCHK(c, copy_async(c, c->d_stats_bak, c->d_stats, STAT_COUNT * 8));
+      const pt_stats stats0 = c->stats;
+      const size_t marks0 = c->marks.size(), evn0 = c->evn;
       const uint32_t cap = max_batch_paths(c, 1 + nsh);
       uint32_t target = P->batch_paths > 0 ? (uint32_t)P->batch_paths : DEFAULT_BATCH_PATHS;
       const uint32_t N = std::min<uint32_t>(std::min<uint32_t>(target, cap), M);
@@ -1817,11 +1850,13 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
           } else {
             HIPCHK(c, pt_launch_shade_push(nsh, c->refa, xl, Gc, c->stream, nullptr, nullptr, &S));
           }
+          if (c->dbg_sync) c->sync_check(pt_ctx::K_SHADE, comp ? 1 : 0, Gc);
           if (comp) {
             hipLaunchKernelGGL(k_compact_wstate, dim3((Gc + TPB - 1) / TPB), dim3(TPB), 0, c->stream, S.wstate, Gc,
                                Gnew, timed ? c->d_stats + STAT_SHADED : (unsigned long long*)nullptr);
             hipLaunchKernelGGL(k_compact_slots, dim3(Gnew), dim3(TPB), 0, c->stream, S.ps0, S.wstate,
                                (const uint32_t*)S.compact, S.creg, c->d_compact + ncomp * CBLK + CREGIONS);
+            if (c->dbg_sync) c->sync_check(100, 0, Gnew);
             HIPCHK(c, hipGetLastError());
             S.nact = c->d_compact + ncomp * CBLK + CREGIONS;
             S.compact = nullptr;
@@ -1836,6 +1871,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
         HIPCHK(c, zero_async(c, c->d_live, LIVE_WORDS * 4));
         hipLaunchKernelGGL(k_live_sum, dim3(LIVE_SUM_BLOCKS), dim3(1024), 0, c->stream, (const uint4*)S.wstate, Gc,
                            (const uint32_t*)c->d_pool, nblocks, c->d_live, (unsigned long long*)nullptr);
+        if (c->dbg_sync) c->sync_check(101, 0, Gc);
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 4 * (g & 1), c->d_live, 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_poll + 4 * (g & 1) + 2, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->ev_poll[g & 1], c->stream));
@@ -1901,6 +1937,18 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
           return fail(c, PT_E_OVERFLOW, "ray queue capacity exceeded (u32 queue offsets)");
         c->qfactor *= 2;
         HIPCHK(c, zero_async(c, c->d_err, 4));
+        // The passes queued behind the overflowing one ran on: their shade
+        // kernels pushed rays into the root targets' queues that no level
+        // consumed, so the (node, lane) counters are not all zero -- a re-run
+        // would read that many stale ids from its reallocated queues (a
+        // memory fault).  Zero them, and take back the abandoned passes' ray
+        // and visit counts.
+        HIPCHK(c, zero_async(c, c->d_cnt, (size_t)c->n_nodes * NLANE * CSTRIDE * 4));
+        HIPCHK(c, copy_async(c, c->d_rcount, c->d_rcount_bak, RCOUNT_SLOTS * 16 * 8));
+        HIPCHK(c, copy_async(c, c->d_stats, c->d_stats_bak, STAT_COUNT * 8));
+        c->stats = stats0;
+        c->marks.resize(marks0);
+        c->evn = evn0;
         continue;
       }
       if (!finished) return fail(c, PT_E_HIP, "paths did not finish within the pass bound");
@@ -2187,6 +2235,9 @@ int pt_intersect_ex(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits, uin
   if (realloc && (rc = set_root_child_offsets(c))) return rc;
   float4* d_in = nullptr;
   HIPCHK(c, hipMalloc((void**)&d_in, (size_t)n * 32));  // rays in, then hit keys out
+  // (the counters before the first try: a retry after a queue overflow counts its rays once)
+  HIPCHK(c, copy_async(c, c->d_rcount_bak, c->d_rcount, RCOUNT_SLOTS * 16 * 8));
+  HIPCHK(c, copy_async(c, c->d_stats_bak, c->d_stats, STAT_COUNT * 8));
   for (;;) {
     HIPCHK(c, hipMemcpyAsync(d_in, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, zero_async(c, c->d_err, 4));
@@ -2217,6 +2268,8 @@ int pt_intersect_ex(pt_ctx* c, const float* rays, int32_t n, uint64_t* hits, uin
       hipFree(d_in);
       return rc;
     }
+    HIPCHK(c, copy_async(c, c->d_rcount, c->d_rcount_bak, RCOUNT_SLOTS * 16 * 8));
+    HIPCHK(c, copy_async(c, c->d_stats, c->d_stats_bak, STAT_COUNT * 8));
   }
   hipLaunchKernelGGL(k_store_hits, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c->stream, c->d_ray,
                      (unsigned long long*)d_in, (uint32_t)n);

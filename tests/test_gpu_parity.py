@@ -107,6 +107,36 @@ def test_queue_overflow_rerun(monkeypatch):
         ctx.close()
 
 
+def test_render_overflow_rerun_counts_and_queues(monkeypatch):
+    """A render (not an intersect) that overflows a level queue at its first
+    chunk: the passes queued behind the abandoned one have pushed rays into
+    the root targets' queues, so the re-run must start from zeroed (node,
+    lane) counters -- stale counts read that many stale ids from the
+    reallocated queues, a memory fault when the recycled memory held floats --
+    and must count only its own rays (the abandoned passes' are taken back):
+    image and ray count equal the oracle's."""
+    rng = np.random.default_rng(11)
+    c = rng.random((3000, 1, 3), dtype=np.float32)
+    tris = (c + 0.6 * (rng.random((3000, 3, 3), dtype=np.float32) - 0.5)).reshape(-1, 9)
+    sc = ptrace.Scene.from_triangles(tris)
+    d = sc.desc()
+    monkeypatch.setenv("PT_QFACTOR", "1")
+    ctx = ptrace.Context(0)
+    monkeypatch.delenv("PT_QFACTOR")
+    try:
+        ctx.load_scene(sc)
+        for k in range(2):  # (the second render runs at the doubled factor, after the first one's buffers)
+            ctx.reset_stats()
+            ctx.clear()
+            ctx.render(64, 64, 4, max_bounces=4, seed=15618 + k)
+            o, orays = pyoracle.image(d, 64, 64, 4, max_bounces=4, seed=15618 + k)
+            assert np.array_equal(ctx.get_image(), o)
+            assert ctx.stats().rays == orays
+        assert ctx.stats().queue_factor > 1  # the overflow path did run
+    finally:
+        ctx.close()
+
+
 def test_overflow_rerun_shrinks_large_batch(gpu_ctx):
     """A large path pool whose level queues overflow: the chunk re-runs with
     twice the queue factor, which the pool no longer fits under u32 queue
