@@ -1656,6 +1656,7 @@ int pt_render(pt_ctx* c, const pt_render_params* P) {
     }
     float4* const res = res_slot;
     ShadeArgs S;
+    S.A.dbg_nprims = (uint32_t)c->n_prims;  // (PT_DBG_BOUNDS; the wavefront branch sets all of S.A)
     S.prims = c->refa ? c->d_prims_ref : c->d_prims;
     S.shade = c->d_shade;
     S.bsdfs = c->d_bsdfs;
