@@ -1206,7 +1206,17 @@ __device__ __forceinline__ void process_wave(const TraceArgs& A, int node, uint3
         }
       }
     };
-    for (int k = 0; k < pcount; ++k, P += PS) leaf_test(load_prim<REFA>(P), k);
+    int k0 = 0;
+    if constexpr (!REFA) {
+      // two records per scalar round trip (one wait per pair)
+      for (; k0 + 1 < pcount; k0 += 2, P += 2 * PS) {
+        Prim qa, qb;
+        load_prim_pair(P, qa, qb);
+        leaf_test(qa, k0);
+        leaf_test(qb, k0 + 1);
+      }
+    }
+    for (int k = k0; k < pcount; ++k, P += PS) leaf_test(load_prim<REFA>(P), k);
 #pragma unroll
     for (int j = 0; j < RPTW; ++j) {
 #ifdef PT_DBG_BOUNDS
