@@ -238,6 +238,46 @@ def test_render_bit_exact(gpu_ctx, name, flags):
     assert o[..., :3].mean() > 0.01
 
 
+def _sparse_soup():
+    """300 small diffuse triangles scattered in a 4-unit cube under a point
+    light, seen from 8 units away: most paths leave the scene early."""
+    rng = np.random.default_rng(5)
+    c = rng.random((300, 1, 3), dtype=np.float32) * 4.0 - 2.0
+    tris = (c + 0.4 * (rng.random((300, 3, 3), dtype=np.float32) - 0.5)).reshape(-1, 9)
+    b = ptrace.pt_bsdf()
+    b.type = ptrace.PT_BSDF_DIFFUSE
+    L = ptrace.pt_light()
+    L.type = ptrace.PT_LIGHT_POINT
+    cam = ptrace.pt_camera()
+    for k in range(3):
+        b.albedo[k] = 0.8
+        L.radiance[k] = 20.0
+        L.position[k] = (0.5, 3.0, 2.5)[k]
+        cam.origin[k], cam.look_at[k], cam.left[k], cam.up[k] = (0, 0, 8)[k], (0, 0, -1)[k], (1, 0, 0)[k], (0, 1, 0)[k]
+    return ptrace.Scene.from_mesh(tris, [b], tri_bsdf=np.zeros(len(tris), np.int32), light=L, camera=cam)
+
+
+@pytest.mark.parametrize("W,H,spp", [(37, 23, 3), (61, 5, 7), (13, 11, 1)])
+def test_shade_tail_workgroups_sparse_paths(gpu_ctx, W, H, spp):
+    """The shade kernel's root pass reads cluster records that its loader
+    waves copied into LDS (global_load_lds, counted by vmcnt): each loader
+    wave waits for its copies before the barrier, also when it holds no live
+    slot.  A sparse soup (most camera rays and nearly every bounce escape)
+    rendered at sizes that are not multiples of the workgroup leaves each
+    pass's last workgroups with loader waves and no live paths; image and ray
+    count equal the oracle's."""
+    sc = _sparse_soup()
+    d = sc.desc()
+    gpu_ctx.load_scene(sc)
+    gpu_ctx.reset_stats()
+    gpu_ctx.clear()
+    gpu_ctx.render(W, H, spp, max_bounces=8, seed=15618)
+    o, orays = pyoracle.image(d, W, H, spp, max_bounces=8, seed=15618)
+    assert np.array_equal(gpu_ctx.get_image(), o)
+    assert gpu_ctx.stats().rays == orays
+    assert orays > W * H * spp  # some paths do bounce
+
+
 @pytest.mark.parametrize("name", ["CBempty", "CBgems", "CBcoil", "CBbunny"])
 def test_closest_hit_ref_arith_bit_exact(gpu_ctx, name):
     """PT_FLAG_REF_ARITH: the literal cu:217-270 triangle test (edge tests
