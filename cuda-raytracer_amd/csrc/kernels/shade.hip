@@ -44,6 +44,24 @@ constexpr uint32_t ERR_KERNARG = 2u;  // pt_ctx::d_err bit: k_path_leaf's kernel
 // slot regions of the tail compaction (ShadeArgs::compact)
 constexpr uint32_t CREGIONS = 64;
 
+// A BSDF on the device: pt_bsdf's fields, then the dielectric's 1 / ior and
+// Fresnel base reflectance r0 = ((1 - ior) / (1 + ior))^2, both computed on the
+// host by IEEE fp32 division (pt_load_scene): the same bits as the kernels'
+// correctly rounded division sequences (rcp_rn, div_rn) gave for an index of
+// refraction in the normal range, without their ~17 instructions at every
+// glass vertex -- a wave with one glass lane ran them all.
+struct alignas(16) BsdfRec {
+  int32_t type;
+  float albedo[3];
+  float transmittance[3];
+  float ior;
+  float roughness;
+  float inv_ior;
+  float r0;
+  float pad;
+};
+static_assert(sizeof(BsdfRec) == 48, "three 16-B loads per BSDF");
+
 struct ShadeArgs {
   float4* ray;  // ray records (trace.h): ext ray of path p in slot p, shadow ray s in slot (1+s)N + p
   float4* ps0;  // T.xyz, flags | vertex << 8
@@ -56,7 +74,7 @@ struct ShadeArgs {
   // normals of a triangle (a sphere: {centre, meta}), built by pt_load_scene
   // from pt_prim + pt_prim_shading so a hit gathers 80 B instead of 96
   const float4* __restrict__ shade;
-  const pt_bsdf* __restrict__ bsdfs;
+  const BsdfRec* __restrict__ bsdfs;  // (BsdfRec: pt_bsdf + the dielectric's host-computed constants)
   const uint32_t* __restrict__ pix_of;
   pt_light light;
   pt_camera cam;
@@ -536,7 +554,7 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
       const f3 n = front ? ns : mk(-ns.x, -ns.y, -ns.z);  // faces the incoming ray (cu:1222)
       // cu:1224 (its.pt += -r->d * 1e-3)
       const f3 pt = mk(__builtin_fmaf(-d.x, EPS, P.x), __builtin_fmaf(-d.y, EPS, P.y), __builtin_fmaf(-d.z, EPS, P.z));
-      pt_bsdf B = S.bsdfs[meta & 0x0FFFFFFFu];
+      BsdfRec B = S.bsdfs[meta & 0x0FFFFFFFu];
       bool emitter = false;
       if (REFA) {
         // cu:1243 (without REAL_TIME): its.light = radiance * importance + light
@@ -701,13 +719,12 @@ __device__ __forceinline__ void shade_vertex(const ShadeArgs& S, uint32_t sidx, 
           float eta = 1.0f, cost = 0.0f;
           if (B.type != PT_BSDF_MIRROR) {
             const float ior = B.ior;
-            eta = front ? rcp_rn(ior) : ior;  // (an index of refraction: normal range)
+            eta = front ? B.inv_ior : ior;
             const float cosi = -dn;
             const float sin2t = (eta * eta) * (1.0f - cosi * cosi);
             if (sin2t < 1.0f) {
               cost = sqrt_rn(1.0f - sin2t);  // (sin2t < 1: 1 - sin2t >= 2^-24)
-              float r0 = div_rn(1.0f - ior, 1.0f + ior);  // (1 - ior: 0 or >= 2^-24 in magnitude)
-              r0 = r0 * r0;
+              const float r0 = B.r0;
               const float c = front ? cosi : cost;
               const float m = 1.0f - c;
               const float F = __builtin_fmaf(1.0f - r0, ((m * m) * (m * m)) * m, r0);

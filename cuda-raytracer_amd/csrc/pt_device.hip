@@ -81,7 +81,7 @@ struct pt_ctx {
   float* d_tmin = nullptr;        // their t_min per ray slot
   size_t tmin_cap = 0;
   float4* d_shade = nullptr;  // hit-shading records (SHADE_REC float4 per primitive)
-  pt_bsdf* d_bsdfs = nullptr;
+  BsdfRec* d_bsdfs = nullptr;
   pt_light* d_lights = nullptr;  // pt_scene_desc.lights (n_lights > 1)
   uint32_t n_lights = 0;
   float* d_cbox = nullptr;  // single-leaf scenes: boxes of the leaf's primitive pairs, 8 floats each
@@ -1397,8 +1397,27 @@ int pt_load_scene(pt_ctx* c, const pt_scene_desc* s) {
     }
     HIPCHK(c, hipMemcpy(c->d_shade, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice));
   }
-  if (s->n_bsdfs > 0)
-    HIPCHK(c, hipMemcpy(c->d_bsdfs, s->bsdfs, sizeof(pt_bsdf) * s->n_bsdfs, hipMemcpyHostToDevice));
+  if (s->n_bsdfs > 0) {
+    // pt_bsdf + the dielectric's 1 / ior and r0 in IEEE fp32 (BsdfRec; this
+    // translation unit is built with -ffp-contract=off)
+    std::vector<BsdfRec> br((size_t)s->n_bsdfs);
+    for (int i = 0; i < s->n_bsdfs; ++i) {
+      const pt_bsdf& b = s->bsdfs[i];
+      BsdfRec& r = br[(size_t)i];
+      r.type = b.type;
+      for (int k = 0; k < 3; ++k) {
+        r.albedo[k] = b.albedo[k];
+        r.transmittance[k] = b.transmittance[k];
+      }
+      r.ior = b.ior;
+      r.roughness = b.roughness;
+      r.inv_ior = 1.0f / b.ior;
+      const float q = (1.0f - b.ior) / (1.0f + b.ior);
+      r.r0 = q * q;
+      r.pad = 0.0f;
+    }
+    HIPCHK(c, hipMemcpy(c->d_bsdfs, br.data(), sizeof(BsdfRec) * br.size(), hipMemcpyHostToDevice));
+  }
   HIPCHK(c, hipMemset(c->d_cnt, 0, (size_t)s->n_nodes * NLANE * CSTRIDE * 4));
   HIPCHK(c, hipMemset(c->d_qoff, 0, (size_t)s->n_nodes * NLANE * 4));
   c->light = s->light;
